@@ -1,0 +1,70 @@
+/*
+ * lddl_amd -- C-ABI of the MI355X (gfx950) preprocessing hot path.
+ *
+ * The reference (alvin-zyl/LDDL) is pure Python; its hot path sits behind
+ * three seams, each replaced here by an entry point of liblddl_amd.so:
+ *
+ *   lddl_create / lddl_destroy
+ *       replaces transformers.BertTokenizerFast(vocab_file)
+ *       (lddl/dask/bert/pretrain.py:584-587, pretrain_codebert.py:617 --
+ *       the latter substituted by WordPiece over codebert_52000/vocab.txt).
+ *   lddl_tokenize
+ *       replaces the per-sentence tokenizer.tokenize(s, max_length=512,
+ *       truncation=True) of _get_documents._to_document
+ *       (pretrain.py:79-80, :82-95) and _get_code_pairs (pretrain_codebert.py:
+ *       123-124), batched over every sentence of a shard.
+ *   lddl_pack_bert / lddl_pack_codebert / lddl_bin / lddl_materialize
+ *       replace _get_pairs._to_partition_pairs (pretrain.py:386-402 with
+ *       create_pairs_from_document :241-365, pretrain_codebert.py:460-477 with
+ *       :343-442) and the binned writer's grouping
+ *       (binning.py:63-93 _to_dataframe_binned).
+ *
+ * Conventions: every pointer named d_* is a DEVICE pointer on the ctx's
+ * device; work is enqueued on `stream` (a hipStream_t, NULL = default) and is
+ * asynchronous.  Return value 0 = ok, < 0 = LDDL_E* (message: lddl_last_error,
+ * thread-local).  One call at a time per ctx (the ctx owns scratch).
+ * Input text must be valid UTF-8 (Python str.encode output).
+ */
+#ifndef LDDL_AMD_H_
+#define LDDL_AMD_H_
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LDDL_EINVAL -1
+#define LDDL_EIO -2
+#define LDDL_EFORMAT -3
+#define LDDL_ENOMEM -4
+#define LDDL_EHIP -5
+#define LDDL_ECAPACITY -6
+/* pretrain_codebert.py:421 _truncate_seq(code, max_num - len(doc)) with a
+ * negative budget raises IndexError in the reference; reported as this code */
+#define LDDL_EINDEX -7
+
+typedef struct lddl_ctx lddl_ctx;
+
+const char *lddl_last_error(void);
+
+/* vocab.txt: line i -> id i (reference: BertTokenizerFast(vocab_file)).
+ * table_path: lddl_amd/data/unicode_table.bin. */
+int lddl_create(const char *vocab_path, const char *table_path, int device, lddl_ctx **out);
+void lddl_destroy(lddl_ctx *ctx);
+int lddl_vocab_size(const lddl_ctx *ctx);
+/* ids of [PAD] [UNK] [CLS] [SEP] [MASK] */
+int lddl_special_ids(const lddl_ctx *ctx, int32_t out[5]);
+/* NUL-terminated vocab entry `id` into buf; returns its length */
+int lddl_vocab_token(const lddl_ctx *ctx, int32_t id, char *buf, int64_t cap);
+
+/* Tokenise n_sent sentences (bytes [d_sent_off[s], d_sent_off[s+1])).
+ * Sentence s's ids go to d_out_ids[d_sent_off[s] - d_sent_off[0] + k],
+ * k < d_out_ntok[s] = min(#tokens, max_tok).  d_out_ids needs
+ * d_sent_off[n_sent] - d_sent_off[0] entries (#tokens <= #bytes). */
+int lddl_tokenize(lddl_ctx *ctx, const uint8_t *d_bytes, const int64_t *d_sent_off, int64_t n_sent,
+                  int32_t max_tok, uint16_t *d_out_ids, int32_t *d_out_ntok, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,48 @@
+"""Build liblddl_amd.so (gfx950) and the oracle's liboracle.so in-tree.
+
+    python -m lddl_amd.build          # both
+The HIP library is the product; the oracle build is test infrastructure.
+"""
+import glob
+import os
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, 'csrc')
+LIB = os.path.join(PKG, 'liblddl_amd.so')
+ARCH = os.environ.get('LDDL_OFFLOAD_ARCH', 'gfx950')
+
+
+def _newer(target, deps):
+  if not os.path.exists(target):
+    return True
+  t = os.path.getmtime(target)
+  return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build_hip(force=False, verbose=False):
+  srcs = sorted(glob.glob(os.path.join(CSRC, '*.hip')))
+  deps = srcs + glob.glob(os.path.join(CSRC, '*.h')) + [os.path.join(ROOT, 'include', 'lddl_amd.h')]
+  if not force and not _newer(LIB, deps):
+    return LIB
+  cmd = ['hipcc', '--offload-arch=%s' % ARCH, '-O3', '-std=c++17', '-fPIC', '-shared',
+         '-Wno-unused-result', '-o', LIB + '.tmp'] + srcs
+  if verbose:
+    print(' '.join(cmd))
+  subprocess.run(cmd, check=True, cwd=CSRC)
+  os.replace(LIB + '.tmp', LIB)
+  return LIB
+
+
+def build_oracle(force=False):
+  odir = os.path.join(ROOT, 'oracle')
+  subprocess.run(['make', '-s'] + (['-B'] if force else []), check=True, cwd=odir)
+  return os.path.join(odir, 'liboracle.so')
+
+
+if __name__ == '__main__':
+  force = '--force' in sys.argv
+  print(build_hip(force, verbose=True))
+  print(build_oracle(force))

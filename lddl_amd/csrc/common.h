@@ -1,0 +1,56 @@
+// Shared host/device definitions for the lddl_amd HIP path (gfx950).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define LDDL_HD __host__ __device__ __forceinline__
+
+namespace lddl {
+
+// ---- Unicode table entry layout (tools/gen_unicode_table.py) -------------
+// bits 0-20 payload (mapped code point / multi index), 21-23 canonical
+// reordering rank (0 = starter), 24-25 pre-tokenizer class, 26-28 kind.
+enum : uint32_t { KIND_IDENT = 0, KIND_MAP = 1, KIND_DROP_T = 2, KIND_DROP_D = 3, KIND_MULTI = 4 };
+enum : uint32_t { CLS_OTHER = 0, CLS_SPACE = 1, CLS_ISOLATE = 2 };
+
+LDDL_HD uint32_t ent_kind(uint32_t e) { return e >> 26; }
+LDDL_HD uint32_t ent_cls(uint32_t e) { return (e >> 24) & 3u; }
+LDDL_HD uint32_t ent_rank(uint32_t e) { return (e >> 21) & 7u; }
+LDDL_HD uint32_t ent_payload(uint32_t e) { return e & 0x1FFFFFu; }
+
+// ---- vocab hash ------------------------------------------------------------
+// Polynomial hash over the bytes of a candidate piece (without "##"), so a
+// candidate can be shrunk by one byte in O(1): H' = (H - (b+1)) * P^-1.
+constexpr uint64_t HASH_P = 0x100000001B3ULL;
+
+constexpr uint64_t inv64(uint64_t a) {
+  uint64_t x = a;  // Newton: x = x * (2 - a*x), 6 steps give 64 bits
+  for (int i = 0; i < 6; ++i) x *= 2 - a * x;
+  return x;
+}
+constexpr uint64_t HASH_PINV = inv64(HASH_P);
+static_assert(HASH_P * HASH_PINV == 1ULL, "inverse");
+
+LDDL_HD uint64_t hash_push(uint64_t h, uint32_t b) { return h * HASH_P + (uint64_t)(b + 1); }
+LDDL_HD uint64_t hash_pop(uint64_t h, uint32_t b) { return (h - (uint64_t)(b + 1)) * HASH_PINV; }
+
+LDDL_HD uint64_t hash_key(uint64_t h, uint32_t len, uint32_t cont) {
+  uint64_t x = h ^ ((uint64_t)len << 56) ^ (cont ? 0x9E3779B97F4A7C15ULL : 0ULL);
+  x ^= x >> 30;
+  x *= 0xBF58476D1CE4E5B9ULL;
+  x ^= x >> 27;
+  x *= 0x94D049BB133111EBULL;
+  x ^= x >> 31;
+  return x;
+}
+
+// slot.y layout: id (16) | len (8) << 16 | cont << 24 | valid << 31
+LDDL_HD uint32_t slot_info(uint32_t id, uint32_t len, uint32_t cont) {
+  return id | (len << 16) | (cont << 24) | 0x80000000u;
+}
+
+// ---- MT19937 (CPython random) ----------------------------------------------
+constexpr int MT_N = 624;
+constexpr int MT_M = 397;
+
+}  // namespace lddl

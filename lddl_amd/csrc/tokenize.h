@@ -1,0 +1,38 @@
+// Kernel parameter blocks for the tokenizer (device side of lddl_tokenize).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace lddl {
+
+constexpr int WB_OVF = 384;  // per-lane overflow word buffer (bytes beyond LDS)
+
+struct TokParams {
+  const uint8_t* bytes;
+  const int64_t* sent_off;
+  int64_t n_sent;
+  int32_t max_tok;
+  int32_t chunk;
+  uint16_t* out_ids;
+  int32_t* out_ntok;
+  // unicode table
+  const uint16_t* top;
+  const uint32_t* pages;
+  const uint4* multi;
+  // vocab
+  const uint2* slots;
+  uint32_t slot_mask;
+  const uint8_t* pool;
+  const uint32_t* voff;
+  uint32_t maxb[2];
+  uint32_t special[5];
+  uint32_t unk;
+  // scratch
+  uint8_t* ovf;
+  uint32_t* work_counter;
+};
+
+hipError_t launch_tokenize(const TokParams& P, int grid, hipStream_t stream);
+const void* tokenize_kernel_ptr();
+
+}  // namespace lddl

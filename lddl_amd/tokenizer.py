@@ -1,0 +1,102 @@
+"""MI355X WordPiece tokenizer: drop-in for the BertTokenizerFast object the
+reference builds in lddl/dask/bert/pretrain.py:584-587 and calls at :79-80.
+
+``Tokenizer(vocab_file).tokenize(s, max_length=512, truncation=True)``
+returns the same token strings (one sentence; convenience / parity surface),
+``tokenize_device(...)`` is the batched hot-path entry: every sentence of a
+shard in one launch, inputs and outputs resident in HBM.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+
+
+def _ptr(t):
+  return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def _stream(stream=None):
+  s = stream if stream is not None else torch.cuda.current_stream()
+  return ctypes.c_void_p(s.cuda_stream)
+
+
+class Tokenizer:
+  """Owns the device vocab/Unicode tables for one GPU (one lddl_ctx)."""
+
+  def __init__(self, vocab_file=_lib.VOCAB_BERT, device=None):
+    if not torch.cuda.is_available():
+      raise RuntimeError('lddl_amd.Tokenizer needs a ROCm GPU (no CPU fallback)')
+    self.device = torch.device('cuda', torch.cuda.current_device() if device is None else device)
+    L = _lib.lib()
+    h = ctypes.c_void_p()
+    _lib.check(L.lddl_create(vocab_file.encode(), _lib.TABLE_PATH.encode(), self.device.index,
+                             ctypes.byref(h)))
+    self._h = h
+    self.vocab_file = vocab_file
+    self.vocab_size = _lib.check(L.lddl_vocab_size(h))
+    ids = (ctypes.c_int32 * 5)()
+    _lib.check(L.lddl_special_ids(h, ids))
+    self.pad_id, self.unk_id, self.cls_id, self.sep_id, self.mask_id = list(ids)
+    with open(vocab_file, encoding='utf-8') as f:
+      self.ids_to_tokens = [l.rstrip('\n').rstrip('\r') for l in f]
+    if self.ids_to_tokens and self.ids_to_tokens[-1] == '' and len(self.ids_to_tokens) > self.vocab_size:
+      self.ids_to_tokens.pop()
+    self.vocab = {t: i for i, t in enumerate(self.ids_to_tokens)}
+
+  def close(self):
+    if getattr(self, '_h', None):
+      _lib.lib().lddl_destroy(self._h)
+      self._h = None
+
+  def __del__(self):
+    try:
+      self.close()
+    except Exception:
+      pass
+
+  @property
+  def handle(self):
+    return self._h
+
+  # ---- batched hot path -------------------------------------------------
+  def tokenize_device(self, data, sent_off, max_tok=512, out_ids=None, out_ntok=None, stream=None):
+    """data: uint8 cuda tensor; sent_off: int64 cuda tensor [n_sent+1].
+    Returns (ids int16 view of uint16 [nbytes], ntok int32 [n_sent]); sentence
+    s's ids start at sent_off[s] - sent_off[0]."""
+    n_sent = sent_off.numel() - 1
+    nbytes = int(data.numel())
+    if out_ids is None:
+      out_ids = torch.empty(max(nbytes, 1), dtype=torch.int16, device=self.device)
+    if out_ntok is None:
+      out_ntok = torch.empty(max(n_sent, 1), dtype=torch.int32, device=self.device)
+    assert data.dtype == torch.uint8 and sent_off.dtype == torch.int64
+    assert data.is_cuda and sent_off.is_cuda and out_ids.numel() >= nbytes
+    _lib.check(_lib.lib().lddl_tokenize(self._h, _ptr(data), _ptr(sent_off), n_sent, max_tok,
+                                        _ptr(out_ids), _ptr(out_ntok), _stream(stream)))
+    return out_ids, out_ntok
+
+  def encode_batch(self, sentences, max_tok=512):
+    """list[str] -> list[list[int]] (compact host result)."""
+    enc = [s.encode('utf-8') for s in sentences]
+    off = np.zeros(len(enc) + 1, dtype=np.int64)
+    np.cumsum([len(b) for b in enc], out=off[1:])
+    raw = np.frombuffer(b''.join(enc) + b'\0' * 16, dtype=np.uint8)
+    d = torch.from_numpy(raw.copy()).to(self.device)
+    o = torch.from_numpy(off).to(self.device)
+    ids, ntok = self.tokenize_device(d, o, max_tok)
+    ids = ids.cpu().numpy().view(np.uint16)
+    ntok = ntok.cpu().numpy()
+    return [ids[off[i]:off[i] + ntok[i]].astype(np.int64).tolist() for i in range(len(enc))]
+
+  # ---- reference-compatible surface --------------------------------------
+  def tokenize(self, text, max_length=512, truncation=True, **kwargs):
+    """Same result as BertTokenizerFast.tokenize as called at pretrain.py:79-80
+    under transformers 4.16.2 (per-sentence truncation to max_length)."""
+    ids = self.encode_batch([text], max_length if truncation else 1 << 30)[0]
+    return [self.ids_to_tokens[i] for i in ids]
+
+  def convert_tokens_to_ids(self, tokens):
+    return [self.vocab.get(t, self.unk_id) for t in tokens]

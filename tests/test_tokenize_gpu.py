@@ -1,0 +1,76 @@
+"""HIP tokenizer vs the golden vectors (tokenizers 0.22.2) and vs the oracle."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import ROOT
+from oracle.oracle import OracleTokenizer, compact
+from test_oracle_golden import VOCABS
+
+pytestmark = pytest.mark.gpu
+
+
+def run_hip(tok, data, sent_off, max_tok=512):
+  d = torch.from_numpy(np.concatenate([data, np.zeros(16, np.uint8)])).cuda()
+  o = torch.from_numpy(np.ascontiguousarray(sent_off)).cuda()
+  ids, ntok = tok.tokenize_device(d, o, max_tok)
+  torch.cuda.synchronize()
+  return ids.cpu().numpy().view(np.uint16), ntok.cpu().numpy()[:len(sent_off) - 1]
+
+
+@pytest.mark.parametrize('name', ['bert', 'codebert'])
+@pytest.mark.parametrize('max_tok', [512, 9])
+def test_hip_tokenize_matches_golden(gpu, golden, name, max_tok):
+  from lddl_amd.tokenizer import Tokenizer
+  g = golden('tok_%s.npz' % name)
+  tok = Tokenizer(VOCABS[name])
+  ids, ntok = run_hip(tok, g['data'], g['sent_off'], max_tok)
+  assert np.array_equal(ntok, np.minimum(g['ntok'], max_tok))
+  exp = np.split(g['ids'], np.cumsum(g['ntok'])[:-1])
+  got = compact(ids, ntok, g['sent_off'])
+  bad = [i for i, (a, b) in enumerate(zip(exp, got)) if not np.array_equal(a[:max_tok], b)]
+  assert not bad, bad[:10]
+
+
+def test_hip_tokenize_matches_oracle_synthetic(gpu):
+  from lddl_amd import synth
+  from lddl_amd.tokenizer import Tokenizer
+  c = synth.make_wiki(8_000_000, seed=5)
+  tok = Tokenizer(VOCABS['bert'])
+  ids, ntok = run_hip(tok, c.data, c.sent_off)
+  oids, ontok = OracleTokenizer(VOCABS['bert']).run(c.data, c.sent_off, 512, nthreads=8)
+  assert np.array_equal(ntok, ontok)
+  mask = np.zeros(c.nbytes, dtype=bool)
+  starts = c.sent_off[:-1] - c.sent_off[0]
+  # compare every emitted id position
+  idx = np.repeat(starts, ntok) + (np.arange(ntok.sum()) - np.repeat(np.cumsum(ntok) - ntok, ntok))
+  assert np.array_equal(ids[idx].astype(np.int64), oids[idx].astype(np.int64))
+  del mask
+
+
+def test_hip_tokenize_code_corpus_codebert_vocab(gpu):
+  from lddl_amd import synth
+  from lddl_amd.tokenizer import Tokenizer
+  c = synth.make_code(3000, seed=9)
+  tok = Tokenizer(VOCABS['codebert'])
+  ids, ntok = run_hip(tok, c.data, c.sent_off)
+  oids, ontok = OracleTokenizer(VOCABS['codebert']).run(c.data, c.sent_off, 512, nthreads=8)
+  assert np.array_equal(ntok, ontok)
+  for a, b in zip(compact(ids, ntok, c.sent_off), compact(oids, ontok, c.sent_off)):
+    assert np.array_equal(a.astype(np.int64), b.astype(np.int64))
+
+
+def test_hip_tokenize_edge_sizes(gpu):
+  from lddl_amd.tokenizer import Tokenizer
+  tok = Tokenizer(VOCABS['bert'])
+  sents = ['', 'a', ' ', '[SEP]', 'x' * 5000, ' '.join(['hello'] * 3000), 'ab' * 400]
+  got = tok.encode_batch(sents)
+  ot = OracleTokenizer(VOCABS['bert'])
+  from lddl_amd.synth import corpus_from_sentences
+  c = corpus_from_sentences(sents, [0, len(sents)])
+  oids, ontok = ot.run(c.data, c.sent_off)
+  assert [list(map(int, x)) for x in compact(oids, ontok, c.sent_off)] == got
+  assert tok.tokenize('Hello, World! foo[SEP]bar') == ['hello', ',', 'world', '!', 'foo', '[SEP]', 'bar']
+  # a shard of 1 sentence and of 0 sentences
+  assert tok.encode_batch(['x']) == [[tok.vocab['x']]]
+  assert tok.encode_batch([]) == []
