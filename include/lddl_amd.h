@@ -42,6 +42,8 @@ extern "C" {
 /* pretrain_codebert.py:421 _truncate_seq(code, max_num - len(doc)) with a
  * negative budget raises IndexError in the reference; reported as this code */
 #define LDDL_EINDEX -7
+/* pretrain.py:330-331 / pretrain_codebert.py:423 assert len(...) >= 1 */
+#define LDDL_EASSERT -8
 
 typedef struct lddl_ctx lddl_ctx;
 
@@ -63,6 +65,43 @@ int lddl_vocab_token(const lddl_ctx *ctx, int32_t id, char *buf, int64_t cap);
  * d_sent_off[n_sent] - d_sent_off[0] entries (#tokens <= #bytes). */
 int lddl_tokenize(lddl_ctx *ctx, const uint8_t *d_bytes, const int64_t *d_sent_off, int64_t n_sent,
                   int32_t max_tok, uint16_t *d_out_ids, int32_t *d_out_ntok, void *stream);
+
+/* Pack every partition of a tokenised shard set.
+ * Partition p = docs [d_part_doc_off[p], d_part_doc_off[p+1]); doc d =
+ * sentences [d_doc_sent_off[d], d_doc_sent_off[d+1]); d_ntok / d_sent_off are
+ * lddl_tokenize's output / input.  Partition p is packed exactly like the
+ * reference's _to_partition_pairs (pretrain.py:386-402) after
+ * random.seed(seed + p): duplicate_factor passes of create_pairs_from_document
+ * (:241-365), then random.shuffle, then (bin_size > 0) the stable bin
+ * grouping of binning.py:63-93.  Synchronises the stream once and returns
+ * out_totals = {#pairs, #tokens (with [CLS]/[SEP]), nbins}; the rows are
+ * then written by lddl_materialize.  masking != 0: static MLM masking
+ * (create_masked_lm_predictions :182-238). */
+int lddl_pack_bert(lddl_ctx *ctx, const int32_t *d_ntok, const int64_t *d_sent_off, int64_t n_sent,
+                   const int64_t *d_doc_sent_off, int64_t n_doc, const int64_t *d_part_doc_off, int64_t n_part,
+                   int32_t target_seq_length, double short_seq_prob, int32_t duplicate_factor, int32_t masking,
+                   double masked_lm_ratio, uint64_t seed, int32_t bin_size, int64_t *out_totals, void *stream);
+
+/* CodeBERT docstring/code packing (pretrain_codebert.py:343-442, :460-477).
+ * Doc d's first d_doc_nseg_doc[d] sentences are its docstring segments, the
+ * rest its code segments (one per source line, pretrain_codebert.py:126-159). */
+int lddl_pack_codebert(lddl_ctx *ctx, const int32_t *d_ntok, const int64_t *d_sent_off, int64_t n_sent,
+                       const int64_t *d_doc_sent_off, const int32_t *d_doc_nseg_doc, int64_t n_doc,
+                       const int64_t *d_part_doc_off, int64_t n_part, int32_t target_seq_length,
+                       double short_seq_prob, int32_t duplicate_factor, uint64_t seed, int32_t bin_size,
+                       int64_t *out_totals, void *stream);
+
+/* Write the rows of the last pack call in output order (partition-major,
+ * bin-major, shuffled order within a bin = the reference's part.{p}.parquet_{b}
+ * row order).  Row g: d_out_tokens[d_out_tok_off[g] .. d_out_tok_off[g+1]) =
+ * [CLS] A [SEP] B [SEP] (CodeBERT: [CLS] doc [SEP] code [SEP], or
+ * [CLS] code [SEP] when the document has no docstring); len0/len1 = len(A),
+ * len(B); flags bit0 = is_random_next, bit1 = segment 0 is followed by [SEP];
+ * bin = bin id; part = partition.  d_bin_count (optional) receives
+ * int64[n_part][nbins] row counts. */
+int lddl_materialize(lddl_ctx *ctx, const uint16_t *d_ids, uint16_t *d_out_tokens, int64_t *d_out_tok_off,
+                     uint16_t *d_out_len0, uint16_t *d_out_len1, uint8_t *d_out_flags, uint8_t *d_out_bin,
+                     int64_t *d_out_part, int64_t *d_bin_count, void *stream);
 
 #ifdef __cplusplus
 }

@@ -15,6 +15,7 @@
 
 #include "../../include/lddl_amd.h"
 #include "common.h"
+#include "pack.h"
 #include "tokenize.h"
 
 using namespace lddl;
@@ -50,6 +51,16 @@ struct lddl_ctx {
   uint8_t* d_pool = nullptr;
   uint32_t* d_voff = nullptr;
   uint32_t maxb[2] = {0, 0};
+  // pack workspace (grown on demand)
+  struct Buf {
+    void* p = nullptr;
+    size_t cap = 0;
+  };
+  Buf ws[20];
+  PackParams pp{};
+  int64_t last_npairs = -1, last_ntok = -1;
+  int64_t* h_tot = nullptr;  // pinned [4]
+  int pack_codebert = 0;
   // scratch
   int tok_grid = 0;
   uint8_t* d_ovf = nullptr;
@@ -68,6 +79,8 @@ static void free_ctx(lddl_ctx* c) {
   (void)hipFree(c->d_voff);
   (void)hipFree(c->d_ovf);
   (void)hipFree(c->d_counter);
+  for (auto& b : c->ws) (void)hipFree(b.p);
+  if (c->h_tot) (void)hipHostFree(c->h_tot);
   delete c;
 }
 
@@ -268,5 +281,165 @@ extern "C" int lddl_tokenize(lddl_ctx* c, const uint8_t* d_bytes, const int64_t*
   int grid = (int)((waves + 3) / 4);
   if (grid > c->tok_grid) grid = c->tok_grid;
   HIP_TRY(launch_tokenize(P, grid, st));
+  return 0;
+}
+
+// ------------------------------------------------------------------ pack --
+template <class T>
+static int ws_get(lddl_ctx* c, int slot, size_t n, T** out) {
+  auto& b = c->ws[slot];
+  const size_t bytes = (n ? n : 1) * sizeof(T);
+  if (b.cap < bytes) {
+    (void)hipFree(b.p);
+    b.p = nullptr;
+    b.cap = 0;
+    HIP_TRY(hipMalloc(&b.p, bytes));
+    b.cap = bytes;
+  }
+  *out = (T*)b.p;
+  return 0;
+}
+
+static int pack_common(lddl_ctx* c, int codebert, const int32_t* d_ntok, const int64_t* d_sent_off, int64_t n_sent,
+                       const int64_t* d_doc_sent_off, const int32_t* d_doc_nseg_doc, int64_t n_doc,
+                       const int64_t* d_part_doc_off, int64_t n_part, int32_t target_seq_length,
+                       double short_seq_prob, int32_t duplicate_factor, uint64_t seed, int32_t bin_size,
+                       int64_t* out_totals, void* stream) {
+  if (!c) return set_err(LDDL_EINVAL, "null ctx");
+  if (n_part < 1 || n_doc < 0 || n_sent < 0) return set_err(LDDL_EINVAL, "bad sizes");
+  if (!d_ntok || !d_sent_off || !d_doc_sent_off || !d_part_doc_off || !out_totals)
+    return set_err(LDDL_EINVAL, "null pointer");
+  if (codebert && !d_doc_nseg_doc) return set_err(LDDL_EINVAL, "codebert needs doc_nseg_doc");
+  if (target_seq_length < 5 || target_seq_length > 32768)
+    return set_err(LDDL_EINVAL, "target_seq_length %d not in [5, 32768]", target_seq_length);
+  if (duplicate_factor < 1) return set_err(LDDL_EINVAL, "duplicate_factor %d < 1", duplicate_factor);
+  int32_t nbins = 1;
+  if (bin_size > 0) {
+    // pretrain.py:566-571
+    if (bin_size > target_seq_length) return set_err(LDDL_EINVAL, "bin size must be <= target-seq-length");
+    if (target_seq_length % bin_size) return set_err(LDDL_EINVAL, "bin size must divide target-seq-length");
+    nbins = target_seq_length / bin_size;
+  } else {
+    bin_size = 1 << 30;
+  }
+  if (nbins > 255) return set_err(LDDL_EINVAL, "more than 255 bins");
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t st = (hipStream_t)stream;
+  PackParams& P = c->pp;
+  P = PackParams{};
+  P.ntok = d_ntok;
+  P.sent_off = d_sent_off;
+  P.doc_sent_off = d_doc_sent_off;
+  P.part_doc_off = d_part_doc_off;
+  P.doc_nseg_doc = d_doc_nseg_doc;
+  P.n_part = n_part;
+  P.max_seq = target_seq_length;
+  P.dup = duplicate_factor;
+  P.short_seq_prob = short_seq_prob;
+  P.seed = seed;
+  P.bin_size = bin_size;
+  P.nbins = nbins;
+  const size_t npair_cap = (size_t)duplicate_factor * (size_t)(n_sent ? n_sent : 1);
+  int rc;
+  if ((rc = ws_get(c, 0, n_sent, &P.fs_ntok)) || (rc = ws_get(c, 1, n_sent, &P.fs_base)) ||
+      (rc = ws_get(c, 2, n_doc, &P.fd_first)) || (rc = ws_get(c, 3, n_doc, &P.fd_n)) ||
+      (rc = ws_get(c, 4, n_doc, &P.fd_nd)) ||
+      (rc = ws_get(c, 5, (size_t)((n_part + 63) / 64) * 156 * 64, &P.mt)) ||
+      (rc = ws_get(c, 6, npair_cap, &P.pairs)) || (rc = ws_get(c, 7, npair_cap, &P.order)) ||
+      (rc = ws_get(c, 8, npair_cap, &P.binned)) || (rc = ws_get(c, 9, npair_cap, &P.tok_local)) ||
+      (rc = ws_get(c, 10, n_part, &P.part_npairs)) || (rc = ws_get(c, 11, n_part, &P.part_ntok)) ||
+      (rc = ws_get(c, 12, (size_t)n_part * nbins, &P.bin_count)) ||
+      (rc = ws_get(c, 13, (size_t)n_part * nbins, &P.bin_cursor)) ||
+      (rc = ws_get(c, 14, n_part, &P.part_err)))
+    return rc;
+  int64_t *pair_base, *tok_base;
+  int32_t* err_any;
+  if ((rc = ws_get(c, 15, n_part + 1, &pair_base)) || (rc = ws_get(c, 16, n_part + 1, &tok_base)) ||
+      (rc = ws_get(c, 17, 4, &err_any)))
+    return rc;
+  if (!c->h_tot) HIP_TRY(hipHostMalloc((void**)&c->h_tot, 4 * sizeof(int64_t)));
+  HIP_TRY(codebert ? launch_pack_codebert(P, st) : launch_pack_bert(P, st));
+  HIP_TRY(launch_scan_parts(P.part_npairs, P.part_ntok, n_part, pair_base, tok_base, P.part_err, err_any, st));
+  HIP_TRY(hipMemcpyAsync(c->h_tot, pair_base + n_part, 8, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(c->h_tot + 1, tok_base + n_part, 8, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(c->h_tot + 2, err_any, 4, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  const int32_t e = (int32_t)(c->h_tot[2] & 0xFFFFFFFF);
+  c->pack_codebert = codebert;
+  if (e & PACK_EINDEX) { c->last_npairs = -1; return set_err(LDDL_EINDEX, "IndexError in _truncate_seq (reference quirk)"); }
+  if (e & PACK_EASSERT) { c->last_npairs = -1; return set_err(LDDL_EASSERT, "AssertionError: empty segment after truncation"); }
+  c->last_npairs = c->h_tot[0];
+  c->last_ntok = c->h_tot[1];
+  out_totals[0] = c->last_npairs;
+  out_totals[1] = c->last_ntok;
+  out_totals[2] = nbins;
+  return 0;
+}
+
+extern "C" int lddl_pack_bert(lddl_ctx* c, const int32_t* d_ntok, const int64_t* d_sent_off, int64_t n_sent,
+                              const int64_t* d_doc_sent_off, int64_t n_doc, const int64_t* d_part_doc_off,
+                              int64_t n_part, int32_t target_seq_length, double short_seq_prob,
+                              int32_t duplicate_factor, int32_t masking, double masked_lm_ratio, uint64_t seed,
+                              int32_t bin_size, int64_t* out_totals, void* stream) {
+  if (masking) return set_err(LDDL_EINVAL, "static masking: use lddl_pack_bert with masking=0 (not built yet)");
+  (void)masked_lm_ratio;
+  return pack_common(c, 0, d_ntok, d_sent_off, n_sent, d_doc_sent_off, nullptr, n_doc, d_part_doc_off, n_part,
+                     target_seq_length, short_seq_prob, duplicate_factor, seed, bin_size, out_totals, stream);
+}
+
+extern "C" int lddl_pack_codebert(lddl_ctx* c, const int32_t* d_ntok, const int64_t* d_sent_off, int64_t n_sent,
+                                  const int64_t* d_doc_sent_off, const int32_t* d_doc_nseg_doc, int64_t n_doc,
+                                  const int64_t* d_part_doc_off, int64_t n_part, int32_t target_seq_length,
+                                  double short_seq_prob, int32_t duplicate_factor, uint64_t seed, int32_t bin_size,
+                                  int64_t* out_totals, void* stream) {
+  return pack_common(c, 1, d_ntok, d_sent_off, n_sent, d_doc_sent_off, d_doc_nseg_doc, n_doc, d_part_doc_off,
+                     n_part, target_seq_length, short_seq_prob, duplicate_factor, seed, bin_size, out_totals, stream);
+}
+
+extern "C" int lddl_materialize(lddl_ctx* c, const uint16_t* d_ids, uint16_t* d_out_tokens, int64_t* d_out_tok_off,
+                                uint16_t* d_out_len0, uint16_t* d_out_len1, uint8_t* d_out_flags, uint8_t* d_out_bin,
+                                int64_t* d_out_part, int64_t* d_bin_count, void* stream) {
+  if (!c) return set_err(LDDL_EINVAL, "null ctx");
+  if (c->last_npairs < 0) return set_err(LDDL_EINVAL, "no successful lddl_pack_* call to materialise");
+  if (!d_ids || !d_out_tokens || !d_out_tok_off || !d_out_len0 || !d_out_len1 || !d_out_flags || !d_out_bin ||
+      !d_out_part)
+    return set_err(LDDL_EINVAL, "null pointer");
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t st = (hipStream_t)stream;
+  const PackParams& P = c->pp;
+  MatParams M{};
+  M.ids = d_ids;
+  M.sent_off = P.sent_off;
+  M.doc_sent_off = P.doc_sent_off;
+  M.part_doc_off = P.part_doc_off;
+  M.fs_base = P.fs_base;
+  M.fs_ntok = P.fs_ntok;
+  M.pairs = P.pairs;
+  M.binned = P.binned;
+  M.tok_local = P.tok_local;
+  M.part_npairs = P.part_npairs;
+  M.pair_base = (const int64_t*)c->ws[15].p;
+  M.tok_base = (const int64_t*)c->ws[16].p;
+  M.n_part = P.n_part;
+  M.dup = P.dup;
+  M.bin_size = P.bin_size;
+  M.nbins = P.nbins;
+  M.cls_id = c->special[2];
+  M.sep_id = c->special[3];
+  M.codebert = c->pack_codebert;
+  M.out_tokens = d_out_tokens;
+  M.out_tok_off = d_out_tok_off;
+  M.out_len0 = d_out_len0;
+  M.out_len1 = d_out_len1;
+  M.out_flags = d_out_flags;
+  M.out_bin = d_out_bin;
+  M.out_part = d_out_part;
+  if (c->last_npairs == 0) {
+    HIP_TRY(hipMemsetAsync(d_out_tok_off, 0, 8, st));
+  } else {
+    HIP_TRY(launch_materialize(M, st));
+  }
+  if (d_bin_count)
+    HIP_TRY(hipMemcpyAsync(d_bin_count, P.bin_count, (size_t)P.n_part * P.nbins * 8, hipMemcpyDeviceToDevice, st));
   return 0;
 }

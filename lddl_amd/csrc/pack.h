@@ -1,0 +1,90 @@
+// Pair packing + binning + materialisation (device side of lddl_pack_* /
+// lddl_materialize).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace lddl {
+
+// One packed instance.  BERT: seg0 = A, seg1 = B; CodeBERT: seg0 = doc,
+// seg1 = code.  A segment is the concatenation of n filtered sentences
+// starting at filtered-sentence slot fs, cut to the token window [lo, hi).
+struct PairRec {
+  int64_t fs0, fs1;
+  uint16_t lo0, hi0, lo1, hi1;
+  uint16_t n0, n1;
+  uint16_t flags;       // bit0 is_random_next; bit1 seg0 present (CodeBERT [SEP] after doc)
+  uint16_t num_tokens;
+};
+static_assert(sizeof(PairRec) == 32, "PairRec is 32 B");
+
+enum : int32_t { PACK_OK = 0, PACK_EASSERT = 1, PACK_EINDEX = 2, PACK_ELIMIT = 3 };
+
+struct PackParams {
+  // tokenizer output + corpus structure
+  const int32_t* ntok;          // [n_sent]
+  const int64_t* sent_off;      // [n_sent+1] byte offsets (token base = sent_off[s]-sent_off[0])
+  const int64_t* doc_sent_off;  // [n_doc+1]
+  const int64_t* part_doc_off;  // [n_part+1]
+  const int32_t* doc_nseg_doc;  // [n_doc] CodeBERT: # leading docstring segments (else null)
+  int64_t n_part;
+  // configuration (reference flag names)
+  int32_t max_seq;              // --target-seq-length
+  int32_t dup;                  // --duplicate-factor
+  double short_seq_prob;        // --short-seq-prob
+  uint64_t seed;                // partition p uses random.seed(seed + p)
+  int32_t bin_size;             // --bin-size (or max_seq when unbinned)
+  int32_t nbins;                // max_seq // bin_size (1 when unbinned)
+  // scratch, indexed like the corpus (sentence / doc / partition slots)
+  int32_t* fs_ntok;             // [n_sent]
+  int64_t* fs_base;             // [n_sent]
+  int64_t* fd_first;            // [n_doc]
+  int32_t* fd_n;                // [n_doc]
+  int32_t* fd_nd;               // [n_doc] CodeBERT docstring segment count
+  uint4* mt;                    // [ceil(n_part/64) * 156 * 64]
+  PairRec* pairs;               // [dup * n_sent]
+  int32_t* order;               // [dup * n_sent]
+  int32_t* binned;              // [dup * n_sent]
+  int64_t* tok_local;           // [dup * n_sent]
+  int64_t* part_npairs;         // [n_part]
+  int64_t* part_ntok;           // [n_part]
+  int64_t* bin_count;           // [n_part * nbins]
+  int64_t* bin_cursor;          // [n_part * nbins] scratch (nbins > 16)
+  int32_t* part_err;            // [n_part]
+};
+
+struct MatParams {
+  const uint16_t* ids;          // tokenizer output (sparse)
+  const int64_t* sent_off;
+  const int64_t* doc_sent_off;
+  const int64_t* part_doc_off;
+  const int64_t* fs_base;
+  const int32_t* fs_ntok;
+  const PairRec* pairs;
+  const int32_t* binned;
+  const int64_t* tok_local;
+  const int64_t* part_npairs;
+  const int64_t* pair_base;     // [n_part+1] exclusive scan of part_npairs
+  const int64_t* tok_base;      // [n_part+1] exclusive scan of part_ntok
+  int64_t n_part;
+  int32_t dup;
+  int32_t bin_size, nbins;
+  uint32_t cls_id, sep_id;
+  int32_t codebert;
+  // outputs, global final order (partition-major, bin-major, shuffled)
+  uint16_t* out_tokens;         // [total tokens]  [CLS] A [SEP] B [SEP]
+  int64_t* out_tok_off;         // [n_pairs + 1]
+  uint16_t* out_len0;           // [n_pairs] len(A) / len(doc)
+  uint16_t* out_len1;           // [n_pairs] len(B) / len(code)
+  uint8_t* out_flags;           // [n_pairs] bit0 is_random_next, bit1 seg0 present
+  uint8_t* out_bin;             // [n_pairs]
+  int64_t* out_part;            // [n_pairs] partition id (for ids / file names)
+};
+
+hipError_t launch_pack_bert(const PackParams& P, hipStream_t s);
+hipError_t launch_pack_codebert(const PackParams& P, hipStream_t s);
+hipError_t launch_scan_parts(const int64_t* a, const int64_t* b, int64_t n, int64_t* sa, int64_t* sb,
+                             const int32_t* err, int32_t* err_any, hipStream_t s);
+hipError_t launch_materialize(const MatParams& M, hipStream_t s);
+
+}  // namespace lddl

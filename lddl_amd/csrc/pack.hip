@@ -1,0 +1,403 @@
+// Pair packing (BERT NSP, CodeBERT doc/code segments), partition shuffle,
+// sequence binning and row materialisation for gfx950.
+//
+// Reference:
+//   BERT      lddl/dask/bert/pretrain.py:241-365 create_pairs_from_document,
+//             :161-176 _truncate_seq_pair, :386-402 _to_partition_pairs
+//   CodeBERT  lddl/dask/bert/pretrain_codebert.py:343-442, :236-247, :460-477
+//   binning   lddl/dask/bert/binning.py:63-93 _to_dataframe_binned
+//             (bin = (num_tokens-1)//bin_size clamped, stable per-bin order)
+// Restated on the CPU in oracle/pack_oracle.py.
+//
+// Partition p (docs [part_doc_off[p], part_doc_off[p+1])) is the unit of
+// independence: the random-next document is drawn from the same partition
+// and the RNG stream (CPython MT19937 seeded with seed + p) is serial within
+// it.  v1 mapping: one lane per partition runs the serial decision logic
+// (filter -> pack -> shuffle -> bin) writing compact pair records (32 B) into
+// the partition's slot range; materialisation (the bulk byte work: gathering
+// token ids into [CLS] A [SEP] B [SEP] rows) is wave-parallel per pair.
+#include "common.h"
+#include "mt19937.h"
+#include "pack.h"
+
+namespace lddl {
+
+struct PartView {
+  int64_t d0, d1;   // doc range
+  int64_t s0;       // first sentence slot
+  int64_t pb;       // first pair slot = dup * s0
+  int64_t nd;       // filtered docs
+};
+
+// Drop empty sentences and empty documents (pretrain.py:89-97,
+// pretrain_codebert.py:143-161 + filter len(d) > 0).
+__device__ PartView filter_partition(const PackParams& P, int64_t p, bool codebert) {
+  PartView v;
+  v.d0 = P.part_doc_off[p];
+  v.d1 = P.part_doc_off[p + 1];
+  v.s0 = P.doc_sent_off[v.d0];
+  v.pb = (int64_t)P.dup * v.s0;
+  const int64_t base = P.sent_off[0];
+  int64_t slot = v.s0, nd = 0;
+  for (int64_t d = v.d0; d < v.d1; ++d) {
+    const int64_t first = slot;
+    const int64_t sa = P.doc_sent_off[d], sb = P.doc_sent_off[d + 1];
+    const int64_t sdoc_end = codebert ? sa + P.doc_nseg_doc[d] : sa;
+    int32_t ndoc_seg = 0;
+    for (int64_t s = sa; s < sb; ++s) {
+      const int32_t n = P.ntok[s];
+      if (n > 0) {
+        P.fs_ntok[slot] = n;
+        P.fs_base[slot] = P.sent_off[s] - base;
+        ++slot;
+        if (s < sdoc_end) ++ndoc_seg;
+      }
+    }
+    const int32_t cnt = (int32_t)(slot - first);
+    // CodeBERT keeps a pair only if it has code segments (len(CodePair) > 0)
+    const bool keep = codebert ? (cnt - ndoc_seg) > 0 : cnt > 0;
+    if (keep) {
+      P.fd_first[v.d0 + nd] = first;
+      P.fd_n[v.d0 + nd] = cnt;
+      if (codebert) P.fd_nd[v.d0 + nd] = ndoc_seg;
+      ++nd;
+    } else {
+      slot = first;
+    }
+  }
+  v.nd = nd;
+  return v;
+}
+
+__device__ __forceinline__ MTLane lane_rng(const PackParams& P, int64_t p) {
+  MTLane r;
+  r.S = P.mt + ((size_t)(p >> 6) * 156) * 64 + (p & 63);
+  r.idx = MT_N;
+  return r;
+}
+
+// random.shuffle(partition_pairs) (pretrain.py:401) on the record order,
+// then the stable bin partition + per-pair token offsets.
+__device__ void shuffle_and_bin(const PackParams& P, int64_t p, const PartView& v, int64_t np, MTLane& rng) {
+  int32_t* order = P.order + v.pb;
+  for (int64_t k = 0; k < np; ++k) order[k] = (int32_t)k;
+  for (int64_t k = np - 1; k >= 1; --k) {
+    const int64_t j = rng.randbelow((uint32_t)(k + 1));
+    const int32_t t = order[k];
+    order[k] = order[j];
+    order[j] = t;
+  }
+  const int32_t nb = P.nbins;
+  int64_t* cnt = P.bin_count + p * nb;
+  for (int32_t b = 0; b < nb; ++b) cnt[b] = 0;
+  const PairRec* pr = P.pairs + v.pb;
+  for (int64_t k = 0; k < np; ++k) {
+    int32_t b = ((int32_t)pr[order[k]].num_tokens - 1) / P.bin_size;
+    cnt[b > nb - 1 ? nb - 1 : b]++;
+  }
+  // exclusive per-bin starts: registers when nb <= 16, else bin_cursor
+  int64_t* cur = P.bin_cursor + p * nb;
+  int64_t acc = 0;
+  int64_t cur_r[16];
+  const bool small = nb <= 16;
+  for (int32_t b = 0; b < nb; ++b) {
+    if (small) cur_r[b] = acc; else cur[b] = acc;
+    acc += cnt[b];
+  }
+  int32_t* binned = P.binned + v.pb;
+  for (int64_t k = 0; k < np; ++k) {
+    const int32_t rec = order[k];
+    int32_t b = ((int32_t)pr[rec].num_tokens - 1) / P.bin_size;
+    b = b > nb - 1 ? nb - 1 : b;
+    int64_t pos;
+    if (small) {
+      pos = 0;
+#pragma unroll
+      for (int q = 0; q < 16; ++q)
+        if (q == b) pos = cur_r[q]++;
+    } else {
+      pos = cur[b]++;
+    }
+    binned[pos] = rec;
+  }
+  int64_t* tl = P.tok_local + v.pb;
+  acc = 0;
+  for (int64_t k = 0; k < np; ++k) {
+    tl[k] = acc;
+    acc += pr[binned[k]].num_tokens;
+  }
+  P.part_npairs[p] = np;
+  P.part_ntok[p] = acc;
+}
+
+// ---------------------------------------------------------------- BERT ----
+__global__ __launch_bounds__(64) void pack_bert_kernel(PackParams P) {
+  const int64_t p = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  if (p >= P.n_part) return;
+  const PartView v = filter_partition(P, p, false);
+  MTLane rng = lane_rng(P, p);
+  rng.seed(P.seed + (uint64_t)p);
+  const int32_t max_num = P.max_seq - 3;
+  PairRec* out = P.pairs + v.pb;
+  int64_t np = 0;
+  int32_t err = PACK_OK;
+  for (int32_t dup = 0; dup < P.dup && !err; ++dup) {
+    for (int64_t di = 0; di < v.nd && !err; ++di) {
+      const int64_t first = P.fd_first[v.d0 + di];
+      const int32_t len = P.fd_n[v.d0 + di];
+      int32_t target = max_num;
+      if (rng.random() < P.short_seq_prob) target = (int32_t)rng.randint(2, max_num);
+      int32_t cs = 0, nchunk = 0, cur = 0;
+      for (int32_t i = 0; i < len; ++i) {
+        if (nchunk == 0) cs = i;
+        ++nchunk;
+        cur += P.fs_ntok[first + i];
+        if (i == len - 1 || cur >= target) {
+          int32_t a_end = 1;
+          if (nchunk >= 2) a_end = (int32_t)rng.randint(1, nchunk - 1);
+          int32_t la = 0;
+          for (int32_t j = 0; j < a_end; ++j) la += P.fs_ntok[first + cs + j];
+          PairRec r;
+          r.fs0 = first + cs;
+          r.n0 = (uint16_t)a_end;
+          int32_t lb = 0;
+          bool rn;
+          if (nchunk == 1 || rng.random() < 0.5) {
+            rn = true;
+            const int32_t tb = target - la;
+            int64_t rdi = 0;
+            for (int t = 0; t < 10; ++t) {
+              rdi = rng.randint(0, v.nd - 1);
+              if (rdi != di) break;
+            }
+            if (rdi == di) rn = false;
+            const int64_t rfirst = P.fd_first[v.d0 + rdi];
+            const int32_t rlen = P.fd_n[v.d0 + rdi];
+            const int32_t rstart = (int32_t)rng.randint(0, rlen - 1);
+            int32_t bn = 0;
+            for (int32_t j = rstart; j < rlen; ++j) {
+              lb += P.fs_ntok[rfirst + j];
+              ++bn;
+              if (lb >= tb) break;
+            }
+            r.fs1 = rfirst + rstart;
+            r.n1 = (uint16_t)bn;
+            i -= nchunk - a_end;
+          } else {
+            rn = false;
+            r.fs1 = first + cs + a_end;
+            r.n1 = (uint16_t)(nchunk - a_end);
+            for (int32_t j = a_end; j < nchunk; ++j) lb += P.fs_ntok[first + cs + j];
+          }
+          // _truncate_seq_pair: longer side (ties -> B), front/back by coin
+          int32_t alo = 0, ahi = la, blo = 0, bhi = lb;
+          while ((ahi - alo) + (bhi - blo) > max_num) {
+            const bool ta = (ahi - alo) > (bhi - blo);
+            if (rng.random() < 0.5) { if (ta) ++alo; else ++blo; }
+            else { if (ta) --ahi; else --bhi; }
+          }
+          if (ahi - alo < 1 || bhi - blo < 1) { err = PACK_EASSERT; break; }
+          r.lo0 = (uint16_t)alo; r.hi0 = (uint16_t)ahi;
+          r.lo1 = (uint16_t)blo; r.hi1 = (uint16_t)bhi;
+          r.flags = (uint16_t)((rn ? 1 : 0) | 2);
+          r.num_tokens = (uint16_t)((ahi - alo) + (bhi - blo) + 3);
+          out[np++] = r;
+          nchunk = 0;
+          cur = 0;
+        }
+      }
+    }
+  }
+  P.part_err[p] = err;
+  if (err) { P.part_npairs[p] = 0; P.part_ntok[p] = 0; return; }
+  shuffle_and_bin(P, p, v, np, rng);
+}
+
+// ------------------------------------------------------------- CodeBERT ----
+// _truncate_seq: 1 coin per excess token; deleting from an empty list is the
+// reference's IndexError (reported as PACK_EINDEX).
+__device__ __forceinline__ bool truncate_seq(MTLane& rng, int32_t& lo, int32_t& hi, int32_t max_n) {
+  while (hi - lo > max_n) {
+    if (hi - lo == 0) return false;
+    if (rng.random() < 0.5) ++lo; else --hi;
+  }
+  return true;
+}
+
+__global__ __launch_bounds__(64) void pack_codebert_kernel(PackParams P) {
+  const int64_t p = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  if (p >= P.n_part) return;
+  const PartView v = filter_partition(P, p, true);
+  MTLane rng = lane_rng(P, p);
+  rng.seed(P.seed + (uint64_t)p);
+  const int32_t max_doc = P.max_seq >= 512 ? 64 : 32;
+  PairRec* out = P.pairs + v.pb;
+  int64_t np = 0;
+  int32_t err = PACK_OK;
+  for (int32_t dup = 0; dup < P.dup && !err; ++dup) {
+    for (int64_t di = 0; di < v.nd && !err; ++di) {
+      const int64_t first = P.fd_first[v.d0 + di];
+      const int32_t nd = P.fd_nd[v.d0 + di];
+      const int32_t nc = P.fd_n[v.d0 + di] - nd;
+      const int64_t cfirst = first + nd;
+      const int32_t special = nd ? 3 : 2;
+      const int32_t max_num = P.max_seq - special;
+      const double sp = rng.random();
+      // docstring part (pretrain_codebert.py:375-396)
+      int64_t dfs = first;
+      int32_t dn = 0, dlo = 0, dhi = 0;
+      if (nd && sp < P.short_seq_prob) {
+        dn = 1;
+        dhi = P.fs_ntok[first];
+      } else {
+        int32_t cur = 0, cn = 0;
+        for (int32_t i = 0; i < nd; ++i) {
+          ++cn;
+          cur += P.fs_ntok[first + i];
+          if (i == nc - 1 || cur > max_doc) {  // quirk: code-segment count
+            const int32_t end = (cur > max_doc && cn > 1) ? cn - 1 : cn;
+            dn = end;
+            for (int32_t j = 0; j < end; ++j) dhi += P.fs_ntok[first + j];
+            if (!truncate_seq(rng, dlo, dhi, max_doc)) err = PACK_EINDEX;
+            break;
+          }
+        }
+      }
+      if (err) break;
+      const int32_t doc_len = dhi - dlo;
+      // code part (:400-440); the chunk is contiguous: [cs, cs + cn)
+      int32_t cs = 0, cn = 0, cur = doc_len;
+      int64_t nout = 0;
+      for (int32_t i = 0; i < nc; ++i) {
+        if (cn == 0) cs = i;
+        ++cn;
+        cur += P.fs_ntok[cfirst + i];
+        if (i == nc - 1 || cur > max_num) {
+          const bool stay = cur > max_num && cn > 1;
+          int32_t clo = 0, chi = 0;
+          for (int32_t j = 0; j < cn; ++j) chi += P.fs_ntok[cfirst + cs + j];
+          if (!truncate_seq(rng, clo, chi, max_num - doc_len)) { err = PACK_EINDEX; break; }
+          if (chi - clo < 1) { err = PACK_EASSERT; break; }
+          if (nout == 0 || chi - clo >= 16) {
+            PairRec r;
+            r.fs0 = dfs; r.n0 = (uint16_t)dn; r.lo0 = (uint16_t)dlo; r.hi0 = (uint16_t)dhi;
+            r.fs1 = cfirst + cs; r.n1 = (uint16_t)cn; r.lo1 = (uint16_t)clo; r.hi1 = (uint16_t)chi;
+            r.flags = (uint16_t)(special == 3 ? 2 : 0);
+            r.num_tokens = (uint16_t)(doc_len + (chi - clo) + special);
+            out[np++] = r;
+            ++nout;
+          }
+          if (stay) { cs = i; cn = 1; cur = P.fs_ntok[cfirst + i] + doc_len; }
+          else { cn = 0; cur = doc_len; }
+        }
+      }
+    }
+  }
+  P.part_err[p] = err;
+  if (err) { P.part_npairs[p] = 0; P.part_ntok[p] = 0; return; }
+  shuffle_and_bin(P, p, v, np, rng);
+}
+
+// ------------------------------------------------- partition scans ----
+// exclusive scans of two int64 arrays (n entries) into n+1 entries, one block
+__global__ __launch_bounds__(1024) void scan_parts_kernel(const int64_t* a, const int64_t* b, int64_t n,
+                                                          int64_t* sa, int64_t* sb, const int32_t* err,
+                                                          int32_t* err_any) {
+  __shared__ int64_t la[1024], lb[1024];
+  __shared__ int32_t le;
+  const int t = threadIdx.x;
+  const int64_t per = (n + 1023) / 1024;
+  const int64_t lo = min(n, t * per), hi = min(n, lo + per);
+  int64_t x = 0, y = 0;
+  int32_t e = 0;
+  for (int64_t i = lo; i < hi; ++i) { x += a[i]; y += b[i]; e |= err[i]; }
+  la[t] = x; lb[t] = y;
+  if (t == 0) le = 0;
+  __syncthreads();
+  if (e) atomicOr(&le, e);
+  for (int off = 1; off < 1024; off <<= 1) {  // Hillis-Steele inclusive
+    int64_t u = t >= off ? la[t - off] : 0, w = t >= off ? lb[t - off] : 0;
+    __syncthreads();
+    la[t] += u; lb[t] += w;
+    __syncthreads();
+  }
+  int64_t ra = la[t] - x, rb = lb[t] - y;
+  for (int64_t i = lo; i < hi; ++i) { sa[i] = ra; sb[i] = rb; ra += a[i]; rb += b[i]; }
+  if (t == 1023) { sa[n] = la[1023]; sb[n] = lb[1023]; *err_any = le; }
+}
+
+// ----------------------------------------------------- materialise ----
+__device__ __forceinline__ void copy_segment(const MatParams& M, int64_t fs, int32_t n, int32_t lo, int32_t hi,
+                                             uint16_t* out, int lane) {
+  int32_t acc = 0;
+  for (int32_t j = 0; j < n && acc < hi; ++j) {
+    const int32_t len = M.fs_ntok[fs + j];
+    const int64_t base = M.fs_base[fs + j];
+    const int32_t a = max(lo, acc), b = min(hi, acc + len);
+    for (int32_t t = a + lane; t < b; t += 64) out[t - lo] = M.ids[base + (t - acc)];
+    acc += len;
+  }
+}
+
+__global__ __launch_bounds__(256) void materialize_kernel(MatParams M) {
+  const int lane = threadIdx.x & 63;
+  const int64_t total = M.pair_base[M.n_part];
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); g < total; g += nw) {
+    // partition of pair g: last p with pair_base[p] <= g
+    int64_t lo = 0, hi = M.n_part;
+    while (hi - lo > 1) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (M.pair_base[mid] <= g) lo = mid; else hi = mid;
+    }
+    const int64_t p = lo;
+    const int64_t i = g - M.pair_base[p];
+    const int64_t s0 = M.doc_sent_off[M.part_doc_off[p]];
+    const int64_t pb = (int64_t)M.dup * s0;
+    const PairRec r = M.pairs[pb + M.binned[pb + i]];
+    const int64_t off = M.tok_base[p] + M.tok_local[pb + i];
+    uint16_t* out = M.out_tokens + off;
+    const int32_t l0 = r.hi0 - r.lo0, l1 = r.hi1 - r.lo1;
+    const bool seg0 = (r.flags & 2) != 0;  // [SEP] after segment 0
+    if (lane == 0) {
+      out[0] = (uint16_t)M.cls_id;
+      if (seg0) out[1 + l0] = (uint16_t)M.sep_id;
+      out[r.num_tokens - 1] = (uint16_t)M.sep_id;
+      M.out_tok_off[g] = off;
+      M.out_len0[g] = (uint16_t)l0;
+      M.out_len1[g] = (uint16_t)l1;
+      M.out_flags[g] = (uint8_t)r.flags;
+      int32_t b = ((int32_t)r.num_tokens - 1) / M.bin_size;
+      M.out_bin[g] = (uint8_t)(b > M.nbins - 1 ? M.nbins - 1 : b);
+      M.out_part[g] = p;
+      if (g == total - 1) M.out_tok_off[total] = off + r.num_tokens;
+    }
+    copy_segment(M, r.fs0, r.n0, r.lo0, r.hi0, out + 1, lane);
+    copy_segment(M, r.fs1, r.n1, r.lo1, r.hi1, out + 1 + l0 + (seg0 ? 1 : 0), lane);
+  }
+}
+
+hipError_t launch_pack_bert(const PackParams& P, hipStream_t s) {
+  const int grid = (int)((P.n_part + 63) / 64);
+  hipLaunchKernelGGL(pack_bert_kernel, dim3(grid), dim3(64), 0, s, P);
+  return hipGetLastError();
+}
+
+hipError_t launch_pack_codebert(const PackParams& P, hipStream_t s) {
+  const int grid = (int)((P.n_part + 63) / 64);
+  hipLaunchKernelGGL(pack_codebert_kernel, dim3(grid), dim3(64), 0, s, P);
+  return hipGetLastError();
+}
+
+hipError_t launch_scan_parts(const int64_t* a, const int64_t* b, int64_t n, int64_t* sa, int64_t* sb,
+                             const int32_t* err, int32_t* err_any, hipStream_t s) {
+  hipLaunchKernelGGL(scan_parts_kernel, dim3(1), dim3(1024), 0, s, a, b, n, sa, sb, err, err_any);
+  return hipGetLastError();
+}
+
+hipError_t launch_materialize(const MatParams& M, hipStream_t s) {
+  hipLaunchKernelGGL(materialize_kernel, dim3(2048), dim3(256), 0, s, M);
+  return hipGetLastError();
+}
+
+}  // namespace lddl

@@ -1,0 +1,210 @@
+"""Host side of the hot path: tokenize -> pack -> bin -> materialise on one GPU.
+
+Mirrors the reference's per-partition callbacks
+(``_get_documents._to_document`` pretrain.py:82-97 and
+``_get_pairs._to_partition_pairs`` :386-402, ``_to_dataframe_binned``
+binning.py:63-93) over a whole set of partitions at once.  All compute runs in
+liblddl_amd.so; this module only moves buffers and calls the C-ABI.
+
+A *shard set* is a sentence-split corpus resident in HBM:
+  data          uint8  [nbytes + 16]   UTF-8 sentences back to back
+  sent_off      int64  [n_sent + 1]
+  doc_sent_off  int64  [n_doc + 1]
+  part_doc_off  int64  [n_part + 1]    partition = consecutive documents
+  doc_nseg_doc  int32  [n_doc]         CodeBERT only: leading docstring segments
+Partition p is packed after random.seed(seed + p) (the reference leaves the
+partition RNG unseeded).
+"""
+import ctypes
+import dataclasses
+
+import numpy as np
+import torch
+
+from . import _lib
+from .tokenizer import Tokenizer, _ptr, _stream
+
+VOCAB_BERT = _lib.VOCAB_BERT
+VOCAB_CODEBERT = _lib.VOCAB_CODEBERT
+
+
+def partition_by_bytes(corpus, n_partitions):
+  """part_doc_off splitting documents into n_partitions of ~equal bytes
+  (the reference sizes Dask partitions by bytes: --block-size/--num-blocks,
+  readers.py:48-57)."""
+  n_doc = corpus.n_doc
+  n_partitions = max(1, min(n_partitions, max(1, n_doc)))
+  doc_bytes = corpus.sent_off[corpus.doc_sent_off[1:]] - corpus.sent_off[corpus.doc_sent_off[:-1]]
+  cum = np.concatenate([[0], np.cumsum(doc_bytes)])
+  cuts = np.searchsorted(cum, np.linspace(0, cum[-1], n_partitions + 1)[1:-1])
+  off = np.concatenate([[0], cuts, [n_doc]]).astype(np.int64)
+  off = np.maximum.accumulate(off)
+  return off
+
+
+@dataclasses.dataclass
+class ShardSet:
+  data: torch.Tensor
+  sent_off: torch.Tensor
+  doc_sent_off: torch.Tensor
+  part_doc_off: torch.Tensor
+  doc_nseg_doc: torch.Tensor = None
+  nbytes: int = 0
+
+  @property
+  def n_sent(self):
+    return self.sent_off.numel() - 1
+
+  @property
+  def n_doc(self):
+    return self.doc_sent_off.numel() - 1
+
+  @property
+  def n_part(self):
+    return self.part_doc_off.numel() - 1
+
+
+def upload(corpus, part_doc_off, device):
+  part_doc_off = np.asarray(part_doc_off, dtype=np.int64)
+  if part_doc_off[0] != 0 or part_doc_off[-1] != corpus.n_doc or np.any(np.diff(part_doc_off) < 0):
+    raise ValueError('part_doc_off must be a non-decreasing cover of [0, n_doc]')
+  if np.any(np.diff(corpus.doc_sent_off) < 0) or np.any(np.diff(corpus.sent_off) < 0):
+    raise ValueError('offsets must be non-decreasing')
+  data = torch.empty(corpus.nbytes + 16, dtype=torch.uint8, device=device)
+  data[:corpus.nbytes].copy_(torch.from_numpy(np.ascontiguousarray(corpus.data[:corpus.nbytes])))
+  data[corpus.nbytes:].zero_()
+  nseg = None
+  if corpus.doc_nseg_doc is not None:
+    nseg = torch.from_numpy(np.ascontiguousarray(corpus.doc_nseg_doc, dtype=np.int32)).to(device)
+  return ShardSet(data,
+                  torch.from_numpy(np.ascontiguousarray(corpus.sent_off - corpus.sent_off[0])).to(device),
+                  torch.from_numpy(np.ascontiguousarray(corpus.doc_sent_off)).to(device),
+                  torch.from_numpy(part_doc_off).to(device), nseg, corpus.nbytes)
+
+
+@dataclasses.dataclass
+class PackResult:
+  n_pairs: int
+  n_tokens: int
+  nbins: int
+  tokens: torch.Tensor     # int16 view of uint16 ids, rows back to back
+  tok_off: torch.Tensor    # int64 [n_pairs + 1]
+  len0: torch.Tensor       # int16 view of uint16
+  len1: torch.Tensor
+  flags: torch.Tensor      # uint8
+  bins: torch.Tensor       # uint8
+  part: torch.Tensor       # int64
+  bin_count: torch.Tensor  # int64 [n_part, nbins]
+  ids: torch.Tensor = None
+  ntok: torch.Tensor = None
+  ntok_host: np.ndarray = None
+  part_doc_off: np.ndarray = None
+
+  def rows(self):
+    """host copy: list of (partition, A ids, B ids, flags, bin)"""
+    tok = self.tokens[:self.n_tokens].cpu().numpy().view(np.uint16).astype(np.int64)
+    off = self.tok_off[:self.n_pairs + 1].cpu().numpy()
+    l0 = self.len0[:self.n_pairs].cpu().numpy().view(np.uint16).astype(np.int64)
+    l1 = self.len1[:self.n_pairs].cpu().numpy().view(np.uint16).astype(np.int64)
+    fl = self.flags[:self.n_pairs].cpu().numpy()
+    bn = self.bins[:self.n_pairs].cpu().numpy()
+    pt = self.part[:self.n_pairs].cpu().numpy()
+    out = []
+    for g in range(self.n_pairs):
+      r = tok[off[g]:off[g + 1]]
+      sep0 = bool(fl[g] & 2)
+      a = r[1:1 + l0[g]]
+      b = r[1 + l0[g] + (1 if sep0 else 0):1 + l0[g] + (1 if sep0 else 0) + l1[g]]
+      out.append((int(pt[g]), a.tolist(), b.tolist(), int(fl[g]), int(bn[g]), r.tolist()))
+    return out
+
+
+class Packer:
+  """One GPU's tokenize -> pack -> bin -> materialise pipeline (one lddl_ctx)."""
+
+  def __init__(self, vocab_file=VOCAB_BERT, device=None):
+    self.tok = Tokenizer(vocab_file, device)
+    self.device = self.tok.device
+    self._out = {}
+
+  def _buf(self, name, n, dtype):
+    t = self._out.get(name)
+    if t is None or t.numel() < n or t.dtype != dtype:
+      t = torch.empty(max(n, 1), dtype=dtype, device=self.device)
+      self._out[name] = t
+    return t
+
+  def tokenize(self, shards, max_tok=512, stream=None):
+    ids = self._buf('ids', shards.nbytes, torch.int16)
+    ntok = self._buf('ntok', shards.n_sent, torch.int32)
+    return self.tok.tokenize_device(shards.data, shards.sent_off, max_tok, ids, ntok, stream)
+
+  def pack(self, shards, ids, ntok, target_seq_length=128, short_seq_prob=0.1, duplicate_factor=5,
+           seed=12345, bin_size=None, codebert=False, masking=False, masked_lm_ratio=0.15, stream=None):
+    L = _lib.lib()
+    tot = (ctypes.c_int64 * 4)()
+    s = _stream(stream)
+    if codebert:
+      if shards.doc_nseg_doc is None:
+        raise ValueError('CodeBERT packing needs doc_nseg_doc')
+      rc = L.lddl_pack_codebert(self.tok.handle, _ptr(ntok), _ptr(shards.sent_off), shards.n_sent,
+                                _ptr(shards.doc_sent_off), _ptr(shards.doc_nseg_doc), shards.n_doc,
+                                _ptr(shards.part_doc_off), shards.n_part, target_seq_length, short_seq_prob,
+                                duplicate_factor, abs(int(seed)), bin_size or 0, tot, s)
+    else:
+      rc = L.lddl_pack_bert(self.tok.handle, _ptr(ntok), _ptr(shards.sent_off), shards.n_sent,
+                            _ptr(shards.doc_sent_off), shards.n_doc, _ptr(shards.part_doc_off), shards.n_part,
+                            target_seq_length, short_seq_prob, duplicate_factor, 1 if masking else 0,
+                            masked_lm_ratio, abs(int(seed)), bin_size or 0, tot, s)
+    if rc == -7:
+      raise IndexError(L.lddl_last_error().decode())
+    if rc == -8:
+      raise AssertionError(L.lddl_last_error().decode())
+    _lib.check(rc)
+    n_pairs, n_tokens, nbins = int(tot[0]), int(tot[1]), int(tot[2])
+    res = PackResult(n_pairs, n_tokens, nbins,
+                     self._buf('tokens', n_tokens, torch.int16), self._buf('tok_off', n_pairs + 1, torch.int64),
+                     self._buf('len0', n_pairs, torch.int16), self._buf('len1', n_pairs, torch.int16),
+                     self._buf('flags', n_pairs, torch.uint8), self._buf('bins', n_pairs, torch.uint8),
+                     self._buf('part', n_pairs, torch.int64),
+                     self._buf('bin_count', shards.n_part * nbins, torch.int64))
+    _lib.check(L.lddl_materialize(self.tok.handle, _ptr(ids), _ptr(res.tokens), _ptr(res.tok_off),
+                                  _ptr(res.len0), _ptr(res.len1), _ptr(res.flags), _ptr(res.bins),
+                                  _ptr(res.part), _ptr(res.bin_count), s))
+    res.bin_count = res.bin_count[:shards.n_part * nbins].view(shards.n_part, nbins)
+    res.ids, res.ntok = ids, ntok
+    return res
+
+  def run(self, shards, **kw):
+    ids, ntok = self.tokenize(shards)
+    return self.pack(shards, ids, ntok, **kw)
+
+
+def run_bert(corpus, vocab_file=VOCAB_BERT, target_seq_length=128, bin_size=None, n_partitions=1, seed=12345,
+             device=None, check_host=False, duplicate_factor=5, short_seq_prob=0.1, part_doc_off=None,
+             codebert=False):
+  device = device or torch.device('cuda', 0)
+  if part_doc_off is None:
+    part_doc_off = partition_by_bytes(corpus, n_partitions)
+  pk = Packer(vocab_file, device.index)
+  sh = upload(corpus, part_doc_off, device)
+  res = pk.run(sh, target_seq_length=target_seq_length, short_seq_prob=short_seq_prob,
+               duplicate_factor=duplicate_factor, seed=seed, bin_size=bin_size, codebert=codebert)
+  torch.cuda.synchronize(device)
+  res.part_doc_off = np.asarray(part_doc_off)
+  if check_host:
+    res.ntok_host = res.ntok[:sh.n_sent].cpu().numpy()
+  return res
+
+
+def assert_same_pairs(res, expected):
+  """expected: per partition, rows (A, B, is_random_next, num_tokens) in the
+  reference's output order (oracle.pack_oracle.run_bert_shards)."""
+  rows = res.rows()
+  flat = [(p, r) for p, part in enumerate(expected) for r in part]
+  assert len(rows) == len(flat), (len(rows), len(flat))
+  for g, ((pp, a, b, fl, bn, tok), (p, (ea, eb, ern, en))) in enumerate(zip(rows, flat)):
+    assert pp == p, ('partition', g, pp, p)
+    assert a == list(ea) and b == list(eb), ('tokens', g)
+    assert bool(fl & 1) == bool(ern), ('is_random_next', g)
+    assert len(tok) == en, ('num_tokens', g)

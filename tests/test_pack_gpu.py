@@ -1,0 +1,157 @@
+"""HIP packer (BERT NSP / CodeBERT / binning / materialise) vs golden rows
+from the reference functions and vs the oracle restatement."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import pack_oracle as po
+from oracle.oracle import OracleTokenizer
+from test_pack_oracle import BERT, CODE
+
+pytestmark = pytest.mark.gpu
+
+
+def shards_from_docs(docs, nseg=None, part_doc_off=None, device='cuda'):
+  """pre-tokenised docs (lists of id lists) -> ShardSet + ids/ntok tensors"""
+  from lddl_amd.pipeline import ShardSet
+  sents = [s for d in docs for s in d]
+  ntok = np.array([len(s) for s in sents], dtype=np.int32)
+  off = np.zeros(len(sents) + 1, dtype=np.int64)
+  np.cumsum(ntok, out=off[1:])
+  ids = np.array([t for s in sents for t in s] + [0], dtype=np.uint16)
+  dso = np.zeros(len(docs) + 1, dtype=np.int64)
+  np.cumsum([len(d) for d in docs], out=dso[1:])
+  pdo = np.array(part_doc_off if part_doc_off is not None else [0, len(docs)], dtype=np.int64)
+  sh = ShardSet(torch.zeros(int(off[-1]) + 16, dtype=torch.uint8, device=device),
+                torch.from_numpy(off).to(device), torch.from_numpy(dso).to(device),
+                torch.from_numpy(pdo).to(device),
+                None if nseg is None else torch.tensor(nseg, dtype=torch.int32, device=device), int(off[-1]))
+  return sh, torch.from_numpy(ids.view(np.int16)).to(device), torch.from_numpy(ntok).to(device)
+
+
+@pytest.fixture(scope='module')
+def packer(gpu):
+  from lddl_amd.pipeline import Packer, VOCAB_BERT
+  return Packer(VOCAB_BERT, 0)
+
+
+@pytest.fixture(scope='module')
+def cpacker(gpu):
+  from lddl_amd.pipeline import Packer, VOCAB_CODEBERT
+  return Packer(VOCAB_CODEBERT, 0)
+
+
+@pytest.mark.parametrize('k', [i for i, c in enumerate(BERT['cases']) if not c['cfg']['masking']])
+@pytest.mark.parametrize('binned', [False, True])
+def test_bert_golden(packer, k, binned):
+  case = BERT['cases'][k]
+  c = case['cfg']
+  sh, ids, ntok = shards_from_docs(case['docs'])
+  kw = dict(target_seq_length=c['max_seq'], short_seq_prob=c['ssp'], duplicate_factor=c['dup'],
+            seed=case['seed'], bin_size=case['bin_size'] if binned else None)
+  if case['error']:
+    with pytest.raises(AssertionError):
+      packer.pack(sh, ids, ntok, **kw)
+    return
+  res = packer.pack(sh, ids, ntok, **kw)
+  rows = res.rows()
+  exp = case['rows']
+  if binned:
+    order, counts = po.binned_order([r['num_tokens'] for r in exp], case['bin_size'], case['nbins'])
+    exp = [exp[i] for i in order]
+    assert res.bin_count.cpu().numpy().tolist() == [counts]
+  assert len(rows) == len(exp)
+  for (p, a, b, fl, bn, tok), e in zip(rows, exp):
+    assert (a, b, bool(fl & 1), len(tok)) == (e['A'], e['B'], e['is_random_next'], e['num_tokens'])
+    assert tok[0] == packer.tok.cls_id and tok[1 + len(a)] == packer.tok.sep_id and tok[-1] == packer.tok.sep_id
+    if binned:
+      assert bn == po.bin_of(e['num_tokens'], case['bin_size'], case['nbins'])
+
+
+@pytest.mark.parametrize('k', range(len(CODE['cases'])))
+def test_codebert_golden(cpacker, k):
+  case = CODE['cases'][k]
+  c = case['cfg']
+  sh, ids, ntok = shards_from_docs(case['docs'], case['ndoc'])
+  kw = dict(target_seq_length=c['max_seq'], short_seq_prob=c['ssp'], duplicate_factor=c['dup'],
+            seed=case['seed'], codebert=True)
+  if case['error']:
+    with pytest.raises(IndexError):
+      cpacker.pack(sh, ids, ntok, **kw)
+    return
+  res = cpacker.pack(sh, ids, ntok, **kw)
+  rows = res.rows()
+  assert len(rows) == len(case['rows'])
+  for (p, a, b, fl, bn, tok), e in zip(rows, case['rows']):
+    assert (a, b, len(tok)) == (e['doc'], e['code'], e['num_tokens'])
+
+
+@pytest.mark.parametrize('seq,bin_size,nparts', [(128, 32, 7), (512, 64, 3), (128, None, 1)])
+def test_bert_end_to_end_vs_oracle(gpu, seq, bin_size, nparts):
+  from lddl_amd import synth, pipeline
+  c = synth.make_wiki(600_000, seed=seq + nparts)
+  res = pipeline.run_bert(c, target_seq_length=seq, bin_size=bin_size, n_partitions=nparts, seed=999,
+                          check_host=True)
+  oids, ontok = OracleTokenizer(pipeline.VOCAB_BERT).run(c.data, c.sent_off, 512, nthreads=8)
+  assert np.array_equal(res.ntok_host, ontok)
+  exp = po.run_bert_shards(c, oids, ontok, res.part_doc_off, seq, 0.1, 5, 999, bin_size)
+  pipeline.assert_same_pairs(res, exp)
+  # bin counts agree with the rows
+  nb = res.nbins
+  bc = res.bin_count.cpu().numpy()
+  for p, part in enumerate(exp):
+    cnt = np.bincount([po.bin_of(r[3], bin_size or (1 << 30), nb) for r in part], minlength=nb)
+    assert np.array_equal(bc[p], cnt)
+
+
+def test_codebert_end_to_end_vs_oracle(gpu):
+  from lddl_amd import synth, pipeline
+  c = synth.make_code(400, seed=31)
+  pdo = pipeline.partition_by_bytes(c, 3)
+  res = pipeline.run_bert(c, vocab_file=pipeline.VOCAB_CODEBERT, target_seq_length=512, bin_size=64,
+                          part_doc_off=pdo, seed=42, duplicate_factor=1, codebert=True, check_host=True)
+  oids, ontok = OracleTokenizer(pipeline.VOCAB_CODEBERT).run(c.data, c.sent_off, 512, nthreads=8)
+  assert np.array_equal(res.ntok_host, ontok)
+  rows = res.rows()
+  g = 0
+  for p in range(len(pdo) - 1):
+    docs, nd = [], []
+    for d in range(pdo[p], pdo[p + 1]):
+      ss = [list(map(int, oids[c.sent_off[s]:c.sent_off[s] + ontok[s]]))
+            for s in range(c.doc_sent_off[d], c.doc_sent_off[d + 1])]
+      k = int(c.doc_nseg_doc[d])
+      ds = [s for s in ss[:k] if s]
+      cs = [s for s in ss[k:] if s]
+      if cs:
+        docs.append(ds + cs)
+        nd.append(len(ds))
+    pairs = po.partition_pairs(docs, 42 + p, lambda D, di, r: po.codebert_pairs(D, nd, di, 512, 0.1, r), 1)
+    exp = []
+    for (doc_s, code_s, dw, cw) in pairs:
+      dt = [t for (d, s) in doc_s for t in docs[d][s]][dw[0]:dw[1]]
+      ct = [t for (d, s) in code_s for t in docs[d][s]][cw[0]:cw[1]]
+      exp.append((dt, ct, len(dt) + len(ct) + (3 if nd[code_s[0][0]] else 2)))
+    order, _ = po.binned_order([e[2] for e in exp], 64, 8)
+    for i in order:
+      pp, a, b, fl, bn, tok = rows[g]
+      assert (pp, a, b, len(tok)) == (p, exp[i][0], exp[i][1], exp[i][2])
+      g += 1
+  assert g == len(rows)
+
+
+def test_many_partitions_and_empty_partitions(packer):
+  # partitions with zero docs and docs with empty sentences
+  docs = [[[5, 6, 7], [], [8, 9]], [[]], [[10] * 40, [11] * 30, [12] * 50], [[13] * 3]] * 20
+  pdo = [0, 0, 5, 5, 17, 40, 80, 80]
+  sh, ids, ntok = shards_from_docs(docs, part_doc_off=pdo)
+  res = packer.pack(sh, ids, ntok, target_seq_length=64, duplicate_factor=2, seed=7, bin_size=16)
+  rows = res.rows()
+  fdocs = [[s for s in d if s] for d in docs]
+  exp = []
+  for p in range(len(pdo) - 1):
+    D = [d for d in fdocs[pdo[p]:pdo[p + 1]] if d]
+    prs = po.partition_pairs(D, 7 + p, lambda X, di, r: po.bert_pairs(X, di, 64, 0.1, r), 2)
+    rr = [po.pair_tokens(D, pr) for pr in prs]
+    order, _ = po.binned_order([len(a) + len(b) + 3 for a, b, _ in rr], 16, 4)
+    exp += [(p,) + rr[i] for i in order]
+  assert [(r[0], r[1], r[2], bool(r[3] & 1)) for r in rows] == [(p, a, b, rn) for p, a, b, rn in exp]

@@ -12,8 +12,9 @@ o = torch.from_numpy(c.sent_off).cuda()
 ids, ntok = tok.tokenize_device(d, o)
 torch.cuda.synchronize()
 ntoks = int(ntok.sum())
-for it in range(3):
+print('n_sent', c.n_sent, 'max sent bytes', int(np.diff(c.sent_off).max()))
+for max_tok in [512, 512, 1, 4]:
   s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-  s.record(); tok.tokenize_device(d, o, out_ids=ids, out_ntok=ntok); e.record(); torch.cuda.synchronize()
+  s.record(); tok.tokenize_device(d, o, max_tok=max_tok, out_ids=ids, out_ntok=ntok); e.record(); torch.cuda.synchronize()
   ms = s.elapsed_time(e)
-  print('bytes %d tokens %d  %.3f ms  %.2f GB/s  %.3f Gtok/s  B/tok %.2f' % (c.nbytes, ntoks, ms, c.nbytes / ms / 1e6, ntoks / ms / 1e6, c.nbytes / ntoks), flush=True)
+  print('max_tok %d: bytes %d tokens %d  %.3f ms  %.2f GB/s  %.3f Gtok/s  B/tok %.2f' % (max_tok, c.nbytes, ntoks, ms, c.nbytes / ms / 1e6, ntoks / ms / 1e6, c.nbytes / ntoks), flush=True)
