@@ -1,0 +1,221 @@
+#!/usr/bin/env python3
+"""Benchmark of the hot path (tokenize -> NSP pack -> bin -> materialise).
+
+Workload (BASELINE.json configs[1]): BERT, --target-seq-length 512,
+--bin-size 64, --duplicate-factor 5, bert-base-uncased vocab, a 20 GB
+synthetic Wikipedia-style sentence-split corpus resident in HBM per GPU.  One
+step = one pass of the whole hot path over that corpus.  Multi-GPU: one
+process per GPU (torch.distributed.run), every rank packs its own 20 GB of
+partitions (weak scaling, no data-path collective); the per-(partition, bin)
+row counts are all-gathered over RCCL at the end of each step (the exchange
+that replaces load_balance.py:222-233's MPI Allreduce).
+
+Synthetic data: a unique corpus of --unique-mb MB is generated on the host
+and tiled on the device up to --corpus-gb (every tile is its own set of
+partitions with its own seeds).  See DESIGN.md "Measurement".
+
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = 'WordPiece tokens/sec (node) BERT seq128/512 at 1-8 GPUs; % HBM roofline'
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+  ap = argparse.ArgumentParser()
+  ap.add_argument('--gpus', type=int, default=1)
+  ap.add_argument('--steps', type=int, default=3)
+  ap.add_argument('--warmup', type=int, default=1)
+  ap.add_argument('--corpus-gb', type=float, default=20.0)
+  ap.add_argument('--unique-mb', type=int, default=256)
+  ap.add_argument('--target-seq-length', type=int, default=512)
+  ap.add_argument('--bin-size', type=int, default=64)
+  ap.add_argument('--duplicate-factor', type=int, default=5)
+  ap.add_argument('--partition-mb', type=float, default=1.0, help='bytes per partition (--block-size)')
+  ap.add_argument('--seed', type=int, default=12345)
+  ap.add_argument('--no-cpu-baseline', action='store_true')
+  ap.add_argument('--cpu-seconds', type=float, default=12.0)
+  return ap.parse_args()
+
+
+def build_shards(args, rank, device):
+  from lddl_amd import synth
+  from lddl_amd.pipeline import ShardSet, partition_by_bytes
+  t0 = time.time()
+  base = synth.make_wiki(args.unique_mb << 20, seed=20261015 + rank)
+  gen_s = time.time() - t0
+  nb = base.nbytes
+  reps = max(1, int(round(args.corpus_gb * (1 << 30) / nb)))
+  n_part_base = max(1, int(round(nb / (args.partition_mb * (1 << 20)))))
+  pdo = partition_by_bytes(base, n_part_base)
+  ns, nd, npb = base.n_sent, base.n_doc, len(pdo) - 1
+  data = torch.empty(nb * reps + 16, dtype=torch.uint8, device=device)
+  src = torch.from_numpy(base.data[:nb]).to(device)
+  for r in range(reps):
+    data[r * nb:(r + 1) * nb].copy_(src)
+  data[nb * reps:].zero_()
+  del src
+  so = torch.from_numpy(base.sent_off - base.sent_off[0]).to(device)
+  sent_off = torch.empty(ns * reps + 1, dtype=torch.int64, device=device)
+  dso = torch.from_numpy(base.doc_sent_off).to(device)
+  doc_sent_off = torch.empty(nd * reps + 1, dtype=torch.int64, device=device)
+  pd = torch.from_numpy(pdo).to(device)
+  part_doc_off = torch.empty(npb * reps + 1, dtype=torch.int64, device=device)
+  for r in range(reps):
+    sent_off[r * ns:(r + 1) * ns + 1] = so + r * nb
+    doc_sent_off[r * nd:(r + 1) * nd + 1] = dso + r * ns
+    part_doc_off[r * npb:(r + 1) * npb + 1] = pd + r * nd
+  sh = ShardSet(data, sent_off, doc_sent_off, part_doc_off, None, nb * reps)
+  return sh, base, pdo, reps, gen_s
+
+
+def cpu_baseline(args, base, pdo, seconds):
+  """oracle/ restatement timed on the host cores on a bounded sample."""
+  from oracle.oracle import OracleTokenizer
+  from oracle import pack_oracle as po
+  from lddl_amd.pipeline import VOCAB_BERT
+  threads = min(os.cpu_count() or 1, 16)
+  ot = OracleTokenizer(VOCAB_BERT)
+  # calibrate on ~1 MB, then size the sample to ~seconds of work
+  ns = int(np.searchsorted(base.sent_off, base.sent_off[0] + (1 << 20)))
+  t = time.time()
+  ot.run(base.data, base.sent_off[:ns + 1], 512, nthreads=threads)
+  rate = (base.sent_off[ns] - base.sent_off[0]) / max(1e-6, time.time() - t)
+  want = min(base.nbytes, int(rate * seconds * 0.7))
+  ns = int(np.searchsorted(base.sent_off, base.sent_off[0] + want))
+  ns = max(1, min(ns, base.n_sent))
+  t = time.time()
+  ids, ntok = ot.run(base.data, base.sent_off[:ns + 1], 512, nthreads=threads)
+  tok_s = time.time() - t
+  tok_rate = float(ntok.sum()) / tok_s
+  # pack+bin (pure-Python restatement, 1 thread) on the first partitions
+  t = time.time()
+  ptoks, p = 0, 0
+  while time.time() - t < seconds * 0.3 and p < len(pdo) - 1 and base.doc_sent_off[pdo[p + 1]] <= ns:
+    docs = po.filtered_docs(ids, ntok, base.sent_off, base.doc_sent_off, int(pdo[p]), int(pdo[p + 1]))
+    pairs = po.partition_pairs(docs, args.seed + p, lambda D, di, r: po.bert_pairs(
+        D, di, args.target_seq_length, 0.1, r), args.duplicate_factor)
+    rows = [po.pair_tokens(docs, pr) for pr in pairs]
+    po.binned_order([len(a) + len(b) + 3 for a, b, _ in rows], args.bin_size,
+                    args.target_seq_length // args.bin_size)
+    ptoks += int(sum(ntok[base.doc_sent_off[pdo[p]]:base.doc_sent_off[pdo[p + 1]]]))
+    p += 1
+  pack_s = time.time() - t
+  pack_rate = ptoks / pack_s if p else None
+  # end-to-end CPU rate: tokenize at `threads`, pack at 1 thread x `threads` processes
+  e2e = None
+  if pack_rate:
+    e2e = 1.0 / (1.0 / tok_rate + 1.0 / (pack_rate * threads))
+  return {'value': e2e if e2e else tok_rate, 'unit': 'tokens/s', 'cores': threads, 'kind': 'port',
+          'sample': ('oracle/tokenizer_oracle.c on %d sentences (%.1f MB, %.1f s, %.3g tok/s at %d threads) + '
+                     'oracle/pack_oracle.py on %d partitions (%.1f s, %.3g input tok/s/thread); value = '
+                     'tokenize and pack at %d cores in series' % (
+                         ns, (base.sent_off[ns] - base.sent_off[0]) / 1e6, tok_s, tok_rate, threads, p, pack_s,
+                         pack_rate or 0, threads)),
+          'tokenize_tokens_per_s': tok_rate, 'pack_tokens_per_s_per_thread': pack_rate}
+
+
+def main():
+  args = parse()
+  rank = int(os.environ.get('RANK', 0))
+  world = int(os.environ.get('WORLD_SIZE', 1))
+  local = int(os.environ.get('LOCAL_RANK', 0))
+  torch.cuda.set_device(local)
+  device = torch.device('cuda', local)
+  dist = None
+  if world > 1:
+    import torch.distributed as dist
+    dist.init_process_group('nccl', device_id=device)
+  from lddl_amd.pipeline import Packer
+  from lddl_amd import build
+  build.build_hip()
+  sh, base, pdo, reps, gen_s = build_shards(args, rank, device)
+  pk = Packer(device=local)
+  kw = dict(target_seq_length=args.target_seq_length, short_seq_prob=0.1, duplicate_factor=args.duplicate_factor,
+            seed=args.seed + rank * 10_000_000, bin_size=args.bin_size)
+  tok_ms = []
+
+  def step(timed):
+    s = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    ids, ntok = pk.tokenize(sh)
+    e1.record(s)
+    res = pk.pack(sh, ids, ntok, **kw)
+    if dist is not None:
+      bc = res.bin_count.reshape(-1)
+      allc = torch.empty(bc.numel() * world, dtype=bc.dtype, device=device)
+      dist.all_gather_into_tensor(allc, bc)
+    if timed:
+      tok_ms.append((e0, e1))
+    return res, ntok
+
+  for _ in range(args.warmup):
+    res, ntok = step(False)
+  torch.cuda.synchronize()
+  n_tok = int(ntok[:sh.n_sent].sum().item())
+  if dist is not None:
+    dist.barrier()
+  torch.cuda.synchronize()
+  t0 = time.perf_counter()
+  for _ in range(args.steps):
+    res, _ = step(True)
+  torch.cuda.synchronize()
+  if dist is not None:
+    dist.barrier()
+  el = time.perf_counter() - t0
+  tk = float(np.mean([a.elapsed_time(b) for a, b in tok_ms]))
+  if dist is not None:
+    t = torch.tensor([el, float(n_tok)], dtype=torch.float64, device=device)
+    mx = t.clone()
+    dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+    sm = t.clone()
+    dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+    el, tot_tok = float(mx[0]), float(sm[1])
+  else:
+    tot_tok = float(n_tok)
+  if rank != 0:
+    dist.destroy_process_group()
+    return
+  value = tot_tok * args.steps / el
+  # roofline of the dominant kernel (tokenize): algorithmic bytes / launch
+  alg = sh.nbytes + 2 * n_tok + 8 * (sh.n_sent + 1) + 4 * sh.n_sent
+  achieved = alg / (tk * 1e-3) / 1e9
+  line = {
+      'metric': METRIC, 'value': value, 'unit': 'tokens/s', 'n_gpus': world, 'steps': args.steps,
+      'warmup': args.warmup, 'ms_per_step': el * 1e3 / args.steps, 'higher_is_better': True,
+      'scaling': 'weak', 'vs_baseline': None, 'dtype': 'u8',
+      'data': 'synthetic (Wikipedia-style, %d MB unique tiled x%d per GPU)' % (args.unique_mb, reps),
+      'config': {'workload': 'bert_seq%d_bin%d_%dGB_per_gpu' % (args.target_seq_length, args.bin_size,
+                                                                 round(sh.nbytes / (1 << 30))),
+                 'target_seq_length': args.target_seq_length, 'bin_size': args.bin_size,
+                 'duplicate_factor': args.duplicate_factor, 'vocab': 'bert-base-uncased (lddl/dask/bert/vocab)',
+                 'corpus_bytes_per_gpu': sh.nbytes, 'sentences_per_gpu': sh.n_sent,
+                 'partitions_per_gpu': sh.n_part, 'wordpiece_tokens_per_gpu': n_tok,
+                 'pairs_per_gpu': res.n_pairs, 'packed_tokens_per_gpu': res.n_tokens,
+                 'parallelism': 'shard%d' % world},
+      'roofline': {'bound': 'hbm', 'kernel': 'lddl::tokenize_kernel', 'achieved': achieved, 'peak': HBM_PEAK_GBS,
+                   'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS, 'traffic': None,
+                   'algorithmic_bytes_per_launch': alg, 'avg_launch_ms': tk},
+      'tokenize_ms': tk, 'gen_s': gen_s,
+  }
+  if not args.no_cpu_baseline:
+    line['cpu_baseline'] = cpu_baseline(args, base, pdo, args.cpu_seconds)
+  print(json.dumps(line), flush=True)
+  if dist is not None:
+    dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+  main()

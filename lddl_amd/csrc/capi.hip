@@ -259,7 +259,7 @@ extern "C" int lddl_tokenize(lddl_ctx* c, const uint8_t* d_bytes, const int64_t*
   P.sent_off = d_sent_off;
   P.n_sent = n_sent;
   P.max_tok = max_tok;
-  P.chunk = 256;
+  P.chunk = 64;
   P.out_ids = d_out_ids;
   P.out_ntok = d_out_ntok;
   P.top = c->d_top;

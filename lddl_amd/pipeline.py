@@ -137,7 +137,7 @@ class Packer:
   def tokenize(self, shards, max_tok=512, stream=None):
     ids = self._buf('ids', shards.nbytes, torch.int16)
     ntok = self._buf('ntok', shards.n_sent, torch.int32)
-    return self.tok.tokenize_device(shards.data, shards.sent_off, max_tok, ids, ntok, stream)
+    return self.tok.tokenize_device(shards.data, shards.sent_off, max_tok, ids, ntok, stream, nbytes=shards.nbytes)
 
   def pack(self, shards, ids, ntok, target_seq_length=128, short_seq_prob=0.1, duplicate_factor=5,
            seed=12345, bin_size=None, codebert=False, masking=False, masked_lm_ratio=0.15, stream=None):

@@ -62,12 +62,15 @@ class Tokenizer:
     return self._h
 
   # ---- batched hot path -------------------------------------------------
-  def tokenize_device(self, data, sent_off, max_tok=512, out_ids=None, out_ntok=None, stream=None):
+  def tokenize_device(self, data, sent_off, max_tok=512, out_ids=None, out_ntok=None, stream=None,
+                      nbytes=None):
     """data: uint8 cuda tensor; sent_off: int64 cuda tensor [n_sent+1].
     Returns (ids int16 view of uint16 [nbytes], ntok int32 [n_sent]); sentence
-    s's ids start at sent_off[s] - sent_off[0]."""
+    s's ids start at sent_off[s] - sent_off[0].  nbytes = sent_off[-1] -
+    sent_off[0] (default: data.numel(), i.e. data holds no padding)."""
     n_sent = sent_off.numel() - 1
-    nbytes = int(data.numel())
+    if nbytes is None:
+      nbytes = int(data.numel())
     if out_ids is None:
       out_ids = torch.empty(max(nbytes, 1), dtype=torch.int16, device=self.device)
     if out_ntok is None:
