@@ -8,6 +8,7 @@
 #include <stdarg.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <string>
@@ -63,6 +64,7 @@ struct lddl_ctx {
   int pack_codebert = 0;
   // scratch
   int tok_grid = 0;
+  int tok_algo = 2;  // 2 = wave-cooperative windows, 1 = lane per sentence
   uint8_t* d_ovf = nullptr;
   uint32_t* d_counter = nullptr;
 };
@@ -215,11 +217,22 @@ extern "C" int lddl_create(const char* vocab_path, const char* table_path, int d
   if (hipGetDeviceProperties(&prop, device) != hipSuccess) { free_ctx(c); return set_err(LDDL_EHIP, "hipGetDeviceProperties"); }
   c->n_cu = prop.multiProcessorCount;
   if ((rc = load_table(c, table_path)) || (rc = load_vocab(c, vocab_path))) { free_ctx(c); return rc; }
+  const char* algo = getenv("LDDL_TOKENIZE_ALGO");
+  c->tok_algo = (algo && algo[0] == '1') ? 1 : 2;
   int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, tokenize_kernel_ptr(), 256, 0) != hipSuccess || per_cu < 1)
-    per_cu = 4;
-  c->tok_grid = c->n_cu * per_cu;
-  if (hipMalloc((void**)&c->d_ovf, (size_t)c->tok_grid * 256 * WB_OVF) != hipSuccess ||
+  if (c->tok_algo == 1) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, tokenize_kernel_ptr(), 256, 0) != hipSuccess || per_cu < 1)
+      per_cu = 4;
+    c->tok_grid = c->n_cu * per_cu;
+  } else {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, tokenize_wave_kernel_ptr(), 64, 0) != hipSuccess ||
+        per_cu < 1)
+      per_cu = 8;
+    c->tok_grid = c->n_cu * per_cu;
+  }
+  const size_t ovf_bytes = c->tok_algo == 1 ? (size_t)c->tok_grid * 256 * WB_OVF
+                                            : (size_t)c->tok_grid * (WB_OVF + 64);
+  if (hipMalloc((void**)&c->d_ovf, ovf_bytes) != hipSuccess ||
       hipMalloc((void**)&c->d_counter, 64) != hipSuccess) {
     free_ctx(c);
     return set_err(LDDL_ENOMEM, "scratch allocation failed");
@@ -259,7 +272,7 @@ extern "C" int lddl_tokenize(lddl_ctx* c, const uint8_t* d_bytes, const int64_t*
   P.sent_off = d_sent_off;
   P.n_sent = n_sent;
   P.max_tok = max_tok;
-  P.chunk = 64;
+  P.chunk = c->tok_algo == 1 ? 64 : 256;
   P.out_ids = d_out_ids;
   P.out_ntok = d_out_ntok;
   P.top = c->d_top;
@@ -277,10 +290,14 @@ extern "C" int lddl_tokenize(lddl_ctx* c, const uint8_t* d_bytes, const int64_t*
   P.work_counter = c->d_counter;
   HIP_TRY(hipMemsetAsync(c->d_counter, 0, 64, st));
   const int64_t chunks = (n_sent + P.chunk - 1) / P.chunk;
-  const int64_t waves = chunks;
-  int grid = (int)((waves + 3) / 4);
-  if (grid > c->tok_grid) grid = c->tok_grid;
-  HIP_TRY(launch_tokenize(P, grid, st));
+  if (c->tok_algo == 1) {
+    int grid = (int)((chunks + 3) / 4);
+    if (grid > c->tok_grid) grid = c->tok_grid;
+    HIP_TRY(launch_tokenize(P, grid, st));
+  } else {
+    int grid = (int)(chunks < c->tok_grid ? chunks : c->tok_grid);
+    HIP_TRY(launch_tokenize_wave(P, grid, st));
+  }
   return 0;
 }
 

@@ -34,5 +34,7 @@ struct TokParams {
 
 hipError_t launch_tokenize(const TokParams& P, int grid, hipStream_t stream);
 const void* tokenize_kernel_ptr();
+hipError_t launch_tokenize_wave(const TokParams& P, int grid, hipStream_t stream);
+const void* tokenize_wave_kernel_ptr();
 
 }  // namespace lddl

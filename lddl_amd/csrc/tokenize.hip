@@ -14,13 +14,23 @@
 //                          (#tokens <= #bytes for every input, so no scan)
 //   out_ntok  i32[n_sent]  min(#tokens, max_tok)
 //
-// Work mapping: persistent grid; each wave pulls chunks of CHUNK sentences
-// from a global counter; inside a chunk every lane owns one sentence and
-// pulls the next one as soon as it finishes (wave-local ballot/popcount
-// refill), so lognormal sentence lengths do not idle the wave.  A step is one
-// word: scan normalised chars into a per-lane LDS word buffer, then WordPiece
-// with an O(1)-shrinking polynomial hash probed in an L2-resident table and
-// verified byte-exactly against the vocab pool.
+// Two kernels, both exact:
+//  * tokenize_wave_kernel (default): a wave owns a chunk of consecutive
+//    sentences and walks it in raw windows of WIN bytes.  Per window the 64
+//    lanes load the bytes coalesced, decode UTF-8 and look every char up in
+//    the per-code-point table in parallel, write the normalised UTF-8 into LDS
+//    (wave prefix scan), find word / punctuation / special units (ballot
+//    compaction), run WordPiece lane-per-unit against the vocab hash, and
+//    scatter the ids with a second scan.  A word cut by the window end is
+//    deferred to the next window.  Inputs the window path does not model
+//    (canonical reordering of ccc>0 survivors, a word longer than a window,
+//    more than PSTAGE pieces on one lane) fall back to the serial path for
+//    that one sentence, on lane 0 of the same wave.
+//  * tokenize_kernel: one lane per sentence, word by word (the serial path;
+//    kept for A/B).  Lanes of a wave pull sentences dynamically (ballot
+//    refill) so lognormal sentence lengths do not idle the wave.
+// WordPiece in both: O(1)-shrinking polynomial hash probed in an L2-resident
+// table, every hit verified byte-exactly against the vocab pool.
 #include "common.h"
 #include "tokenize.h"
 
@@ -34,7 +44,7 @@ constexpr int BLOCK = 256;
 // lanes touch the same i), the rest in a per-lane global overflow slab.
 __shared__ uint32_t g_wlds[WB_LDS / 4][BLOCK];
 
-struct WordBuf {
+struct LdsWordBuf {
   uint8_t* ovf;  // bytes >= WB_LDS
   __device__ __forceinline__ uint32_t get(int i) const {
     if (i < WB_LDS) return (g_wlds[i >> 2][threadIdx.x] >> ((i & 3) * 8)) & 0xFFu;
@@ -51,6 +61,13 @@ struct WordBuf {
   }
 };
 
+// all bytes in a global slab (v2's single-lane fallback)
+struct GlobalWordBuf {
+  uint8_t* ovf;  // WB_LDS + WB_OVF bytes
+  __device__ __forceinline__ uint32_t get(int i) const { return ovf[i]; }
+  __device__ __forceinline__ void put(int i, uint32_t v) const { ovf[i] = (uint8_t)v; }
+};
+
 struct SentState {
   int64_t p, e;     // byte cursor / end
   int64_t obase;    // output index of token 0
@@ -63,8 +80,10 @@ __device__ __forceinline__ void emit(const TokParams& P, SentState& st, uint32_t
 }
 
 __device__ __forceinline__ int utf8_len(uint32_t b) { return b < 0x80 ? 1 : b >= 0xF0 ? 4 : b >= 0xE0 ? 3 : 2; }
+__device__ __forceinline__ int utf8_enc_len(uint32_t c) { return c < 0x80 ? 1 : c < 0x800 ? 2 : c < 0x10000 ? 3 : 4; }
 
-__device__ __forceinline__ int put_utf8(const WordBuf& wb, int at, uint32_t c) {
+template <class WB>
+__device__ __forceinline__ int put_utf8(const WB& wb, int at, uint32_t c) {
   if (at > WB_LDS + WB_OVF - 4) return 0;  // never reached for words <= 100 chars
   if (c < 0x80) { wb.put(at, c); return 1; }
   if (c < 0x800) { wb.put(at, 0xC0 | (c >> 6)); wb.put(at + 1, 0x80 | (c & 0x3F)); return 2; }
@@ -93,8 +112,9 @@ __device__ __forceinline__ int match_special(const uint8_t* s, int64_t p, int64_
   return -1;
 }
 
-// Exact vocab lookup of (cont, word[s, s+len)); h = poly hash of those bytes.
-__device__ int probe(const TokParams& P, const WordBuf& wb, int s, int len, uint32_t cont, uint64_t h) {
+// Exact vocab lookup of (cont, bytes[s, s+len)); h = poly hash of those bytes.
+template <class GET>
+__device__ __forceinline__ int probe(const TokParams& P, const GET& get, int s, int len, uint32_t cont, uint64_t h) {
   const uint64_t key = hash_key(h, (uint32_t)len, cont);
   uint32_t idx = (uint32_t)key & P.slot_mask;
   const uint32_t fp = (uint32_t)(key >> 32);
@@ -107,40 +127,54 @@ __device__ int probe(const TokParams& P, const WordBuf& wb, int s, int len, uint
       const uint8_t* v = P.pool + P.voff[id];
       bool eq = true;
       for (int k = 0; k < len; ++k)
-        if (v[k] != wb.get(s + k)) { eq = false; break; }
+        if (v[k] != get(s + k)) { eq = false; break; }
       if (eq) return (int)id;
     }
     idx = (idx + 1) & P.slot_mask;
   }
 }
 
-// WordPiece over the buffered normalised word (nb bytes, nch chars).
-__device__ void wordpiece(const TokParams& P, SentState& st, const WordBuf& wb, int nb, int nch) {
-  if (nch > 100) { emit(P, st, P.unk); return; }
-  const int32_t mark = st.ntok;
-  int s = 0;
+// Greedy longest-match-first over bytes [0, nb) of a normalised word.
+// EMIT(n, id) is called per piece; returns #pieces, or -1 when some position
+// has no match (the caller then emits the single [UNK]).
+template <class GET, class EMIT>
+__device__ __forceinline__ int wordpiece_core(const TokParams& P, const GET& get, int nb, const EMIT& emit_fn) {
+  int s = 0, n = 0;
   uint32_t cont = 0;
   while (s < nb) {
     int e = min(nb, s + (int)P.maxb[cont]);
-    while (e < nb && e > s && (wb.get(e) & 0xC0u) == 0x80u) --e;
+    while (e < nb && e > s && (get(e) & 0xC0u) == 0x80u) --e;
     uint64_t h = 0;
-    for (int k = s; k < e; ++k) h = hash_push(h, wb.get(k));
+    for (int k = s; k < e; ++k) h = hash_push(h, get(k));
     int id = -1;
     while (e > s) {
-      id = probe(P, wb, s, e - s, cont, h);
+      id = probe(P, get, s, e - s, cont, h);
       if (id >= 0) break;
-      do { --e; h = hash_pop(h, wb.get(e)); } while (e > s && (wb.get(e) & 0xC0u) == 0x80u);
+      do { --e; h = hash_pop(h, get(e)); } while (e > s && (get(e) & 0xC0u) == 0x80u);
     }
-    if (id < 0) { st.ntok = mark; emit(P, st, P.unk); return; }
-    emit(P, st, (uint32_t)id);
+    if (id < 0) return -1;
+    emit_fn(n, (uint32_t)id);
+    ++n;
     s = e;
     cont = 1;
   }
+  return n;
+}
+
+// WordPiece over the buffered normalised word (nb bytes, nch chars).
+template <class WB>
+__device__ void wordpiece(const TokParams& P, SentState& st, const WB& wb, int nb, int nch) {
+  if (nch > 100) { emit(P, st, P.unk); return; }
+  const int32_t mark = st.ntok;
+  auto get = [&](int i) { return wb.get(i); };
+  auto em = [&](int, uint32_t id) { emit(P, st, id); };
+  if (wordpiece_core(P, get, nb, em) < 0) { st.ntok = mark; emit(P, st, P.unk); }
 }
 
 // Append one normalised char; keeps each run of ccc>0 chars stably sorted by
 // rank (NFD canonical ordering).  Rare path only for chars with rank > 0.
-__device__ __forceinline__ void append_char(const TokParams& P, const WordBuf& wb, int& nb, int& nch,
+template <class WB>
+__device__ __forceinline__ void append_char(const TokParams& P, const WB& wb, int& nb, int& nch,
                                             uint32_t c, uint32_t rank, uint32_t& prev_rank, int& run_start) {
   ++nch;
   if (nch > 100) return;  // word becomes [UNK]; stop buffering
@@ -157,14 +191,15 @@ __device__ __forceinline__ void append_char(const TokParams& P, const WordBuf& w
     if (ent_rank(table_entry(P, cp)) > rank) break;
     pos += l;
   }
-  const int l = c < 0x80 ? 1 : c < 0x800 ? 2 : c < 0x10000 ? 3 : 4;
+  const int l = utf8_enc_len(c);
   for (int k = nb - 1; k >= pos; --k) wb.put(k + l, wb.get(k));
   put_utf8(wb, pos, c);
   nb += l;
 }
 
 // One step: the next word (or special token / isolated char) of the sentence.
-__device__ void step(const TokParams& P, SentState& st, const WordBuf& wb, const uint32_t* ascii_tab) {
+template <class WB>
+__device__ void step(const TokParams& P, SentState& st, const WB& wb, const uint32_t* ascii_tab) {
   int nb = 0, nch = 0, run_start = 0;
   uint32_t prev_rank = 0;
   const uint8_t* bytes = P.bytes;
@@ -227,7 +262,7 @@ __global__ __launch_bounds__(BLOCK) void tokenize_kernel(TokParams P) {
   if (threadIdx.x < 128) ascii_tab[threadIdx.x] = P.pages[(uint32_t)P.top[0] * 256u + threadIdx.x];
   __syncthreads();
   const int lane = threadIdx.x & 63;
-  const WordBuf wb{P.ovf + ((size_t)blockIdx.x * BLOCK + threadIdx.x) * WB_OVF};
+  const LdsWordBuf wb{P.ovf + ((size_t)blockIdx.x * BLOCK + threadIdx.x) * WB_OVF};
   const int64_t base = P.sent_off[0];
   for (;;) {
     uint32_t chunk = 0;
@@ -262,10 +297,420 @@ __global__ __launch_bounds__(BLOCK) void tokenize_kernel(TokParams P) {
   }
 }
 
+// --------------------------------------------------------------------------
+// v2: wave-cooperative windows (default).  A wave (= one workgroup) owns a
+// chunk of consecutive sentences and walks it in raw windows of WIN bytes.
+// --------------------------------------------------------------------------
+constexpr int WIN = 256;             // raw bytes per window (one dword per lane)
+constexpr int NBCAP = 3 * WIN + 16;  // normalised bytes (<= 3x expansion)
+constexpr int PSTAGE = 24;           // staged pieces per lane per window
+constexpr int64_t I64MAX = 0x7fffffffffffffffLL;
+
+// flags of a normalised byte (every byte of a char carries the char's flags)
+enum : uint32_t { NF_CLS = 3u, NF_START = 4u, NF_SPECIAL = 8u };
+
+struct WaveLds {
+  uint8_t raw[WIN + 16];        // raw bytes [base4, base4 + WIN + 16)
+  uint8_t nb[NBCAP];            // normalised UTF-8 (special: its index 0..4)
+  uint8_t nf[NBCAP];            // flags
+  uint8_t nord[NBCAP];          // sentence ordinal of the char
+  uint16_t nraw[NBCAP];         // raw offset (from base4) of the owning char
+  uint16_t ustart[WIN];         // unit start (normalised offset); a unit
+  uint16_t ucnt[WIN];           //   covers >= 1 raw byte, so <= WIN units
+  uint16_t ustage[WIN];         // unit's first staged piece (lane-local)
+  uint16_t upos[WIN];           // unit's first token index in the window
+  uint16_t stage[64][PSTAGE];   // staged piece ids per lane
+  int64_t sst[64];              // starts of sentences sc+1 .. sc+64
+  int32_t ordcnt[65];           // tokens per sentence ordinal in the window
+  int32_t ordfirst[65];         // window token index of an ordinal's first unit
+};
+
+__device__ __forceinline__ int wave_excl_scan(int v, int lane, int* total) {
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  *total = __shfl(x, 63);
+  return x - v;
+}
+
+__device__ __forceinline__ int64_t wave_min64(int64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const int64_t y = __shfl_xor(v, o);
+    v = y < v ? y : v;
+  }
+  return v;
+}
+
+// number of sentence starts <= pos among sst[0..63] (sorted ascending)
+__device__ __forceinline__ int ordinal_of(const WaveLds& L, int64_t pos) {
+  int lo = 0, hi = 64;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (L.sst[mid] <= pos) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+// literal special token at raw window index i (raw[i] == '['), ending <= lim
+__device__ __forceinline__ int match_special_lds(const WaveLds& L, int i, int lim, int* len) {
+  if (i + 5 > lim) return -1;
+  const uint32_t c1 = L.raw[i + 1], c2 = L.raw[i + 2], c3 = L.raw[i + 3], c4 = L.raw[i + 4];
+  if (c1 == 'P' && c2 == 'A' && c3 == 'D' && c4 == ']') { *len = 5; return 0; }
+  if (c1 == 'U' && c2 == 'N' && c3 == 'K' && c4 == ']') { *len = 5; return 1; }
+  if (c1 == 'C' && c2 == 'L' && c3 == 'S' && c4 == ']') { *len = 5; return 2; }
+  if (c1 == 'S' && c2 == 'E' && c3 == 'P' && c4 == ']') { *len = 5; return 3; }
+  if (c1 == 'M' && c2 == 'A' && c3 == 'S' && c4 == 'K' && i + 6 <= lim && L.raw[i + 5] == ']') { *len = 6; return 4; }
+  return -1;
+}
+
+__device__ __forceinline__ void load_sst(WaveLds& L, const TokParams& P, int64_t sc, int64_t s_hi, int lane) {
+  const int64_t j = sc + 1 + lane;
+  L.sst[lane] = j <= s_hi ? P.sent_off[j] : I64MAX;
+}
+
+__global__ __launch_bounds__(64) void tokenize_wave_kernel(TokParams P) {
+  __shared__ WaveLds L;
+  __shared__ uint32_t ascii_tab[128];
+  const int lane = threadIdx.x;
+  ascii_tab[lane] = P.pages[(uint32_t)P.top[0] * 256u + lane];
+  ascii_tab[lane + 64] = P.pages[(uint32_t)P.top[0] * 256u + lane + 64];
+  __syncthreads();
+  const int64_t base = P.sent_off[0];
+  const int64_t data_end = P.sent_off[P.n_sent];
+  const GlobalWordBuf fb{P.ovf + (size_t)blockIdx.x * (WB_LDS + WB_OVF)};
+  for (;;) {
+    uint32_t chunk = 0;
+    if (lane == 0) chunk = atomicAdd(P.work_counter, 1u);
+    chunk = __shfl(chunk, 0);
+    const int64_t s_lo = (int64_t)chunk * P.chunk;
+    if (s_lo >= P.n_sent) break;
+    const int64_t s_hi = min(s_lo + (int64_t)P.chunk, P.n_sent);
+    const int64_t chunk_end = P.sent_off[s_hi];
+    int64_t sc = s_lo;               // current sentence
+    int64_t cur = P.sent_off[s_lo];  // next unprocessed raw byte
+    int32_t stok = 0;                // tokens of sentence sc emitted so far
+    load_sst(L, P, sc, s_hi, lane);
+    __syncthreads();
+    while (sc < s_hi) {
+      const int64_t base4 = cur & ~(int64_t)3;
+      const int64_t wend = min(base4 + WIN, chunk_end);
+      // ---- raw bytes [base4, base4 + WIN + 16), bounded by the data -------
+      {
+        const int64_t a = base4 + 4 * lane;
+        uint32_t v = 0;
+        if (a + 4 <= data_end) v = *reinterpret_cast<const uint32_t*>(P.bytes + a);
+        else for (int q = 0; q < 4; ++q) if (a + q < data_end) v |= (uint32_t)P.bytes[a + q] << (8 * q);
+        *reinterpret_cast<uint32_t*>(&L.raw[4 * lane]) = v;
+        if (lane < 4) {
+          const int64_t a2 = base4 + WIN + 4 * lane;
+          uint32_t w = 0;
+          for (int q = 0; q < 4; ++q) if (a2 + q < data_end) w |= (uint32_t)P.bytes[a2 + q] << (8 * q);
+          *reinterpret_cast<uint32_t*>(&L.raw[WIN + 4 * lane]) = w;
+        }
+      }
+      __syncthreads();
+      // ---- pass A: char starts, table entries, effective window end -------
+      uint32_t ent[4], cps[4];
+      bool ok[4], spec[4];
+      int64_t cut = wend, hard_pos = I64MAX;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int i = 4 * lane + k;
+        const int64_t pos = base4 + i;
+        const uint32_t b = L.raw[i];
+        ok[k] = false;
+        spec[k] = false;
+        ent[k] = 0;
+        cps[k] = b;
+        if (pos < cur || pos >= wend || (b & 0xC0u) == 0x80u) continue;
+        const int a = utf8_len(b);
+        if (wend < chunk_end && (pos + a > wend || (b == '[' && pos + 6 > wend))) { cut = min(cut, pos); continue; }
+        ok[k] = true;
+        if (b < 0x80) {
+          ent[k] = ascii_tab[b];
+        } else {
+          uint32_t cp = b & (0x3Fu >> (a - 1));
+          for (int q = 1; q < a; ++q) cp = (cp << 6) | (L.raw[i + q] & 0x3Fu);
+          if (cp > 0x10FFFF) cp = 0xFFFD;
+          cps[k] = cp;
+          ent[k] = table_entry(P, cp);
+          bool h = ent_rank(ent[k]) != 0;
+          if (ent_kind(ent[k]) == KIND_MULTI) {
+            const uint4 m = P.multi[ent_payload(ent[k])];
+            h = h || (ent_rank(m.y) | ent_rank(m.z) | ent_rank(m.w)) != 0;
+          }
+          if (h) hard_pos = min(hard_pos, pos);
+        }
+      }
+      int64_t wend_eff = wave_min64(min(cut, L.sst[63]));
+      // a ccc>0 survivor (canonical reordering): stop before its sentence,
+      // or run the serial fallback when it is in the current sentence
+      bool fallback = false;
+      const int64_t hp = wave_min64(hard_pos);
+      if (hp < wend_eff) {
+        const int o = ordinal_of(L, hp);
+        if (o == 0) fallback = true;
+        else wend_eff = min(wend_eff, L.sst[o - 1]);
+      }
+      int64_t cur_new = max(wend_eff, cur);
+      int ntot = 0, nunits = 0;
+      if (!fallback) {
+        // ---- pass B: specials (raw text, inside their sentence) ----------
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int i = 4 * lane + k;
+          const int64_t pos = base4 + i;
+          if (!ok[k] || pos >= wend_eff) { ok[k] = false; continue; }
+          if (cps[k] == '[') {
+            const int o = ordinal_of(L, pos);
+            const int64_t send = min(o < 64 ? L.sst[o] : I64MAX, chunk_end);
+            int sl;
+            const int sk = match_special_lds(L, i, (int)min(send - base4, (int64_t)(WIN + 16)), &sl);
+            if (sk >= 0) { spec[k] = true; ent[k] = ((uint32_t)sk << 8) | (uint32_t)sl; }
+          }
+        }
+        __syncthreads();
+        // bytes covered by a special emit nothing: clear them in raw[] (the
+        // covered chars are ASCII, in this lane or the next)
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (spec[k])
+            for (int q = 1; q < (int)(ent[k] & 0xFF); ++q) L.raw[4 * lane + k + q] = 0;
+        __syncthreads();
+        int nout[4], my = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          nout[k] = 0;
+          if (!ok[k]) continue;
+          if (spec[k]) { nout[k] = 1; my += 1; continue; }
+          if (L.raw[4 * lane + k] == 0 && cps[k] != 0) { ok[k] = false; continue; }  // inside a special
+          const uint32_t kind = ent_kind(ent[k]);
+          if (kind == KIND_DROP_T || kind == KIND_DROP_D) continue;
+          if (kind == KIND_MULTI) {
+            const uint4 m = P.multi[ent_payload(ent[k])];
+            nout[k] = utf8_enc_len(ent_payload(m.y)) + utf8_enc_len(ent_payload(m.z)) +
+                      (m.x > 2 ? utf8_enc_len(ent_payload(m.w)) : 0);
+          } else {
+            nout[k] = utf8_enc_len(kind == KIND_IDENT ? cps[k] : ent_payload(ent[k]));
+          }
+          my += nout[k];
+        }
+        const int obeg = wave_excl_scan(my, lane, &ntot);
+        // ---- write normalised bytes + flags --------------------------------
+        int o = obeg;
+        int ord = -1;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (!ok[k] || nout[k] == 0) continue;
+          const int i = 4 * lane + k;
+          const int64_t pos = base4 + i;
+          if (ord < 0) ord = ordinal_of(L, pos);
+          while (ord < 64 && L.sst[ord] <= pos) ++ord;
+          if (spec[k]) {
+            L.nb[o] = (uint8_t)(ent[k] >> 8);
+            L.nf[o] = NF_SPECIAL | NF_START | CLS_ISOLATE;
+            L.nord[o] = (uint8_t)ord;
+            L.nraw[o] = (uint16_t)i;
+            ++o;
+            continue;
+          }
+          const uint32_t kind = ent_kind(ent[k]);
+          uint32_t ch[3] = {0, 0, 0};
+          int nc = 1;
+          uint32_t cls = ent_cls(ent[k]);
+          if (kind == KIND_MULTI) {
+            const uint4 m = P.multi[ent_payload(ent[k])];
+            ch[0] = ent_payload(m.y); ch[1] = ent_payload(m.z); ch[2] = ent_payload(m.w);
+            nc = (int)m.x;
+            cls = CLS_OTHER;
+          } else {
+            ch[0] = kind == KIND_IDENT ? cps[k] : ent_payload(ent[k]);
+          }
+          for (int q = 0; q < nc; ++q) {
+            const uint32_t c = ch[q];
+            const int l = utf8_enc_len(c);
+            uint32_t u8;
+            if (l == 1) u8 = c;
+            else if (l == 2) u8 = (0xC0 | (c >> 6)) | ((0x80 | (c & 0x3F)) << 8);
+            else if (l == 3) u8 = (0xE0 | (c >> 12)) | ((0x80 | ((c >> 6) & 0x3F)) << 8) | ((0x80 | (c & 0x3F)) << 16);
+            else u8 = (0xF0 | (c >> 18)) | ((0x80 | ((c >> 12) & 0x3F)) << 8) |
+                      ((0x80 | ((c >> 6) & 0x3F)) << 16) | ((0x80 | (c & 0x3F)) << 24);
+            for (int q2 = 0; q2 < l; ++q2) {
+              L.nb[o] = (uint8_t)(u8 >> (8 * q2));
+              L.nf[o] = (uint8_t)(cls | (q2 == 0 ? NF_START : 0u));
+              L.nord[o] = (uint8_t)ord;
+              L.nraw[o] = (uint16_t)i;
+              ++o;
+            }
+          }
+        }
+        __syncthreads();
+        // ---- units: words (runs of OTHER chars inside one sentence),
+        //      isolated chars and specials, compacted in order --------------
+        for (int r0 = 0; r0 < ntot; r0 += 256) {
+          uint32_t sm = 0;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int j = r0 + 4 * lane + k;
+            if (j >= ntot) break;
+            const uint32_t f = L.nf[j];
+            if (!(f & NF_START)) continue;
+            const uint32_t c = f & NF_CLS;
+            bool st = (f & NF_SPECIAL) || c == CLS_ISOLATE;
+            if (c == CLS_OTHER) {
+              st = j == 0 || (L.nf[j - 1] & (NF_CLS | NF_SPECIAL)) != CLS_OTHER || L.nord[j - 1] != L.nord[j];
+            }
+            if (st) sm |= 1u << k;
+          }
+          int tot;
+          int at = nunits + wave_excl_scan(__popc(sm), lane, &tot);
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            if (sm & (1u << k)) L.ustart[at++] = (uint16_t)(r0 + 4 * lane + k);
+          nunits += tot;
+        }
+        __syncthreads();
+        // ---- a word cut by the window end is deferred to the next window --
+        if (nunits > 0 && wend_eff < chunk_end) {
+          const int j = L.ustart[nunits - 1];
+          if ((L.nf[j] & (NF_CLS | NF_SPECIAL)) == CLS_OTHER) {
+            int e = j + 1;
+            while (e < ntot && (L.nf[e] & (NF_CLS | NF_SPECIAL)) == CLS_OTHER && L.nord[e] == L.nord[j]) ++e;
+            if (e == ntot) {
+              const int o2 = L.nord[j];
+              bool complete = wend_eff >= (o2 < 64 ? L.sst[o2] : I64MAX);
+              if (!complete) {
+                const uint32_t b0 = L.raw[wend_eff - base4];  // next raw char
+                if (b0 < 0x80 && b0 != 0) {
+                  const uint32_t c = ent_cls(ascii_tab[b0]);
+                  complete = ent_kind(ascii_tab[b0]) != KIND_DROP_T && (c == CLS_SPACE || c == CLS_ISOLATE);
+                }
+              }
+              if (!complete) {
+                cur_new = base4 + L.nraw[j];
+                --nunits;
+                if (cur_new <= cur) fallback = true;  // a word longer than the window
+              }
+            }
+          }
+        }
+      }
+      if (!fallback) {
+        // ---- WordPiece, lane per unit -------------------------------------
+        L.ordcnt[lane] = 0;
+        if (lane == 0) L.ordcnt[64] = 0;
+        __syncthreads();
+        int used = 0;
+        bool ovfl = false;
+        for (int u = lane; u < nunits; u += 64) {
+          const int j = L.ustart[u];
+          const uint32_t f = L.nf[j];
+          int cnt;
+          L.ustage[u] = (uint16_t)used;
+          if (f & NF_SPECIAL) {
+            if (used < PSTAGE) L.stage[lane][used] = (uint16_t)P.special[L.nb[j]];
+            cnt = 1;
+          } else {
+            int e = j + 1, nch = 1;
+            if ((f & NF_CLS) == CLS_OTHER) {
+              while (e < ntot && (L.nf[e] & (NF_CLS | NF_SPECIAL)) == CLS_OTHER && L.nord[e] == L.nord[j]) {
+                nch += (L.nf[e] & NF_START) ? 1 : 0;
+                ++e;
+              }
+            } else {
+              while (e < ntot && !(L.nf[e] & NF_START)) ++e;
+            }
+            cnt = -1;
+            if (nch <= 100) {
+              auto get = [&](int i) -> uint32_t { return L.nb[j + i]; };
+              auto em = [&](int n, uint32_t id) { if (used + n < PSTAGE) L.stage[lane][used + n] = (uint16_t)id; };
+              cnt = wordpiece_core(P, get, e - j, em);
+            }
+            if (cnt < 0) {
+              if (used < PSTAGE) L.stage[lane][used] = (uint16_t)P.unk;
+              cnt = 1;
+            }
+          }
+          if (used + cnt > PSTAGE) ovfl = true;
+          used += cnt;
+          L.ucnt[u] = (uint16_t)cnt;
+          atomicAdd(&L.ordcnt[L.nord[j]], cnt);
+        }
+        fallback = __ballot(ovfl) != 0;
+        __syncthreads();
+        if (!fallback) {
+          // ---- window token index of every unit (scan over units) ---------
+          int carry = 0;
+          for (int r0 = 0; r0 < nunits; r0 += 64) {
+            const int u = r0 + lane;
+            const int c = u < nunits ? L.ucnt[u] : 0;
+            int tot;
+            const int pre = carry + wave_excl_scan(c, lane, &tot);
+            if (u < nunits) {
+              const int o = L.nord[L.ustart[u]];
+              if (u == 0 || L.nord[L.ustart[u - 1]] != o) L.ordfirst[o] = pre;
+              L.upos[u] = (uint16_t)pre;
+            }
+            carry += tot;
+          }
+          __syncthreads();
+          // ---- scatter ids (sentence s's ids start at sent_off[s]-base) ----
+          for (int u = lane; u < nunits; u += 64) {
+            const int o = L.nord[L.ustart[u]];
+            const int c = L.ucnt[u];
+            const int32_t t0 = (o == 0 ? stok : 0) + (L.upos[u] - L.ordfirst[o]);
+            const int64_t ob = (o == 0 ? P.sent_off[sc] : L.sst[o - 1]) - base;
+            const int st0 = L.ustage[u];
+            for (int q = 0; q < c; ++q)
+              if (t0 + q < P.max_tok) P.out_ids[ob + t0 + q] = L.stage[lane][st0 + q];
+          }
+          // ---- sentences that ended inside the window ----------------------
+          const int on = ordinal_of(L, cur_new);
+          if (lane < on) P.out_ntok[sc + lane] = min((lane == 0 ? stok : 0) + L.ordcnt[lane], P.max_tok);
+          const int32_t stok_new = (on == 0 ? stok : 0) + L.ordcnt[on];
+          __syncthreads();
+          stok = stok_new;
+          cur = cur_new;
+          if (on > 0) {
+            sc += on;
+            load_sst(L, P, sc, s_hi, lane);
+          }
+          __syncthreads();
+          continue;
+        }
+      }
+      // ---- serial fallback: the rest of sentence sc on lane 0 (exact) -----
+      __syncthreads();
+      const int64_t sc_end = L.sst[0];
+      if (lane == 0) {
+        SentState st{cur, sc_end, P.sent_off[sc] - base, stok};
+        while (st.p < st.e && st.ntok < P.max_tok) step(P, st, fb, ascii_tab);
+        P.out_ntok[sc] = min(st.ntok, P.max_tok);
+      }
+      cur = sc_end;
+      stok = 0;
+      sc += 1;
+      __syncthreads();
+      load_sst(L, P, sc, s_hi, lane);
+      __syncthreads();
+    }
+  }
+}
+
 const void* tokenize_kernel_ptr() { return reinterpret_cast<const void*>(&tokenize_kernel); }
+const void* tokenize_wave_kernel_ptr() { return reinterpret_cast<const void*>(&tokenize_wave_kernel); }
 
 hipError_t launch_tokenize(const TokParams& P, int grid, hipStream_t stream) {
   hipLaunchKernelGGL(tokenize_kernel, dim3(grid), dim3(BLOCK), 0, stream, P);
+  return hipGetLastError();
+}
+
+hipError_t launch_tokenize_wave(const TokParams& P, int grid, hipStream_t stream) {
+  hipLaunchKernelGGL(tokenize_wave_kernel, dim3(grid), dim3(64), 0, stream, P);
   return hipGetLastError();
 }
 

@@ -74,3 +74,66 @@ def test_hip_tokenize_edge_sizes(gpu):
   # a shard of 1 sentence and of 0 sentences
   assert tok.encode_batch(['x']) == [[tok.vocab['x']]]
   assert tok.encode_batch([]) == []
+
+
+def adversarial_sentences(rng, n):
+  """Mixtures that stress the window path: empty / 1-byte sentences, specials
+  at every offset, multi-byte chars across window edges, >256-byte words,
+  90-110 char words, ccc>0 survivors, CJK, controls."""
+  import json
+  import os
+  from conftest import GOLDEN
+  fz = [c[0] for c in json.load(open(os.path.join(GOLDEN, 'normalize_fuzz.json')))['cases']]
+  atoms = ['a', 'the', 'Hello', ',', '.', ' ', '  ', '[SEP]', '[MASK]', '[CLS', '[sep]', 'naïve', 'İ', '中文',
+           '한국어', '😀', '\x07', '\t', 'ﬁ', '\U0001D16D\U0001D165', 'm̀́', ' ', '##', 'x' * 300,
+           'ab' * 55, 'q' * 99, 'q' * 101, 'é' * 120, 'unaffable', 'electroencephalographically' * 3]
+  out = []
+  for _ in range(n):
+    r = rng.random()
+    if r < 0.05:
+      out.append('')
+    elif r < 0.1:
+      out.append(str(rng.choice(list('ab[.'))))
+    else:
+      k = int(rng.integers(1, 60))
+      parts = []
+      for _ in range(k):
+        if rng.random() < 0.15:
+          parts.append(fz[int(rng.integers(0, len(fz)))])
+        else:
+          parts.append(atoms[int(rng.integers(0, len(atoms)))])
+        parts.append(' ' if rng.random() < 0.7 else '')
+      out.append(''.join(parts).strip())
+  return out
+
+
+@pytest.mark.parametrize('algo', ['1', '2'])
+@pytest.mark.parametrize('name', ['bert', 'codebert'])
+def test_hip_tokenize_adversarial_vs_oracle(gpu, monkeypatch, algo, name):
+  from lddl_amd.synth import corpus_from_sentences
+  from lddl_amd.tokenizer import Tokenizer
+  monkeypatch.setenv('LDDL_TOKENIZE_ALGO', algo)
+  rng = np.random.default_rng(int(algo) * 7 + len(name))
+  sents = adversarial_sentences(rng, 6000)
+  c = corpus_from_sentences(sents, [0, len(sents)])
+  tok = Tokenizer(VOCABS[name])
+  for max_tok in (512, 3):
+    ids, ntok = run_hip(tok, c.data, c.sent_off, max_tok)
+    oids, ontok = OracleTokenizer(VOCABS[name]).run(c.data, c.sent_off, max_tok, nthreads=8)
+    bad = [i for i in range(len(sents)) if ntok[i] != ontok[i]]
+    assert not bad, [(i, repr(sents[i][:80]), ntok[i], ontok[i]) for i in bad[:5]]
+    for i, (a, b) in enumerate(zip(compact(ids, ntok, c.sent_off), compact(oids, ontok, c.sent_off))):
+      assert np.array_equal(a.astype(np.int64), b.astype(np.int64)), (i, repr(sents[i][:80]))
+
+
+@pytest.mark.parametrize('algo', ['1', '2'])
+def test_hip_tokenize_algos_agree_on_wiki(gpu, monkeypatch, algo):
+  from lddl_amd import synth
+  from lddl_amd.tokenizer import Tokenizer
+  monkeypatch.setenv('LDDL_TOKENIZE_ALGO', algo)
+  c = synth.make_wiki(3_000_000, seed=17)
+  ids, ntok = run_hip(Tokenizer(VOCABS['bert']), c.data, c.sent_off)
+  oids, ontok = OracleTokenizer(VOCABS['bert']).run(c.data, c.sent_off, 512, nthreads=8)
+  assert np.array_equal(ntok, ontok)
+  for a, b in zip(compact(ids, ntok, c.sent_off), compact(oids, ontok, c.sent_off)):
+    assert np.array_equal(a.astype(np.int64), b.astype(np.int64))
