@@ -47,7 +47,7 @@ struct lddl_ctx {
   uint16_t* d_top = nullptr;
   uint32_t* d_pages = nullptr;
   uint4* d_multi = nullptr;
-  uint2* d_slots = nullptr;
+  uint4* d_slots = nullptr;
   uint32_t slot_mask = 0;
   uint8_t* d_pool = nullptr;
   uint32_t* d_voff = nullptr;
@@ -159,7 +159,7 @@ static int load_vocab(lddl_ctx* c, const char* path) {
     if (found < 0) return set_err(LDDL_EFORMAT, "vocab %s lacks %s", path, sp[k]);
     c->special[k] = (uint32_t)found;
   }
-  // pool of (cont, bytes) keys; "##x" -> cont=1 "x"
+  // pool of (cont, bytes) keys; "##x" -> cont=1 "x"; every key 4-aligned
   std::vector<uint8_t> pool;
   std::vector<uint32_t> voff(V), vlen(V), vcont(V);
   for (size_t i = 0; i < V; ++i) {
@@ -172,21 +172,24 @@ static int load_vocab(lddl_ctx* c, const char* path) {
     vlen[i] = n;
     vcont[i] = cont;
     pool.insert(pool.end(), s, s + n);
+    pool.resize((pool.size() + 3) & ~(size_t)3, 0);
     if (n > c->maxb[cont]) c->maxb[cont] = n;
   }
   pool.resize(pool.size() + 16, 0);
   uint32_t cap = 1;
-  while (cap < V * 5 / 2) cap <<= 1;
-  std::vector<uint2> slots(cap, make_uint2(0, 0));
+  while (cap < V * 2) cap <<= 1;
+  std::vector<uint4> slots(cap, make_uint4(0, 0, 0, 0));
   for (size_t i = 0; i < V; ++i) {
     if (vlen[i] == 0) continue;  // "##" alone: unreachable
     uint64_t h = 0;
     for (uint32_t k = 0; k < vlen[i]; ++k) h = hash_push(h, pool[voff[i] + k]);
     uint64_t key = hash_key(h, vlen[i], vcont[i]);
     uint32_t idx = (uint32_t)key & (cap - 1), fp = (uint32_t)(key >> 32);
+    uint32_t pre[2] = {0, 0};
+    memcpy(pre, &pool[voff[i]], vlen[i] < 8 ? vlen[i] : 8);
     for (;;) {
-      uint2& s = slots[idx];
-      if (!(s.y & 0x80000000u)) { s = make_uint2(fp, slot_info((uint32_t)i, vlen[i], vcont[i])); break; }
+      uint4& s = slots[idx];
+      if (!(s.y & 0x80000000u)) { s = make_uint4(fp, slot_info((uint32_t)i, vlen[i], vcont[i]), pre[0], pre[1]); break; }
       uint32_t j = s.y & 0xFFFFu;
       if (vlen[j] == vlen[i] && vcont[j] == vcont[i] && memcmp(&pool[voff[j]], &pool[voff[i]], vlen[i]) == 0) {
         s.y = slot_info((uint32_t)i, vlen[i], vcont[i]);  // duplicate line: last id wins
@@ -197,7 +200,7 @@ static int load_vocab(lddl_ctx* c, const char* path) {
   }
   c->slot_mask = cap - 1;
   int rc;
-  if ((rc = upload(&c->d_slots, slots.data(), slots.size() * sizeof(uint2)))) return rc;
+  if ((rc = upload(&c->d_slots, slots.data(), slots.size() * sizeof(uint4)))) return rc;
   if ((rc = upload(&c->d_pool, pool.data(), pool.size()))) return rc;
   if ((rc = upload(&c->d_voff, voff.data(), voff.size() * 4))) return rc;
   return 0;

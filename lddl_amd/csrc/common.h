@@ -44,6 +44,9 @@ LDDL_HD uint64_t hash_key(uint64_t h, uint32_t len, uint32_t cont) {
   return x;
 }
 
+// vocab hash slot (uint4): x = 32-bit fingerprint, y = info, z/w = the
+// first 8 bytes of the key (zero padded) -- keys of <= 8 bytes verify from
+// the slot alone; longer keys compare the rest against the 4-aligned pool.
 // slot.y layout: id (16) | len (8) << 16 | cont << 24 | valid << 31
 LDDL_HD uint32_t slot_info(uint32_t id, uint32_t len, uint32_t cont) {
   return id | (len << 16) | (cont << 24) | 0x80000000u;

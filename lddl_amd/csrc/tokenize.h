@@ -20,7 +20,7 @@ struct TokParams {
   const uint32_t* pages;
   const uint4* multi;
   // vocab
-  const uint2* slots;
+  const uint4* slots;
   uint32_t slot_mask;
   const uint8_t* pool;
   const uint32_t* voff;

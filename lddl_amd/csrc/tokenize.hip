@@ -113,21 +113,35 @@ __device__ __forceinline__ int match_special(const uint8_t* s, int64_t p, int64_
 }
 
 // Exact vocab lookup of (cont, bytes[s, s+len)); h = poly hash of those bytes.
+// One 16-byte slot load per probe; keys of <= 8 bytes verify against the
+// slot's prefix, longer ones additionally against the 4-aligned pool (all
+// dword loads issued together, no per-byte dependent chain).
 template <class GET>
 __device__ __forceinline__ int probe(const TokParams& P, const GET& get, int s, int len, uint32_t cont, uint64_t h) {
   const uint64_t key = hash_key(h, (uint32_t)len, cont);
   uint32_t idx = (uint32_t)key & P.slot_mask;
   const uint32_t fp = (uint32_t)(key >> 32);
   const uint32_t want = ((uint32_t)len << 16) | (cont << 24) | 0x80000000u;
+  uint32_t c0 = 0, c1 = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const uint32_t b = k < len ? get(s + k) : 0u;
+    if (k < 4) c0 |= b << (8 * k); else c1 |= b << (8 * (k - 4));
+  }
   for (;;) {
-    const uint2 sl = P.slots[idx];
+    const uint4 sl = P.slots[idx];
     if (!(sl.y & 0x80000000u)) return -1;
-    if (sl.x == fp && (sl.y & 0xFFFF0000u) == want) {
+    if (sl.x == fp && (sl.y & 0xFFFF0000u) == want && sl.z == c0 && sl.w == c1) {
       const uint32_t id = sl.y & 0xFFFFu;
-      const uint8_t* v = P.pool + P.voff[id];
+      if (len <= 8) return (int)id;
+      const uint32_t* v = reinterpret_cast<const uint32_t*>(P.pool + P.voff[id]);
       bool eq = true;
-      for (int k = 0; k < len; ++k)
-        if (v[k] != get(s + k)) { eq = false; break; }
+      for (int k = 8; k < len; k += 4) {
+        const uint32_t w = v[k >> 2];
+        uint32_t cw = 0;
+        for (int q = 0; q < 4; ++q) cw |= (k + q < len ? get(s + k + q) : 0u) << (8 * q);
+        eq = eq && (w == cw);
+      }
       if (eq) return (int)id;
     }
     idx = (idx + 1) & P.slot_mask;
