@@ -48,6 +48,7 @@ struct lddl_ctx {
   uint32_t* d_pages = nullptr;
   uint4* d_multi = nullptr;
   uint4* d_slots = nullptr;
+  uint32_t* d_bloom = nullptr;
   uint32_t slot_mask = 0;
   uint8_t* d_pool = nullptr;
   uint32_t* d_voff = nullptr;
@@ -77,6 +78,7 @@ static void free_ctx(lddl_ctx* c) {
   (void)hipFree(c->d_pages);
   (void)hipFree(c->d_multi);
   (void)hipFree(c->d_slots);
+  (void)hipFree(c->d_bloom);
   (void)hipFree(c->d_pool);
   (void)hipFree(c->d_voff);
   (void)hipFree(c->d_ovf);
@@ -148,6 +150,7 @@ static int load_vocab(lddl_ctx* c, const char* path) {
   }
   if (!cur.empty()) c->vocab.push_back(cur);
   fclose(f);
+  int rc0;
   const size_t V = c->vocab.size();
   if (V == 0 || V > 65536) return set_err(LDDL_EFORMAT, "vocab size %zu not in [1, 65536]", V);
   c->vocab_size = (int)V;
@@ -199,6 +202,17 @@ static int load_vocab(lddl_ctx* c, const char* path) {
     }
   }
   c->slot_mask = cap - 1;
+  // blocked Bloom filter over the same keys: word = key bits 40..52, two bit
+  // positions from key bits 0..9.  A clear bit proves absence (exact negative).
+  std::vector<uint32_t> bloom(BLOOM_WORDS, 0);
+  for (size_t i = 0; i < V; ++i) {
+    if (vlen[i] == 0) continue;
+    uint64_t h = 0;
+    for (uint32_t k = 0; k < vlen[i]; ++k) h = hash_push(h, pool[voff[i] + k]);
+    const uint64_t key = hash_key(h, vlen[i], vcont[i]);
+    bloom[(uint32_t)(key >> 40) & (BLOOM_WORDS - 1)] |= (1u << (key & 31)) | (1u << ((key >> 5) & 31));
+  }
+  if ((rc0 = upload(&c->d_bloom, bloom.data(), bloom.size() * 4))) return rc0;
   int rc;
   if ((rc = upload(&c->d_slots, slots.data(), slots.size() * sizeof(uint4)))) return rc;
   if ((rc = upload(&c->d_pool, pool.data(), pool.size()))) return rc;
@@ -228,13 +242,14 @@ extern "C" int lddl_create(const char* vocab_path, const char* table_path, int d
       per_cu = 4;
     c->tok_grid = c->n_cu * per_cu;
   } else {
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, tokenize_wave_kernel_ptr(), 64, 0) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, tokenize_wave_kernel_ptr(), 64 * TOK_WAVES, 0) !=
+            hipSuccess ||
         per_cu < 1)
-      per_cu = 8;
+      per_cu = 2;
     c->tok_grid = c->n_cu * per_cu;
   }
   const size_t ovf_bytes = c->tok_algo == 1 ? (size_t)c->tok_grid * 256 * WB_OVF
-                                            : (size_t)c->tok_grid * (WB_OVF + 64);
+                                            : (size_t)c->tok_grid * TOK_WAVES * (WB_OVF + 64);
   if (hipMalloc((void**)&c->d_ovf, ovf_bytes) != hipSuccess ||
       hipMalloc((void**)&c->d_counter, 64) != hipSuccess) {
     free_ctx(c);
@@ -275,7 +290,7 @@ extern "C" int lddl_tokenize(lddl_ctx* c, const uint8_t* d_bytes, const int64_t*
   P.sent_off = d_sent_off;
   P.n_sent = n_sent;
   P.max_tok = max_tok;
-  P.chunk = c->tok_algo == 1 ? 64 : 256;
+  P.chunk = c->tok_algo == 1 ? 64 : 128;
   P.out_ids = d_out_ids;
   P.out_ntok = d_out_ntok;
   P.top = c->d_top;
@@ -283,6 +298,7 @@ extern "C" int lddl_tokenize(lddl_ctx* c, const uint8_t* d_bytes, const int64_t*
   P.multi = c->d_multi;
   P.slots = c->d_slots;
   P.slot_mask = c->slot_mask;
+  P.bloom = c->d_bloom;
   P.pool = c->d_pool;
   P.voff = c->d_voff;
   P.maxb[0] = c->maxb[0];
@@ -292,14 +308,32 @@ extern "C" int lddl_tokenize(lddl_ctx* c, const uint8_t* d_bytes, const int64_t*
   P.ovf = c->d_ovf;
   P.work_counter = c->d_counter;
   HIP_TRY(hipMemsetAsync(c->d_counter, 0, 64, st));
+  const char* dbgenv = getenv("LDDL_TOK_DEBUG");
+  static uint64_t* d_dbg = nullptr;
+  if (dbgenv && dbgenv[0] == '1') {
+    if (!d_dbg) HIP_TRY(hipMalloc((void**)&d_dbg, 16 * 8));
+    HIP_TRY(hipMemsetAsync(d_dbg, 0, 16 * 8, st));
+    P.dbg = d_dbg;
+  }
   const int64_t chunks = (n_sent + P.chunk - 1) / P.chunk;
   if (c->tok_algo == 1) {
     int grid = (int)((chunks + 3) / 4);
     if (grid > c->tok_grid) grid = c->tok_grid;
     HIP_TRY(launch_tokenize(P, grid, st));
   } else {
-    int grid = (int)(chunks < c->tok_grid ? chunks : c->tok_grid);
+    const int64_t wg_needed = (chunks + TOK_WAVES - 1) / TOK_WAVES;
+    int grid = (int)(wg_needed < c->tok_grid ? wg_needed : c->tok_grid);
     HIP_TRY(launch_tokenize_wave(P, grid, st));
+    if (P.dbg) {
+      uint64_t h[16];
+      HIP_TRY(hipMemcpyAsync(h, P.dbg, sizeof h, hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipStreamSynchronize(st));
+      const char* nm[10] = {"chunk/loop", "rawload", "passA", "passB+write", "units+defer", "wordpiece", "scan+scatter",
+                            "finish", "windows", "units"};
+      fprintf(stderr, "[lddl tok dbg] grid=%d chunks=%lld", grid, (long long)chunks);
+      for (int k = 0; k < 10; ++k) fprintf(stderr, " %s=%llu", nm[k], (unsigned long long)h[k]);
+      fprintf(stderr, " probes=%llu fallbacks=%llu\n", (unsigned long long)h[12], (unsigned long long)h[13]);
+    }
   }
   return 0;
 }

@@ -6,6 +6,8 @@
 namespace lddl {
 
 constexpr int WB_OVF = 384;  // per-lane overflow word buffer (bytes beyond LDS)
+constexpr int TOK_WAVES = 4;        // waves per workgroup of the window kernel
+constexpr int BLOOM_WORDS = 8192;   // 32 KiB blocked Bloom filter (2 bits/key)
 
 struct TokParams {
   const uint8_t* bytes;
@@ -21,6 +23,7 @@ struct TokParams {
   const uint4* multi;
   // vocab
   const uint4* slots;
+  const uint32_t* bloom;  // [BLOOM_WORDS]
   uint32_t slot_mask;
   const uint8_t* pool;
   const uint32_t* voff;
@@ -30,6 +33,7 @@ struct TokParams {
   // scratch
   uint8_t* ovf;
   uint32_t* work_counter;
+  uint64_t* dbg;  // optional phase stamps (LDDL_TOK_DEBUG=1), else null
 };
 
 hipError_t launch_tokenize(const TokParams& P, int grid, hipStream_t stream);

@@ -116,9 +116,15 @@ __device__ __forceinline__ int match_special(const uint8_t* s, int64_t p, int64_
 // One 16-byte slot load per probe; keys of <= 8 bytes verify against the
 // slot's prefix, longer ones additionally against the 4-aligned pool (all
 // dword loads issued together, no per-byte dependent chain).
-template <class GET>
-__device__ __forceinline__ int probe(const TokParams& P, const GET& get, int s, int len, uint32_t cont, uint64_t h) {
+struct NoFilter {
+  __device__ __forceinline__ bool operator()(uint64_t) const { return true; }
+};
+
+template <class GET, class FILT>
+__device__ __forceinline__ int probe(const TokParams& P, const GET& get, int s, int len, uint32_t cont, uint64_t h,
+                                     const FILT& filt) {
   const uint64_t key = hash_key(h, (uint32_t)len, cont);
+  if (!filt(key)) return -1;  // exact negative
   uint32_t idx = (uint32_t)key & P.slot_mask;
   const uint32_t fp = (uint32_t)(key >> 32);
   const uint32_t want = ((uint32_t)len << 16) | (cont << 24) | 0x80000000u;
@@ -151,8 +157,9 @@ __device__ __forceinline__ int probe(const TokParams& P, const GET& get, int s, 
 // Greedy longest-match-first over bytes [0, nb) of a normalised word.
 // EMIT(n, id) is called per piece; returns #pieces, or -1 when some position
 // has no match (the caller then emits the single [UNK]).
-template <class GET, class EMIT>
-__device__ __forceinline__ int wordpiece_core(const TokParams& P, const GET& get, int nb, const EMIT& emit_fn) {
+template <class GET, class EMIT, class FILT = NoFilter>
+__device__ __forceinline__ int wordpiece_core(const TokParams& P, const GET& get, int nb, const EMIT& emit_fn,
+                                              const FILT& filt = FILT()) {
   int s = 0, n = 0;
   uint32_t cont = 0;
   while (s < nb) {
@@ -162,7 +169,7 @@ __device__ __forceinline__ int wordpiece_core(const TokParams& P, const GET& get
     for (int k = s; k < e; ++k) h = hash_push(h, get(k));
     int id = -1;
     while (e > s) {
-      id = probe(P, get, s, e - s, cont, h);
+      id = probe(P, get, s, e - s, cont, h, filt);
       if (id >= 0) break;
       do { --e; h = hash_pop(h, get(e)); } while (e > s && (get(e) & 0xC0u) == 0x80u);
     }
@@ -386,16 +393,40 @@ __device__ __forceinline__ void load_sst(WaveLds& L, const TokParams& P, int64_t
   L.sst[lane] = j <= s_hi ? P.sent_off[j] : I64MAX;
 }
 
-__global__ __launch_bounds__(64) void tokenize_wave_kernel(TokParams P) {
-  __shared__ WaveLds L;
+// LDS ordering between lanes of ONE wave (waves of a workgroup run
+// independent chunks, so no workgroup barrier inside the loop)
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__global__ __launch_bounds__(64 * TOK_WAVES) void tokenize_wave_kernel(TokParams P) {
+  __shared__ WaveLds Ls[TOK_WAVES];
   __shared__ uint32_t ascii_tab[128];
-  const int lane = threadIdx.x;
-  ascii_tab[lane] = P.pages[(uint32_t)P.top[0] * 256u + lane];
-  ascii_tab[lane + 64] = P.pages[(uint32_t)P.top[0] * 256u + lane + 64];
+  __shared__ uint32_t bloom[BLOOM_WORDS];  // exact-negative filter of vocab keys
+  for (int i = threadIdx.x; i < BLOOM_WORDS; i += 64 * TOK_WAVES) bloom[i] = P.bloom[i];
+  if (threadIdx.x < 128) ascii_tab[threadIdx.x] = P.pages[(uint32_t)P.top[0] * 256u + threadIdx.x];
   __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  WaveLds& L = Ls[wave];
+  auto filt = [&](uint64_t key) -> bool {
+    const uint32_t w = bloom[(uint32_t)(key >> 40) & (BLOOM_WORDS - 1)];
+    return ((w >> (key & 31)) & (w >> ((key >> 5) & 31)) & 1u) != 0;
+  };
   const int64_t base = P.sent_off[0];
   const int64_t data_end = P.sent_off[P.n_sent];
-  const GlobalWordBuf fb{P.ovf + (size_t)blockIdx.x * (WB_LDS + WB_OVF)};
+  const GlobalWordBuf fb{P.ovf + ((size_t)blockIdx.x * TOK_WAVES + wave) * (WB_LDS + WB_OVF)};
+  const bool dbg = P.dbg != nullptr;
+  uint64_t acc[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t tprev = dbg ? __builtin_amdgcn_s_memtime() : 0;
+#define STAMP(k)                                        \
+  if (dbg) {                                            \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime();   \
+    acc[k] += t_ - tprev;                               \
+    tprev = t_;                                         \
+  }
   for (;;) {
     uint32_t chunk = 0;
     if (lane == 0) chunk = atomicAdd(P.work_counter, 1u);
@@ -408,10 +439,12 @@ __global__ __launch_bounds__(64) void tokenize_wave_kernel(TokParams P) {
     int64_t cur = P.sent_off[s_lo];  // next unprocessed raw byte
     int32_t stok = 0;                // tokens of sentence sc emitted so far
     load_sst(L, P, sc, s_hi, lane);
-    __syncthreads();
+    wave_sync();
     while (sc < s_hi) {
       const int64_t base4 = cur & ~(int64_t)3;
       const int64_t wend = min(base4 + WIN, chunk_end);
+      STAMP(0);
+      if (dbg) acc[8] += 1;
       // ---- raw bytes [base4, base4 + WIN + 16), bounded by the data -------
       {
         const int64_t a = base4 + 4 * lane;
@@ -426,7 +459,8 @@ __global__ __launch_bounds__(64) void tokenize_wave_kernel(TokParams P) {
           *reinterpret_cast<uint32_t*>(&L.raw[WIN + 4 * lane]) = w;
         }
       }
-      __syncthreads();
+      wave_sync();
+      STAMP(1);
       // ---- pass A: char starts, table entries, effective window end -------
       uint32_t ent[4], cps[4];
       bool ok[4], spec[4];
@@ -473,6 +507,7 @@ __global__ __launch_bounds__(64) void tokenize_wave_kernel(TokParams P) {
       int64_t cur_new = max(wend_eff, cur);
       int ntot = 0, nunits = 0;
       if (!fallback) {
+        STAMP(2);
         // ---- pass B: specials (raw text, inside their sentence) ----------
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -487,14 +522,14 @@ __global__ __launch_bounds__(64) void tokenize_wave_kernel(TokParams P) {
             if (sk >= 0) { spec[k] = true; ent[k] = ((uint32_t)sk << 8) | (uint32_t)sl; }
           }
         }
-        __syncthreads();
+        wave_sync();
         // bytes covered by a special emit nothing: clear them in raw[] (the
         // covered chars are ASCII, in this lane or the next)
 #pragma unroll
         for (int k = 0; k < 4; ++k)
           if (spec[k])
             for (int q = 1; q < (int)(ent[k] & 0xFF); ++q) L.raw[4 * lane + k + q] = 0;
-        __syncthreads();
+        wave_sync();
         int nout[4], my = 0;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -562,7 +597,8 @@ __global__ __launch_bounds__(64) void tokenize_wave_kernel(TokParams P) {
             }
           }
         }
-        __syncthreads();
+        wave_sync();
+        STAMP(3);
         // ---- units: words (runs of OTHER chars inside one sentence),
         //      isolated chars and specials, compacted in order --------------
         for (int r0 = 0; r0 < ntot; r0 += 256) {
@@ -587,7 +623,7 @@ __global__ __launch_bounds__(64) void tokenize_wave_kernel(TokParams P) {
             if (sm & (1u << k)) L.ustart[at++] = (uint16_t)(r0 + 4 * lane + k);
           nunits += tot;
         }
-        __syncthreads();
+        wave_sync();
         // ---- a word cut by the window end is deferred to the next window --
         if (nunits > 0 && wend_eff < chunk_end) {
           const int j = L.ustart[nunits - 1];
@@ -614,10 +650,12 @@ __global__ __launch_bounds__(64) void tokenize_wave_kernel(TokParams P) {
         }
       }
       if (!fallback) {
+        STAMP(4);
+        if (dbg) acc[9] += nunits;
         // ---- WordPiece, lane per unit -------------------------------------
         L.ordcnt[lane] = 0;
         if (lane == 0) L.ordcnt[64] = 0;
-        __syncthreads();
+        wave_sync();
         int used = 0;
         bool ovfl = false;
         for (int u = lane; u < nunits; u += 64) {
@@ -642,7 +680,7 @@ __global__ __launch_bounds__(64) void tokenize_wave_kernel(TokParams P) {
             if (nch <= 100) {
               auto get = [&](int i) -> uint32_t { return L.nb[j + i]; };
               auto em = [&](int n, uint32_t id) { if (used + n < PSTAGE) L.stage[lane][used + n] = (uint16_t)id; };
-              cnt = wordpiece_core(P, get, e - j, em);
+              cnt = wordpiece_core(P, get, e - j, em, filt);
             }
             if (cnt < 0) {
               if (used < PSTAGE) L.stage[lane][used] = (uint16_t)P.unk;
@@ -655,8 +693,9 @@ __global__ __launch_bounds__(64) void tokenize_wave_kernel(TokParams P) {
           atomicAdd(&L.ordcnt[L.nord[j]], cnt);
         }
         fallback = __ballot(ovfl) != 0;
-        __syncthreads();
+        wave_sync();
         if (!fallback) {
+          STAMP(5);
           // ---- window token index of every unit (scan over units) ---------
           int carry = 0;
           for (int r0 = 0; r0 < nunits; r0 += 64) {
@@ -671,7 +710,7 @@ __global__ __launch_bounds__(64) void tokenize_wave_kernel(TokParams P) {
             }
             carry += tot;
           }
-          __syncthreads();
+          wave_sync();
           // ---- scatter ids (sentence s's ids start at sent_off[s]-base) ----
           for (int u = lane; u < nunits; u += 64) {
             const int o = L.nord[L.ustart[u]];
@@ -682,23 +721,26 @@ __global__ __launch_bounds__(64) void tokenize_wave_kernel(TokParams P) {
             for (int q = 0; q < c; ++q)
               if (t0 + q < P.max_tok) P.out_ids[ob + t0 + q] = L.stage[lane][st0 + q];
           }
+          STAMP(6);
           // ---- sentences that ended inside the window ----------------------
           const int on = ordinal_of(L, cur_new);
           if (lane < on) P.out_ntok[sc + lane] = min((lane == 0 ? stok : 0) + L.ordcnt[lane], P.max_tok);
           const int32_t stok_new = (on == 0 ? stok : 0) + L.ordcnt[on];
-          __syncthreads();
+          wave_sync();
           stok = stok_new;
           cur = cur_new;
           if (on > 0) {
             sc += on;
             load_sst(L, P, sc, s_hi, lane);
           }
-          __syncthreads();
+          wave_sync();
+          STAMP(7);
           continue;
         }
       }
+      if (dbg && lane == 0) atomicAdd((unsigned long long*)&P.dbg[13], 1ull);
       // ---- serial fallback: the rest of sentence sc on lane 0 (exact) -----
-      __syncthreads();
+      wave_sync();
       const int64_t sc_end = L.sst[0];
       if (lane == 0) {
         SentState st{cur, sc_end, P.sent_off[sc] - base, stok};
@@ -708,11 +750,14 @@ __global__ __launch_bounds__(64) void tokenize_wave_kernel(TokParams P) {
       cur = sc_end;
       stok = 0;
       sc += 1;
-      __syncthreads();
+      wave_sync();
       load_sst(L, P, sc, s_hi, lane);
-      __syncthreads();
+      wave_sync();
     }
   }
+  if (dbg && lane == 0)
+    for (int k = 0; k < 11; ++k) atomicAdd((unsigned long long*)&P.dbg[k], (unsigned long long)acc[k]);
+#undef STAMP
 }
 
 const void* tokenize_kernel_ptr() { return reinterpret_cast<const void*>(&tokenize_kernel); }
@@ -724,7 +769,7 @@ hipError_t launch_tokenize(const TokParams& P, int grid, hipStream_t stream) {
 }
 
 hipError_t launch_tokenize_wave(const TokParams& P, int grid, hipStream_t stream) {
-  hipLaunchKernelGGL(tokenize_wave_kernel, dim3(grid), dim3(64), 0, stream, P);
+  hipLaunchKernelGGL(tokenize_wave_kernel, dim3(grid), dim3(64 * TOK_WAVES), 0, stream, P);
   return hipGetLastError();
 }
 
