@@ -58,7 +58,7 @@ struct lddl_ctx {
     void* p = nullptr;
     size_t cap = 0;
   };
-  Buf ws[20];
+  Buf ws[24];
   PackParams pp{};
   int64_t last_npairs = -1, last_ntok = -1;
   int64_t* h_tot = nullptr;  // pinned [4]
@@ -308,6 +308,8 @@ extern "C" int lddl_tokenize(lddl_ctx* c, const uint8_t* d_bytes, const int64_t*
   P.ovf = c->d_ovf;
   P.work_counter = c->d_counter;
   HIP_TRY(hipMemsetAsync(c->d_counter, 0, 64, st));
+  const char* abl = getenv("LDDL_TOK_ABLATE");
+  P.dbg_mode = abl ? atoi(abl) : 0;
   const char* dbgenv = getenv("LDDL_TOK_DEBUG");
   static uint64_t* d_dbg = nullptr;
   if (dbgenv && dbgenv[0] == '1') {
@@ -404,7 +406,7 @@ static int pack_common(lddl_ctx* c, int codebert, const int32_t* d_ntok, const i
       (rc = ws_get(c, 10, n_part, &P.part_npairs)) || (rc = ws_get(c, 11, n_part, &P.part_ntok)) ||
       (rc = ws_get(c, 12, (size_t)n_part * nbins, &P.bin_count)) ||
       (rc = ws_get(c, 13, (size_t)n_part * nbins, &P.bin_cursor)) ||
-      (rc = ws_get(c, 14, n_part, &P.part_err)))
+      (rc = ws_get(c, 14, n_part, &P.part_err)) || (rc = ws_get(c, 18, n_sent + n_part + 1, &P.kept)))
     return rc;
   int64_t *pair_base, *tok_base;
   int32_t* err_any;
@@ -412,7 +414,9 @@ static int pack_common(lddl_ctx* c, int codebert, const int32_t* d_ntok, const i
       (rc = ws_get(c, 17, 4, &err_any)))
     return rc;
   if (!c->h_tot) HIP_TRY(hipHostMalloc((void**)&c->h_tot, 4 * sizeof(int64_t)));
-  HIP_TRY(codebert ? launch_pack_codebert(P, st) : launch_pack_bert(P, st));
+  const char* palgo = getenv("LDDL_PACK_ALGO");
+  const bool lane_packer = palgo && palgo[0] == '1';
+  HIP_TRY(codebert ? launch_pack_codebert(P, st) : lane_packer ? launch_pack_bert(P, st) : launch_pack_bert_wave(P, st));
   HIP_TRY(launch_scan_parts(P.part_npairs, P.part_ntok, n_part, pair_base, tok_base, P.part_err, err_any, st));
   HIP_TRY(hipMemcpyAsync(c->h_tot, pair_base + n_part, 8, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipMemcpyAsync(c->h_tot + 1, tok_base + n_part, 8, hipMemcpyDeviceToHost, st));

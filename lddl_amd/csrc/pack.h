@@ -51,6 +51,7 @@ struct PackParams {
   int64_t* bin_count;           // [n_part * nbins]
   int64_t* bin_cursor;          // [n_part * nbins] scratch (nbins > 16)
   int32_t* part_err;            // [n_part]
+  int32_t* kept;                // [n_sent + n_part] wave packer scratch
 };
 
 struct MatParams {
@@ -82,6 +83,7 @@ struct MatParams {
 };
 
 hipError_t launch_pack_bert(const PackParams& P, hipStream_t s);
+hipError_t launch_pack_bert_wave(const PackParams& P, hipStream_t s);
 hipError_t launch_pack_codebert(const PackParams& P, hipStream_t s);
 hipError_t launch_scan_parts(const int64_t* a, const int64_t* b, int64_t n, int64_t* sa, int64_t* sb,
                              const int32_t* err, int32_t* err_any, hipStream_t s);

@@ -1,0 +1,414 @@
+// BERT NSP packing with one WAVE per partition (default packer).
+//
+// Same contract and results as pack_bert_kernel in pack.hip (reference:
+// lddl/dask/bert/pretrain.py:241-365 create_pairs_from_document, :161-176
+// _truncate_seq_pair, :386-402 _to_partition_pairs; binning.py:63-93), but
+// the partition's serial decision chain runs out of LDS and uses the 64 lanes
+// wherever the reference's loops are data-parallel:
+//   * MT19937 state in LDS; the twist (in 64-word chunks, ascending -- the
+//     in-place dependences of the sequential generator hold chunk-wise) and
+//     the tempering run on all lanes; a draw is one LDS read.
+//   * sentence filtering (drop empty sentences / documents) = wave scans.
+//   * "accumulate sentences until len >= target" (chunk flush, random-next
+//     B) = a wave prefix sum over the next 64 sentence lengths + ballot.
+//   * _truncate_seq_pair: the side of every step is a closed form of the two
+//     lengths, and random() < 0.5 <=> the first tempered word's MSB is 0, so
+//     64 steps are decided per wave instruction (ballot + popcount).
+//   * shuffle: Fisher-Yates on a u16 order array in LDS; binning: a stable
+//     ballot partition per bin; token offsets: wave scan.
+// Partitions larger than the LDS capacities (PW_*) run the same code with the
+// arrays in global memory (wave-uniform branch).
+#include "common.h"
+#include "pack.h"
+
+namespace lddl {
+
+constexpr int PW_LENS = 4096;   // filtered sentences resident in LDS
+constexpr int PW_DOCS = 1024;   // filtered documents resident in LDS
+constexpr int PW_PAIRS = 4096;  // pairs resident in LDS (order + num_tokens)
+
+struct PackWaveLds {
+  uint32_t mt[MT_N];
+  uint32_t tw[MT_N];            // tempered outputs of the current state
+  uint16_t lens[PW_LENS];
+  uint16_t dfirst[PW_DOCS];     // relative to the partition's first slot
+  uint16_t dn[PW_DOCS];
+  uint16_t order[PW_PAIRS];
+  uint16_t ntk[PW_PAIRS];       // num_tokens per pair record
+  int32_t red[64];
+};
+
+__device__ __forceinline__ void wsync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ int wscan_incl(int v, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(v, o);
+    if (lane >= o) v += y;
+  }
+  return v;
+}
+
+__device__ __forceinline__ int wsum(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// ---- CPython MT19937 with the state in LDS -----------------------------
+struct WaveRng {
+  PackWaveLds& L;
+  int lane;
+  int idx;  // wave-uniform
+
+  __device__ void seed(uint64_t n) {
+    if (lane == 0) {
+      uint32_t* mt = L.mt;
+      uint32_t key[2] = {(uint32_t)n, (uint32_t)(n >> 32)};
+      const int klen = (n >> 32) ? 2 : 1;
+      mt[0] = 19650218u;
+      for (int i = 1; i < MT_N; ++i) mt[i] = 1812433253u * (mt[i - 1] ^ (mt[i - 1] >> 30)) + (uint32_t)i;
+      int i = 1, j = 0;
+      for (int k = MT_N > klen ? MT_N : klen; k; --k) {
+        mt[i] = (mt[i] ^ ((mt[i - 1] ^ (mt[i - 1] >> 30)) * 1664525u)) + key[j] + (uint32_t)j;
+        ++i; ++j;
+        if (i >= MT_N) { mt[0] = mt[MT_N - 1]; i = 1; }
+        if (j >= klen) j = 0;
+      }
+      for (int k = MT_N - 1; k; --k) {
+        mt[i] = (mt[i] ^ ((mt[i - 1] ^ (mt[i - 1] >> 30)) * 1566083941u)) - (uint32_t)i;
+        ++i;
+        if (i >= MT_N) { mt[0] = mt[MT_N - 1]; i = 1; }
+      }
+      mt[0] = 0x80000000u;
+    }
+    wsync();
+    idx = MT_N;
+  }
+
+  __device__ static __forceinline__ uint32_t temper(uint32_t y) {
+    y ^= y >> 11;
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= y >> 18;
+    return y;
+  }
+
+  // twist + temper on all lanes
+  __device__ void refill() {
+    uint32_t* mt = L.mt;
+    for (int c = 0; c < MT_N; c += 64) {
+      const int i = c + lane;
+      uint32_t v = 0;
+      if (i < MT_N) {
+        const uint32_t a = mt[i], b = mt[i + 1 == MT_N ? 0 : i + 1];
+        const uint32_t m = mt[i + MT_M >= MT_N ? i + MT_M - MT_N : i + MT_M];
+        const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
+        v = m ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+      }
+      wsync();
+      if (i < MT_N) mt[i] = v;
+      wsync();
+    }
+    for (int i = lane; i < MT_N; i += 64) L.tw[i] = temper(mt[i]);
+    wsync();
+    idx = 0;
+  }
+
+  __device__ __forceinline__ uint32_t next() {
+    if (idx >= MT_N) refill();
+    return L.tw[idx++];
+  }
+  __device__ __forceinline__ double random() {
+    const uint32_t a = next() >> 5, b = next() >> 6;
+    return ((double)a * 67108864.0 + (double)b) * (1.0 / 9007199254740992.0);
+  }
+  // random() < 0.5  <=>  MSB of the first word is 0 (second word consumed)
+  __device__ __forceinline__ bool coin_lt_half() {
+    const uint32_t a = next();
+    next();
+    return (a >> 31) == 0;
+  }
+  __device__ __forceinline__ uint32_t randbelow(uint32_t n) {
+    const int k = 32 - __clz(n);
+    uint32_t r = next() >> (32 - k);
+    while (r >= n) r = next() >> (32 - k);
+    return r;
+  }
+  __device__ __forceinline__ int64_t randint(int64_t a, int64_t b) {
+    return a + (int64_t)randbelow((uint32_t)(b - a + 1));
+  }
+};
+
+// smallest k in [k0, n) with (k == n-1) or (sum lens[k0..k] >= target);
+// returns k and the sum.  lens via GET (LDS or global).
+template <class GET>
+__device__ __forceinline__ int find_fill(const GET& len_at, int k0, int n, int target, int lane, int* sum_out) {
+  int base = 0;
+  for (int k = k0; k < n; k += 64) {
+    const int kk = k + lane;
+    const int l = kk < n ? len_at(kk) : 0;
+    const int ps = base + wscan_incl(l, lane);
+    const bool cond = kk < n && (kk == n - 1 || ps >= target);
+    const uint64_t m = __ballot(cond);
+    if (m) {
+      const int j = __ffsll((unsigned long long)m) - 1;
+      *sum_out = __shfl(ps, j);
+      return k + j;
+    }
+    base = __shfl(ps, 63);
+  }
+  *sum_out = base;
+  return n - 1;  // unreachable for n > 0
+}
+
+template <class GET>
+__device__ __forceinline__ int range_sum(const GET& len_at, int k0, int k1, int lane) {
+  int s = 0;
+  for (int k = k0 + lane; k < k1; k += 64) s += len_at(k);
+  return wsum(s);
+}
+
+__global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
+  __shared__ PackWaveLds L;
+  const int lane = threadIdx.x;
+  const int64_t p = blockIdx.x;
+  if (p >= P.n_part) return;
+  const int64_t d0 = P.part_doc_off[p], d1 = P.part_doc_off[p + 1];
+  const int64_t s0 = P.doc_sent_off[d0], s1 = P.doc_sent_off[d1];
+  const int64_t pb = (int64_t)P.dup * s0;
+  const int64_t base = P.sent_off[0];
+  const int nsent = (int)(s1 - s0), ndoc = (int)(d1 - d0);
+
+  // ---- filter: kept sentence slots via a running wave scan ---------------
+  // kept_before[k] = #kept sentences before sentence s0 + k (k <= nsent)
+  int32_t* kept_before = P.kept + s0 + p;
+  {
+    int run = 0;
+    for (int k = 0; k < nsent; k += 64) {
+      const int kk = k + lane;
+      int n = 0;
+      if (kk < nsent) n = P.ntok[s0 + kk];
+      const int keep = (kk < nsent && n > 0) ? 1 : 0;
+      const int incl = wscan_incl(keep, lane);
+      if (kk < nsent) {
+        const int slot = run + incl - keep;
+        kept_before[kk] = slot;
+        if (keep) {
+          P.fs_ntok[s0 + slot] = n;
+          P.fs_base[s0 + slot] = P.sent_off[s0 + kk] - base;
+        }
+      }
+      run += __shfl(incl, 63);
+    }
+    if (lane == 0) kept_before[nsent] = run;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  // documents with >= 1 kept sentence, compacted
+  int nd = 0;
+  for (int k = 0; k < ndoc; k += 64) {
+    const int kk = k + lane;
+    int first = 0, cnt = 0;
+    if (kk < ndoc) {
+      const int a = (int)(P.doc_sent_off[d0 + kk] - s0), b = (int)(P.doc_sent_off[d0 + kk + 1] - s0);
+      first = a < nsent ? kept_before[a] : kept_before[nsent];
+      const int last = b < nsent ? kept_before[b] : kept_before[nsent];
+      cnt = last - first;
+    }
+    const int keep = (kk < ndoc && cnt > 0) ? 1 : 0;
+    const int incl = wscan_incl(keep, lane);
+    if (keep) {
+      const int di = nd + incl - 1;
+      P.fd_first[d0 + di] = s0 + first;
+      P.fd_n[d0 + di] = cnt;
+    }
+    nd += __shfl(incl, 63);
+  }
+  const int nfs = kept_before[nsent];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  const bool lres = nfs <= PW_LENS && nd <= PW_DOCS;
+  if (lres) {
+    for (int k = lane; k < nfs; k += 64) L.lens[k] = (uint16_t)P.fs_ntok[s0 + k];
+    for (int k = lane; k < nd; k += 64) {
+      L.dfirst[k] = (uint16_t)(P.fd_first[d0 + k] - s0);
+      L.dn[k] = (uint16_t)P.fd_n[d0 + k];
+    }
+  }
+  wsync();
+  // slot-relative accessors
+  auto len_at = [&](int k) -> int { return lres ? (int)L.lens[k] : P.fs_ntok[s0 + k]; };
+  auto doc_first = [&](int d) -> int { return lres ? (int)L.dfirst[d] : (int)(P.fd_first[d0 + d] - s0); };
+  auto doc_n = [&](int d) -> int { return lres ? (int)L.dn[d] : P.fd_n[d0 + d]; };
+
+  WaveRng rng{L, lane, MT_N};
+  rng.seed(P.seed + (uint64_t)p);
+  const int max_num = P.max_seq - 3;
+  PairRec* out = P.pairs + pb;
+  int np = 0;
+  int err = PACK_OK;
+  const int pcap = PW_PAIRS;
+  for (int dup = 0; dup < P.dup && !err; ++dup) {
+    for (int di = 0; di < nd && !err; ++di) {
+      const int first = doc_first(di), len = doc_n(di);
+      int target = max_num;
+      if (rng.random() < P.short_seq_prob) target = (int)rng.randint(2, max_num);
+      int i = 0;
+      while (i < len) {
+        const int cs = i;
+        int cur;
+        const int j = find_fill([&](int k) { return len_at(first + k); }, cs, len, target, lane, &cur);
+        const int nchunk = j - cs + 1;
+        int a_end = 1;
+        if (nchunk >= 2) a_end = (int)rng.randint(1, nchunk - 1);
+        const int la = a_end == nchunk ? cur : range_sum([&](int k) { return len_at(first + k); }, cs, cs + a_end, lane);
+        PairRec r;
+        r.fs0 = s0 + first + cs;
+        r.n0 = (uint16_t)a_end;
+        int lb;
+        bool rn;
+        int i_next;
+        if (nchunk == 1 || rng.coin_lt_half()) {
+          rn = true;
+          const int tb = target - la;
+          int rdi = 0;
+          for (int t = 0; t < 10; ++t) {
+            rdi = (int)rng.randint(0, nd - 1);
+            if (rdi != di) break;
+          }
+          if (rdi == di) rn = false;
+          const int rfirst = doc_first(rdi), rlen = doc_n(rdi);
+          const int rstart = (int)rng.randint(0, rlen - 1);
+          const int k = find_fill([&](int q) { return len_at(rfirst + q); }, rstart, rlen, tb, lane, &lb);
+          r.fs1 = s0 + rfirst + rstart;
+          r.n1 = (uint16_t)(k - rstart + 1);
+          i_next = j - (nchunk - a_end) + 1;
+        } else {
+          rn = false;
+          lb = cur - la;
+          r.fs1 = s0 + first + cs + a_end;
+          r.n1 = (uint16_t)(nchunk - a_end);
+          i_next = j + 1;
+        }
+        // _truncate_seq_pair, 64 steps per round
+        int alo = 0, ahi = la, blo = 0, bhi = lb;
+        int E = la + lb - max_num;
+        int t0 = 0;
+        const int d0l = la - lb;
+        const int nb0 = 1 - d0l;  // initial B steps when d0 <= 0
+        while (E > 0) {
+          int avail = (MT_N - rng.idx) >> 1;
+          if (avail == 0) {  // a step straddles the twist: one serial step
+            const int t = t0;
+            bool sideA = d0l > 0 ? (t < d0l ? true : ((t - d0l) & 1) != 0) : (t < nb0 ? false : ((t - nb0) & 1) == 0);
+            const bool front = rng.coin_lt_half();
+            if (sideA) { if (front) ++alo; else --ahi; } else { if (front) ++blo; else --bhi; }
+            ++t0;
+            --E;
+            continue;
+          }
+          const int n = min(min(E, 64), avail);
+          const int t = t0 + lane;
+          bool sideA = d0l > 0 ? (t < d0l ? true : ((t - d0l) & 1) != 0) : (t < nb0 ? false : ((t - nb0) & 1) == 0);
+          const bool front = lane < n ? (L.tw[rng.idx + 2 * lane] >> 31) == 0 : false;
+          const bool act = lane < n;
+          alo += __popcll(__ballot(act && sideA && front));
+          ahi -= __popcll(__ballot(act && sideA && !front));
+          blo += __popcll(__ballot(act && !sideA && front));
+          bhi -= __popcll(__ballot(act && !sideA && !front));
+          rng.idx += 2 * n;
+          t0 += n;
+          E -= n;
+        }
+        if (ahi - alo < 1 || bhi - blo < 1) { err = PACK_EASSERT; break; }
+        r.lo0 = (uint16_t)alo; r.hi0 = (uint16_t)ahi;
+        r.lo1 = (uint16_t)blo; r.hi1 = (uint16_t)bhi;
+        r.flags = (uint16_t)((rn ? 1 : 0) | 2);
+        r.num_tokens = (uint16_t)((ahi - alo) + (bhi - blo) + 3);
+        if (lane == 0) {
+          out[np] = r;
+          if (np < pcap) L.ntk[np] = r.num_tokens;
+        }
+        ++np;
+        i = i_next;
+      }
+    }
+  }
+  if (lane == 0) P.part_err[p] = err;
+  if (err) {
+    if (lane == 0) { P.part_npairs[p] = 0; P.part_ntok[p] = 0; }
+    return;
+  }
+  wsync();
+  // ---- random.shuffle(partition_pairs) -----------------------------------
+  const bool ores = np <= pcap;
+  int32_t* gorder = P.order + pb;
+  if (ores) for (int k = lane; k < np; k += 64) L.order[k] = (uint16_t)k;
+  else for (int k = lane; k < np; k += 64) gorder[k] = k;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  for (int k = np - 1; k >= 1; --k) {
+    const int j = (int)rng.randbelow((uint32_t)(k + 1));
+    if (lane == 0) {
+      if (ores) { const uint16_t t = L.order[k]; L.order[k] = L.order[j]; L.order[j] = t; }
+      else { const int32_t t = gorder[k]; gorder[k] = gorder[j]; gorder[j] = t; }
+    }
+    wsync();
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  auto ord_at = [&](int k) -> int { return ores ? (int)L.order[k] : gorder[k]; };
+  auto ntk_at = [&](int rec) -> int { return ores ? (int)L.ntk[rec] : (int)out[rec].num_tokens; };
+  // ---- stable bin partition + token offsets -------------------------------
+  const int nb = P.nbins;
+  int32_t* binned = P.binned + pb;
+  int64_t* tl = P.tok_local + pb;
+  int pos = 0;
+  int64_t acc = 0;
+  for (int b = 0; b < nb; ++b) {
+    int cnt = 0;
+    for (int k = 0; k < np; k += 64) {
+      const int kk = k + lane;
+      int rec = 0, nt = 0;
+      bool in = false;
+      if (kk < np) {
+        rec = ord_at(kk);
+        nt = ntk_at(rec);
+        int bb = (nt - 1) / P.bin_size;
+        bb = bb > nb - 1 ? nb - 1 : bb;
+        in = bb == b;
+      }
+      const uint64_t m = __ballot(in);
+      const int before = __popcll(m & ((1ull << lane) - 1ull));
+      const int tinc = wscan_incl(in ? nt : 0, lane);
+      if (in) {
+        binned[pos + before] = rec;
+        tl[pos + before] = acc + tinc - nt;
+      }
+      pos += __popcll(m);
+      cnt += __popcll(m);
+      acc += __shfl(tinc, 63);
+    }
+    if (lane == 0) P.bin_count[p * nb + b] = cnt;
+  }
+  if (lane == 0) {
+    P.part_npairs[p] = np;
+    P.part_ntok[p] = acc;
+  }
+}
+
+hipError_t launch_pack_bert_wave(const PackParams& P, hipStream_t s) {
+  hipLaunchKernelGGL(pack_bert_wave_kernel, dim3((unsigned)P.n_part), dim3(64), 0, s, P);
+  return hipGetLastError();
+}
+
+}  // namespace lddl

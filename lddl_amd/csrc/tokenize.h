@@ -34,6 +34,7 @@ struct TokParams {
   uint8_t* ovf;
   uint32_t* work_counter;
   uint64_t* dbg;  // optional phase stamps (LDDL_TOK_DEBUG=1), else null
+  int32_t dbg_mode;  // ablation (LDDL_TOK_ABLATE): 1 = skip WordPiece, 2 = filter-only lookups
 };
 
 hipError_t launch_tokenize(const TokParams& P, int grid, hipStream_t stream);

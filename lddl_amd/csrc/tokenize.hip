@@ -125,6 +125,7 @@ __device__ __forceinline__ int probe(const TokParams& P, const GET& get, int s, 
                                      const FILT& filt) {
   const uint64_t key = hash_key(h, (uint32_t)len, cont);
   if (!filt(key)) return -1;  // exact negative
+  if (P.dbg_mode == 2) return (int)(key & 0x3FFF);  // ablation: no global probe
   uint32_t idx = (uint32_t)key & P.slot_mask;
   const uint32_t fp = (uint32_t)(key >> 32);
   const uint32_t want = ((uint32_t)len << 16) | (cont << 24) | 0x80000000u;
@@ -677,7 +678,10 @@ __global__ __launch_bounds__(64 * TOK_WAVES) void tokenize_wave_kernel(TokParams
               while (e < ntot && !(L.nf[e] & NF_START)) ++e;
             }
             cnt = -1;
-            if (nch <= 100) {
+            if (P.dbg_mode == 1) {
+              if (used < PSTAGE) L.stage[lane][used] = (uint16_t)P.unk;
+              cnt = 1;
+            } else if (nch <= 100) {
               auto get = [&](int i) -> uint32_t { return L.nb[j + i]; };
               auto em = [&](int n, uint32_t id) { if (used + n < PSTAGE) L.stage[lane][used + n] = (uint16_t)id; };
               cnt = wordpiece_core(P, get, e - j, em, filt);
