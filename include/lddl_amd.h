@@ -61,10 +61,11 @@ int lddl_vocab_token(const lddl_ctx *ctx, int32_t id, char *buf, int64_t cap);
 
 /* Tokenise n_sent sentences (bytes [d_sent_off[s], d_sent_off[s+1])).
  * Sentence s's ids go to d_out_ids[d_sent_off[s] - d_sent_off[0] + k],
- * k < d_out_ntok[s] = min(#tokens, max_tok).  d_out_ids needs
- * d_sent_off[n_sent] - d_sent_off[0] entries (#tokens <= #bytes). */
-int lddl_tokenize(lddl_ctx *ctx, const uint8_t *d_bytes, const int64_t *d_sent_off, int64_t n_sent,
-                  int32_t max_tok, uint16_t *d_out_ids, int32_t *d_out_ntok, void *stream);
+ * k < d_out_ntok[s] = min(#tokens, max_tok).  nbytes must be >=
+ * d_sent_off[n_sent] - d_sent_off[0]; d_out_ids needs nbytes entries
+ * (#tokens <= #bytes).  d_bytes: 4-byte aligned. */
+int lddl_tokenize(lddl_ctx *ctx, const uint8_t *d_bytes, int64_t nbytes, const int64_t *d_sent_off,
+                  int64_t n_sent, int32_t max_tok, uint16_t *d_out_ids, int32_t *d_out_ntok, void *stream);
 
 /* Pack every partition of a tokenised shard set.
  * Partition p = docs [d_part_doc_off[p], d_part_doc_off[p+1]); doc d =

@@ -70,6 +70,23 @@ struct lddl_ctx {
   uint32_t* d_counter = nullptr;
 };
 
+// ------------------------------------------------------------------ pack --
+template <class T>
+static int ws_get(lddl_ctx* c, int slot, size_t n, T** out) {
+  auto& b = c->ws[slot];
+  const size_t bytes = (n ? n : 1) * sizeof(T);
+  if (b.cap < bytes) {
+    (void)hipFree(b.p);
+    b.p = nullptr;
+    b.cap = 0;
+    HIP_TRY(hipMalloc(&b.p, bytes));
+    b.cap = bytes;
+  }
+  *out = (T*)b.p;
+  return 0;
+}
+
+
 extern "C" const char* lddl_last_error(void) { return g_err; }
 
 static void free_ctx(lddl_ctx* c) {
@@ -235,9 +252,9 @@ extern "C" int lddl_create(const char* vocab_path, const char* table_path, int d
   c->n_cu = prop.multiProcessorCount;
   if ((rc = load_table(c, table_path)) || (rc = load_vocab(c, vocab_path))) { free_ctx(c); return rc; }
   const char* algo = getenv("LDDL_TOKENIZE_ALGO");
-  c->tok_algo = (algo && algo[0] == '1') ? 1 : 2;
+  c->tok_algo = (algo && algo[0] >= '1' && algo[0] <= '3') ? algo[0] - '0' : 3;
   int per_cu = 0;
-  if (c->tok_algo == 1) {
+  if (c->tok_algo != 2) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, tokenize_kernel_ptr(), 256, 0) != hipSuccess || per_cu < 1)
       per_cu = 4;
     c->tok_grid = c->n_cu * per_cu;
@@ -248,7 +265,7 @@ extern "C" int lddl_create(const char* vocab_path, const char* table_path, int d
       per_cu = 2;
     c->tok_grid = c->n_cu * per_cu;
   }
-  const size_t ovf_bytes = c->tok_algo == 1 ? (size_t)c->tok_grid * 256 * WB_OVF
+  const size_t ovf_bytes = c->tok_algo != 2 ? (size_t)c->tok_grid * 256 * WB_OVF
                                             : (size_t)c->tok_grid * TOK_WAVES * (WB_OVF + 64);
   if (hipMalloc((void**)&c->d_ovf, ovf_bytes) != hipSuccess ||
       hipMalloc((void**)&c->d_counter, 64) != hipSuccess) {
@@ -277,10 +294,11 @@ extern "C" int lddl_vocab_token(const lddl_ctx* c, int32_t id, char* buf, int64_
   return (int)w.size();
 }
 
-extern "C" int lddl_tokenize(lddl_ctx* c, const uint8_t* d_bytes, const int64_t* d_sent_off, int64_t n_sent,
-                             int32_t max_tok, uint16_t* d_out_ids, int32_t* d_out_ntok, void* stream) {
+extern "C" int lddl_tokenize(lddl_ctx* c, const uint8_t* d_bytes, int64_t nbytes, const int64_t* d_sent_off,
+                             int64_t n_sent, int32_t max_tok, uint16_t* d_out_ids, int32_t* d_out_ntok, void* stream) {
   if (!c) return set_err(LDDL_EINVAL, "null ctx");
-  if (n_sent < 0 || max_tok < 1) return set_err(LDDL_EINVAL, "n_sent %lld max_tok %d", (long long)n_sent, max_tok);
+  if (n_sent < 0 || max_tok < 1 || nbytes < 0)
+    return set_err(LDDL_EINVAL, "n_sent %lld nbytes %lld max_tok %d", (long long)n_sent, (long long)nbytes, max_tok);
   if (n_sent == 0) return 0;
   if (!d_bytes || !d_sent_off || !d_out_ids || !d_out_ntok) return set_err(LDDL_EINVAL, "null device pointer");
   HIP_TRY(hipSetDevice(c->device));
@@ -318,7 +336,16 @@ extern "C" int lddl_tokenize(lddl_ctx* c, const uint8_t* d_bytes, const int64_t*
     P.dbg = d_dbg;
   }
   const int64_t chunks = (n_sent + P.chunk - 1) / P.chunk;
-  if (c->tok_algo == 1) {
+  if (c->tok_algo == 3) {
+    const int64_t nt = tile_count(nbytes);
+    int64_t* tile_sent;
+    int32_t *fb_list, *fb_count;
+    int rc;
+    if ((rc = ws_get(c, 19, nt + 1, &tile_sent)) || (rc = ws_get(c, 20, nt, &fb_list)) ||
+        (rc = ws_get(c, 21, 16, &fb_count)))
+      return rc;
+    HIP_TRY(launch_tokenize_tiles(P, nbytes, tile_sent, fb_list, fb_count, c->tok_grid, st));
+  } else if (c->tok_algo == 1) {
     int grid = (int)((chunks + 3) / 4);
     if (grid > c->tok_grid) grid = c->tok_grid;
     HIP_TRY(launch_tokenize(P, grid, st));
@@ -337,22 +364,6 @@ extern "C" int lddl_tokenize(lddl_ctx* c, const uint8_t* d_bytes, const int64_t*
       fprintf(stderr, " probes=%llu fallbacks=%llu\n", (unsigned long long)h[12], (unsigned long long)h[13]);
     }
   }
-  return 0;
-}
-
-// ------------------------------------------------------------------ pack --
-template <class T>
-static int ws_get(lddl_ctx* c, int slot, size_t n, T** out) {
-  auto& b = c->ws[slot];
-  const size_t bytes = (n ? n : 1) * sizeof(T);
-  if (b.cap < bytes) {
-    (void)hipFree(b.p);
-    b.p = nullptr;
-    b.cap = 0;
-    HIP_TRY(hipMalloc(&b.p, bytes));
-    b.cap = bytes;
-  }
-  *out = (T*)b.p;
   return 0;
 }
 

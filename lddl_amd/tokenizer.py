@@ -77,7 +77,7 @@ class Tokenizer:
       out_ntok = torch.empty(max(n_sent, 1), dtype=torch.int32, device=self.device)
     assert data.dtype == torch.uint8 and sent_off.dtype == torch.int64
     assert data.is_cuda and sent_off.is_cuda and out_ids.numel() >= nbytes
-    _lib.check(_lib.lib().lddl_tokenize(self._h, _ptr(data), _ptr(sent_off), n_sent, max_tok,
+    _lib.check(_lib.lib().lddl_tokenize(self._h, _ptr(data), nbytes, _ptr(sent_off), n_sent, max_tok,
                                         _ptr(out_ids), _ptr(out_ntok), _stream(stream)))
     return out_ids, out_ntok
 
