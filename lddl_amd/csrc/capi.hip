@@ -345,6 +345,18 @@ extern "C" int lddl_tokenize(lddl_ctx* c, const uint8_t* d_bytes, int64_t nbytes
         (rc = ws_get(c, 21, 16, &fb_count)))
       return rc;
     HIP_TRY(launch_tokenize_tiles(P, nbytes, tile_sent, fb_list, fb_count, c->tok_grid, st));
+    if (P.dbg) {
+      uint64_t h[16];
+      int32_t nfb = 0;
+      HIP_TRY(hipMemcpyAsync(h, P.dbg, sizeof h, hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipMemcpyAsync(&nfb, fb_count, 4, hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipStreamSynchronize(st));
+      const char* nm[12] = {"setup", "A1", "A2", "B", "Cinit", "Cround_A", "Cround_B", "Cfinish", "D", "write",
+                            "rounds", "tiles"};
+      fprintf(stderr, "[lddl tile dbg] ntiles=%lld fallback=%d", (long long)nt, nfb);
+      for (int k = 0; k < 12; ++k) fprintf(stderr, " %s=%llu", nm[k], (unsigned long long)h[k]);
+      fprintf(stderr, "\n");
+    }
   } else if (c->tok_algo == 1) {
     int grid = (int)((chunks + 3) / 4);
     if (grid > c->tok_grid) grid = c->tok_grid;

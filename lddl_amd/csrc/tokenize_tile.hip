@@ -19,10 +19,12 @@
 //      count of boundary spaces before it.  Block scan -> normalised UTF-8.
 //   B  units (words = runs of word chars, isolated punctuation / CJK,
 //      specials) by a block-wide compaction.
-//   C  WordPiece, thread per unit: whole-word probe first (one 16-byte slot
-//      load, verified against the slot's key prefix), greedy longest-match-
-//      first for the rest; pieces staged at the unit's normalised offset
-//      (#pieces <= #chars <= #bytes, so they always fit).
+//   C  WordPiece, thread per unit: greedy longest-match-first, one 16-byte
+//      slot load per candidate (verified against the slot's key prefix);
+//      pieces staged at the unit's normalised offset (#pieces <= #chars <=
+//      #bytes, so they always fit).  (A block-synchronous variant that probes
+//      all candidate lengths of a piece in parallel measured slower: git
+//      history, commit "block-wide WordPiece rounds".)
 //   D  segmented block scan of piece counts by sentence -> ids written
 //      straight to their final slots; per-sentence counts.
 // Tiles the LDS path does not model (ccc>0 survivors needing canonical
@@ -51,21 +53,15 @@ struct TileLds {
   uint8_t nf[TNB + 16];
   uint16_t piece[TNB];
   uint16_t ustart[TUNITS];
-  uint16_t uend[TUNITS];
   uint16_t ucnt[TUNITS];
   uint16_t usent[TUNITS];
   uint16_t upos[TUNITS];
-  uint16_t ucur[TUNITS];         // WordPiece cursor (bytes into the word)
-  uint16_t coff[TUNITS + 1];     // candidate offsets of a B round
-  uint32_t ubest[TUNITS];        // (end << 16) | id of the longest hit
-  uint8_t ustate[TUNITS];        // 0 done, 1 probe longest, 2 probe the rest
   uint16_t sstart[TSENT + 1];
   int32_t stot[TSENT];
   uint32_t cover[TRAW / 32 + 1]; // raw bytes consumed by a special token
   uint32_t ascii[128];
   int32_t red[2 * (TT / 64)];
   int32_t flag;
-  int32_t active;
 };
 
 // exclusive block scan of two ints (256 threads)
@@ -112,6 +108,14 @@ __global__ __launch_bounds__(TT) void tokenize_tile_kernel(TokParams P, const in
   __shared__ TileLds L;
   const int tid = threadIdx.x;
   const int64_t t = blockIdx.x;
+  const bool dbg = P.dbg != nullptr && tid == 0;
+  uint64_t tprev = dbg ? __builtin_amdgcn_s_memtime() : 0;
+#define TSTAMP(k)                                                                    \
+  if (dbg) {                                                                         \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime();                                \
+    atomicAdd((unsigned long long*)&P.dbg[k], (unsigned long long)(t_ - tprev));     \
+    tprev = t_;                                                                      \
+  }
   const int64_t sa = tile_sent[t], sb = tile_sent[t + 1];
   if (sa >= sb) return;
   const int64_t A = P.sent_off[sa], B = P.sent_off[sb];
@@ -132,6 +136,7 @@ __global__ __launch_bounds__(TT) void tokenize_tile_kernel(TokParams P, const in
   if (tid == 0) L.flag = 0;
   __syncthreads();
   for (int i = 1 + tid; i < ns; i += TT) atomicAdd((uint32_t*)&L.scount[L.sstart[i] & ~3], 1u << (8 * (L.sstart[i] & 3)));
+  TSTAMP(0);
   // ---- A1: char starts, entries, specials ---------------------------------
   constexpr int RPT = TRAW / TT;  // raw bytes per thread (8)
   uint32_t ent[RPT], cpv[RPT];
@@ -188,6 +193,7 @@ __global__ __launch_bounds__(TT) void tokenize_tile_kernel(TokParams P, const in
     if (tid == 0) fb_list[atomicAdd(fb_count, 1)] = (int32_t)t;
     return;
   }
+  TSTAMP(1);
   // ---- A2: output sizes (+ boundary spaces), block scan, write ------------
   int nout[RPT], my = 0;
 #pragma unroll
@@ -260,6 +266,7 @@ __global__ __launch_bounds__(TT) void tokenize_tile_kernel(TokParams P, const in
     }
   }
   __syncthreads();
+  TSTAMP(2);
   // ---- B: units + sentence of each unit (block compaction) ---------------
   constexpr int NPT = TNB / TT;  // normalised bytes per thread (12)
   uint32_t um = 0;
@@ -295,157 +302,41 @@ __global__ __launch_bounds__(TT) void tokenize_tile_kernel(TokParams P, const in
   }
   for (int i = tid; i < ns; i += TT) L.stot[i] = 0;
   __syncthreads();
-  // ---- C: WordPiece in block-wide rounds -----------------------------------
-  // Every unit alternates A rounds (probe the longest candidate of its next
-  // piece: one slot load) and, when that misses, a B round in which ALL the
-  // remaining candidate lengths of that piece are probed in parallel by the
-  // whole block (one item per (unit, length)); the longest hit wins
-  // (atomicMax on (end << 16 | id)).  Same result as greedy longest-match-
-  // first, but a word's latency is ~2 probe round trips per piece instead of
-  // one round trip per candidate length.
-  auto nbget = [&](int i) -> uint32_t { return L.nb[i]; };
+  TSTAMP(3);
+  // ---- C: WordPiece, thread per unit --------------------------------------
   for (int u = tid; u < nunits; u += TT) {
     const int j = L.ustart[u];
     const uint32_t f = L.nf[j];
-    L.ubest[u] = 0;
-    L.ucur[u] = 0;
+    int cnt;
     if (f & F_SPECIAL) {
       L.piece[j] = (uint16_t)P.special[L.nb[j]];
-      L.ucnt[u] = 1;
-      L.ustate[u] = 0;
-      continue;
-    }
-    int e = j + 1, nch = 1;
-    if ((f & F_CLS) == CLS_OTHER) {
-      while (e < nlen && (L.nf[e] & (F_CLS | F_SPECIAL)) == CLS_OTHER) {
-        nch += (L.nf[e] & F_START) ? 1 : 0;
-        ++e;
+      cnt = 1;
+    } else {
+      int e = j + 1, nch = 1;
+      if ((f & F_CLS) == CLS_OTHER) {
+        while (e < nlen && (L.nf[e] & (F_CLS | F_SPECIAL)) == CLS_OTHER) {
+          nch += (L.nf[e] & F_START) ? 1 : 0;
+          ++e;
+        }
+      } else {
+        while (e < nlen && !(L.nf[e] & F_START)) ++e;
       }
-    } else {
-      while (e < nlen && !(L.nf[e] & F_START)) ++e;
+      cnt = -1;
+      if (nch <= 100) {
+        auto get = [&](int i) -> uint32_t { return L.nb[j + i]; };
+        auto em = [&](int n, uint32_t id) { L.piece[j + n] = (uint16_t)id; };
+        cnt = wordpiece_core(P, get, e - j, em);
+      }
+      if (cnt < 0) {
+        L.piece[j] = (uint16_t)P.unk;
+        cnt = 1;
+      }
     }
-    L.uend[u] = (uint16_t)(e - j);
-    L.ucnt[u] = 0;
-    if (nch > 100) {
-      L.piece[j] = (uint16_t)P.unk;
-      L.ucnt[u] = 1;
-      L.ustate[u] = 0;
-    } else {
-      L.ustate[u] = 1;
-    }
+    L.ucnt[u] = (uint16_t)cnt;
   }
   __syncthreads();
-  // longest candidate end (exclusive, bytes from the word start) of the piece
-  // starting at cur: char boundary <= min(len, cur + maxb[cont])
-  auto emax_of = [&](int j, int cur, int len, uint32_t cont) -> int {
-    int e = min(len, cur + (int)P.maxb[cont]);
-    while (e < len && e > cur && (L.nb[j + e] & 0xC0u) == 0x80u) --e;
-    return e;
-  };
-  for (int round = 0; round < 2 * 110; ++round) {
-    // ---- A: longest candidate ---------------------------------------------
-    if (tid == 0) L.active = 0;
-    __syncthreads();
-    int act = 0;
-    for (int u = tid; u < nunits; u += TT) {
-      if (L.ustate[u] != 1) continue;
-      const int j = L.ustart[u], len = L.uend[u], cur = L.ucur[u];
-      const uint32_t cont = L.ucnt[u] > 0 ? 1u : 0u;
-      const int e = emax_of(j, cur, len, cont);
-      int id = -1;
-      if (e > cur) {
-        uint64_t h = 0;
-        for (int k = j + cur; k < j + e; ++k) h = hash_push(h, L.nb[k]);
-        id = probe(P, nbget, j + cur, e - cur, cont, h, NoFilter());
-      }
-      if (id >= 0) {
-        L.piece[j + L.ucnt[u]] = (uint16_t)id;
-        L.ucnt[u] = L.ucnt[u] + 1;
-        L.ucur[u] = (uint16_t)e;
-        if (e == len) L.ustate[u] = 0; else act = 1;
-      } else {
-        L.ustate[u] = 2;
-        act = 1;
-      }
-    }
-    if (act) L.active = 1;
-    __syncthreads();
-    if (!L.active) break;
-    // ---- B: every remaining candidate of the B units, block-parallel ------
-    constexpr int UPT0 = TUNITS / TT;
-    int nc[UPT0];
-    int mysum = 0;
-#pragma unroll
-    for (int k = 0; k < UPT0; ++k) {
-      const int u = tid * UPT0 + k;
-      nc[k] = 0;
-      if (u < nunits && L.ustate[u] == 2) {
-        const int j = L.ustart[u], len = L.uend[u], cur = L.ucur[u];
-        const int e = emax_of(j, cur, len, L.ucnt[u] > 0 ? 1u : 0u);
-        int c = 0;
-        for (int b = cur + 1; b < e; ++b) c += ((L.nb[j + b] & 0xC0u) != 0x80u) ? 1 : 0;
-        nc[k] = c;
-      }
-      mysum += nc[k];
-    }
-    int cbeg, d0, ctot, d1;
-    block_scan2(L, mysum, 0, &cbeg, &d0, &ctot, &d1);
-#pragma unroll
-    for (int k = 0; k < UPT0; ++k) {
-      const int u = tid * UPT0 + k;
-      if (u < nunits) L.coff[u] = (uint16_t)min(cbeg, 65535);
-      cbeg += nc[k];
-    }
-    if (tid == 0) L.coff[nunits] = (uint16_t)min(ctot, 65535);
-    __syncthreads();
-    for (int it = tid; it < ctot; it += TT) {
-      int lo = 0, hi = nunits;  // last u with coff[u] <= it
-      while (hi - lo > 1) { const int m = (lo + hi) >> 1; if (L.coff[m] <= it) lo = m; else hi = m; }
-      const int u = lo;
-      const int j = L.ustart[u], len = L.uend[u], cur = L.ucur[u];
-      const uint32_t cont = L.ucnt[u] > 0 ? 1u : 0u;
-      int e = emax_of(j, cur, len, cont);
-      for (int q = it - L.coff[u]; q >= 0; --q) {  // (q+1)-th boundary below emax
-        --e;
-        while (e > cur && (L.nb[j + e] & 0xC0u) == 0x80u) --e;
-      }
-      uint64_t h = 0;
-      for (int k = j + cur; k < j + e; ++k) h = hash_push(h, L.nb[k]);
-      const int id = probe(P, nbget, j + cur, e - cur, cont, h, NoFilter());
-      if (id >= 0) atomicMax(&L.ubest[u], ((uint32_t)e << 16) | (uint32_t)id);
-    }
-    __syncthreads();
-    for (int u = tid; u < nunits; u += TT) {
-      if (L.ustate[u] != 2) continue;
-      const uint32_t b = L.ubest[u];
-      const int j = L.ustart[u];
-      if (b == 0) {  // no piece matches here: the whole word is [UNK]
-        L.piece[j] = (uint16_t)P.unk;
-        L.ucnt[u] = 1;
-        L.ustate[u] = 0;
-        continue;
-      }
-      const int e = (int)(b >> 16);
-      L.piece[j + L.ucnt[u]] = (uint16_t)(b & 0xFFFFu);
-      L.ucnt[u] = L.ucnt[u] + 1;
-      L.ucur[u] = (uint16_t)e;
-      L.ubest[u] = 0;
-      L.ustate[u] = e == L.uend[u] ? 0 : 1;
-    }
-    __syncthreads();
-  }
-  {  // defensive: a unit still active here (never expected) -> exact fallback
-    int left = 0;
-    for (int u = tid; u < nunits; u += TT) left |= L.ustate[u];
-    if (tid == 0) L.flag = 0;
-    __syncthreads();
-    if (left) L.flag = 1;
-    __syncthreads();
-    if (L.flag) {
-      if (tid == 0) fb_list[atomicAdd(fb_count, 1)] = (int32_t)t;
-      return;
-    }
-  }
+  TSTAMP(4);
+  TSTAMP(7);
   // ---- D: token index inside the sentence (segmented scan) ---------------
   constexpr int UPT = TUNITS / TT;  // units per thread (4), contiguous
   int run = 0, headseen = 0;
@@ -493,6 +384,7 @@ __global__ __launch_bounds__(TT) void tokenize_tile_kernel(TokParams P, const in
     }
     __syncthreads();
   }
+  TSTAMP(8);
   // ---- write ids and per-sentence counts ----------------------------------
   for (int u = tid; u < nunits; u += TT) {
     const int s = L.usent[u];
@@ -506,6 +398,9 @@ __global__ __launch_bounds__(TT) void tokenize_tile_kernel(TokParams P, const in
   }
   __syncthreads();
   for (int i = tid; i < ns; i += TT) P.out_ntok[sa + i] = min(L.stot[i], P.max_tok);
+  TSTAMP(9);
+  if (dbg) atomicAdd((unsigned long long*)&P.dbg[11], 1ull);
+#undef TSTAMP
 }
 
 // Exact serial path for the listed tiles: lane per sentence (tokenize.hip).
