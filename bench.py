@@ -165,6 +165,11 @@ def main():
     res, ntok = step(False)
   torch.cuda.synchronize()
   n_tok = int(ntok[:sh.n_sent].sum().item())
+  # full-size property check (outside the timed region): every replica of the
+  # unique corpus must tokenize to the same number of tokens
+  per_rep = ntok[:reps * base.n_sent].view(reps, base.n_sent).to(torch.int64).sum(1)
+  if not bool((per_rep == per_rep[0]).all()):
+    raise RuntimeError('tokenize: replicas disagree: %s' % per_rep.tolist()[:16])
   if dist is not None:
     dist.barrier()
   torch.cuda.synchronize()
@@ -205,7 +210,7 @@ def main():
                  'partitions_per_gpu': sh.n_part, 'wordpiece_tokens_per_gpu': n_tok,
                  'pairs_per_gpu': res.n_pairs, 'packed_tokens_per_gpu': res.n_tokens,
                  'parallelism': 'shard%d' % world},
-      'roofline': {'bound': 'hbm', 'kernel': 'lddl::tokenize_kernel', 'achieved': achieved, 'peak': HBM_PEAK_GBS,
+      'roofline': {'bound': 'hbm', 'kernel': 'lddl::tokenize_tile_kernel', 'achieved': achieved, 'peak': HBM_PEAK_GBS,
                    'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS, 'traffic': None,
                    'algorithmic_bytes_per_launch': alg, 'avg_launch_ms': tk},
       'tokenize_ms': tk, 'gen_s': gen_s,

@@ -65,7 +65,8 @@ struct lddl_ctx {
   int pack_codebert = 0;
   // scratch
   int tok_grid = 0;
-  int tok_algo = 2;  // 2 = wave-cooperative windows, 1 = lane per sentence
+  int tok_algo = 3;  // 3 = workgroup tiles, 2 = wave windows, 1 = lane per sentence
+  int64_t tile_chunk = 0;  // tiles per tile-kernel launch (0 = default)
   uint8_t* d_ovf = nullptr;
   uint32_t* d_counter = nullptr;
 };
@@ -253,6 +254,8 @@ extern "C" int lddl_create(const char* vocab_path, const char* table_path, int d
   if ((rc = load_table(c, table_path)) || (rc = load_vocab(c, vocab_path))) { free_ctx(c); return rc; }
   const char* algo = getenv("LDDL_TOKENIZE_ALGO");
   c->tok_algo = (algo && algo[0] >= '1' && algo[0] <= '3') ? algo[0] - '0' : 3;
+  const char* tchunk = getenv("LDDL_TILE_CHUNK");  // tiles per launch (tests force several launches)
+  c->tile_chunk = tchunk ? atoll(tchunk) : 0;
   int per_cu = 0;
   if (c->tok_algo != 2) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, tokenize_kernel_ptr(), 256, 0) != hipSuccess || per_cu < 1)
@@ -344,7 +347,7 @@ extern "C" int lddl_tokenize(lddl_ctx* c, const uint8_t* d_bytes, int64_t nbytes
     if ((rc = ws_get(c, 19, nt + 1, &tile_sent)) || (rc = ws_get(c, 20, nt, &fb_list)) ||
         (rc = ws_get(c, 21, 16, &fb_count)))
       return rc;
-    HIP_TRY(launch_tokenize_tiles(P, nbytes, tile_sent, fb_list, fb_count, c->tok_grid, st));
+    HIP_TRY(launch_tokenize_tiles(P, nbytes, tile_sent, fb_list, fb_count, c->tok_grid, c->tile_chunk, st));
     if (P.dbg) {
       uint64_t h[16];
       int32_t nfb = 0;

@@ -43,6 +43,6 @@ hipError_t launch_tokenize_wave(const TokParams& P, int grid, hipStream_t stream
 const void* tokenize_wave_kernel_ptr();
 int64_t tile_count(int64_t nbytes);
 hipError_t launch_tokenize_tiles(const TokParams& P, int64_t nbytes, int64_t* tile_sent, int32_t* fb_list,
-                                 int32_t* fb_count, int fb_grid, hipStream_t s);
+                                 int32_t* fb_count, int fb_grid, int64_t chunk, hipStream_t s);
 
 }  // namespace lddl

@@ -104,10 +104,10 @@ __global__ void tile_bounds_kernel(const int64_t* sent_off, int64_t n_sent, int6
 }
 
 __global__ __launch_bounds__(TT) void tokenize_tile_kernel(TokParams P, const int64_t* tile_sent, int32_t* fb_list,
-                                                          int32_t* fb_count) {
+                                                          int32_t* fb_count, int64_t t_base) {
   __shared__ TileLds L;
   const int tid = threadIdx.x;
-  const int64_t t = blockIdx.x;
+  const int64_t t = t_base + blockIdx.x;
   const bool dbg = P.dbg != nullptr && tid == 0;
   uint64_t tprev = dbg ? __builtin_amdgcn_s_memtime() : 0;
 #define TSTAMP(k)                                                                    \
@@ -427,17 +427,24 @@ __global__ __launch_bounds__(256) void tokenize_fallback_kernel(TokParams P, con
 
 int64_t tile_count(int64_t nbytes) { return (nbytes >> TILE_SHIFT) + 1; }
 
+// The dispatch packet's grid size is 32-bit in work-items, so a launch of
+// more than 2^32 / TT tiles would wrap: tiles go out in chunks of at most
+// `chunk` workgroups (default 2^22, i.e. 4 GiB of input per launch).
 hipError_t launch_tokenize_tiles(const TokParams& P, int64_t nbytes, int64_t* tile_sent, int32_t* fb_list,
-                                 int32_t* fb_count, int fb_grid, hipStream_t s) {
+                                 int32_t* fb_count, int fb_grid, int64_t chunk, hipStream_t s) {
   const int64_t n_tiles = tile_count(nbytes);
   hipLaunchKernelGGL(tile_bounds_kernel, dim3(4096), dim3(256), 0, s, P.sent_off, P.n_sent, n_tiles, tile_sent);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   e = hipMemsetAsync(fb_count, 0, 4, s);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(tokenize_tile_kernel, dim3((unsigned)n_tiles), dim3(TT), 0, s, P, tile_sent, fb_list, fb_count);
-  e = hipGetLastError();
-  if (e != hipSuccess) return e;
+  if (chunk <= 0 || chunk > (int64_t(1) << 22)) chunk = int64_t(1) << 22;
+  for (int64_t t0 = 0; t0 < n_tiles; t0 += chunk) {
+    const int64_t nt = n_tiles - t0 < chunk ? n_tiles - t0 : chunk;
+    hipLaunchKernelGGL(tokenize_tile_kernel, dim3((unsigned)nt), dim3(TT), 0, s, P, tile_sent, fb_list, fb_count, t0);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
   hipLaunchKernelGGL(tokenize_fallback_kernel, dim3(fb_grid), dim3(256), 0, s, P, tile_sent, fb_list, fb_count);
   return hipGetLastError();
 }
