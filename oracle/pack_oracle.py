@@ -8,6 +8,9 @@ own ``random`` module (MT19937, the RNG the reference uses):
                         create_pairs_from_document (+ _truncate_seq_pair :161-176)
   * ``codebert_pairs``  lddl/dask/bert/pretrain_codebert.py:343-442
                         create_pairs_from_document (+ _truncate_seq :236-247)
+  * ``masked_lm``       pretrain.py:182-238 create_masked_lm_predictions
+                        (static masking, --masking; vocab_words = the vocab
+                        file's tokens in file order, i.e. token id = index)
   * ``partition_pairs`` pretrain.py:386-402 / pretrain_codebert.py:460-477
                         _to_partition_pairs: duplicate_factor passes over the
                         partition's documents, then random.shuffle
@@ -42,11 +45,36 @@ def _truncate_seq_pair(a, b, max_num_tokens, rnd):
       t[1] -= 1
 
 
-def bert_pairs(docs, di, max_seq_length, short_seq_prob, rnd):
-  """One document -> list of pairs (a_sents, b_sents, a_win, b_win, is_random_next).
+def masked_lm(tokens_a, tokens_b, ratio, n_vocab, cls_id, sep_id, mask_id, rnd):
+  """create_masked_lm_predictions over token ids -> (A', B', positions, labels)."""
+  tokens = [cls_id] + list(tokens_a) + [sep_id] + list(tokens_b) + [sep_id]
+  cand = [i for i, t in enumerate(tokens) if t != cls_id and t != sep_id]
+  rnd.shuffle(cand)
+  out = list(tokens)
+  num_to_predict = max(1, int(round(len(tokens) * ratio)))
+  picked = []
+  for index in cand:
+    if len(picked) >= num_to_predict:
+      break
+    if rnd.random() < 0.8:
+      new = mask_id
+    elif rnd.random() < 0.5:
+      new = tokens[index]
+    else:
+      new = rnd.randint(0, n_vocab - 1)
+    out[index] = new
+    picked.append(index)
+  picked.sort()
+  la, lb = len(tokens_a), len(tokens_b)
+  return out[1:1 + la], out[2 + la:2 + la + lb], picked, [tokens[i] for i in picked]
+
+
+def bert_pairs(docs, di, max_seq_length, short_seq_prob, rnd, masking=None):
+  """One document -> list of pairs (a_sents, b_sents, a_win, b_win, is_random_next[, mask]).
 
   a_sents/b_sents: list of (doc, sentence) ids; *_win: [lo, hi) over their
-  concatenated tokens."""
+  concatenated tokens.  masking = (ratio, n_vocab, cls_id, sep_id, mask_id)
+  appends mask = (A', B', positions, labels) from masked_lm."""
   document = docs[di]
   max_num_tokens = max_seq_length - 3
   target = max_num_tokens
@@ -92,7 +120,12 @@ def bert_pairs(docs, di, max_seq_length, short_seq_prob, rnd):
         a_w, b_w = [0, la], [0, lb]
         _truncate_seq_pair(a_w, b_w, max_num_tokens, rnd)
         assert a_w[1] - a_w[0] >= 1 and b_w[1] - b_w[0] >= 1
-        out.append((a_s, b_s, a_w, b_w, is_random_next))
+        if masking is not None:
+          ta = [t for (d, s) in a_s for t in docs[d][s]][a_w[0]:a_w[1]]
+          tb = [t for (d, s) in b_s for t in docs[d][s]][b_w[0]:b_w[1]]
+          out.append((a_s, b_s, a_w, b_w, is_random_next, masked_lm(ta, tb, *masking, rnd)))
+        else:
+          out.append((a_s, b_s, a_w, b_w, is_random_next))
       chunk = []
       cur = 0
     i += 1
@@ -216,27 +249,33 @@ def filtered_docs(ids, ntok, sent_off, doc_sent_off, d0, d1):
 
 
 def pair_tokens(docs, pair):
-  a_s, b_s, a_w, b_w, rn = pair
+  a_s, b_s, a_w, b_w, rn = pair[:5]
   a = [t for (d, s) in a_s for t in docs[d][s]][a_w[0]:a_w[1]]
   b = [t for (d, s) in b_s for t in docs[d][s]][b_w[0]:b_w[1]]
   return a, b, rn
 
 
 def run_bert_shards(corpus, ids, ntok, part_doc_off, target_seq_length, short_seq_prob, dup, seed,
-                    bin_size=None):
+                    bin_size=None, masking=None):
   """Every partition of a corpus -> list (per partition) of rows
-  (A ids, B ids, is_random_next, num_tokens), in the reference's output order
-  (binned when bin_size is given)."""
+  (A ids, B ids, is_random_next, num_tokens[, positions, labels]), in the
+  reference's output order (binned when bin_size is given); with masking
+  (see bert_pairs) A/B are the masked segments."""
   out = []
   for p in range(len(part_doc_off) - 1):
     docs = filtered_docs(ids, ntok, corpus.sent_off, corpus.doc_sent_off,
                          int(part_doc_off[p]), int(part_doc_off[p + 1]))
     pairs = partition_pairs(docs, seed + p,
-                            lambda D, di, r: bert_pairs(D, di, target_seq_length, short_seq_prob, r), dup)
+                            lambda D, di, r: bert_pairs(D, di, target_seq_length, short_seq_prob, r, masking),
+                            dup)
     rows = []
     for pr in pairs:
       a, b, rn = pair_tokens(docs, pr)
-      rows.append((a, b, rn, len(a) + len(b) + 3))
+      if masking is not None:
+        ma, mb, pos, lab = pr[5]
+        rows.append((ma, mb, rn, len(a) + len(b) + 3, pos, lab))
+      else:
+        rows.append((a, b, rn, len(a) + len(b) + 3))
     if bin_size is not None:
       nbins = target_seq_length // bin_size
       order, _ = binned_order([r[3] for r in rows], bin_size, nbins)

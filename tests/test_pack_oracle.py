@@ -71,3 +71,32 @@ def test_codebert_pairs_match_reference(k):
     ct = [t for (d, s) in code_s for t in docs[d][s]][cw[0]:cw[1]]
     special = 3 if nd[code_s[0][0]] else 2
     assert (dt, ct, len(dt) + len(ct) + special) == (row['doc'], row['code'], row['num_tokens'])
+
+
+BERT_MASK = (0.15, 30522, 101, 102, 103)  # ratio, |vocab|, [CLS], [SEP], [MASK]
+
+
+@pytest.mark.parametrize('k', [i for i, c in enumerate(BERT['cases']) if c['cfg']['masking']])
+def test_bert_masked_pairs_match_reference(k):
+  """Static masking (pretrain.py:182-238) on the reference's own rows."""
+  case = BERT['cases'][k]
+  c = case['cfg']
+  docs = [[s for s in d if s] for d in case['docs']]
+  docs = [d for d in docs if d]
+  if case['error']:
+    with pytest.raises(AssertionError):
+      po.partition_pairs(docs, case['seed'],
+                         lambda D, di, r: po.bert_pairs(D, di, c['max_seq'], c['ssp'], r, BERT_MASK), c['dup'])
+    return
+  pairs = po.partition_pairs(docs, case['seed'],
+                             lambda D, di, r: po.bert_pairs(D, di, c['max_seq'], c['ssp'], r, BERT_MASK), c['dup'])
+  rows = case['rows']
+  assert len(pairs) == len(rows)
+  n_masked = 0
+  for pr, row in zip(pairs, rows):
+    a, b, rn = po.pair_tokens(docs, pr)
+    ma, mb, pos, lab = pr[5]
+    assert (ma, mb, rn, len(a) + len(b) + 3) == (row['A'], row['B'], row['is_random_next'], row['num_tokens'])
+    assert pos == row['masked_lm_positions'] and lab == row['masked_lm_labels']
+    n_masked += len(pos)
+  assert n_masked > 0 or not rows
