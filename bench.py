@@ -44,6 +44,7 @@ def parse():
   ap.add_argument('--duplicate-factor', type=int, default=5)
   ap.add_argument('--partition-mb', type=float, default=1.0, help='bytes per partition (--block-size)')
   ap.add_argument('--seed', type=int, default=12345)
+  ap.add_argument('--masking', action='store_true', help='static masking (--masking of the reference)')
   ap.add_argument('--no-cpu-baseline', action='store_true')
   ap.add_argument('--cpu-seconds', type=float, default=12.0)
   return ap.parse_args()
@@ -143,7 +144,7 @@ def main():
   sh, base, pdo, reps, gen_s = build_shards(args, rank, device)
   pk = Packer(device=local)
   kw = dict(target_seq_length=args.target_seq_length, short_seq_prob=0.1, duplicate_factor=args.duplicate_factor,
-            seed=args.seed + rank * 10_000_000, bin_size=args.bin_size)
+            seed=args.seed + rank * 10_000_000, bin_size=args.bin_size, masking=args.masking)
   tok_ms = []
 
   def step(timed):
@@ -202,13 +203,15 @@ def main():
       'warmup': args.warmup, 'ms_per_step': el * 1e3 / args.steps, 'higher_is_better': True,
       'scaling': 'weak', 'vs_baseline': None, 'dtype': 'u8',
       'data': 'synthetic (Wikipedia-style, %d MB unique tiled x%d per GPU)' % (args.unique_mb, reps),
-      'config': {'workload': 'bert_seq%d_bin%d_%dGB_per_gpu' % (args.target_seq_length, args.bin_size,
-                                                                 round(sh.nbytes / (1 << 30))),
+      'config': {'workload': 'bert_seq%d_bin%d_%dGB_per_gpu%s' % (args.target_seq_length, args.bin_size,
+                                                                   round(sh.nbytes / (1 << 30)),
+                                                                   '_masking' if args.masking else ''),
                  'target_seq_length': args.target_seq_length, 'bin_size': args.bin_size,
                  'duplicate_factor': args.duplicate_factor, 'vocab': 'bert-base-uncased (lddl/dask/bert/vocab)',
                  'corpus_bytes_per_gpu': sh.nbytes, 'sentences_per_gpu': sh.n_sent,
                  'partitions_per_gpu': sh.n_part, 'wordpiece_tokens_per_gpu': n_tok,
                  'pairs_per_gpu': res.n_pairs, 'packed_tokens_per_gpu': res.n_tokens,
+                 'masked_positions_per_gpu': res.n_masked,
                  'parallelism': 'shard%d' % world},
       'roofline': {'bound': 'hbm', 'kernel': 'lddl::tokenize_tile_kernel', 'achieved': achieved, 'peak': HBM_PEAK_GBS,
                    'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS, 'traffic': None,

@@ -13,10 +13,11 @@
  *       truncation=True) of _get_documents._to_document
  *       (pretrain.py:79-80, :82-95) and _get_code_pairs (pretrain_codebert.py:
  *       123-124), batched over every sentence of a shard.
- *   lddl_pack_bert / lddl_pack_codebert / lddl_bin / lddl_materialize
+ *   lddl_pack_bert / lddl_pack_codebert / lddl_materialize / lddl_masked_lm
  *       replace _get_pairs._to_partition_pairs (pretrain.py:386-402 with
- *       create_pairs_from_document :241-365, pretrain_codebert.py:460-477 with
- *       :343-442) and the binned writer's grouping
+ *       create_pairs_from_document :241-365 and, with --masking,
+ *       create_masked_lm_predictions :182-238; pretrain_codebert.py:460-477
+ *       with :343-442) and the binned writer's grouping
  *       (binning.py:63-93 _to_dataframe_binned).
  *
  * Conventions: every pointer named d_* is a DEVICE pointer on the ctx's
@@ -69,19 +70,23 @@ int lddl_tokenize(lddl_ctx *ctx, const uint8_t *d_bytes, int64_t nbytes, const i
 
 /* Pack every partition of a tokenised shard set.
  * Partition p = docs [d_part_doc_off[p], d_part_doc_off[p+1]); doc d =
- * sentences [d_doc_sent_off[d], d_doc_sent_off[d+1]); d_ntok / d_sent_off are
- * lddl_tokenize's output / input.  Partition p is packed exactly like the
- * reference's _to_partition_pairs (pretrain.py:386-402) after
- * random.seed(seed + p): duplicate_factor passes of create_pairs_from_document
- * (:241-365), then random.shuffle, then (bin_size > 0) the stable bin
- * grouping of binning.py:63-93.  Synchronises the stream once and returns
- * out_totals = {#pairs, #tokens (with [CLS]/[SEP]), nbins}; the rows are
- * then written by lddl_materialize.  masking != 0: static MLM masking
- * (create_masked_lm_predictions :182-238). */
-int lddl_pack_bert(lddl_ctx *ctx, const int32_t *d_ntok, const int64_t *d_sent_off, int64_t n_sent,
-                   const int64_t *d_doc_sent_off, int64_t n_doc, const int64_t *d_part_doc_off, int64_t n_part,
-                   int32_t target_seq_length, double short_seq_prob, int32_t duplicate_factor, int32_t masking,
-                   double masked_lm_ratio, uint64_t seed, int32_t bin_size, int64_t *out_totals, void *stream);
+ * sentences [d_doc_sent_off[d], d_doc_sent_off[d+1]); d_ids / d_ntok /
+ * d_sent_off are lddl_tokenize's output / input (d_ids may be NULL unless
+ * masking).  Partition p is packed exactly like the reference's
+ * _to_partition_pairs (pretrain.py:386-402) after random.seed(seed + p):
+ * duplicate_factor passes of create_pairs_from_document (:241-365), then
+ * random.shuffle, then (bin_size > 0) the stable bin grouping of
+ * binning.py:63-93.  Synchronises the stream once and returns
+ * out_totals[4] = {#pairs, #tokens (with [CLS]/[SEP]), nbins, #masked}.
+ * masking != 0: static MLM masking, create_masked_lm_predictions
+ * (:182-238) with vocab_words = the vocab file's tokens in file order
+ * (target_seq_length <= 1024); the rows are then written by
+ * lddl_materialize and masked by lddl_masked_lm. */
+int lddl_pack_bert(lddl_ctx *ctx, const uint16_t *d_ids, const int32_t *d_ntok, const int64_t *d_sent_off,
+                   int64_t n_sent, const int64_t *d_doc_sent_off, int64_t n_doc, const int64_t *d_part_doc_off,
+                   int64_t n_part, int32_t target_seq_length, double short_seq_prob, int32_t duplicate_factor,
+                   int32_t masking, double masked_lm_ratio, uint64_t seed, int32_t bin_size, int64_t *out_totals,
+                   void *stream);
 
 /* CodeBERT docstring/code packing (pretrain_codebert.py:343-442, :460-477).
  * Doc d's first d_doc_nseg_doc[d] sentences are its docstring segments, the
@@ -103,6 +108,15 @@ int lddl_pack_codebert(lddl_ctx *ctx, const int32_t *d_ntok, const int64_t *d_se
 int lddl_materialize(lddl_ctx *ctx, const uint16_t *d_ids, uint16_t *d_out_tokens, int64_t *d_out_tok_off,
                      uint16_t *d_out_len0, uint16_t *d_out_len1, uint8_t *d_out_flags, uint8_t *d_out_bin,
                      int64_t *d_out_part, int64_t *d_bin_count, void *stream);
+
+/* After lddl_pack_bert(masking=1) + lddl_materialize: apply the masking to
+ * the materialised rows in place (A/B become output_tokens[1:1+len(A)] /
+ * [2+len(A):...], pretrain.py:232-233) and write, per row g,
+ * d_out_mlm_pos[d_out_mlm_off[g] .. d_out_mlm_off[g+1]) = masked_lm_positions
+ * (ascending, row coordinates incl. [CLS]) and d_out_mlm_label[...] =
+ * masked_lm_labels as token ids (pretrain.py:225-238, :340-361). */
+int lddl_masked_lm(lddl_ctx *ctx, int64_t *d_out_mlm_off, uint16_t *d_out_mlm_pos, uint16_t *d_out_mlm_label,
+                   void *stream);
 
 #ifdef __cplusplus
 }

@@ -58,10 +58,14 @@ struct lddl_ctx {
     void* p = nullptr;
     size_t cap = 0;
   };
-  Buf ws[24];
+  Buf ws[40];
   PackParams pp{};
   int64_t last_npairs = -1, last_ntok = -1;
-  int64_t* h_tot = nullptr;  // pinned [4]
+  int64_t* h_tot = nullptr;  // pinned [8]
+  int64_t last_nmask = -1;
+  uint16_t* last_tokens = nullptr;  // rows of the last lddl_materialize
+  const int64_t* last_tok_off = nullptr;   // masked entries of the last pack (-1: no masking)
+  uint64_t mlm_cap = 0;      // masking arena capacity that last sufficed
   int pack_codebert = 0;
   // scratch
   int tok_grid = 0;
@@ -256,6 +260,8 @@ extern "C" int lddl_create(const char* vocab_path, const char* table_path, int d
   c->tok_algo = (algo && algo[0] >= '1' && algo[0] <= '3') ? algo[0] - '0' : 3;
   const char* tchunk = getenv("LDDL_TILE_CHUNK");  // tiles per launch (tests force several launches)
   c->tile_chunk = tchunk ? atoll(tchunk) : 0;
+  const char* mcap = getenv("LDDL_MLM_CAP");  // initial masking arena (tests force the regrow path)
+  c->mlm_cap = mcap ? (uint64_t)atoll(mcap) : 0;
   int per_cu = 0;
   if (c->tok_algo != 2) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, tokenize_kernel_ptr(), 256, 0) != hipSuccess || per_cu < 1)
@@ -386,8 +392,17 @@ static int pack_common(lddl_ctx* c, int codebert, const int32_t* d_ntok, const i
                        const int64_t* d_doc_sent_off, const int32_t* d_doc_nseg_doc, int64_t n_doc,
                        const int64_t* d_part_doc_off, int64_t n_part, int32_t target_seq_length,
                        double short_seq_prob, int32_t duplicate_factor, uint64_t seed, int32_t bin_size,
-                       int64_t* out_totals, void* stream) {
+                       int64_t* out_totals, void* stream, const uint16_t* d_ids = nullptr, int32_t masking = 0,
+                       double masked_lm_ratio = 0.15) {
   if (!c) return set_err(LDDL_EINVAL, "null ctx");
+  if (masking) {
+    if (!d_ids) return set_err(LDDL_EINVAL, "masking needs the tokenizer ids");
+    if (target_seq_length > MLM_MAX_SEQ)
+      return set_err(LDDL_EINVAL, "masking supports target_seq_length <= %d", MLM_MAX_SEQ);
+    if (!(masked_lm_ratio >= 0.0 && masked_lm_ratio <= 1.0))
+      return set_err(LDDL_EINVAL, "masked_lm_ratio %g not in [0, 1]", masked_lm_ratio);
+    if (c->vocab_size > 65535) return set_err(LDDL_EINVAL, "masking: vocab larger than 65535");
+  }
   if (n_part < 1 || n_doc < 0 || n_sent < 0) return set_err(LDDL_EINVAL, "bad sizes");
   if (!d_ntok || !d_sent_off || !d_doc_sent_off || !d_part_doc_off || !out_totals)
     return set_err(LDDL_EINVAL, "null pointer");
@@ -439,17 +454,58 @@ static int pack_common(lddl_ctx* c, int codebert, const int32_t* d_ntok, const i
   if ((rc = ws_get(c, 15, n_part + 1, &pair_base)) || (rc = ws_get(c, 16, n_part + 1, &tok_base)) ||
       (rc = ws_get(c, 17, 4, &err_any)))
     return rc;
-  if (!c->h_tot) HIP_TRY(hipHostMalloc((void**)&c->h_tot, 4 * sizeof(int64_t)));
+  if (!c->h_tot) HIP_TRY(hipHostMalloc((void**)&c->h_tot, 8 * sizeof(int64_t)));
+  int64_t *mask_base = nullptr, *mask_base2 = nullptr;
+  if (masking) {
+    P.masking = 1;
+    P.mlm_ratio = masked_lm_ratio;
+    P.n_vocab = (uint32_t)c->vocab_size;
+    P.cls_id = c->special[2];
+    P.sep_id = c->special[3];
+    P.mask_id = c->special[4];
+    P.ids = d_ids;
+    uint8_t *sent_spec, *fs_spec;
+    if ((rc = ws_get(c, 22, n_sent, &sent_spec)) || (rc = ws_get(c, 23, n_sent, &fs_spec)) ||
+        (rc = ws_get(c, 24, npair_cap, &P.mref)) || (rc = ws_get(c, 25, npair_cap, &P.mloc)) ||
+        (rc = ws_get(c, 26, n_part, &P.part_nmask)) || (rc = ws_get(c, 27, n_part + 1, &mask_base)) ||
+        (rc = ws_get(c, 28, n_part + 1, &mask_base2)) || (rc = ws_get(c, 29, 1, &P.mcounter)))
+      return rc;
+    P.sent_spec = sent_spec;
+    P.fs_spec = fs_spec;
+    HIP_TRY(launch_sent_special(d_ids, d_sent_off, d_ntok, n_sent, P.cls_id, P.sep_id, sent_spec, st));
+    if (!c->mlm_cap) c->mlm_cap = (uint64_t)n_part * 4 * MLM_CHUNK + (uint64_t)duplicate_factor * n_sent * 4;
+  }
   const char* palgo = getenv("LDDL_PACK_ALGO");
-  const bool lane_packer = palgo && palgo[0] == '1';
-  HIP_TRY(codebert ? launch_pack_codebert(P, st) : lane_packer ? launch_pack_bert(P, st) : launch_pack_bert_wave(P, st));
-  HIP_TRY(launch_scan_parts(P.part_npairs, P.part_ntok, n_part, pair_base, tok_base, P.part_err, err_any, st));
-  HIP_TRY(hipMemcpyAsync(c->h_tot, pair_base + n_part, 8, hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipMemcpyAsync(c->h_tot + 1, tok_base + n_part, 8, hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipMemcpyAsync(c->h_tot + 2, err_any, 4, hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipStreamSynchronize(st));
+  const bool lane_packer = !masking && palgo && palgo[0] == '1';
+  for (int attempt = 0;; ++attempt) {
+    if (masking) {
+      if ((rc = ws_get(c, 30, c->mlm_cap, &P.marena))) return rc;
+      P.mcap = c->mlm_cap;
+      HIP_TRY(hipMemsetAsync(P.mcounter, 0, 8, st));
+    }
+    HIP_TRY(codebert ? launch_pack_codebert(P, st) : lane_packer ? launch_pack_bert(P, st) : launch_pack_bert_wave(P, st));
+    HIP_TRY(launch_scan_parts(P.part_npairs, P.part_ntok, n_part, pair_base, tok_base, P.part_err, err_any, st));
+    HIP_TRY(hipMemcpyAsync(c->h_tot, pair_base + n_part, 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(c->h_tot + 1, tok_base + n_part, 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(c->h_tot + 2, err_any, 4, hipMemcpyDeviceToHost, st));
+    if (masking) {
+      HIP_TRY(launch_scan_parts(P.part_nmask, P.part_nmask, n_part, mask_base, mask_base2, P.part_err, err_any, st));
+      HIP_TRY(hipMemcpyAsync(c->h_tot + 3, mask_base + n_part, 8, hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipMemcpyAsync(c->h_tot + 4, P.mcounter, 8, hipMemcpyDeviceToHost, st));
+    }
+    HIP_TRY(hipStreamSynchronize(st));
+    // the bump allocator overshot the arena: grow it and pack again (the
+    // pack is deterministic, so the rerun reproduces the same rows)
+    if (masking && (uint64_t)c->h_tot[4] > c->mlm_cap && attempt == 0) {
+      c->mlm_cap = (uint64_t)c->h_tot[4] + (uint64_t)n_part * MLM_CHUNK;
+      continue;
+    }
+    if (masking && (uint64_t)c->h_tot[4] > c->mlm_cap) return set_err(LDDL_ECAPACITY, "masking arena overflow");
+    break;
+  }
   const int32_t e = (int32_t)(c->h_tot[2] & 0xFFFFFFFF);
   c->pack_codebert = codebert;
+  c->last_nmask = masking ? c->h_tot[3] : -1;
   if (e & PACK_EINDEX) { c->last_npairs = -1; return set_err(LDDL_EINDEX, "IndexError in _truncate_seq (reference quirk)"); }
   if (e & PACK_EASSERT) { c->last_npairs = -1; return set_err(LDDL_EASSERT, "AssertionError: empty segment after truncation"); }
   c->last_npairs = c->h_tot[0];
@@ -457,18 +513,19 @@ static int pack_common(lddl_ctx* c, int codebert, const int32_t* d_ntok, const i
   out_totals[0] = c->last_npairs;
   out_totals[1] = c->last_ntok;
   out_totals[2] = nbins;
+  out_totals[3] = masking ? c->last_nmask : 0;
   return 0;
 }
 
-extern "C" int lddl_pack_bert(lddl_ctx* c, const int32_t* d_ntok, const int64_t* d_sent_off, int64_t n_sent,
-                              const int64_t* d_doc_sent_off, int64_t n_doc, const int64_t* d_part_doc_off,
-                              int64_t n_part, int32_t target_seq_length, double short_seq_prob,
-                              int32_t duplicate_factor, int32_t masking, double masked_lm_ratio, uint64_t seed,
-                              int32_t bin_size, int64_t* out_totals, void* stream) {
-  if (masking) return set_err(LDDL_EINVAL, "static masking: use lddl_pack_bert with masking=0 (not built yet)");
-  (void)masked_lm_ratio;
+extern "C" int lddl_pack_bert(lddl_ctx* c, const uint16_t* d_ids, const int32_t* d_ntok, const int64_t* d_sent_off,
+                              int64_t n_sent, const int64_t* d_doc_sent_off, int64_t n_doc,
+                              const int64_t* d_part_doc_off, int64_t n_part, int32_t target_seq_length,
+                              double short_seq_prob, int32_t duplicate_factor, int32_t masking,
+                              double masked_lm_ratio, uint64_t seed, int32_t bin_size, int64_t* out_totals,
+                              void* stream) {
   return pack_common(c, 0, d_ntok, d_sent_off, n_sent, d_doc_sent_off, nullptr, n_doc, d_part_doc_off, n_part,
-                     target_seq_length, short_seq_prob, duplicate_factor, seed, bin_size, out_totals, stream);
+                     target_seq_length, short_seq_prob, duplicate_factor, seed, bin_size, out_totals, stream, d_ids,
+                     masking, masked_lm_ratio);
 }
 
 extern "C" int lddl_pack_codebert(lddl_ctx* c, const int32_t* d_ntok, const int64_t* d_sent_off, int64_t n_sent,
@@ -525,5 +582,42 @@ extern "C" int lddl_materialize(lddl_ctx* c, const uint16_t* d_ids, uint16_t* d_
   }
   if (d_bin_count)
     HIP_TRY(hipMemcpyAsync(d_bin_count, P.bin_count, (size_t)P.n_part * P.nbins * 8, hipMemcpyDeviceToDevice, st));
+  c->last_tokens = d_out_tokens;
+  c->last_tok_off = d_out_tok_off;
+  return 0;
+}
+
+extern "C" int lddl_masked_lm(lddl_ctx* c, int64_t* d_out_mlm_off, uint16_t* d_out_mlm_pos, uint16_t* d_out_mlm_label,
+                              void* stream) {
+  if (!c) return set_err(LDDL_EINVAL, "null ctx");
+  if (c->last_npairs < 0 || c->last_nmask < 0 || !c->last_tokens)
+    return set_err(LDDL_EINVAL, "lddl_masked_lm needs lddl_pack_bert(masking=1) then lddl_materialize");
+  if (!d_out_mlm_off || (c->last_nmask > 0 && (!d_out_mlm_pos || !d_out_mlm_label)))
+    return set_err(LDDL_EINVAL, "null pointer");
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t st = (hipStream_t)stream;
+  const PackParams& P = c->pp;
+  if (c->last_npairs == 0) {
+    HIP_TRY(hipMemsetAsync(d_out_mlm_off, 0, 8, st));
+  } else {
+    MlmParams M{};
+    M.doc_sent_off = P.doc_sent_off;
+    M.part_doc_off = P.part_doc_off;
+    M.pair_base = (const int64_t*)c->ws[15].p;
+    M.binned = P.binned;
+    M.mref = P.mref;
+    M.mloc = P.mloc;
+    M.mask_base = (const int64_t*)c->ws[27].p;
+    M.marena = P.marena;
+    M.n_part = P.n_part;
+    M.dup = P.dup;
+    M.tokens = c->last_tokens;
+    M.tok_off = c->last_tok_off;
+    M.out_off = d_out_mlm_off;
+    M.out_pos = d_out_mlm_pos;
+    M.out_label = d_out_mlm_label;
+    HIP_TRY(launch_masked_lm(M, st));
+  }
+  c->last_nmask = -1;  // the rows are masked in place exactly once
   return 0;
 }

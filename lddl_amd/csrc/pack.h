@@ -52,6 +52,42 @@ struct PackParams {
   int64_t* bin_cursor;          // [n_part * nbins] scratch (nbins > 16)
   int32_t* part_err;            // [n_part]
   int32_t* kept;                // [n_sent + n_part] wave packer scratch
+  // static masking (create_masked_lm_predictions, pretrain.py:182-238)
+  int32_t masking;
+  double mlm_ratio;             // --masked-lm-ratio
+  uint32_t n_vocab;             // len(vocab_words); vocab_words[i] = token id i
+  uint32_t cls_id, sep_id, mask_id;
+  const uint8_t* sent_spec;     // [n_sent] sentence holds a [CLS]/[SEP] token
+  const uint16_t* ids;          // tokenizer output (sparse)
+  uint8_t* fs_spec;             // [n_sent] sent_spec per filtered slot
+  int64_t* mref;                // [dup*n_sent] per record: arena offset | #masked << 48
+  int64_t* mloc;                // [dup*n_sent] per binned position: masked entries before it
+  int64_t* part_nmask;          // [n_part]
+  uint32_t* marena;             // masked entries: position | (new id or 0xFFFF = keep) << 16
+  uint64_t mcap;                // arena capacity (entries)
+  unsigned long long* mcounter; // arena bump allocator (entries handed out)
+};
+
+constexpr int MLM_CHUNK = 1024;     // arena entries grabbed per allocation
+constexpr int MLM_MAX_SEQ = 1024;   // masking: target_seq_length limit (LDS lists)
+constexpr uint32_t MLM_KEEP = 0xFFFFu;
+
+struct MlmParams {
+  const int64_t* doc_sent_off;
+  const int64_t* part_doc_off;
+  const int64_t* pair_base;
+  const int32_t* binned;
+  const int64_t* mref;
+  const int64_t* mloc;
+  const int64_t* mask_base;     // [n_part+1] exclusive scan of part_nmask
+  const uint32_t* marena;
+  int64_t n_part;
+  int32_t dup;
+  uint16_t* tokens;             // rows written by lddl_materialize (masked in place)
+  const int64_t* tok_off;
+  int64_t* out_off;             // [n_pairs+1]
+  uint16_t* out_pos;            // [n_masked]
+  uint16_t* out_label;          // [n_masked]
 };
 
 struct MatParams {
@@ -88,5 +124,8 @@ hipError_t launch_pack_codebert(const PackParams& P, hipStream_t s);
 hipError_t launch_scan_parts(const int64_t* a, const int64_t* b, int64_t n, int64_t* sa, int64_t* sb,
                              const int32_t* err, int32_t* err_any, hipStream_t s);
 hipError_t launch_materialize(const MatParams& M, hipStream_t s);
+hipError_t launch_sent_special(const uint16_t* ids, const int64_t* sent_off, const int32_t* ntok, int64_t n_sent,
+                               uint32_t cls, uint32_t sep, uint8_t* out, hipStream_t s);
+hipError_t launch_masked_lm(const MlmParams& M, hipStream_t s);
 
 }  // namespace lddl

@@ -395,6 +395,74 @@ hipError_t launch_scan_parts(const int64_t* a, const int64_t* b, int64_t n, int6
   return hipGetLastError();
 }
 
+// ----------------------------------------------------- static masking ----
+// sentence s holds a token equal to [CLS] or [SEP] (literal special tokens in
+// the text): create_masked_lm_predictions excludes those from the candidates
+// (pretrain.py:187-190), so pairs touching such a sentence build an explicit
+// candidate list; all others use the implicit one.
+__global__ __launch_bounds__(256) void sent_special_kernel(const uint16_t* ids, const int64_t* sent_off,
+                                                           const int32_t* ntok, int64_t n_sent, uint32_t cls,
+                                                           uint32_t sep, uint8_t* out) {
+  const int64_t base = sent_off[0];
+  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n_sent; s += (int64_t)gridDim.x * blockDim.x) {
+    const uint16_t* t = ids + (sent_off[s] - base);
+    const int n = ntok[s];
+    uint32_t f = 0;
+    for (int k = 0; k < n; ++k) {
+      const uint32_t v = t[k];
+      f |= (v == cls) | (v == sep);
+    }
+    out[s] = (uint8_t)f;
+  }
+}
+
+// Row g of the materialised output: copy its masked entries (sorted by
+// position, pretrain.py:225) to the global position/label lists and apply the
+// replacement in place.  label = the row's token before replacement.
+__global__ __launch_bounds__(256) void masked_lm_kernel(MlmParams M) {
+  const int lane = threadIdx.x & 63;
+  const int64_t total = M.pair_base[M.n_part];
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); g < total; g += nw) {
+    int64_t lo = 0, hi = M.n_part;
+    while (hi - lo > 1) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (M.pair_base[mid] <= g) lo = mid; else hi = mid;
+    }
+    const int64_t p = lo;
+    const int64_t i = g - M.pair_base[p];
+    const int64_t pb = (int64_t)M.dup * M.doc_sent_off[M.part_doc_off[p]];
+    const int64_t ref = M.mref[pb + M.binned[pb + i]];
+    const int nm = (int)((uint64_t)ref >> 48);
+    const int64_t aoff = ref & ((int64_t(1) << 48) - 1);
+    const int64_t ooff = M.mask_base[p] + M.mloc[pb + i];
+    uint16_t* row = M.tokens + M.tok_off[g];
+    if (lane == 0) {
+      M.out_off[g] = ooff;
+      if (g == total - 1) M.out_off[total] = ooff + nm;
+    }
+    for (int k = lane; k < nm; k += 64) {
+      const uint32_t e = M.marena[aoff + k];
+      const uint32_t pos = e & 0xFFFFu, nid = e >> 16;
+      const uint16_t label = row[pos];
+      M.out_pos[ooff + k] = (uint16_t)pos;
+      M.out_label[ooff + k] = label;
+      if (nid != MLM_KEEP) row[pos] = (uint16_t)nid;
+    }
+  }
+}
+
+hipError_t launch_sent_special(const uint16_t* ids, const int64_t* sent_off, const int32_t* ntok, int64_t n_sent,
+                               uint32_t cls, uint32_t sep, uint8_t* out, hipStream_t s) {
+  hipLaunchKernelGGL(sent_special_kernel, dim3(4096), dim3(256), 0, s, ids, sent_off, ntok, n_sent, cls, sep, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_masked_lm(const MlmParams& M, hipStream_t s) {
+  hipLaunchKernelGGL(masked_lm_kernel, dim3(2048), dim3(256), 0, s, M);
+  return hipGetLastError();
+}
+
 hipError_t launch_materialize(const MatParams& M, hipStream_t s) {
   hipLaunchKernelGGL(materialize_kernel, dim3(2048), dim3(256), 0, s, M);
   return hipGetLastError();

@@ -21,6 +21,8 @@
 #include "common.h"
 #include "pack.h"
 
+#include <type_traits>
+
 namespace lddl {
 
 constexpr int PW_LENS = 4096;   // filtered sentences resident in LDS
@@ -37,6 +39,16 @@ struct PackWaveLds {
   uint16_t ntk[PW_PAIRS];       // num_tokens per pair record
   int32_t red[64];
 };
+
+// static masking lists (MASK instantiation only)
+struct MaskLds {
+  uint16_t cand[MLM_MAX_SEQ];   // explicit candidate positions (pairs with [CLS]/[SEP] tokens)
+  uint16_t jb[MLM_MAX_SEQ];     // shuffle draws: swap x[i] <-> x[jb[i]]
+  uint16_t mpos[MLM_MAX_SEQ];   // picked positions in pick order
+  uint16_t mid[MLM_MAX_SEQ];    // their replacement ids (MLM_KEEP = unchanged)
+  uint32_t spec[PW_LENS / 32];  // filtered slot holds a [CLS]/[SEP] token
+};
+struct NoMaskLds {};
 
 __device__ __forceinline__ void wsync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -63,9 +75,11 @@ __device__ __forceinline__ int wsum(int v) {
 struct WaveRng {
   PackWaveLds& L;
   int lane;
-  int idx;  // wave-uniform
+  int idx;            // wave-uniform
+  int wbase = -1024;  // tw[wbase + lane] is held in `win` (one LDS read per 64 draws)
+  uint32_t win = 0;
 
-  __device__ void seed(uint64_t n) {
+  __device__ __forceinline__ void seed(uint64_t n) {
     if (lane == 0) {
       uint32_t* mt = L.mt;
       uint32_t key[2] = {(uint32_t)n, (uint32_t)(n >> 32)};
@@ -99,7 +113,7 @@ struct WaveRng {
   }
 
   // twist + temper on all lanes
-  __device__ void refill() {
+  __device__ __forceinline__ void refill() {
     uint32_t* mt = L.mt;
     for (int c = 0; c < MT_N; c += 64) {
       const int i = c + lane;
@@ -117,11 +131,19 @@ struct WaveRng {
     for (int i = lane; i < MT_N; i += 64) L.tw[i] = temper(mt[i]);
     wsync();
     idx = 0;
+    wbase = -1024;
   }
 
   __device__ __forceinline__ uint32_t next() {
     if (idx >= MT_N) refill();
-    return L.tw[idx++];
+    int o = idx - wbase;
+    if (o < 0 || o >= 64) {
+      wbase = idx;
+      win = L.tw[idx + lane < MT_N ? idx + lane : MT_N - 1];
+      o = 0;
+    }
+    ++idx;
+    return (uint32_t)__builtin_amdgcn_readlane((int)win, o);
   }
   __device__ __forceinline__ double random() {
     const uint32_t a = next() >> 5, b = next() >> 6;
@@ -173,8 +195,10 @@ __device__ __forceinline__ int range_sum(const GET& len_at, int k0, int k1, int 
   return wsum(s);
 }
 
+template <bool MASK>
 __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
   __shared__ PackWaveLds L;
+  __shared__ typename std::conditional<MASK, MaskLds, NoMaskLds>::type ML;
   const int lane = threadIdx.x;
   const int64_t p = blockIdx.x;
   if (p >= P.n_part) return;
@@ -201,6 +225,7 @@ __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
         if (keep) {
           P.fs_ntok[s0 + slot] = n;
           P.fs_base[s0 + slot] = P.sent_off[s0 + kk] - base;
+          if (MASK) P.fs_spec[s0 + slot] = P.sent_spec[s0 + kk];
         }
       }
       run += __shfl(incl, 63);
@@ -241,6 +266,12 @@ __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
       L.dfirst[k] = (uint16_t)(P.fd_first[d0 + k] - s0);
       L.dn[k] = (uint16_t)P.fd_n[d0 + k];
     }
+    if constexpr (MASK) {
+      for (int k = 0; k < nfs; k += 64) {
+        const uint64_t m = __ballot(k + lane < nfs && P.fs_spec[s0 + k + lane] != 0);
+        if (lane == 0) { ML.spec[k >> 5] = (uint32_t)m; if ((k >> 5) + 1 < PW_LENS / 32) ML.spec[(k >> 5) + 1] = (uint32_t)(m >> 32); }
+      }
+    }
   }
   wsync();
   // slot-relative accessors
@@ -255,6 +286,22 @@ __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
   int np = 0;
   int err = PACK_OK;
   const int pcap = PW_PAIRS;
+  int64_t mcur = 0, mend = 0;  // this partition's current arena chunk
+  int nmask_part = 0;
+  (void)mcur; (void)mend; (void)nmask_part;
+  // any filtered slot in [k0, k0 + n) holding a [CLS]/[SEP] token
+  auto any_spec = [&](int k0, int n) -> bool {
+    bool f = false;
+    if constexpr (MASK) {
+      for (int k = 0; k < n; k += 64) {
+        const int kk = k0 + k + lane;
+        bool x = false;
+        if (k + lane < n) x = lres ? ((ML.spec[kk >> 5] >> (kk & 31)) & 1u) != 0 : P.fs_spec[s0 + kk] != 0;
+        if (__ballot(x)) { f = true; break; }
+      }
+    }
+    return f;
+  };
   for (int dup = 0; dup < P.dup && !err; ++dup) {
     for (int di = 0; di < nd && !err; ++di) {
       const int first = doc_first(di), len = doc_n(di);
@@ -332,9 +379,91 @@ __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
         r.lo1 = (uint16_t)blo; r.hi1 = (uint16_t)bhi;
         r.flags = (uint16_t)((rn ? 1 : 0) | 2);
         r.num_tokens = (uint16_t)((ahi - alo) + (bhi - blo) + 3);
+        int64_t mref = 0;
+        if constexpr (MASK) {
+          // ---- create_masked_lm_predictions (pretrain.py:182-238) ----------
+          const int la2 = ahi - alo, lb2 = bhi - blo;
+          const int ntp = max(1, (int)rint((double)(la2 + lb2 + 3) * P.mlm_ratio));
+          const int fa = first + cs, fb = (int)(r.fs1 - s0);
+          const bool expl = any_spec(fa, a_end) || any_spec(fb, r.n1);
+          int m = la2 + lb2;
+          if (expl) {  // candidates = positions whose token is not [CLS]/[SEP]
+            m = 0;
+            auto seg = [&](int fs, int ns, int lo, int hi, int pos0) {
+              int acc = 0;
+              for (int q = 0; q < ns && acc < hi; ++q) {
+                const int ln = len_at(fs + q);
+                const int64_t sb = P.fs_base[s0 + fs + q];
+                const int a0 = max(lo, acc), a1 = min(hi, acc + ln);
+                for (int t = a0; t < a1; t += 64) {
+                  const int tt = t + lane;
+                  bool keep = false;
+                  if (tt < a1) {
+                    const uint32_t v = P.ids[sb + (tt - acc)];
+                    keep = v != P.cls_id && v != P.sep_id;
+                  }
+                  const uint64_t bm = __ballot(keep);
+                  if (keep) ML.cand[m + __popcll(bm & ((1ull << lane) - 1ull))] = (uint16_t)(pos0 + tt - lo);
+                  m += __popcll(bm);
+                }
+                acc += ln;
+              }
+            };
+            seg(fa, a_end, alo, ahi, 1);
+            seg(fb, r.n1, blo, bhi, 2 + la2);
+          }
+          // random.shuffle(cand_indexes): record the swaps, then undo them
+          // per picked slot (lane per pick) instead of permuting the list
+          for (int q = m - 1; q >= 1; --q) {
+            const uint32_t j = rng.randbelow((uint32_t)(q + 1));
+            if (lane == 0) ML.jb[q] = (uint16_t)j;
+          }
+          wsync();
+          const int nm = min(ntp, m);
+          for (int pb0 = 0; pb0 < nm; pb0 += 64) {
+            const int pk = pb0 + lane;
+            if (pk < nm) {
+              int q = pk;
+              for (int i2 = 1; i2 < m; ++i2) {
+                const int j = ML.jb[i2];
+                q = q == i2 ? j : (q == j ? i2 : q);
+              }
+              ML.mpos[pk] = (uint16_t)(expl ? (int)ML.cand[q] : (q < la2 ? 1 + q : 2 + q));
+            }
+          }
+          // 80% [MASK], 10% keep, 10% random word, in pick order
+          for (int pk = 0; pk < nm; ++pk) {
+            uint32_t nid;
+            if (rng.random() < 0.8) nid = P.mask_id;
+            else if (rng.random() < 0.5) nid = MLM_KEEP;
+            else nid = rng.randbelow(P.n_vocab);
+            if (lane == 0) ML.mid[pk] = (uint16_t)nid;
+          }
+          wsync();
+          if (mcur + nm > mend) {
+            unsigned long long b0 = 0;
+            if (lane == 0) b0 = atomicAdd(P.mcounter, (unsigned long long)MLM_CHUNK);
+            mcur = (int64_t)__shfl((long long)b0, 0);
+            mend = mcur + MLM_CHUNK;
+          }
+          const bool fits = (uint64_t)mend <= P.mcap;
+          for (int pb0 = 0; pb0 < nm; pb0 += 64) {
+            const int pk = pb0 + lane;
+            if (pk < nm && fits) {
+              const uint32_t pos = ML.mpos[pk];
+              int rank = 0;
+              for (int k2 = 0; k2 < nm; ++k2) rank += ML.mpos[k2] < pos;
+              P.marena[mcur + rank] = pos | ((uint32_t)ML.mid[pk] << 16);
+            }
+          }
+          mref = mcur | ((int64_t)nm << 48);
+          mcur += nm;
+          wsync();
+        }
         if (lane == 0) {
           out[np] = r;
           if (np < pcap) L.ntk[np] = r.num_tokens;
+          if (MASK) P.mref[pb + np] = mref;
         }
         ++np;
         i = i_next;
@@ -343,7 +472,7 @@ __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
   }
   if (lane == 0) P.part_err[p] = err;
   if (err) {
-    if (lane == 0) { P.part_npairs[p] = 0; P.part_ntok[p] = 0; }
+    if (lane == 0) { P.part_npairs[p] = 0; P.part_ntok[p] = 0; if (MASK) P.part_nmask[p] = 0; }
     return;
   }
   wsync();
@@ -373,7 +502,7 @@ __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
   int32_t* binned = P.binned + pb;
   int64_t* tl = P.tok_local + pb;
   int pos = 0;
-  int64_t acc = 0;
+  int64_t acc = 0, macc = 0;
   for (int b = 0; b < nb; ++b) {
     int cnt = 0;
     for (int k = 0; k < np; k += 64) {
@@ -394,6 +523,12 @@ __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
         binned[pos + before] = rec;
         tl[pos + before] = acc + tinc - nt;
       }
+      if constexpr (MASK) {
+        const int nmk = in ? (int)((uint64_t)P.mref[pb + rec] >> 48) : 0;
+        const int minc = wscan_incl(nmk, lane);
+        if (in) P.mloc[pb + pos + before] = macc + minc - nmk;
+        macc += __shfl(minc, 63);
+      }
       pos += __popcll(m);
       cnt += __popcll(m);
       acc += __shfl(tinc, 63);
@@ -403,11 +538,15 @@ __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
   if (lane == 0) {
     P.part_npairs[p] = np;
     P.part_ntok[p] = acc;
+    if (MASK) P.part_nmask[p] = macc;
   }
 }
 
 hipError_t launch_pack_bert_wave(const PackParams& P, hipStream_t s) {
-  hipLaunchKernelGGL(pack_bert_wave_kernel, dim3((unsigned)P.n_part), dim3(64), 0, s, P);
+  if (P.masking)
+    hipLaunchKernelGGL(pack_bert_wave_kernel<true>, dim3((unsigned)P.n_part), dim3(64), 0, s, P);
+  else
+    hipLaunchKernelGGL(pack_bert_wave_kernel<false>, dim3((unsigned)P.n_part), dim3(64), 0, s, P);
   return hipGetLastError();
 }
 

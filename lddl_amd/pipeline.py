@@ -97,6 +97,10 @@ class PackResult:
   bin_count: torch.Tensor  # int64 [n_part, nbins]
   ids: torch.Tensor = None
   ntok: torch.Tensor = None
+  n_masked: int = 0
+  mlm_off: torch.Tensor = None    # int64 [n_pairs + 1] (masking only)
+  mlm_pos: torch.Tensor = None    # int16 view of uint16 positions (row coordinates)
+  mlm_label: torch.Tensor = None  # int16 view of uint16 label ids
   ntok_host: np.ndarray = None
   part_doc_off: np.ndarray = None
 
@@ -109,13 +113,20 @@ class PackResult:
     fl = self.flags[:self.n_pairs].cpu().numpy()
     bn = self.bins[:self.n_pairs].cpu().numpy()
     pt = self.part[:self.n_pairs].cpu().numpy()
+    if self.mlm_off is not None:
+      moff = self.mlm_off[:self.n_pairs + 1].cpu().numpy()
+      mpos = self.mlm_pos[:self.n_masked].cpu().numpy().view(np.uint16).astype(np.int64)
+      mlab = self.mlm_label[:self.n_masked].cpu().numpy().view(np.uint16).astype(np.int64)
     out = []
     for g in range(self.n_pairs):
       r = tok[off[g]:off[g + 1]]
       sep0 = bool(fl[g] & 2)
       a = r[1:1 + l0[g]]
       b = r[1 + l0[g] + (1 if sep0 else 0):1 + l0[g] + (1 if sep0 else 0) + l1[g]]
-      out.append((int(pt[g]), a.tolist(), b.tolist(), int(fl[g]), int(bn[g]), r.tolist()))
+      row = (int(pt[g]), a.tolist(), b.tolist(), int(fl[g]), int(bn[g]), r.tolist())
+      if self.mlm_off is not None:
+        row += (mpos[moff[g]:moff[g + 1]].tolist(), mlab[moff[g]:moff[g + 1]].tolist())
+      out.append(row)
     return out
 
 
@@ -152,7 +163,8 @@ class Packer:
                                 _ptr(shards.part_doc_off), shards.n_part, target_seq_length, short_seq_prob,
                                 duplicate_factor, abs(int(seed)), bin_size or 0, tot, s)
     else:
-      rc = L.lddl_pack_bert(self.tok.handle, _ptr(ntok), _ptr(shards.sent_off), shards.n_sent,
+      rc = L.lddl_pack_bert(self.tok.handle, _ptr(ids) if masking else None, _ptr(ntok), _ptr(shards.sent_off),
+                            shards.n_sent,
                             _ptr(shards.doc_sent_off), shards.n_doc, _ptr(shards.part_doc_off), shards.n_part,
                             target_seq_length, short_seq_prob, duplicate_factor, 1 if masking else 0,
                             masked_lm_ratio, abs(int(seed)), bin_size or 0, tot, s)
@@ -173,6 +185,12 @@ class Packer:
                                   _ptr(res.part), _ptr(res.bin_count), s))
     res.bin_count = res.bin_count[:shards.n_part * nbins].view(shards.n_part, nbins)
     res.ids, res.ntok = ids, ntok
+    if masking and not codebert:
+      res.n_masked = int(tot[3])
+      res.mlm_off = self._buf('mlm_off', n_pairs + 1, torch.int64)
+      res.mlm_pos = self._buf('mlm_pos', res.n_masked, torch.int16)
+      res.mlm_label = self._buf('mlm_label', res.n_masked, torch.int16)
+      _lib.check(L.lddl_masked_lm(self.tok.handle, _ptr(res.mlm_off), _ptr(res.mlm_pos), _ptr(res.mlm_label), s))
     return res
 
   def run(self, shards, **kw):
@@ -182,14 +200,15 @@ class Packer:
 
 def run_bert(corpus, vocab_file=VOCAB_BERT, target_seq_length=128, bin_size=None, n_partitions=1, seed=12345,
              device=None, check_host=False, duplicate_factor=5, short_seq_prob=0.1, part_doc_off=None,
-             codebert=False):
+             codebert=False, masking=False, masked_lm_ratio=0.15):
   device = device or torch.device('cuda', 0)
   if part_doc_off is None:
     part_doc_off = partition_by_bytes(corpus, n_partitions)
   pk = Packer(vocab_file, device.index)
   sh = upload(corpus, part_doc_off, device)
   res = pk.run(sh, target_seq_length=target_seq_length, short_seq_prob=short_seq_prob,
-               duplicate_factor=duplicate_factor, seed=seed, bin_size=bin_size, codebert=codebert)
+               duplicate_factor=duplicate_factor, seed=seed, bin_size=bin_size, codebert=codebert,
+               masking=masking, masked_lm_ratio=masked_lm_ratio)
   torch.cuda.synchronize(device)
   res.part_doc_off = np.asarray(part_doc_off)
   if check_host:
@@ -203,8 +222,12 @@ def assert_same_pairs(res, expected):
   rows = res.rows()
   flat = [(p, r) for p, part in enumerate(expected) for r in part]
   assert len(rows) == len(flat), (len(rows), len(flat))
-  for g, ((pp, a, b, fl, bn, tok), (p, (ea, eb, ern, en))) in enumerate(zip(rows, flat)):
+  for g, (row, (p, e)) in enumerate(zip(rows, flat)):
+    pp, a, b, fl, bn, tok = row[:6]
+    ea, eb, ern, en = e[:4]
     assert pp == p, ('partition', g, pp, p)
     assert a == list(ea) and b == list(eb), ('tokens', g)
     assert bool(fl & 1) == bool(ern), ('is_random_next', g)
     assert len(tok) == en, ('num_tokens', g)
+    if len(e) > 4:  # masking: positions and labels
+      assert row[6] == list(e[4]) and row[7] == list(e[5]), ('masked_lm', g)

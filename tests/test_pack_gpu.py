@@ -155,3 +155,87 @@ def test_many_partitions_and_empty_partitions(packer):
     order, _ = po.binned_order([len(a) + len(b) + 3 for a, b, _ in rr], 16, 4)
     exp += [(p,) + rr[i] for i in order]
   assert [(r[0], r[1], r[2], bool(r[3] & 1)) for r in rows] == [(p, a, b, rn) for p, a, b, rn in exp]
+
+
+# ---------------------------------------------------------------- masking --
+MASK = (0.15, 30522, 101, 102, 103)  # ratio, |vocab|, [CLS], [SEP], [MASK] of bert-base-uncased
+
+
+@pytest.mark.parametrize('k', [i for i, c in enumerate(BERT['cases']) if c['cfg']['masking']])
+@pytest.mark.parametrize('binned', [False, True])
+def test_bert_masked_golden(packer, k, binned):
+  """--masking rows against the reference's create_masked_lm_predictions."""
+  case = BERT['cases'][k]
+  c = case['cfg']
+  sh, ids, ntok = shards_from_docs(case['docs'])
+  kw = dict(target_seq_length=c['max_seq'], short_seq_prob=c['ssp'], duplicate_factor=c['dup'],
+            seed=case['seed'], bin_size=case['bin_size'] if binned else None, masking=True)
+  if case['error']:
+    with pytest.raises(AssertionError):
+      packer.pack(sh, ids, ntok, **kw)
+    return
+  res = packer.pack(sh, ids, ntok, **kw)
+  rows = res.rows()
+  exp = case['rows']
+  if binned:
+    order, _ = po.binned_order([r['num_tokens'] for r in exp], case['bin_size'], case['nbins'])
+    exp = [exp[i] for i in order]
+  assert len(rows) == len(exp)
+  assert res.n_masked == sum(len(e['masked_lm_positions']) for e in exp)
+  for (p, a, b, fl, bn, tok, pos, lab), e in zip(rows, exp):
+    assert (a, b, bool(fl & 1), len(tok)) == (e['A'], e['B'], e['is_random_next'], e['num_tokens'])
+    assert pos == e['masked_lm_positions'] and lab == e['masked_lm_labels']
+    # serialize_np_array(np.asarray(positions, np.uint16)) bytes
+    assert np.asarray(pos, dtype=np.uint16).tobytes().hex() in e['masked_lm_positions_npy']
+
+
+@pytest.mark.parametrize('seq,bin_size,nparts', [(128, 32, 5), (512, 64, 2)])
+def test_bert_masked_end_to_end_vs_oracle(gpu, seq, bin_size, nparts):
+  from lddl_amd import synth, pipeline
+  c = synth.make_wiki(500_000, seed=seq + 3 * nparts)
+  res = pipeline.run_bert(c, target_seq_length=seq, bin_size=bin_size, n_partitions=nparts, seed=4242,
+                          check_host=True, masking=True)
+  oids, ontok = OracleTokenizer(pipeline.VOCAB_BERT).run(c.data, c.sent_off, 512, nthreads=8)
+  assert np.array_equal(res.ntok_host, ontok)
+  exp = po.run_bert_shards(c, oids, ontok, res.part_doc_off, seq, 0.1, 5, 4242, bin_size, masking=MASK)
+  pipeline.assert_same_pairs(res, exp)
+  # statistical sanity of the 80/10/10 split over the whole run
+  rows = res.rows()
+  n = sum(len(r[6]) for r in rows)
+  n_mask = sum(1 for r in rows for q in r[6] if r[5][q] == 103)
+  assert 0.75 < n_mask / n < 0.85
+
+
+def test_bert_masked_special_tokens_and_arena_regrow(gpu, monkeypatch):
+  """Sentences holding literal [CLS]/[SEP] tokens take the explicit candidate
+  list (pretrain.py:187-190); a tiny initial arena forces the regrow path."""
+  from lddl_amd.pipeline import Packer, VOCAB_BERT
+  monkeypatch.setenv('LDDL_MLM_CAP', '1000')
+  pk = Packer(VOCAB_BERT, 0)
+  rng = np.random.default_rng(3)
+  docs = []
+  for d in range(60):
+    doc = []
+    for s in range(int(rng.integers(1, 9))):
+      n = int(rng.integers(1, 40))
+      sent = [int(x) for x in rng.integers(999, 30000, n)]
+      for _ in range(int(rng.integers(0, 3))):
+        sent[int(rng.integers(0, n))] = int(rng.choice([101, 102, 103]))
+      doc.append(sent)
+    docs.append(doc)
+  pdo = [0, 20, 41, 60]
+  sh, ids, ntok = shards_from_docs(docs, part_doc_off=pdo)
+  res = pk.pack(sh, ids, ntok, target_seq_length=64, duplicate_factor=3, seed=11, bin_size=16, masking=True)
+  exp = []
+  for p in range(len(pdo) - 1):
+    D = docs[pdo[p]:pdo[p + 1]]
+    prs = po.partition_pairs(D, 11 + p, lambda X, di, r: po.bert_pairs(X, di, 64, 0.1, r, MASK), 3)
+    rr = []
+    for pr in prs:
+      a, b, rn = po.pair_tokens(D, pr)
+      ma, mb, pos, lab = pr[5]
+      rr.append((ma, mb, rn, len(a) + len(b) + 3, pos, lab))
+    order, _ = po.binned_order([r[3] for r in rr], 16, 4)
+    exp.append([rr[i] for i in order])
+  from lddl_amd.pipeline import assert_same_pairs
+  assert_same_pairs(res, exp)
