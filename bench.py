@@ -213,7 +213,7 @@ def main():
                  'pairs_per_gpu': res.n_pairs, 'packed_tokens_per_gpu': res.n_tokens,
                  'masked_positions_per_gpu': res.n_masked,
                  'parallelism': 'shard%d' % world},
-      'roofline': {'bound': 'hbm', 'kernel': 'lddl::tokenize_tile_kernel', 'achieved': achieved, 'peak': HBM_PEAK_GBS,
+      'roofline': {'bound': 'hbm', 'kernel': os.environ.get('LDDL_BENCH_KERNEL', 'lddl::tok4::tok4_kernel'), 'achieved': achieved, 'peak': HBM_PEAK_GBS,
                    'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS, 'traffic': None,
                    'algorithmic_bytes_per_launch': alg, 'avg_launch_ms': tk},
       'tokenize_ms': tk, 'gen_s': gen_s,

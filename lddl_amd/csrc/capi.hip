@@ -53,6 +53,11 @@ struct lddl_ctx {
   uint8_t* d_pool = nullptr;
   uint32_t* d_voff = nullptr;
   uint32_t maxb[2] = {0, 0};
+  uint4* d_vt = nullptr;         // v4 bucketed vocab table
+  uint32_t vt_mask = 0;
+  uint32_t* d_vbloom = nullptr;  // its Bloom filter
+  bool tok4_ok = false;          // the ASCII page fits tokenize_stream's class table
+  int tok4_cfg = 0;
   // pack workspace (grown on demand)
   struct Buf {
     void* p = nullptr;
@@ -103,6 +108,8 @@ static void free_ctx(lddl_ctx* c) {
   (void)hipFree(c->d_bloom);
   (void)hipFree(c->d_pool);
   (void)hipFree(c->d_voff);
+  (void)hipFree(c->d_vt);
+  (void)hipFree(c->d_vbloom);
   (void)hipFree(c->d_ovf);
   (void)hipFree(c->d_counter);
   for (auto& b : c->ws) (void)hipFree(b.p);
@@ -149,6 +156,18 @@ static int load_table(lddl_ctx* c, const char* path) {
       if (ent_cls(multi[i * 4 + 1 + k]) != CLS_OTHER)
         return set_err(LDDL_EFORMAT, "unicode table multi entry %zu has a non-word char", i);
   }
+  // tokenize_stream derives its per-byte class table from the ASCII page: it
+  // needs rank-0, single-char entries whose only mapping is A-Z -> a-z
+  c->tok4_ok = true;
+  for (uint32_t b = 0; b < 128; ++b) {
+    const uint32_t e = pages[(size_t)top[0] * 256 + b];
+    const uint32_t kind = ent_kind(e), cls = ent_cls(e);
+    if (ent_rank(e) != 0 || kind == KIND_MULTI) c->tok4_ok = false;
+    if (kind == KIND_MAP && cls == CLS_ISOLATE) c->tok4_ok = false;
+    if (kind == KIND_MAP && cls == CLS_OTHER && !(b >= 'A' && b <= 'Z' && ent_payload(e) == b + 32))
+      c->tok4_ok = false;
+  }
+  if (ent_cls(pages[(size_t)top[0] * 256 + '[']) != CLS_ISOLATE) c->tok4_ok = false;
   int rc;
   if ((rc = upload(&c->d_top, top.data(), top.size() * 2))) return rc;
   if ((rc = upload(&c->d_pages, pages.data(), pages.size() * 4))) return rc;
@@ -235,6 +254,39 @@ static int load_vocab(lddl_ctx* c, const char* path) {
     bloom[(uint32_t)(key >> 40) & (BLOOM_WORDS - 1)] |= (1u << (key & 31)) | (1u << ((key >> 5) & 31));
   }
   if ((rc0 = upload(&c->d_bloom, bloom.data(), bloom.size() * 4))) return rc0;
+  // v4 table: >= V buckets of two 32-B slots (load <= 1/2), linear probing
+  // over buckets; Bloom filter over the same hashes (common.h vhash)
+  {
+    uint32_t nbk = 1;
+    while (nbk < V) nbk <<= 1;
+    std::vector<uint32_t> vt((size_t)nbk * 16, 0u);
+    std::vector<uint32_t> vbl(BLOOM_WORDS, 0u);
+    for (size_t i = 0; i < V; ++i) {
+      if (vlen[i] == 0) continue;
+      uint32_t d[VKEY_DW] = {0, 0, 0, 0, 0, 0};
+      memcpy(d, &pool[voff[i]], vlen[i] < 24 ? vlen[i] : 24);
+      const uint32_t h = vhash(d, vlen[i], vcont[i]);
+      vbl[vbloom_word(h)] |= vbloom_bits(h);
+      bool done = false;
+      for (uint32_t b = h & (nbk - 1); !done; b = (b + 1) & (nbk - 1)) {
+        for (int sl = 0; sl < 2 && !done; ++sl) {
+          uint32_t* s = &vt[((size_t)b * 2 + sl) * 8];
+          if (s[6] != 0) {
+            const uint32_t j = s[6] & 0xFFFFu;
+            if (!(vlen[j] == vlen[i] && vcont[j] == vcont[i] && memcmp(&pool[voff[j]], &pool[voff[i]], vlen[i]) == 0))
+              continue;  // occupied by another key
+          }
+          memcpy(s, d, sizeof d);  // empty slot, or a duplicate line: last id wins
+          s[6] = slot_info((uint32_t)i, vlen[i], vcont[i]);
+          s[7] = voff[i];
+          done = true;
+        }
+      }
+    }
+    c->vt_mask = nbk - 1;
+    if ((rc0 = upload(&c->d_vt, vt.data(), vt.size() * 4))) return rc0;
+    if ((rc0 = upload(&c->d_vbloom, vbl.data(), vbl.size() * 4))) return rc0;
+  }
   int rc;
   if ((rc = upload(&c->d_slots, slots.data(), slots.size() * sizeof(uint4)))) return rc;
   if ((rc = upload(&c->d_pool, pool.data(), pool.size()))) return rc;
@@ -257,7 +309,10 @@ extern "C" int lddl_create(const char* vocab_path, const char* table_path, int d
   c->n_cu = prop.multiProcessorCount;
   if ((rc = load_table(c, table_path)) || (rc = load_vocab(c, vocab_path))) { free_ctx(c); return rc; }
   const char* algo = getenv("LDDL_TOKENIZE_ALGO");
-  c->tok_algo = (algo && algo[0] >= '1' && algo[0] <= '3') ? algo[0] - '0' : 3;
+  c->tok_algo = (algo && algo[0] >= '1' && algo[0] <= '4') ? algo[0] - '0' : 4;
+  if (c->tok_algo == 4 && !c->tok4_ok) c->tok_algo = 3;
+  const char* cfg = getenv("LDDL_TOK4_CFG");  // waves per workgroup / Bloom (tokenize.h)
+  c->tok4_cfg = cfg ? atoi(cfg) : 0;
   const char* tchunk = getenv("LDDL_TILE_CHUNK");  // tiles per launch (tests force several launches)
   c->tile_chunk = tchunk ? atoll(tchunk) : 0;
   const char* mcap = getenv("LDDL_MLM_CAP");  // initial masking arena (tests force the regrow path)
@@ -332,6 +387,9 @@ extern "C" int lddl_tokenize(lddl_ctx* c, const uint8_t* d_bytes, int64_t nbytes
   P.maxb[1] = c->maxb[1];
   for (int k = 0; k < 5; ++k) P.special[k] = c->special[k];
   P.unk = c->special[1];
+  P.vt = c->d_vt;
+  P.vt_mask = c->vt_mask;
+  P.vbloom = c->d_vbloom;
   P.ovf = c->d_ovf;
   P.work_counter = c->d_counter;
   HIP_TRY(hipMemsetAsync(c->d_counter, 0, 64, st));
@@ -345,7 +403,28 @@ extern "C" int lddl_tokenize(lddl_ctx* c, const uint8_t* d_bytes, int64_t nbytes
     P.dbg = d_dbg;
   }
   const int64_t chunks = (n_sent + P.chunk - 1) / P.chunk;
-  if (c->tok_algo == 3) {
+  if (c->tok_algo == 4) {
+    const int64_t nt = tile_count(nbytes);
+    int64_t* tile_sent;
+    int32_t *fb_list, *fb_count;
+    int rc;
+    if ((rc = ws_get(c, 19, nt + 1, &tile_sent)) || (rc = ws_get(c, 20, nt, &fb_list)) ||
+        (rc = ws_get(c, 21, 16, &fb_count)))
+      return rc;
+    HIP_TRY(launch_tokenize_stream(P, nbytes, tile_sent, fb_list, fb_count, c->tok_grid, c->n_cu, c->tok4_cfg, st));
+    if (P.dbg) {
+      uint64_t h[16];
+      int32_t nfb = 0;
+      HIP_TRY(hipMemcpyAsync(h, P.dbg, sizeof h, hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipMemcpyAsync(&nfb, fb_count, 4, hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipStreamSynchronize(st));
+      const char* nm[12] = {"bytes", "exceptions", "units", "prep", "wordpiece", "output",
+                            "probes", "bloom_rejects", "nunits", "wp_iters", "tiles", "fallback"};
+      fprintf(stderr, "[lddl tok4 dbg] cfg=%d ntiles=%lld fallback_list=%d", c->tok4_cfg, (long long)nt, nfb);
+      for (int k = 0; k < 12; ++k) fprintf(stderr, " %s=%llu", nm[k], (unsigned long long)h[k]);
+      fprintf(stderr, "\n");
+    }
+  } else if (c->tok_algo == 3) {
     const int64_t nt = tile_count(nbytes);
     int64_t* tile_sent;
     int32_t *fb_list, *fb_count;

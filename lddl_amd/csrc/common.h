@@ -52,6 +52,34 @@ LDDL_HD uint32_t slot_info(uint32_t id, uint32_t len, uint32_t cont) {
   return id | (len << 16) | (cont << 24) | 0x80000000u;
 }
 
+// ---- v4 vocab table (tokenize_stream.hip) -----------------------------------
+// A candidate piece is hashed from its first 24 bytes held as six
+// little-endian dwords (bytes >= len zero), its byte length and the "##"
+// flag.  The table is an array of 64-byte buckets of two 32-byte slots
+// {key dwords 0..5, info, pool offset} probed linearly bucket by bucket, so
+// one probe is one cache line and a key of <= 24 bytes verifies from the
+// slot alone.  info uses slot_info()'s layout; info == 0 marks an empty slot.
+constexpr int VKEY_DW = 6;
+LDDL_HD uint32_t vhash(const uint32_t* d, uint32_t len, uint32_t cont) {
+  uint32_t h = 0x9E3779B9u * (len + 1u) + (cont ? 0x7F4A7C15u : 0u);
+  for (int k = 0; k < VKEY_DW; ++k) {
+    h ^= d[k];
+    h = ((h << 5) | (h >> 27)) * 0x85EBCA77u;
+  }
+  h ^= h >> 15;
+  h *= 0x2C1B3C6Du;
+  h ^= h >> 12;
+  h *= 0x297A2D39u;
+  h ^= h >> 15;
+  return h;
+}
+// blocked Bloom filter over the same keys (BLOOM_WORDS dwords, 2 bits/key)
+LDDL_HD uint32_t vbloom_word(uint32_t h) { return (h * 0x9E3779B1u) >> 19; }  // 13 bits
+LDDL_HD uint32_t vbloom_bits(uint32_t h) {
+  const uint32_t g = h * 0x85EBCA77u;
+  return (1u << (g & 31u)) | (1u << ((g >> 5) & 31u));
+}
+
 // ---- MT19937 (CPython random) ----------------------------------------------
 constexpr int MT_N = 624;
 constexpr int MT_M = 397;

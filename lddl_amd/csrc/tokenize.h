@@ -30,6 +30,10 @@ struct TokParams {
   uint32_t maxb[2];
   uint32_t special[5];
   uint32_t unk;
+  // v4 vocab table (common.h vhash): 64-B buckets of two 32-B slots + Bloom
+  const uint4* vt;
+  uint32_t vt_mask;  // #buckets - 1
+  const uint32_t* vbloom;
   // scratch
   uint8_t* ovf;
   uint32_t* work_counter;
@@ -44,5 +48,13 @@ const void* tokenize_wave_kernel_ptr();
 int64_t tile_count(int64_t nbytes);
 hipError_t launch_tokenize_tiles(const TokParams& P, int64_t nbytes, int64_t* tile_sent, int32_t* fb_list,
                                  int32_t* fb_count, int fb_grid, int64_t chunk, hipStream_t s);
+hipError_t launch_tile_bounds(const int64_t* sent_off, int64_t n_sent, int64_t n_tiles, int64_t* tile_sent,
+                              hipStream_t s);
+hipError_t launch_tokenize_fallback(const TokParams& P, const int64_t* tile_sent, const int32_t* fb_list,
+                                    const int32_t* fb_count, int grid, hipStream_t s);
+// v4 (tokenize_stream.hip): wave per 1 KiB tile, persistent; cfg selects
+// waves per workgroup / Bloom filter (0: 4+Bloom, 1: 4, 2: 12+Bloom, 3: 8+Bloom)
+hipError_t launch_tokenize_stream(const TokParams& P, int64_t nbytes, int64_t* tile_sent, int32_t* fb_list,
+                                  int32_t* fb_count, int fb_grid, int n_cu, int cfg, hipStream_t s);
 
 }  // namespace lddl

@@ -1,0 +1,712 @@
+// Tokenizer v4 (default): one WAVE per sentence-aligned tile, every wave
+// independent (no workgroup barrier after the prologue), persistent grid.
+//
+// Same contract and results as tokenize_tile.hip / tokenize.hip (reference:
+// HF tokenizers' BertNormalizer / BertPreTokenizer / WordPiece behind
+// tokenizer.tokenize(s, max_length=512, truncation=True),
+// lddl/dask/bert/pretrain.py:79-80; restated in oracle/tokenizer_oracle.c).
+//
+// Tile t = the sentences whose first byte lies in [t*1KiB, (t+1)*1KiB)
+// (tile_bounds_kernel).  A wave owns a tile; its window is the 16-byte
+// aligned span of those sentences, <= 2 KiB, 32 bytes per lane.
+//
+//  1 bytes    two 16-B loads per lane, raw copy in LDS.  A 256-entry class
+//             table gives per-lane bit masks (word char, isolate, space, char
+//             start, dirty, exception) and the normalised bytes IN PLACE
+//             (ASCII lower-cased, dropped chars -> 0xFF filler).  Exceptions
+//             (non-ASCII lead bytes, '[') run a short loop: literal specials on
+//             the raw text, the per-code-point table for non-ASCII chars; an
+//             output longer than its input leaves an expansion marker
+//             (0xFD, index) resolved in step 3.
+//  2 units    unit starts = isolate chars, specials, and word chars not
+//             preceded by a word char (fillers count as word chars, so dropped
+//             chars are transparent, and every sentence start breaks); one wave
+//             scan -> unit list (position, sentence).
+//  3 prep     span of each unit (next break bit); dirty spans compacted /
+//             expanded into a side buffer; specials and >100-char words done.
+//  4 WordPiece greedy longest-match-first on a per-wave work queue, every
+//             lane one vocab probe per step: candidate = its first 24 bytes as
+//             6 dwords from LDS, hash, LDS Bloom filter (exact negatives cost no
+//             memory access), one 64-B bucket load for the rest; pieces stored
+//             at the unit's raw position (#pieces <= #raw bytes of the unit).
+//  5 output   segmented wave scan of piece counts by sentence, ids written to
+//             their final slots, per-sentence counts.
+// Tiles it does not model (window > 2 KiB, > 64 sentences, > 256 units, side
+// buffer or marker overflow, ccc>0 survivors needing canonical reordering)
+// are listed and re-run by tokenize_fallback_kernel (exact serial path).
+#include "common.h"
+#include "tokenize.h"
+#include "tokenize_serial.h"
+
+namespace lddl {
+namespace tok4 {
+
+constexpr int CAP = 2048;             // window bytes (32 per lane)
+constexpr int DCAP = 256;             // side buffer for dirty words
+constexpr int NBUF = CAP + DCAP + 64; // + over-read pad of the candidate loads
+constexpr int UCAP = 256;             // units per tile
+constexpr int NSCAP = 64;             // sentences per tile
+constexpr int XCAP = 32;              // expansion markers per tile
+constexpr uint32_t BF = 0xFFu, BX = 0xFDu, BS = 0xF8u;  // filler, expansion, special k = BS+k
+
+// class byte per input byte value
+enum : uint32_t { C_W = 1, C_I = 2, C_S = 4, C_D = 8, C_UP = 16, C_X = 32, C_CS = 64 };
+
+struct WaveLds {
+  uint32_t rp[CAP / 2 + 4];  // raw bytes (step 1), then u16 pieces by raw position
+  uint32_t nb[NBUF / 4];     // normalised bytes in window coordinates; side buffer at [CAP, CAP+DCAP)
+  uint32_t brk[64];          // break bits: unit starts, spaces, sentence starts
+  uint32_t dm[64];           // dirty bits: filler / expansion marker bytes
+  uint32_t sb[64];           // sentence-start bits
+  uint32_t urec[UCAP];       // window position | sentence << 16
+  uint32_t uwp[UCAP];        // byte source | byte length << 12
+  uint16_t wl[UCAP];         // WordPiece work list
+  uint8_t ucnt[UCAP];        // pieces per unit
+  uint16_t sst[NSCAP + 2];   // sentence starts (window coordinates)
+  uint16_t stot[NSCAP];      // tokens per sentence
+  uint32_t xent[XCAP];       // table entry of each expansion marker
+  uint8_t xlen[XCAP];        // its normalised byte length
+  int32_t misc[4];           // 0 side-buffer cursor, 1 #markers, 2 overflow
+};
+
+__device__ __forceinline__ void wsync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__device__ __forceinline__ uint32_t rawb(const WaveLds& L, int p) { return reinterpret_cast<const uint8_t*>(L.rp)[p]; }
+__device__ __forceinline__ uint32_t nbyte(const WaveLds& L, int p) { return reinterpret_cast<const uint8_t*>(L.nb)[p]; }
+__device__ __forceinline__ void nput(WaveLds& L, int p, uint32_t v) { reinterpret_cast<uint8_t*>(L.nb)[p] = (uint8_t)v; }
+
+// bit q of each byte of c -> 4 bits (byte 0 -> bit 0)
+__device__ __forceinline__ uint32_t gather4(uint32_t c, int q) { return (((c >> q) & 0x01010101u) * 0x01020408u) >> 24; }
+
+__device__ __forceinline__ int64_t uni64(int64_t x) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)(uint64_t)x);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)x >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+__device__ __forceinline__ int lane_rank(uint64_t m) {
+  return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+__device__ __forceinline__ uint32_t wave_excl(uint32_t v, int lane, uint32_t* total) {
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  *total = __shfl(x, 63);
+  return x - v;
+}
+
+__device__ __forceinline__ int utf8_put(WaveLds& L, int p, uint32_t c) {
+  if (c < 0x80) { nput(L, p, c); return 1; }
+  if (c < 0x800) { nput(L, p, 0xC0 | (c >> 6)); nput(L, p + 1, 0x80 | (c & 0x3F)); return 2; }
+  if (c < 0x10000) {
+    nput(L, p, 0xE0 | (c >> 12)); nput(L, p + 1, 0x80 | ((c >> 6) & 0x3F)); nput(L, p + 2, 0x80 | (c & 0x3F));
+    return 3;
+  }
+  nput(L, p, 0xF0 | (c >> 18)); nput(L, p + 1, 0x80 | ((c >> 12) & 0x3F));
+  nput(L, p + 2, 0x80 | ((c >> 6) & 0x3F)); nput(L, p + 3, 0x80 | (c & 0x3F));
+  return 4;
+}
+
+// first break position > p (a unit's span end), at most nb
+__device__ __forceinline__ int span_end(const WaveLds& L, int p, int nb) {
+  int w = p >> 5;
+  uint32_t m = L.brk[w] & ~((2u << (p & 31)) - 1u);
+  while (m == 0) {
+    ++w;
+    if ((w << 5) >= nb) return nb;
+    m = L.brk[w];
+  }
+  return min((w << 5) + __ffs(m) - 1, nb);
+}
+
+__device__ __forceinline__ bool span_dirty(const WaveLds& L, int p, int q) {
+  for (int w = p >> 5; (w << 5) < q; ++w) {
+    const int lo = max(p - (w << 5), 0), hi = min(q - (w << 5), 32);
+    const uint32_t m = (hi >= 32 ? ~0u : ((1u << hi) - 1u)) & ~((1u << lo) - 1u);
+    if (L.dm[w] & m) return true;
+  }
+  return false;
+}
+
+// Compact / expand the dirty span [p, q) into the side buffer.  Returns its
+// normalised length (source in *src), -1 on overflow (flagged in misc[2]).
+__device__ int dirty_normalize(WaveLds& L, const TokParams& P, int p, int q, int* src) {
+  int len = 0;
+  for (int i = p; i < q;) {
+    const uint32_t b = nbyte(L, i);
+    if (b == BF) {
+      ++i;
+    } else if (b == BX) {
+      len += L.xlen[nbyte(L, i + 1)];
+      i += 2;
+    } else {
+      ++len;
+      ++i;
+    }
+  }
+  if (len == 0) return 0;
+  const int off = atomicAdd(&L.misc[0], len);
+  if (off + len > DCAP) {
+    L.misc[2] = 1;
+    return -1;
+  }
+  int o = CAP + off;
+  *src = o;
+  for (int i = p; i < q;) {
+    const uint32_t b = nbyte(L, i);
+    if (b == BF) {
+      ++i;
+    } else if (b == BX) {
+      const uint32_t e = L.xent[nbyte(L, i + 1)];
+      if (ent_kind(e) == KIND_MULTI) {
+        const uint4 m = P.multi[ent_payload(e)];
+        o += utf8_put(L, o, ent_payload(m.y));
+        o += utf8_put(L, o, ent_payload(m.z));
+        if (m.x > 2) o += utf8_put(L, o, ent_payload(m.w));
+      } else {
+        o += utf8_put(L, o, ent_payload(e));
+      }
+      i += 2;
+    } else {
+      nput(L, o++, b);
+      ++i;
+    }
+  }
+  return len;
+}
+
+__device__ __forceinline__ int count_chars(const WaveLds& L, int src, int len) {
+  int n = 0;
+  for (int i = 0; i < len; ++i) n += (nbyte(L, src + i) & 0xC0u) != 0x80u;
+  return n;
+}
+
+// bytes [24, len) of a candidate against the vocab pool
+__device__ __noinline__ bool long_eq(const WaveLds& L, const TokParams& P, int s, int len, uint32_t off) {
+  for (int k = 24; k < len; ++k)
+    if (nbyte(L, s + k) != P.pool[off + k]) return false;
+  return true;
+}
+
+template <int WAVES, bool BLOOM, bool DBG>
+__global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int64_t* tile_sent, int64_t n_tiles,
+                                                          int32_t* fb_list, int32_t* fb_count) {
+  __shared__ WaveLds Ls[WAVES];
+  __shared__ uint32_t ctab32[64];
+  __shared__ uint32_t bloom[BLOOM ? BLOOM_WORDS : 1];
+  // ---- prologue: class table (from the unicode table's ASCII page), Bloom --
+  if (threadIdx.x < 64) {
+    uint32_t word = 0;
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t b = threadIdx.x * 4 + k;
+      uint32_t c;
+      if (b < 128) {
+        const uint32_t e = P.pages[(uint32_t)P.top[0] * 256u + b];
+        const uint32_t kind = ent_kind(e), cls = ent_cls(e);
+        c = C_CS;
+        if (kind == KIND_DROP_T || kind == KIND_DROP_D) c |= C_W | C_D;
+        else if (cls == CLS_SPACE) c |= C_S;
+        else if (cls == CLS_ISOLATE) c |= C_I;
+        else c |= C_W;
+        if (kind == KIND_MAP && cls == CLS_OTHER) c |= C_UP;  // A-Z -> a-z (checked at lddl_create)
+        if (b == '[') c |= C_X;
+      } else {
+        c = b >= 0xC0 ? (C_X | C_CS) : 0u;
+      }
+      word |= c << (8 * k);
+    }
+    ctab32[threadIdx.x] = word;
+  }
+  if (BLOOM)
+    for (int i = threadIdx.x; i < BLOOM_WORDS; i += 64 * WAVES) bloom[i] = P.vbloom[i];
+  __syncthreads();
+  const uint8_t* ctab = reinterpret_cast<const uint8_t*>(ctab32);
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  WaveLds& L = Ls[wv];
+  uint16_t* pc = reinterpret_cast<uint16_t*>(L.rp);
+  const int64_t base = P.sent_off[0];
+  const int64_t nwaves = (int64_t)gridDim.x * WAVES;
+  constexpr bool dbg = DBG;
+  uint64_t acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t tprev = 0;
+#define STAMP(k)                                      \
+  if (dbg) {                                          \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
+    acc[k] += t_ - tprev;                             \
+    tprev = t_;                                       \
+  }
+  for (int64_t t = (int64_t)blockIdx.x * WAVES + wv; t < n_tiles; t += nwaves) {
+    wsync();
+    if (dbg) tprev = __builtin_amdgcn_s_memtime();
+    const int64_t sa = uni64(tile_sent[t]), sb = uni64(tile_sent[t + 1]);
+    if (sa >= sb) continue;
+    const int64_t A = uni64(P.sent_off[sa]), B = uni64(P.sent_off[sb]);
+    const uint8_t* wbase =
+        reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(P.bytes + A) & ~(uintptr_t)15);
+    const int aoff = (int)((P.bytes + A) - wbase);
+    const int64_t nb64 = (B - A) + aoff;
+    const int ns = (int)(sb - sa);
+    if (dbg) acc[10] += 1;
+    if (nb64 > CAP || ns > NSCAP) {
+      if (lane == 0) fb_list[atomicAdd(fb_count, 1)] = (int32_t)t;
+      if (dbg) acc[11] += 1;
+      continue;
+    }
+    const int nb = (int)nb64;
+    // ---- sentence starts ----------------------------------------------------
+    L.sb[lane] = 0;
+    if (lane == 0) {
+      L.misc[0] = 0;
+      L.misc[1] = 0;
+      L.misc[2] = 0;
+    }
+    if (lane < ns) L.stot[lane] = 0;
+    wsync();
+    if (lane < ns) {
+      const int pos = (int)(P.sent_off[sa + lane] - A) + aoff;
+      L.sst[lane] = (uint16_t)pos;
+      if (pos < nb) atomicOr(&L.sb[pos >> 5], 1u << (pos & 31));
+    }
+    // ---- 1: raw bytes -> masks + normalised bytes in place ------------------
+    const int p0 = lane * 32;
+    uint4 v0 = make_uint4(0, 0, 0, 0), v1 = v0;
+    {
+      // 16-B aligned blocks holding >= 1 window byte: never past a page
+      const uint4* gp = reinterpret_cast<const uint4*>(wbase) + 2 * lane;
+      if (p0 < nb) v0 = gp[0];
+      if (p0 + 16 < nb) v1 = gp[1];
+    }
+    *reinterpret_cast<uint4*>(&L.rp[lane * 8]) = v0;
+    *reinterpret_cast<uint4*>(&L.rp[lane * 8 + 4]) = v1;
+    const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+    uint32_t W = 0, I = 0, S = 0, CS = 0, D = 0, X = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const uint32_t x = w[k];
+      const uint32_t c = (uint32_t)ctab[x & 0xFFu] | ((uint32_t)ctab[(x >> 8) & 0xFFu] << 8) |
+                         ((uint32_t)ctab[(x >> 16) & 0xFFu] << 16) | ((uint32_t)ctab[x >> 24] << 24);
+      L.nb[lane * 8 + k] = (x + ((c & 0x10101010u) << 1)) | (((c >> 3) & 0x01010101u) * 0xFFu);
+      const int sh = 4 * k;
+      W |= gather4(c, 0) << sh;
+      I |= gather4(c, 1) << sh;
+      S |= gather4(c, 2) << sh;
+      D |= gather4(c, 3) << sh;
+      X |= gather4(c, 5) << sh;
+      CS |= gather4(c, 6) << sh;
+    }
+    const int wlo = min(max(aoff - p0, 0), 32), whi = min(max(nb - p0, 0), 32);
+    const uint32_t inwin = (whi >= 32 ? ~0u : ((1u << whi) - 1u)) & (wlo >= 32 ? 0u : ~((1u << wlo) - 1u));
+    X &= inwin;
+    wsync();
+    STAMP(0);
+    uint32_t sp_m = 0, sp_w = 0, sp_d = 0;  // this lane's last char / special running into the next lane
+    bool bad = false;
+    for (uint32_t xm = X; xm;) {
+      const int i = __ffs(xm) - 1;
+      xm &= xm - 1;
+      const int p = p0 + i;
+      const uint32_t b = rawb(L, p);
+      if (b == '[') {
+        int se = nb;  // end of p's sentence
+        for (int j = 1; j < ns; ++j)
+          if (L.sst[j] > p) { se = L.sst[j]; break; }
+        int len = 0, sk = -1;
+        if (p + 5 <= se) {
+          const uint32_t c1 = rawb(L, p + 1), c2 = rawb(L, p + 2), c3 = rawb(L, p + 3), c4 = rawb(L, p + 4);
+          if (c1 == 'P' && c2 == 'A' && c3 == 'D' && c4 == ']') { sk = 0; len = 5; }
+          else if (c1 == 'U' && c2 == 'N' && c3 == 'K' && c4 == ']') { sk = 1; len = 5; }
+          else if (c1 == 'C' && c2 == 'L' && c3 == 'S' && c4 == ']') { sk = 2; len = 5; }
+          else if (c1 == 'S' && c2 == 'E' && c3 == 'P' && c4 == ']') { sk = 3; len = 5; }
+          else if (c1 == 'M' && c2 == 'A' && c3 == 'S' && c4 == 'K' && p + 6 <= se && rawb(L, p + 5) == ']') { sk = 4; len = 6; }
+        }
+        if (sk >= 0) {
+          nput(L, p, BS + (uint32_t)sk);
+          const uint64_t cov = ((1ull << (len - 1)) - 1ull) << (i + 1);
+          const uint32_t cl = (uint32_t)cov;
+          W &= ~cl;
+          I &= ~cl;
+          S &= ~cl;
+          CS &= ~cl;
+          D &= ~cl;
+          sp_m |= (uint32_t)(cov >> 32);
+        }
+      } else {
+        const int n = utf8_len(b);
+        uint32_t cp = b & (0x3Fu >> (n - 1));
+        for (int q = 1; q < n; ++q) cp = (cp << 6) | (rawb(L, p + q) & 0x3Fu);
+        if (cp > 0x10FFFF) cp = 0xFFFD;
+        const uint32_t e = table_entry(P, cp);
+        const uint32_t kind = ent_kind(e), cls = ent_cls(e);
+        const uint64_t span = ((1ull << n) - 1ull) << i;
+        bool dirty = false, wordc = false;
+        if (ent_rank(e) != 0) bad = true;
+        if (kind == KIND_DROP_T || kind == KIND_DROP_D) {
+          for (int q = 0; q < n; ++q) nput(L, p + q, BF);
+          dirty = true;
+          wordc = true;
+        } else if (cls == CLS_SPACE) {
+          S |= 1u << i;
+        } else {
+          if (cls == CLS_ISOLATE) I |= 1u << i;
+          else wordc = true;
+          if (kind != KIND_IDENT) {
+            uint32_t c0 = ent_payload(e), c1 = 0, c2 = 0;
+            int nc = 1;
+            if (kind == KIND_MULTI) {
+              const uint4 m = P.multi[ent_payload(e)];
+              nc = (int)m.x;
+              c0 = ent_payload(m.y);
+              c1 = ent_payload(m.z);
+              c2 = ent_payload(m.w);
+              if ((ent_rank(m.y) | ent_rank(m.z) | (nc > 2 ? ent_rank(m.w) : 0u)) != 0) bad = true;
+            }
+            const int T = utf8_enc_len(c0) + (nc > 1 ? utf8_enc_len(c1) : 0) + (nc > 2 ? utf8_enc_len(c2) : 0);
+            if (T <= n) {
+              int o = p + utf8_put(L, p, c0);
+              if (nc > 1) o += utf8_put(L, o, c1);
+              if (nc > 2) o += utf8_put(L, o, c2);
+              for (; o < p + n; ++o) nput(L, o, BF);
+              dirty = T < n;
+            } else {
+              const int xi = atomicAdd(&L.misc[1], 1);
+              if (xi >= XCAP) {
+                bad = true;
+              } else {
+                L.xent[xi] = e;
+                L.xlen[xi] = (uint8_t)T;
+                nput(L, p, BX);
+                nput(L, p + 1, (uint32_t)xi);
+                for (int q = 2; q < n; ++q) nput(L, p + q, BF);
+              }
+              dirty = true;
+            }
+          }
+        }
+        const uint32_t slo = (uint32_t)span, shi = (uint32_t)(span >> 32);
+        if (wordc) {
+          W |= slo;
+          sp_w |= shi;
+        }
+        if (dirty) {
+          D |= slo;
+          sp_d |= shi;
+        }
+        sp_m |= shi;
+      }
+    }
+    {
+      uint32_t im = __shfl_up(sp_m, 1), iw = __shfl_up(sp_w, 1), id = __shfl_up(sp_d, 1);
+      if (lane == 0) im = iw = id = 0;
+      W = ((W & ~im) | iw) & inwin;
+      I &= ~im & inwin;
+      S &= ~im & inwin;
+      CS &= ~im & inwin;
+      D = ((D & ~im) | id) & inwin;
+    }
+    const bool wbad = __any(bad);
+    wsync();
+    STAMP(1);
+    // ---- 2: units -----------------------------------------------------------
+    const uint32_t SB = L.sb[lane];
+    const uint32_t carry = __shfl_up(W, 1) >> 31;
+    const uint32_t pw = (W << 1) | (lane ? carry : 0u);
+    const uint32_t U = CS & (I | (W & (~pw | SB)));
+    L.brk[lane] = U | (S & CS) | SB;
+    L.dm[lane] = D;
+    uint32_t tot;
+    const int ub = (int)wave_excl((uint32_t)__popc(U), lane, &tot);
+    const int n = (int)tot;
+    if (wbad || n > UCAP) {
+      if (lane == 0) fb_list[atomicAdd(fb_count, 1)] = (int32_t)t;
+      if (dbg) acc[11] += 1;
+      continue;
+    }
+    {
+      int u = ub;
+      for (uint32_t m = U; m; m &= m - 1) {
+        const int p = p0 + __ffs(m) - 1;
+        int lo = 0, hi = ns - 1;  // last sentence starting at or before p
+        while (lo < hi) {
+          const int mid = (lo + hi + 1) >> 1;
+          if ((int)L.sst[mid] <= p) lo = mid;
+          else hi = mid - 1;
+        }
+        L.urec[u++] = (uint32_t)p | ((uint32_t)lo << 16);
+      }
+    }
+    wsync();
+    STAMP(2);
+    // ---- 3: prep (spans, dirty words, specials, long words) -----------------
+    int nwl = 0;
+    for (int r = 0; r < n; r += 64) {
+      const int u = r + lane;
+      bool need = false;
+      if (u < n) {
+        const int p = (int)(L.urec[u] & 0xFFFFu);
+        const uint32_t b0 = nbyte(L, p);
+        int cnt = -1;
+        if (b0 >= BS && b0 < BS + 5) {
+          pc[p] = (uint16_t)P.special[b0 - BS];
+          cnt = 1;
+        } else {
+          const int q = span_end(L, p, nb);
+          int src = p, len = q - p;
+          if (span_dirty(L, p, q)) len = max(dirty_normalize(L, P, p, q, &src), 0);
+          if (len == 0) {
+            cnt = 0;
+          } else if (len > 100 && count_chars(L, src, len) > 100) {
+            pc[p] = (uint16_t)P.unk;
+            cnt = 1;
+          } else {
+            L.uwp[u] = (uint32_t)src | ((uint32_t)len << 12);
+            need = true;
+          }
+        }
+        if (cnt >= 0) L.ucnt[u] = (uint8_t)cnt;
+      }
+      const uint64_t bm = __ballot(need);
+      if (need) L.wl[nwl + lane_rank(bm)] = (uint16_t)u;
+      nwl += __popcll(bm);
+    }
+    wsync();
+    if (L.misc[2]) {
+      if (lane == 0) fb_list[atomicAdd(fb_count, 1)] = (int32_t)t;
+      if (dbg) acc[11] += 1;
+      continue;
+    }
+    STAMP(3);
+    if (dbg) acc[8] += n;
+    // ---- 4: WordPiece on the work queue --------------------------------------
+    {
+      const int mb0 = (int)P.maxb[0], mb1 = (int)P.maxb[1];
+      const uint32_t vmask = P.vt_mask;
+      int u = -1, s = 0, we = 0, e = 0, pb = 0, np = 0, slot = -1;
+      uint32_t cont = 0;
+      uint32_t cd[6] = {0, 0, 0, 0, 0, 0};
+      auto load_cand = [&]() {
+        const int a = s >> 2;
+        const uint32_t sh = (uint32_t)(s & 3);
+        uint32_t x[7];
+#pragma unroll
+        for (int k = 0; k < 7; ++k) x[k] = L.nb[a + k];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) cd[k] = __builtin_amdgcn_alignbyte(x[k + 1], x[k], sh);
+      };
+      auto backoff = [&]() {
+        if (e < we)
+          while (e > s && (nbyte(L, e) & 0xC0u) == 0x80u) --e;
+      };
+      auto begin = [&](int uu) {
+        u = uu;
+        const uint32_t wp = L.uwp[uu];
+        s = (int)(wp & 0xFFFu);
+        we = s + (int)(wp >> 12);
+        pb = (int)(L.urec[uu] & 0xFFFFu);
+        np = 0;
+        cont = 0;
+        slot = -1;
+        load_cand();
+        e = min(we, s + mb0);
+        backoff();
+      };
+      if (lane < nwl) begin(L.wl[lane]);
+      int next = 64;
+      for (;;) {
+        if (__ballot(u >= 0) == 0 && next >= nwl) break;
+        if (dbg) acc[9] += 1;
+        if (u >= 0) {
+          bool fail = false;
+          uint32_t cm[6];
+          int len = e - s;
+          auto maskc = [&]() {
+#pragma unroll
+            for (int k = 0; k < 6; ++k) {
+              const int rem = len - 4 * k;
+              cm[k] = rem >= 4 ? cd[k] : rem <= 0 ? 0u : (cd[k] & ((1u << (8 * rem)) - 1u));
+            }
+          };
+          if (slot < 0) {
+            for (;;) {
+              if (e <= s) {
+                fail = true;
+                break;
+              }
+              len = e - s;
+              maskc();
+              const uint32_t h = vhash(cm, (uint32_t)len, cont);
+              if (!BLOOM) {
+                slot = (int)(h & vmask);
+                break;
+              }
+              const uint32_t bb = vbloom_bits(h);
+              if ((bloom[vbloom_word(h)] & bb) == bb) {
+                slot = (int)(h & vmask);
+                break;
+              }
+              if (dbg) acc[7] += 1;
+              --e;
+              while (e > s && (nbyte(L, e) & 0xC0u) == 0x80u) --e;
+            }
+          } else {
+            maskc();
+          }
+          if (fail) {
+            pc[pb] = (uint16_t)P.unk;
+            L.ucnt[u] = 1;
+            u = -1;
+          } else {
+            if (dbg) acc[6] += 1;
+            const uint4* bk = P.vt + 4 * (uint32_t)slot;
+            const uint4 a0 = bk[0], a1 = bk[1], b0 = bk[2], b1 = bk[3];
+            const uint32_t want = ((uint32_t)len << 16) | (cont << 24) | 0x80000000u;
+            bool m0 = (a1.z & 0xFFFF0000u) == want && a0.x == cm[0] && a0.y == cm[1] && a0.z == cm[2] &&
+                      a0.w == cm[3] && a1.x == cm[4] && a1.y == cm[5];
+            bool m1 = (b1.z & 0xFFFF0000u) == want && b0.x == cm[0] && b0.y == cm[1] && b0.z == cm[2] &&
+                      b0.w == cm[3] && b1.x == cm[4] && b1.y == cm[5];
+            if (m0 && len > 24) m0 = long_eq(L, P, s, len, a1.w);
+            if (m1 && len > 24) m1 = long_eq(L, P, s, len, b1.w);
+            if (m0 || m1) {
+              pc[pb + np] = (uint16_t)((m0 ? a1.z : b1.z) & 0xFFFFu);
+              ++np;
+              s = e;
+              slot = -1;
+              if (s >= we) {
+                L.ucnt[u] = (uint8_t)np;
+                u = -1;
+              } else {
+                cont = 1;
+                load_cand();
+                e = min(we, s + mb1);
+                backoff();
+              }
+            } else if (!(a1.z & 0x80000000u) || !(b1.z & 0x80000000u)) {
+              slot = -1;  // an empty slot ends the probe sequence: no such key
+              --e;
+              while (e > s && (nbyte(L, e) & 0xC0u) == 0x80u) --e;
+            } else {
+              slot = (int)(((uint32_t)slot + 1u) & vmask);
+            }
+          }
+        }
+        const uint64_t idle = __ballot(u < 0);
+        if (next < nwl) {
+          if (u < 0) {
+            const int r = next + lane_rank(idle);
+            if (r < nwl) begin(L.wl[r]);
+          }
+          next += __popcll(idle);
+        }
+      }
+    }
+    wsync();
+    STAMP(4);
+    // ---- 5: token positions (segmented scan by sentence) and output ---------
+    {
+      constexpr int K = UCAP / 64;
+      const int per = (n + 63) >> 6;
+      const int u0 = lane * per;
+      int run = 0, head = 0;
+      int lpre[K];
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        lpre[k] = 0;
+        const int uu = u0 + k;
+        if (k < per && uu < n) {
+          const uint32_t sj = L.urec[uu] >> 16;
+          if (uu == 0 || (L.urec[uu - 1] >> 16) != sj) {
+            run = 0;
+            head = 1;
+          }
+          lpre[k] = run;
+          run += L.ucnt[uu];
+        }
+      }
+      int hv = head, sv = run;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int ph = __shfl_up(hv, o), ps = __shfl_up(sv, o);
+        if (lane >= o && !hv) {
+          sv += ps;
+          hv = ph;
+        }
+      }
+      int ex = __shfl_up(sv, 1);
+      if (lane == 0) ex = 0;
+      bool before = true;
+      const int64_t obase = (A - base) - aoff;
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const int uu = u0 + k;
+        if (k < per && uu < n) {
+          const uint32_t rec = L.urec[uu];
+          const int sj = (int)(rec >> 16), p = (int)(rec & 0xFFFFu);
+          if (uu == 0 || (int)(L.urec[uu - 1] >> 16) != sj) before = false;
+          const int pos = lpre[k] + (before ? ex : 0);
+          const int c = L.ucnt[uu];
+          uint16_t* out = P.out_ids + (obase + (int64_t)L.sst[sj] + pos);
+          for (int q = 0; q < c && pos + q < P.max_tok; ++q) out[q] = pc[p + q];
+          if (uu == n - 1 || (int)(L.urec[uu + 1] >> 16) != sj) L.stot[sj] = (uint16_t)(pos + c);
+        }
+      }
+      wsync();
+      if (lane < ns) P.out_ntok[sa + lane] = min((int)L.stot[lane], P.max_tok);
+    }
+    STAMP(5);
+  }
+  if (dbg && lane == 0)
+    for (int k = 0; k < 12; ++k) atomicAdd((unsigned long long*)&P.dbg[k], (unsigned long long)acc[k]);
+#undef STAMP
+}
+
+template <int WAVES, bool BLOOM, bool DBG>
+hipError_t launch_cfg(const TokParams& P, int64_t n_tiles, const int64_t* tile_sent, int32_t* fb_list,
+                      int32_t* fb_count, int n_cu, hipStream_t s) {
+  static int per_cu = 0;
+  if (per_cu == 0) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, tok4_kernel<WAVES, BLOOM, DBG>, 64 * WAVES, 0) !=
+            hipSuccess ||
+        per_cu < 1)
+      per_cu = 1;
+  }
+  int64_t grid = (int64_t)n_cu * per_cu;
+  const int64_t need = (n_tiles + WAVES - 1) / WAVES;
+  if (grid > need) grid = need;
+  if (grid < 1) grid = 1;
+  hipLaunchKernelGGL((tok4_kernel<WAVES, BLOOM, DBG>), dim3((unsigned)grid), dim3(64 * WAVES), 0, s, P, tile_sent,
+                     n_tiles, fb_list, fb_count);
+  return hipGetLastError();
+}
+
+}  // namespace tok4
+
+hipError_t launch_tokenize_stream(const TokParams& P, int64_t nbytes, int64_t* tile_sent, int32_t* fb_list,
+                                  int32_t* fb_count, int fb_grid, int n_cu, int cfg, hipStream_t s) {
+  const int64_t n_tiles = tile_count(nbytes);
+  hipError_t e = launch_tile_bounds(P.sent_off, P.n_sent, n_tiles, tile_sent, s);
+  if (e != hipSuccess) return e;
+  e = hipMemsetAsync(fb_count, 0, 4, s);
+  if (e != hipSuccess) return e;
+  if (P.dbg) {  // phase stamps + counters (LDDL_TOK_DEBUG=1), separate instantiation
+    e = cfg == 1 ? tok4::launch_cfg<4, false, true>(P, n_tiles, tile_sent, fb_list, fb_count, n_cu, s)
+                 : tok4::launch_cfg<4, true, true>(P, n_tiles, tile_sent, fb_list, fb_count, n_cu, s);
+  } else {
+    switch (cfg) {
+      case 1: e = tok4::launch_cfg<4, false, false>(P, n_tiles, tile_sent, fb_list, fb_count, n_cu, s); break;
+      case 2: e = tok4::launch_cfg<12, true, false>(P, n_tiles, tile_sent, fb_list, fb_count, n_cu, s); break;
+      case 3: e = tok4::launch_cfg<8, true, false>(P, n_tiles, tile_sent, fb_list, fb_count, n_cu, s); break;
+      default: e = tok4::launch_cfg<4, true, false>(P, n_tiles, tile_sent, fb_list, fb_count, n_cu, s); break;
+    }
+  }
+  if (e != hipSuccess) return e;
+  return launch_tokenize_fallback(P, tile_sent, fb_list, fb_count, fb_grid, s);
+}
+
+}  // namespace lddl

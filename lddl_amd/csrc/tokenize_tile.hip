@@ -433,8 +433,7 @@ int64_t tile_count(int64_t nbytes) { return (nbytes >> TILE_SHIFT) + 1; }
 hipError_t launch_tokenize_tiles(const TokParams& P, int64_t nbytes, int64_t* tile_sent, int32_t* fb_list,
                                  int32_t* fb_count, int fb_grid, int64_t chunk, hipStream_t s) {
   const int64_t n_tiles = tile_count(nbytes);
-  hipLaunchKernelGGL(tile_bounds_kernel, dim3(4096), dim3(256), 0, s, P.sent_off, P.n_sent, n_tiles, tile_sent);
-  hipError_t e = hipGetLastError();
+  hipError_t e = launch_tile_bounds(P.sent_off, P.n_sent, n_tiles, tile_sent, s);
   if (e != hipSuccess) return e;
   e = hipMemsetAsync(fb_count, 0, 4, s);
   if (e != hipSuccess) return e;
@@ -445,7 +444,18 @@ hipError_t launch_tokenize_tiles(const TokParams& P, int64_t nbytes, int64_t* ti
     e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(tokenize_fallback_kernel, dim3(fb_grid), dim3(256), 0, s, P, tile_sent, fb_list, fb_count);
+  return launch_tokenize_fallback(P, tile_sent, fb_list, fb_count, fb_grid, s);
+}
+
+hipError_t launch_tile_bounds(const int64_t* sent_off, int64_t n_sent, int64_t n_tiles, int64_t* tile_sent,
+                              hipStream_t s) {
+  hipLaunchKernelGGL(tile_bounds_kernel, dim3(4096), dim3(256), 0, s, sent_off, n_sent, n_tiles, tile_sent);
+  return hipGetLastError();
+}
+
+hipError_t launch_tokenize_fallback(const TokParams& P, const int64_t* tile_sent, const int32_t* fb_list,
+                                    const int32_t* fb_count, int grid, hipStream_t s) {
+  hipLaunchKernelGGL(tokenize_fallback_kernel, dim3(grid), dim3(256), 0, s, P, tile_sent, fb_list, fb_count);
   return hipGetLastError();
 }
 

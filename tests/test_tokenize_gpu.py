@@ -107,7 +107,7 @@ def adversarial_sentences(rng, n):
   return out
 
 
-@pytest.mark.parametrize('algo', ['1', '2', '3'])
+@pytest.mark.parametrize('algo', ['1', '2', '3', '4'])
 @pytest.mark.parametrize('name', ['bert', 'codebert'])
 def test_hip_tokenize_adversarial_vs_oracle(gpu, monkeypatch, algo, name):
   from lddl_amd.synth import corpus_from_sentences
@@ -126,7 +126,7 @@ def test_hip_tokenize_adversarial_vs_oracle(gpu, monkeypatch, algo, name):
       assert np.array_equal(a.astype(np.int64), b.astype(np.int64)), (i, repr(sents[i][:80]))
 
 
-@pytest.mark.parametrize('algo', ['1', '2', '3'])
+@pytest.mark.parametrize('algo', ['1', '2', '3', '4'])
 def test_hip_tokenize_algos_agree_on_wiki(gpu, monkeypatch, algo):
   from lddl_amd import synth
   from lddl_amd.tokenizer import Tokenizer

@@ -1,0 +1,73 @@
+"""GPU tokenizer check + timing for the kernel variants (GPU box tool).
+
+    python tools/tok_check.py [MB] [algo[:cfg] ...]
+
+Tokenizes a synthetic Wikipedia-style corpus of MB megabytes with each
+variant, compares ids / counts with the oracle (first MB only, for speed)
+and prints throughput.  LDDL_TOK_DEBUG=1 adds the kernels' phase stamps.
+"""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def main():
+  mb = int(sys.argv[1]) if len(sys.argv) > 1 else 64
+  variants = sys.argv[2:] or ['3', '4']
+  from lddl_amd import synth
+  from lddl_amd.tokenizer import Tokenizer
+  from lddl_amd.pipeline import VOCAB_BERT
+  from oracle.oracle import OracleTokenizer, compact
+  t0 = time.time()
+  c = synth.make_wiki(mb << 20, seed=1)
+  print('gen %.1fs: %d bytes %d sentences' % (time.time() - t0, c.nbytes, c.n_sent), flush=True)
+  d = torch.from_numpy(np.concatenate([c.data, np.zeros(16, np.uint8)])).cuda()
+  o = torch.from_numpy(c.sent_off).cuda()
+  ns_chk = int(np.searchsorted(c.sent_off, min(c.nbytes, 4 << 20)))
+  oids, ontok = OracleTokenizer(VOCAB_BERT).run(
+      c.data, c.sent_off[:ns_chk + 1], 512, nthreads=8)
+  for v in variants:
+    algo, _, cfg = v.partition(':')
+    os.environ['LDDL_TOKENIZE_ALGO'] = algo
+    os.environ['LDDL_TOK4_CFG'] = cfg or '0'
+    tok = Tokenizer()
+    ids, ntok = tok.tokenize_device(d, o)
+    torch.cuda.synchronize()
+    h_ntok = ntok.cpu().numpy()[:c.n_sent]
+    h_ids = ids.cpu().numpy().view(np.uint16)
+    bad = np.nonzero(h_ntok[:ns_chk] != ontok)[0]
+    nbad_ids = 0
+    if len(bad) == 0:
+      for i, (a, b) in enumerate(zip(compact(h_ids, h_ntok[:ns_chk], c.sent_off[:ns_chk + 1]),
+                                     compact(oids, ontok, c.sent_off[:ns_chk + 1]))):
+        if not np.array_equal(a.astype(np.int64), b.astype(np.int64)):
+          nbad_ids += 1
+          if nbad_ids <= 3:
+            print('  ids differ in sentence %d: %r\n   gpu %s\n   ref %s' % (
+                i, c.sentence(i)[:200], a[:40].tolist(), b[:40].tolist()))
+    else:
+      for i in bad[:3]:
+        print('  ntok differs in sentence %d (%d vs %d): %r' % (i, h_ntok[i], ontok[i], c.sentence(i)[:200]))
+    ok = len(bad) == 0 and nbad_ids == 0
+    ntoks = int(h_ntok.sum())
+    times = []
+    for _ in range(3):
+      s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+      s.record()
+      tok.tokenize_device(d, o, out_ids=ids, out_ntok=ntok)
+      e.record()
+      torch.cuda.synchronize()
+      times.append(s.elapsed_time(e))
+    ms = min(times)
+    print('variant %s: parity(%d sents) %s (ntok bad %d, ids bad %d)  %.3f ms  %.1f GB/s  %.2f Gtok/s' % (
+        v, ns_chk, 'OK' if ok else 'FAIL', len(bad), nbad_ids, ms, c.nbytes / ms / 1e6, ntoks / ms / 1e6),
+          flush=True)
+    tok.close()
+
+
+if __name__ == '__main__':
+  main()
