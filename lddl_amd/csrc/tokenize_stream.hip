@@ -62,6 +62,7 @@ struct WaveLds {
   uint32_t uwp[UCAP];        // byte source | byte length << 12
   uint16_t wl[UCAP];         // WordPiece work list
   uint8_t ucnt[UCAP];        // pieces per unit
+  uint8_t uneed[UCAP];       // 0 done in prep, 1 short / 2 long word for WordPiece
   uint16_t sst[NSCAP + 2];   // sentence starts (window coordinates)
   uint16_t stot[NSCAP];      // tokens per sentence
   uint32_t xent[XCAP];       // table entry of each expansion marker
@@ -189,7 +190,7 @@ __device__ __forceinline__ int count_chars(const WaveLds& L, int src, int len) {
 }
 
 // bytes [24, len) of a candidate against the vocab pool
-__device__ __noinline__ bool long_eq(const WaveLds& L, const TokParams& P, int s, int len, uint32_t off) {
+__device__ __forceinline__ bool long_eq(const WaveLds& L, const TokParams& P, int s, int len, uint32_t off) {
   for (int k = 24; k < len; ++k)
     if (nbyte(L, s + k) != P.pool[off + k]) return false;
   return true;
@@ -235,7 +236,7 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
   const int64_t base = P.sent_off[0];
   const int64_t nwaves = (int64_t)gridDim.x * WAVES;
   constexpr bool dbg = DBG;
-  uint64_t acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t acc[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t tprev = 0;
 #define STAMP(k)                                      \
   if (dbg) {                                          \
@@ -257,7 +258,7 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
     if (dbg) acc[10] += 1;
     if (nb64 > CAP || ns > NSCAP) {
       if (lane == 0) fb_list[atomicAdd(fb_count, 1)] = (int32_t)t;
-      if (dbg) acc[11] += 1;
+      if (dbg) { acc[11] += 1; acc[12] += 1; }
       continue;
     }
     const int nb = (int)nb64;
@@ -424,32 +425,39 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
     uint32_t tot;
     const int ub = (int)wave_excl((uint32_t)__popc(U), lane, &tot);
     const int n = (int)tot;
-    if (wbad || n > UCAP) {
+    if (wbad) {
       if (lane == 0) fb_list[atomicAdd(fb_count, 1)] = (int32_t)t;
-      if (dbg) acc[11] += 1;
+      if (dbg) { acc[11] += 1; acc[13] += 1; }
       continue;
     }
-    {
-      int u = ub;
-      for (uint32_t m = U; m; m &= m - 1) {
-        const int p = p0 + __ffs(m) - 1;
-        int lo = 0, hi = ns - 1;  // last sentence starting at or before p
-        while (lo < hi) {
-          const int mid = (lo + hi + 1) >> 1;
-          if ((int)L.sst[mid] <= p) lo = mid;
-          else hi = mid - 1;
+    // units are processed in rounds of UCAP; a sentence running across two
+    // rounds continues its token count (stot) in the next one
+    int prev_sent = -1;
+    for (int rb = 0; rb < n; rb += UCAP) {
+      const int nr = min(UCAP, n - rb);
+      if (lane == 0) L.misc[0] = 0;
+      {
+        int u = ub;
+        for (uint32_t m = U; m; m &= m - 1, ++u) {
+          if (u < rb || u >= rb + nr) continue;
+          const int p = p0 + __ffs(m) - 1;
+          int lo = 0, hi = ns - 1;  // last sentence starting at or before p
+          while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if ((int)L.sst[mid] <= p) lo = mid;
+            else hi = mid - 1;
+          }
+          L.urec[u - rb] = (uint32_t)p | ((uint32_t)lo << 16);
         }
-        L.urec[u++] = (uint32_t)p | ((uint32_t)lo << 16);
       }
-    }
-    wsync();
-    STAMP(2);
+      wsync();
+      STAMP(2);
     // ---- 3: prep (spans, dirty words, specials, long words) -----------------
     int nwl = 0;
-    for (int r = 0; r < n; r += 64) {
+    for (int r = 0; r < nr; r += 64) {
       const int u = r + lane;
       bool need = false;
-      if (u < n) {
+      if (u < nr) {
         const int p = (int)(L.urec[u] & 0xFFFFu);
         const uint32_t b0 = nbyte(L, p);
         int cnt = -1;
@@ -472,18 +480,28 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
         }
         if (cnt >= 0) L.ucnt[u] = (uint8_t)cnt;
       }
+      if (u < UCAP) L.uneed[u] = need ? (uint8_t)(1 + (L.uwp[u] >> 12 >= 10u)) : (uint8_t)0;
       const uint64_t bm = __ballot(need);
-      if (need) L.wl[nwl + lane_rank(bm)] = (uint16_t)u;
       nwl += __popcll(bm);
     }
     wsync();
-    if (L.misc[2]) {
-      if (lane == 0) fb_list[atomicAdd(fb_count, 1)] = (int32_t)t;
-      if (dbg) acc[11] += 1;
-      continue;
+    // work list, longest first: long words are the OOV ones needing many
+    // probes, and starting them first keeps the queue's tail short
+    {
+      int at = 0;
+      for (int pass = 2; pass >= 1; --pass)
+        for (int r = 0; r < nr; r += 64) {
+          const int u = r + lane;
+          const bool take = u < nr && L.uneed[u] == pass;
+          const uint64_t bm = __ballot(take);
+          if (take) L.wl[at + lane_rank(bm)] = (uint16_t)u;
+          at += __popcll(bm);
+        }
     }
+    wsync();
+    if (L.misc[2]) break;  // side buffer overflow: the whole tile falls back
     STAMP(3);
-    if (dbg) acc[8] += n;
+    if (dbg) acc[8] += nr;
     // ---- 4: WordPiece on the work queue --------------------------------------
     {
       const int mb0 = (int)P.maxb[0], mb1 = (int)P.maxb[1];
@@ -611,17 +629,22 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
     // ---- 5: token positions (segmented scan by sentence) and output ---------
     {
       constexpr int K = UCAP / 64;
-      const int per = (n + 63) >> 6;
+      const int per = (nr + 63) >> 6;
       const int u0 = lane * per;
+      const int first_sent = (int)(L.urec[0] >> 16);
+      const int carry0 = first_sent == prev_sent ? (int)L.stot[first_sent] : 0;
+      auto is_head = [&](int uu, int sj) {
+        return uu == 0 ? sj != prev_sent : (int)(L.urec[uu - 1] >> 16) != sj;
+      };
       int run = 0, head = 0;
       int lpre[K];
 #pragma unroll
       for (int k = 0; k < K; ++k) {
         lpre[k] = 0;
         const int uu = u0 + k;
-        if (k < per && uu < n) {
-          const uint32_t sj = L.urec[uu] >> 16;
-          if (uu == 0 || (L.urec[uu - 1] >> 16) != sj) {
+        if (k < per && uu < nr) {
+          const int sj = (int)(L.urec[uu] >> 16);
+          if (is_head(uu, sj)) {
             run = 0;
             head = 1;
           }
@@ -638,31 +661,40 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
           hv = ph;
         }
       }
-      int ex = __shfl_up(sv, 1);
-      if (lane == 0) ex = 0;
+      int ex = __shfl_up(sv, 1), exh = __shfl_up(hv, 1);
+      if (lane == 0) ex = exh = 0;
+      if (!exh) ex += carry0;  // units before any head continue the previous round's sentence
       bool before = true;
       const int64_t obase = (A - base) - aoff;
 #pragma unroll
       for (int k = 0; k < K; ++k) {
         const int uu = u0 + k;
-        if (k < per && uu < n) {
+        if (k < per && uu < nr) {
           const uint32_t rec = L.urec[uu];
           const int sj = (int)(rec >> 16), p = (int)(rec & 0xFFFFu);
-          if (uu == 0 || (int)(L.urec[uu - 1] >> 16) != sj) before = false;
+          if (is_head(uu, sj)) before = false;
           const int pos = lpre[k] + (before ? ex : 0);
           const int c = L.ucnt[uu];
           uint16_t* out = P.out_ids + (obase + (int64_t)L.sst[sj] + pos);
           for (int q = 0; q < c && pos + q < P.max_tok; ++q) out[q] = pc[p + q];
-          if (uu == n - 1 || (int)(L.urec[uu + 1] >> 16) != sj) L.stot[sj] = (uint16_t)(pos + c);
+          if (uu == nr - 1 || (int)(L.urec[uu + 1] >> 16) != sj) L.stot[sj] = (uint16_t)(pos + c);
         }
       }
       wsync();
-      if (lane < ns) P.out_ntok[sa + lane] = min((int)L.stot[lane], P.max_tok);
+      prev_sent = (int)(L.urec[nr - 1] >> 16);
+      wsync();
     }
+    }  // rounds
+    if (L.misc[2]) {
+      if (lane == 0) fb_list[atomicAdd(fb_count, 1)] = (int32_t)t;
+      if (dbg) { acc[11] += 1; acc[15] += 1; }
+      continue;
+    }
+    if (lane < ns) P.out_ntok[sa + lane] = min((int)L.stot[lane], P.max_tok);
     STAMP(5);
   }
   if (dbg && lane == 0)
-    for (int k = 0; k < 12; ++k) atomicAdd((unsigned long long*)&P.dbg[k], (unsigned long long)acc[k]);
+    for (int k = 0; k < 16; ++k) atomicAdd((unsigned long long*)&P.dbg[k], (unsigned long long)acc[k]);
 #undef STAMP
 }
 
