@@ -60,18 +60,29 @@ LDDL_HD uint32_t slot_info(uint32_t id, uint32_t len, uint32_t cont) {
 // one probe is one cache line and a key of <= 24 bytes verifies from the
 // slot alone.  info uses slot_info()'s layout; info == 0 marks an empty slot.
 constexpr int VKEY_DW = 6;
-LDDL_HD uint32_t vhash(const uint32_t* d, uint32_t len, uint32_t cont) {
-  uint32_t h = 0x9E3779B9u * (len + 1u) + (cont ? 0x7F4A7C15u : 0u);
-  for (int k = 0; k < VKEY_DW; ++k) {
-    h ^= d[k];
-    h = ((h << 5) | (h >> 27)) * 0x85EBCA77u;
-  }
+constexpr uint32_t VSEED = 0x1B873593u;
+LDDL_HD uint32_t vmix(uint32_t h, uint32_t d) {
+  h ^= d;
+  return ((h << 5) | (h >> 27)) * 0x85EBCA77u;
+}
+LDDL_HD uint32_t vfinal(uint32_t h, uint32_t len, uint32_t cont) {
+  h ^= len * 0x9E3779B9u ^ (cont ? 0x7F4A7C15u : 0u);
   h ^= h >> 15;
   h *= 0x2C1B3C6Du;
   h ^= h >> 12;
   h *= 0x297A2D39u;
   h ^= h >> 15;
   return h;
+}
+// Prefix-structured, so a kernel holding the mixes of the first k dwords of
+// a candidate re-hashes any shorter candidate with one mix: full dwords, then
+// the masked tail dword (only if len % 4), over the first 24 bytes.
+LDDL_HD uint32_t vhash(const uint32_t* d, uint32_t len, uint32_t cont) {
+  const uint32_t l = len < 24u ? len : 24u, q = l >> 2, r = l & 3u;
+  uint32_t h = VSEED;
+  for (uint32_t k = 0; k < q; ++k) h = vmix(h, d[k]);
+  if (r) h = vmix(h, d[q] & ((1u << (8 * r)) - 1u));
+  return vfinal(h, len, cont);
 }
 // blocked Bloom filter over the same keys (BLOOM_WORDS dwords, 2 bits/key)
 LDDL_HD uint32_t vbloom_word(uint32_t h) { return (h * 0x9E3779B1u) >> 19; }  // 13 bits

@@ -59,10 +59,8 @@ struct WaveLds {
   uint32_t dm[64];           // dirty bits: filler / expansion marker bytes
   uint32_t sb[64];           // sentence-start bits
   uint32_t urec[UCAP];       // window position | sentence << 16
-  uint32_t uwp[UCAP];        // byte source | byte length << 12
-  uint16_t wl[UCAP];         // WordPiece work list
+  uint32_t uwp[UCAP];        // WordPiece unit | source << 8 | length << 20 (0: none), then the work list in place
   uint8_t ucnt[UCAP];        // pieces per unit
-  uint8_t uneed[UCAP];       // 0 done in prep, 1 short / 2 long word for WordPiece
   uint16_t sst[NSCAP + 2];   // sentence starts (window coordinates)
   uint16_t stot[NSCAP];      // tokens per sentence
   uint32_t xent[XCAP];       // table entry of each expansion marker
@@ -250,9 +248,8 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
     const int64_t sa = uni64(tile_sent[t]), sb = uni64(tile_sent[t + 1]);
     if (sa >= sb) continue;
     const int64_t A = uni64(P.sent_off[sa]), B = uni64(P.sent_off[sb]);
-    const uint8_t* wbase =
-        reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(P.bytes + A) & ~(uintptr_t)15);
-    const int aoff = (int)((P.bytes + A) - wbase);
+    const int aoff = (int)(reinterpret_cast<uintptr_t>(P.bytes + A) & 15u);
+    const uint8_t* wbase = P.bytes + (A - aoff);  // 16-B aligned (derived from the global pointer: global loads)
     const int64_t nb64 = (B - A) + aoff;
     const int ns = (int)(sb - sa);
     if (dbg) acc[10] += 1;
@@ -474,27 +471,33 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
             pc[p] = (uint16_t)P.unk;
             cnt = 1;
           } else {
-            L.uwp[u] = (uint32_t)src | ((uint32_t)len << 12);
             need = true;
+            L.uwp[u] = (uint32_t)u | ((uint32_t)src << 8) | ((uint32_t)len << 20);
           }
         }
         if (cnt >= 0) L.ucnt[u] = (uint8_t)cnt;
+        if (!need) L.uwp[u] = 0;
       }
-      if (u < UCAP) L.uneed[u] = need ? (uint8_t)(1 + (L.uwp[u] >> 12 >= 10u)) : (uint8_t)0;
       const uint64_t bm = __ballot(need);
       nwl += __popcll(bm);
     }
     wsync();
-    // work list, longest first: long words are the OOV ones needing many
-    // probes, and starting them first keeps the queue's tail short
+    // work list (in place over uwp), longest first: long words are the OOV
+    // ones needing many probes, and starting them first keeps the tail short
     {
+      constexpr int K = UCAP / 64;
+      uint32_t ent[K];
+#pragma unroll
+      for (int k = 0; k < K; ++k) ent[k] = k * 64 + lane < nr ? L.uwp[k * 64 + lane] : 0u;
+      wsync();
       int at = 0;
-      for (int pass = 2; pass >= 1; --pass)
-        for (int r = 0; r < nr; r += 64) {
-          const int u = r + lane;
-          const bool take = u < nr && L.uneed[u] == pass;
+#pragma unroll
+      for (int pass = 0; pass < 2; ++pass)
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          const bool take = ent[k] != 0 && ((ent[k] >> 20) >= 10u) == (pass == 0);
           const uint64_t bm = __ballot(take);
-          if (take) L.wl[at + lane_rank(bm)] = (uint16_t)u;
+          if (take) L.uwp[at + lane_rank(bm)] = ent[k];
           at += __popcll(bm);
         }
     }
@@ -507,74 +510,112 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
       const int mb0 = (int)P.maxb[0], mb1 = (int)P.maxb[1];
       const uint32_t vmask = P.vt_mask;
       int u = -1, s = 0, we = 0, e = 0, pb = 0, np = 0, slot = -1;
-      uint32_t cont = 0;
-      uint32_t cd[6] = {0, 0, 0, 0, 0, 0};
+      uint32_t cont = 0, hcur = 0;
+      bool asc = false;
+      // candidate bytes [s, s+24) as dwords c0..c5 and the prefix mixes
+      // H0..H6 (H(k+1) = vmix(Hk, ck)): named scalars, never an indexed
+      // array, so nothing is demoted to scratch by dynamic indexing
+      uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0, c4 = 0, c5 = 0;
+      uint32_t H0 = VSEED, H1 = 0, H2 = 0, H3 = 0, H4 = 0, H5 = 0, H6 = 0;
       auto load_cand = [&]() {
         const int a = s >> 2;
         const uint32_t sh = (uint32_t)(s & 3);
-        uint32_t x[7];
-#pragma unroll
-        for (int k = 0; k < 7; ++k) x[k] = L.nb[a + k];
-#pragma unroll
-        for (int k = 0; k < 6; ++k) cd[k] = __builtin_amdgcn_alignbyte(x[k + 1], x[k], sh);
+        const uint32_t x0 = L.nb[a], x1 = L.nb[a + 1], x2 = L.nb[a + 2], x3 = L.nb[a + 3], x4 = L.nb[a + 4],
+                       x5 = L.nb[a + 5], x6 = L.nb[a + 6];
+        c0 = __builtin_amdgcn_alignbyte(x1, x0, sh);
+        c1 = __builtin_amdgcn_alignbyte(x2, x1, sh);
+        c2 = __builtin_amdgcn_alignbyte(x3, x2, sh);
+        c3 = __builtin_amdgcn_alignbyte(x4, x3, sh);
+        c4 = __builtin_amdgcn_alignbyte(x5, x4, sh);
+        c5 = __builtin_amdgcn_alignbyte(x6, x5, sh);
+        H1 = vmix(H0, c0);
+        H2 = vmix(H1, c1);
+        H3 = vmix(H2, c2);
+        H4 = vmix(H3, c3);
+        H5 = vmix(H4, c4);
+        H6 = vmix(H5, c5);
+        asc = ((c0 | c1 | c2 | c3 | c4 | c5) & 0x80808080u) == 0;
       };
-      auto backoff = [&]() {
-        if (e < we)
+      auto selH = [&](int q) {
+        return q <= 0 ? H0 : q == 1 ? H1 : q == 2 ? H2 : q == 3 ? H3 : q == 4 ? H4 : q == 5 ? H5 : H6;
+      };
+      auto selD = [&](int q) {
+        return q <= 0 ? c0 : q == 1 ? c1 : q == 2 ? c2 : q == 3 ? c3 : q == 4 ? c4 : c5;
+      };
+      auto hash_len = [&](int l) {  // == vhash of the candidate [s, s+l)
+        const int lc = min(l, 24), q = lc >> 2, r = lc & 3;
+        uint32_t h = selH(q);
+        if (r) h = vmix(h, selD(q) & ((1u << (8 * r)) - 1u));
+        return vfinal(h, (uint32_t)l, cont);
+      };
+      auto bloom_ok = [&](uint32_t h) {
+        if (!BLOOM) return true;
+        const uint32_t bb = vbloom_bits(h);
+        return (bloom[vbloom_word(h)] & bb) == bb;
+      };
+      auto shrink = [&]() {  // previous char boundary
+        --e;
+        if (!(asc && e - s < 24))
           while (e > s && (nbyte(L, e) & 0xC0u) == 0x80u) --e;
       };
-      auto begin = [&](int uu) {
-        u = uu;
-        const uint32_t wp = L.uwp[uu];
-        s = (int)(wp & 0xFFFu);
-        we = s + (int)(wp >> 12);
-        pb = (int)(L.urec[uu] & 0xFFFFu);
-        np = 0;
-        cont = 0;
+      auto start_piece = [&](int maxb) {
         slot = -1;
         load_cand();
-        e = min(we, s + mb0);
-        backoff();
+        e = min(we, s + maxb);
+        if (e < we && !(asc && e - s < 24))
+          while (e > s && (nbyte(L, e) & 0xC0u) == 0x80u) --e;
       };
-      if (lane < nwl) begin(L.wl[lane]);
+      auto begin = [&](uint32_t w) {
+        u = (int)(w & 0xFFu);
+        s = (int)((w >> 8) & 0xFFFu);
+        we = s + (int)(w >> 20);
+        pb = (int)(L.urec[u] & 0xFFFFu);
+        np = 0;
+        cont = 0;
+        start_piece(mb0);
+      };
+      if (lane < nwl) begin(L.uwp[lane]);
       int next = 64;
       for (;;) {
         if (__ballot(u >= 0) == 0 && next >= nwl) break;
         if (dbg) acc[9] += 1;
         if (u >= 0) {
           bool fail = false;
-          uint32_t cm[6];
-          int len = e - s;
-          auto maskc = [&]() {
-#pragma unroll
-            for (int k = 0; k < 6; ++k) {
-              const int rem = len - 4 * k;
-              cm[k] = rem >= 4 ? cd[k] : rem <= 0 ? 0u : (cd[k] & ((1u << (8 * rem)) - 1u));
-            }
-          };
           if (slot < 0) {
-            for (;;) {
-              if (e <= s) {
-                fail = true;
-                break;
+            // longest candidate <= e - s the Bloom filter does not rule out
+            int len = e - s;
+            bool found = false;
+            if (asc && len <= 24) {
+              // ASCII: every length is a char boundary; 4 lengths per step
+              while (len > 0) {
+                const uint32_t h0 = hash_len(len), h1 = hash_len(len - 1), h2 = hash_len(len - 2),
+                               h3 = hash_len(len - 3);
+                const bool o0 = bloom_ok(h0), o1 = len > 1 && bloom_ok(h1), o2 = len > 2 && bloom_ok(h2),
+                           o3 = len > 3 && bloom_ok(h3);
+                if (o0 | o1 | o2 | o3) {
+                  const int d = o0 ? 0 : o1 ? 1 : o2 ? 2 : 3;
+                  hcur = o0 ? h0 : o1 ? h1 : o2 ? h2 : h3;
+                  len -= d;
+                  found = true;
+                  break;
+                }
+                if (dbg) acc[7] += min(len, 4);
+                len -= 4;
               }
-              len = e - s;
-              maskc();
-              const uint32_t h = vhash(cm, (uint32_t)len, cont);
-              if (!BLOOM) {
-                slot = (int)(h & vmask);
-                break;
+              e = s + max(len, 0);
+            } else {
+              while (e > s) {
+                hcur = hash_len(e - s);
+                if (bloom_ok(hcur)) {
+                  found = true;
+                  break;
+                }
+                if (dbg) acc[7] += 1;
+                shrink();
               }
-              const uint32_t bb = vbloom_bits(h);
-              if ((bloom[vbloom_word(h)] & bb) == bb) {
-                slot = (int)(h & vmask);
-                break;
-              }
-              if (dbg) acc[7] += 1;
-              --e;
-              while (e > s && (nbyte(L, e) & 0xC0u) == 0x80u) --e;
             }
-          } else {
-            maskc();
+            if (found) slot = (int)(hcur & vmask);
+            else fail = true;
           }
           if (fail) {
             pc[pb] = (uint16_t)P.unk;
@@ -582,33 +623,36 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
             u = -1;
           } else {
             if (dbg) acc[6] += 1;
+            const int len = e - s;
+            const int lc = min(len, 24), q = lc >> 2, r = lc & 3;
+            auto msk = [&](int k, uint32_t c) {
+              return k < q ? c : (k == q && r) ? (c & ((1u << (8 * r)) - 1u)) : 0u;
+            };
+            const uint32_t m0c = msk(0, c0), m1c = msk(1, c1), m2c = msk(2, c2), m3c = msk(3, c3), m4c = msk(4, c4),
+                           m5c = msk(5, c5);
             const uint4* bk = P.vt + 4 * (uint32_t)slot;
             const uint4 a0 = bk[0], a1 = bk[1], b0 = bk[2], b1 = bk[3];
             const uint32_t want = ((uint32_t)len << 16) | (cont << 24) | 0x80000000u;
-            bool m0 = (a1.z & 0xFFFF0000u) == want && a0.x == cm[0] && a0.y == cm[1] && a0.z == cm[2] &&
-                      a0.w == cm[3] && a1.x == cm[4] && a1.y == cm[5];
-            bool m1 = (b1.z & 0xFFFF0000u) == want && b0.x == cm[0] && b0.y == cm[1] && b0.z == cm[2] &&
-                      b0.w == cm[3] && b1.x == cm[4] && b1.y == cm[5];
+            bool m0 = (a1.z & 0xFFFF0000u) == want && a0.x == m0c && a0.y == m1c && a0.z == m2c && a0.w == m3c &&
+                      a1.x == m4c && a1.y == m5c;
+            bool m1 = (b1.z & 0xFFFF0000u) == want && b0.x == m0c && b0.y == m1c && b0.z == m2c && b0.w == m3c &&
+                      b1.x == m4c && b1.y == m5c;
             if (m0 && len > 24) m0 = long_eq(L, P, s, len, a1.w);
             if (m1 && len > 24) m1 = long_eq(L, P, s, len, b1.w);
             if (m0 || m1) {
               pc[pb + np] = (uint16_t)((m0 ? a1.z : b1.z) & 0xFFFFu);
               ++np;
               s = e;
-              slot = -1;
               if (s >= we) {
                 L.ucnt[u] = (uint8_t)np;
                 u = -1;
               } else {
                 cont = 1;
-                load_cand();
-                e = min(we, s + mb1);
-                backoff();
+                start_piece(mb1);
               }
             } else if (!(a1.z & 0x80000000u) || !(b1.z & 0x80000000u)) {
               slot = -1;  // an empty slot ends the probe sequence: no such key
-              --e;
-              while (e > s && (nbyte(L, e) & 0xC0u) == 0x80u) --e;
+              shrink();
             } else {
               slot = (int)(((uint32_t)slot + 1u) & vmask);
             }
@@ -618,7 +662,7 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
         if (next < nwl) {
           if (u < 0) {
             const int r = next + lane_rank(idle);
-            if (r < nwl) begin(L.wl[r]);
+            if (r < nwl) begin(L.uwp[r]);
           }
           next += __popcll(idle);
         }
