@@ -420,7 +420,7 @@ extern "C" int lddl_tokenize(lddl_ctx* c, const uint8_t* d_bytes, int64_t nbytes
       HIP_TRY(hipStreamSynchronize(st));
       const char* nm[16] = {"bytes", "exceptions", "units", "prep", "wordpiece", "output",
                             "probes_l0", "bloom_rejects_l0", "nunits", "wp_iters", "tiles", "fallback",
-                            "fb_size", "fb_chars", "fb_units", "fb_dirty"};
+                            "wp_scan", "wp_probe", "wp_refill", "fb_dirty"};
       fprintf(stderr, "[lddl tok4 dbg] cfg=%d ntiles=%lld fallback_list=%d", c->tok4_cfg, (long long)nt, nfb);
       for (int k = 0; k < 16; ++k) fprintf(stderr, " %s=%llu", nm[k], (unsigned long long)h[k]);
       fprintf(stderr, "\n");

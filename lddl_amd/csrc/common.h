@@ -84,12 +84,11 @@ LDDL_HD uint32_t vhash(const uint32_t* d, uint32_t len, uint32_t cont) {
   if (r) h = vmix(h, d[q] & ((1u << (8 * r)) - 1u));
   return vfinal(h, len, cont);
 }
-// blocked Bloom filter over the same keys (BLOOM_WORDS dwords, 2 bits/key)
-LDDL_HD uint32_t vbloom_word(uint32_t h) { return (h * 0x9E3779B1u) >> 19; }  // 13 bits
-LDDL_HD uint32_t vbloom_bits(uint32_t h) {
-  const uint32_t g = h * 0x85EBCA77u;
-  return (1u << (g & 31u)) | (1u << ((g >> 5) & 31u));
-}
+// blocked Bloom filter over the same keys (BLOOM_WORDS dwords, 2 bits/key),
+// indexed straight from the (finalised) hash: word = top 13 bits, bits = the
+// two low 5-bit fields (the bucket index reuses the low bits; harmless)
+LDDL_HD uint32_t vbloom_word(uint32_t h) { return h >> 19; }
+LDDL_HD uint32_t vbloom_bits(uint32_t h) { return (1u << (h & 31u)) | (1u << ((h >> 5) & 31u)); }
 
 // ---- MT19937 (CPython random) ----------------------------------------------
 constexpr int MT_N = 624;

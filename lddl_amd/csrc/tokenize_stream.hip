@@ -255,7 +255,7 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
     if (dbg) acc[10] += 1;
     if (nb64 > CAP || ns > NSCAP) {
       if (lane == 0) fb_list[atomicAdd(fb_count, 1)] = (int32_t)t;
-      if (dbg) { acc[11] += 1; acc[12] += 1; }
+      if (dbg) acc[11] += 1;
       continue;
     }
     const int nb = (int)nb64;
@@ -278,9 +278,16 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
     uint4 v0 = make_uint4(0, 0, 0, 0), v1 = v0;
     {
       // 16-B aligned blocks holding >= 1 window byte: never past a page
-      const uint4* gp = reinterpret_cast<const uint4*>(wbase) + 2 * lane;
-      if (p0 < nb) v0 = gp[0];
-      if (p0 + 16 < nb) v1 = gp[1];
+      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+      const u32x4* gp = reinterpret_cast<const u32x4*>(wbase) + 2 * lane;
+      if (p0 < nb) {  // streamed once: non-temporal, keep L2 for the vocab table
+        const u32x4 a = __builtin_nontemporal_load(gp);
+        v0 = make_uint4(a.x, a.y, a.z, a.w);
+      }
+      if (p0 + 16 < nb) {
+        const u32x4 a = __builtin_nontemporal_load(gp + 1);
+        v1 = make_uint4(a.x, a.y, a.z, a.w);
+      }
     }
     *reinterpret_cast<uint4*>(&L.rp[lane * 8]) = v0;
     *reinterpret_cast<uint4*>(&L.rp[lane * 8 + 4]) = v1;
@@ -424,7 +431,7 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
     const int n = (int)tot;
     if (wbad) {
       if (lane == 0) fb_list[atomicAdd(fb_count, 1)] = (int32_t)t;
-      if (dbg) { acc[11] += 1; acc[13] += 1; }
+      if (dbg) acc[11] += 1;
       continue;
     }
     // units are processed in rounds of UCAP; a sentence running across two
@@ -579,6 +586,7 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
       for (;;) {
         if (__ballot(u >= 0) == 0 && next >= nwl) break;
         if (dbg) acc[9] += 1;
+        STAMP(4);
         if (u >= 0) {
           bool fail = false;
           if (slot < 0) {
@@ -617,6 +625,7 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
             if (found) slot = (int)(hcur & vmask);
             else fail = true;
           }
+          STAMP(12);
           if (fail) {
             pc[pb] = (uint16_t)P.unk;
             L.ucnt[u] = 1;
@@ -658,6 +667,7 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
             }
           }
         }
+        STAMP(13);
         const uint64_t idle = __ballot(u < 0);
         if (next < nwl) {
           if (u < 0) {
@@ -666,6 +676,7 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
           }
           next += __popcll(idle);
         }
+        STAMP(14);
       }
     }
     wsync();
