@@ -194,6 +194,47 @@ __device__ __forceinline__ bool long_eq(const WaveLds& L, const TokParams& P, in
   return true;
 }
 
+
+// the first min(len, 24) bytes at s as six little-endian dwords, zero beyond
+struct Key6 {
+  uint32_t d0, d1, d2, d3, d4, d5;
+};
+__device__ __forceinline__ Key6 load_key(const WaveLds& L, int s, int len) {
+  const int a = s >> 2;
+  const uint32_t sh = (uint32_t)(s & 3);
+  const uint32_t x0 = L.nb[a], x1 = L.nb[a + 1], x2 = L.nb[a + 2], x3 = L.nb[a + 3], x4 = L.nb[a + 4],
+                 x5 = L.nb[a + 5], x6 = L.nb[a + 6];
+  const int lc = min(len, 24);
+  auto m = [&](int i, uint32_t c) {
+    const int rem = lc - 4 * i;
+    return rem >= 4 ? c : rem <= 0 ? 0u : (c & ((1u << (8 * rem)) - 1u));
+  };
+  Key6 k;
+  k.d0 = m(0, __builtin_amdgcn_alignbyte(x1, x0, sh));
+  k.d1 = m(1, __builtin_amdgcn_alignbyte(x2, x1, sh));
+  k.d2 = m(2, __builtin_amdgcn_alignbyte(x3, x2, sh));
+  k.d3 = m(3, __builtin_amdgcn_alignbyte(x4, x3, sh));
+  k.d4 = m(4, __builtin_amdgcn_alignbyte(x5, x4, sh));
+  k.d5 = m(5, __builtin_amdgcn_alignbyte(x6, x5, sh));
+  return k;
+}
+// == vhash (common.h) of a loaded key
+__device__ __forceinline__ uint32_t key_hash(const Key6& k, int len, uint32_t cont) {
+  const int lc = min(len, 24);
+  uint32_t h = VSEED;
+  if (lc > 0) h = vmix(h, k.d0);
+  if (lc > 4) h = vmix(h, k.d1);
+  if (lc > 8) h = vmix(h, k.d2);
+  if (lc > 12) h = vmix(h, k.d3);
+  if (lc > 16) h = vmix(h, k.d4);
+  if (lc > 20) h = vmix(h, k.d5);
+  return vfinal(h, (uint32_t)len, cont);
+}
+__device__ __forceinline__ bool slot_eq(const uint4& a, const uint4& b, const Key6& k, uint32_t want) {
+  return (b.z & 0xFFFF0000u) == want && a.x == k.d0 && a.y == k.d1 && a.z == k.d2 && a.w == k.d3 && b.x == k.d4 &&
+         b.y == k.d5;
+}
+
 template <int WAVES, bool BLOOM, bool DBG>
 __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int64_t* tile_sent, int64_t n_tiles,
                                                           int32_t* fb_list, int32_t* fb_count) {
@@ -489,6 +530,59 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
       nwl += __popcll(bm);
     }
     wsync();
+    // ---- 3b: first probe of every pending unit (its whole word, the common
+    //      hit) with 4 bucket loads in flight per lane; hits leave the queue
+    {
+      const int mb0 = (int)P.maxb[0];
+      const uint32_t vmask = P.vt_mask;
+      auto bl_ok = [&](uint32_t h) {
+        if (!BLOOM) return true;
+        const uint32_t bb = vbloom_bits(h);
+        return (bloom[vbloom_word(h)] & bb) == bb;
+      };
+#define TOK4_FP_ISSUE(k)                                                       \
+  uint4 fa##k = make_uint4(0, 0, 0, 0), fb##k = fa##k;                         \
+  bool fact##k = false;                                                        \
+  {                                                                            \
+    const int u = (k) * 64 + lane;                                             \
+    const uint32_t w = u < nr ? L.uwp[u] : 0u;                                 \
+    const int len = (int)(w >> 20);                                            \
+    if (w != 0 && len <= 24 && len <= mb0) {                                   \
+      const uint32_t h = key_hash(load_key(L, (int)((w >> 8) & 0xFFFu), len), len, 0u); \
+      if (bl_ok(h)) {                                                          \
+        const uint4* bk = P.vt + 4 * (h & vmask);                              \
+        fa##k = bk[0];                                                         \
+        fb##k = bk[1];                                                         \
+        fact##k = true;                                                        \
+      }                                                                        \
+    }                                                                          \
+  }
+#define TOK4_FP_CHECK(k)                                                       \
+  if (fact##k) {                                                               \
+    const int u = (k) * 64 + lane;                                             \
+    const uint32_t w = L.uwp[u];                                               \
+    const int len = (int)(w >> 20);                                            \
+    const Key6 key = load_key(L, (int)((w >> 8) & 0xFFFu), len);               \
+    if (slot_eq(fa##k, fb##k, key, ((uint32_t)len << 16) | 0x80000000u)) {      \
+      pc[L.urec[u] & 0xFFFFu] = (uint16_t)(fb##k.z & 0xFFFFu);                 \
+      L.ucnt[u] = 1;                                                           \
+      L.uwp[u] = 0;                                                            \
+      if (dbg) acc[6] += 1;                                                    \
+    }                                                                          \
+  }
+      TOK4_FP_ISSUE(0)
+      TOK4_FP_ISSUE(1)
+      TOK4_FP_ISSUE(2)
+      TOK4_FP_ISSUE(3)
+      TOK4_FP_CHECK(0)
+      TOK4_FP_CHECK(1)
+      TOK4_FP_CHECK(2)
+      TOK4_FP_CHECK(3)
+#undef TOK4_FP_ISSUE
+#undef TOK4_FP_CHECK
+      static_assert(UCAP == 256, "first-probe batch is unrolled for 4 units per lane");
+    }
+    wsync();
     // work list (in place over uwp), longest first: long words are the OOV
     // ones needing many probes, and starting them first keeps the tail short
     {
@@ -594,23 +688,32 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
             int len = e - s;
             bool found = false;
             if (asc && len <= 24) {
-              // ASCII: every length is a char boundary; 4 lengths per step
-              while (len > 0) {
-                const uint32_t h0 = hash_len(len), h1 = hash_len(len - 1), h2 = hash_len(len - 2),
-                               h3 = hash_len(len - 3);
-                const bool o0 = bloom_ok(h0), o1 = len > 1 && bloom_ok(h1), o2 = len > 2 && bloom_ok(h2),
-                           o3 = len > 3 && bloom_ok(h3);
-                if (o0 | o1 | o2 | o3) {
-                  const int d = o0 ? 0 : o1 ? 1 : o2 ? 2 : 3;
-                  hcur = o0 ? h0 : o1 ? h1 : o2 ? h2 : h3;
-                  len -= d;
-                  found = true;
-                  break;
-                }
-                if (dbg) acc[7] += min(len, 4);
-                len -= 4;
-              }
-              e = s + max(len, 0);
+              // ASCII: every length is a char boundary.  Dword group k holds
+              // lengths 4k+1..4k+4, hashed from Hk / H(k+1) with constant
+              // register indices; groups from the top down.
+              int fl = 0;
+#define TOK4_GROUP(k, Hk, Hk1, ck)                                                                  \
+  if (fl == 0 && 4 * (k) < len) {                                                                   \
+    const uint32_t g4 = vfinal(Hk1, 4 * (k) + 4, cont), g3 = vfinal(vmix(Hk, (ck) & 0xFFFFFFu), 4 * (k) + 3, cont), \
+                   g2 = vfinal(vmix(Hk, (ck) & 0xFFFFu), 4 * (k) + 2, cont),                        \
+                   g1 = vfinal(vmix(Hk, (ck) & 0xFFu), 4 * (k) + 1, cont);                          \
+    const bool o4 = 4 * (k) + 4 <= len && bloom_ok(g4), o3 = 4 * (k) + 3 <= len && bloom_ok(g3),   \
+               o2 = 4 * (k) + 2 <= len && bloom_ok(g2), o1 = bloom_ok(g1);                          \
+    if (o4 | o3 | o2 | o1) {                                                                        \
+      fl = o4 ? 4 * (k) + 4 : o3 ? 4 * (k) + 3 : o2 ? 4 * (k) + 2 : 4 * (k) + 1;                    \
+      hcur = o4 ? g4 : o3 ? g3 : o2 ? g2 : g1;                                                      \
+    }                                                                                               \
+  }
+              TOK4_GROUP(5, H5, H6, c5)
+              TOK4_GROUP(4, H4, H5, c4)
+              TOK4_GROUP(3, H3, H4, c3)
+              TOK4_GROUP(2, H2, H3, c2)
+              TOK4_GROUP(1, H1, H2, c1)
+              TOK4_GROUP(0, H0, H1, c0)
+#undef TOK4_GROUP
+              if (dbg) acc[7] += len - fl;
+              found = fl > 0;
+              e = s + fl;
             } else {
               while (e > s) {
                 hcur = hash_len(e - s);
