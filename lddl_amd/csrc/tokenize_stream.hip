@@ -601,6 +601,7 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
           if (take) L.uwp[at + lane_rank(bm)] = ent[k];
           at += __popcll(bm);
         }
+      nwl = at;  // first-probe hits have left the queue
     }
     wsync();
     if (L.misc[2]) break;  // side buffer overflow: the whole tile falls back
