@@ -68,6 +68,7 @@ struct lddl_ctx {
   int64_t last_npairs = -1, last_ntok = -1;
   int64_t* h_tot = nullptr;  // pinned [8]
   int64_t last_nmask = -1;
+  int64_t last_nsent = 0, last_ndense = 0;  // sentences / tokens of the last pack (dense id array)
   uint16_t* last_tokens = nullptr;  // rows of the last lddl_materialize
   const int64_t* last_tok_off = nullptr;   // masked entries of the last pack (-1: no masking)
   uint64_t mlm_cap = 0;      // masking arena capacity that last sufficed
@@ -527,8 +528,15 @@ static int pack_common(lddl_ctx* c, int codebert, const int32_t* d_ntok, const i
       (rc = ws_get(c, 10, n_part, &P.part_npairs)) || (rc = ws_get(c, 11, n_part, &P.part_ntok)) ||
       (rc = ws_get(c, 12, (size_t)n_part * nbins, &P.bin_count)) ||
       (rc = ws_get(c, 13, (size_t)n_part * nbins, &P.bin_cursor)) ||
-      (rc = ws_get(c, 14, n_part, &P.part_err)) || (rc = ws_get(c, 18, n_sent + n_part + 1, &P.kept)))
+      (rc = ws_get(c, 14, n_part, &P.part_err)) || (rc = ws_get(c, 18, n_sent + n_part + 1, &P.kept)) ||
+      (rc = ws_get(c, 33, n_sent, &P.fs_dense)))
     return rc;
+  {  // dense id offsets: tokoff = exclusive scan of the token counts
+    int64_t *tokoff, *bsum;
+    if ((rc = ws_get(c, 31, n_sent + 1, &tokoff)) || (rc = ws_get(c, 32, scan_blocks(n_sent) + 1, &bsum))) return rc;
+    HIP_TRY(launch_scan_ntok(d_ntok, n_sent, tokoff, bsum, st));
+    P.tokoff = tokoff;
+  }
   int64_t *pair_base, *tok_base;
   int32_t* err_any;
   if ((rc = ws_get(c, 15, n_part + 1, &pair_base)) || (rc = ws_get(c, 16, n_part + 1, &tok_base)) ||
@@ -568,6 +576,7 @@ static int pack_common(lddl_ctx* c, int codebert, const int32_t* d_ntok, const i
     HIP_TRY(hipMemcpyAsync(c->h_tot, pair_base + n_part, 8, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipMemcpyAsync(c->h_tot + 1, tok_base + n_part, 8, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipMemcpyAsync(c->h_tot + 2, err_any, 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(c->h_tot + 5, P.tokoff + n_sent, 8, hipMemcpyDeviceToHost, st));
     if (masking) {
       HIP_TRY(launch_scan_parts(P.part_nmask, P.part_nmask, n_part, mask_base, mask_base2, P.part_err, err_any, st));
       HIP_TRY(hipMemcpyAsync(c->h_tot + 3, mask_base + n_part, 8, hipMemcpyDeviceToHost, st));
@@ -590,6 +599,8 @@ static int pack_common(lddl_ctx* c, int codebert, const int32_t* d_ntok, const i
   if (e & PACK_EASSERT) { c->last_npairs = -1; return set_err(LDDL_EASSERT, "AssertionError: empty segment after truncation"); }
   c->last_npairs = c->h_tot[0];
   c->last_ntok = c->h_tot[1];
+  c->last_nsent = n_sent;
+  c->last_ndense = c->h_tot[5];
   out_totals[0] = c->last_npairs;
   out_totals[1] = c->last_ntok;
   out_totals[2] = nbins;
@@ -630,6 +641,12 @@ extern "C" int lddl_materialize(lddl_ctx* c, const uint16_t* d_ids, uint16_t* d_
   const PackParams& P = c->pp;
   MatParams M{};
   M.ids = d_ids;
+  uint16_t* dense;
+  int rc;
+  if ((rc = ws_get(c, 34, (size_t)c->last_ndense + 1, &dense))) return rc;
+  HIP_TRY(launch_compact_ids(d_ids, P.sent_off, P.ntok, P.tokoff, c->last_nsent, dense, st));
+  M.dense = dense;
+  M.fs_dense = P.fs_dense;
   M.sent_off = P.sent_off;
   M.doc_sent_off = P.doc_sent_off;
   M.part_doc_off = P.part_doc_off;

@@ -37,7 +37,9 @@ struct PackParams {
   int32_t nbins;                // max_seq // bin_size (1 when unbinned)
   // scratch, indexed like the corpus (sentence / doc / partition slots)
   int32_t* fs_ntok;             // [n_sent]
-  int64_t* fs_base;             // [n_sent]
+  int64_t* fs_base;             // [n_sent] sparse id offset (sent_off - base) per filtered slot
+  int64_t* fs_dense;            // [n_sent] dense id offset (tokoff) per filtered slot
+  const int64_t* tokoff;        // [n_sent+1] exclusive scan of ntok: sentence s's ids in the dense array
   int64_t* fd_first;            // [n_doc]
   int32_t* fd_n;                // [n_doc]
   int32_t* fd_nd;               // [n_doc] CodeBERT docstring segment count
@@ -92,6 +94,8 @@ struct MlmParams {
 
 struct MatParams {
   const uint16_t* ids;          // tokenizer output (sparse)
+  const uint16_t* dense;        // the same ids compacted per sentence (tokoff)
+  const int64_t* fs_dense;      // dense offset per filtered slot
   const int64_t* sent_off;
   const int64_t* doc_sent_off;
   const int64_t* part_doc_off;
@@ -124,6 +128,13 @@ hipError_t launch_pack_codebert(const PackParams& P, hipStream_t s);
 hipError_t launch_scan_parts(const int64_t* a, const int64_t* b, int64_t n, int64_t* sa, int64_t* sb,
                              const int32_t* err, int32_t* err_any, hipStream_t s);
 hipError_t launch_materialize(const MatParams& M, hipStream_t s);
+// tokoff[0..n] = exclusive scan of ntok[0..n) (int64); blocksums: scratch of
+// scan_blocks(n) + 1 entries
+int64_t scan_blocks(int64_t n);
+hipError_t launch_scan_ntok(const int32_t* ntok, int64_t n, int64_t* tokoff, int64_t* blocksums, hipStream_t s);
+// dense[tokoff[s] + k] = ids[sent_off[s] - sent_off[0] + k], k < ntok[s]
+hipError_t launch_compact_ids(const uint16_t* ids, const int64_t* sent_off, const int32_t* ntok,
+                              const int64_t* tokoff, int64_t n_sent, uint16_t* dense, hipStream_t s);
 hipError_t launch_sent_special(const uint16_t* ids, const int64_t* sent_off, const int32_t* ntok, int64_t n_sent,
                                uint32_t cls, uint32_t sep, uint8_t* out, hipStream_t s);
 hipError_t launch_masked_lm(const MlmParams& M, hipStream_t s);

@@ -49,6 +49,7 @@ __device__ PartView filter_partition(const PackParams& P, int64_t p, bool codebe
       if (n > 0) {
         P.fs_ntok[slot] = n;
         P.fs_base[slot] = P.sent_off[s] - base;
+        P.fs_dense[slot] = P.tokoff[s];
         ++slot;
         if (s < sdoc_end) ++ndoc_seg;
       }
@@ -327,54 +328,213 @@ __global__ __launch_bounds__(1024) void scan_parts_kernel(const int64_t* a, cons
 }
 
 // ----------------------------------------------------- materialise ----
-__device__ __forceinline__ void copy_segment(const MatParams& M, int64_t fs, int32_t n, int32_t lo, int32_t hi,
-                                             uint16_t* out, int lane) {
-  int32_t acc = 0;
-  for (int32_t j = 0; j < n && acc < hi; ++j) {
-    const int32_t len = M.fs_ntok[fs + j];
-    const int64_t base = M.fs_base[fs + j];
-    const int32_t a = max(lo, acc), b = min(hi, acc + len);
-    for (int32_t t = a + lane; t < b; t += 64) out[t - lo] = M.ids[base + (t - acc)];
-    acc += len;
+// A segment is n consecutive filtered sentences cut to [lo, hi); in the dense
+// id array (sentences' ids back to back) that is ONE run starting at
+// fs_dense[fs] + lo.  One wave per partition (no row -> partition search):
+// chunks of 64 rows are staged in LDS (record, offsets, runs), then copied by
+// half-waves, one row each, 16 tokens per lane in flight.
+struct RowStage {
+  int64_t off;        // first output token of the row
+  int64_t src0, src1; // dense offsets of segment 0 / 1
+  int32_t l0, l1;     // segment lengths
+  int32_t nt;         // num_tokens
+  int32_t seg0;       // [SEP] after segment 0
+};
+
+__global__ __launch_bounds__(256) void materialize_kernel(MatParams M) {
+  __shared__ RowStage st[4][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t total = M.pair_base[M.n_part];
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t p = (int64_t)blockIdx.x * 4 + wv; p < M.n_part; p += nw) {
+    const int64_t s0 = M.doc_sent_off[M.part_doc_off[p]];
+    const int64_t pb = (int64_t)M.dup * s0;
+    const int64_t g0 = M.pair_base[p], np = M.pair_base[p + 1] - g0, tb = M.tok_base[p];
+    for (int64_t c = 0; c < np; c += 64) {
+      const int64_t i = c + lane;
+      if (i < np) {
+        const PairRec r = M.pairs[pb + M.binned[pb + i]];
+        const int64_t off = tb + M.tok_local[pb + i];
+        const int32_t l0 = r.hi0 - r.lo0, l1 = r.hi1 - r.lo1;
+        const int64_t g = g0 + i;
+        RowStage& x = st[wv][lane];
+        x.off = off;
+        x.src0 = l0 > 0 ? M.fs_dense[r.fs0] + r.lo0 : 0;
+        x.src1 = l1 > 0 ? M.fs_dense[r.fs1] + r.lo1 : 0;
+        x.l0 = l0;
+        x.l1 = l1;
+        x.nt = r.num_tokens;
+        x.seg0 = (r.flags & 2) != 0;
+        M.out_tok_off[g] = off;
+        M.out_len0[g] = (uint16_t)l0;
+        M.out_len1[g] = (uint16_t)l1;
+        M.out_flags[g] = (uint8_t)r.flags;
+        const int32_t b = ((int32_t)r.num_tokens - 1) / M.bin_size;
+        M.out_bin[g] = (uint8_t)(b > M.nbins - 1 ? M.nbins - 1 : b);
+        M.out_part[g] = p;
+        if (g == total - 1) M.out_tok_off[total] = off + r.num_tokens;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const int nr = (int)min((int64_t)64, np - c);
+      const int hl = lane & 31;
+      for (int r0 = 0; r0 < nr; r0 += 2) {
+        const int rr = r0 + (lane >> 5);
+        if (rr >= nr) continue;
+        const RowStage x = st[wv][rr];
+        uint16_t* out = M.out_tokens + x.off;
+        const int b1 = 1 + x.l0 + x.seg0;  // first token of segment 1
+        for (int t0 = 0; t0 < x.nt; t0 += 512) {
+          uint16_t v[16];
+#pragma unroll
+          for (int k = 0; k < 16; ++k) {
+            const int t = t0 + hl + 32 * k;
+            uint16_t y = (uint16_t)M.sep_id;
+            if (t == 0) y = (uint16_t)M.cls_id;
+            else if (t <= x.l0) y = M.dense[x.src0 + (t - 1)];
+            else if (t >= b1 && t < b1 + x.l1) y = M.dense[x.src1 + (t - b1)];
+            v[k] = y;
+          }
+#pragma unroll
+          for (int k = 0; k < 16; ++k) {
+            const int t = t0 + hl + 32 * k;
+            if (t < x.nt) out[t] = v[k];
+          }
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
   }
 }
 
-__global__ __launch_bounds__(256) void materialize_kernel(MatParams M) {
-  const int lane = threadIdx.x & 63;
-  const int64_t total = M.pair_base[M.n_part];
-  const int64_t nw = (int64_t)gridDim.x * 4;
-  for (int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); g < total; g += nw) {
-    // partition of pair g: last p with pair_base[p] <= g
-    int64_t lo = 0, hi = M.n_part;
-    while (hi - lo > 1) {
-      const int64_t mid = (lo + hi) >> 1;
-      if (M.pair_base[mid] <= g) lo = mid; else hi = mid;
-    }
-    const int64_t p = lo;
-    const int64_t i = g - M.pair_base[p];
-    const int64_t s0 = M.doc_sent_off[M.part_doc_off[p]];
-    const int64_t pb = (int64_t)M.dup * s0;
-    const PairRec r = M.pairs[pb + M.binned[pb + i]];
-    const int64_t off = M.tok_base[p] + M.tok_local[pb + i];
-    uint16_t* out = M.out_tokens + off;
-    const int32_t l0 = r.hi0 - r.lo0, l1 = r.hi1 - r.lo1;
-    const bool seg0 = (r.flags & 2) != 0;  // [SEP] after segment 0
-    if (lane == 0) {
-      out[0] = (uint16_t)M.cls_id;
-      if (seg0) out[1 + l0] = (uint16_t)M.sep_id;
-      out[r.num_tokens - 1] = (uint16_t)M.sep_id;
-      M.out_tok_off[g] = off;
-      M.out_len0[g] = (uint16_t)l0;
-      M.out_len1[g] = (uint16_t)l1;
-      M.out_flags[g] = (uint8_t)r.flags;
-      int32_t b = ((int32_t)r.num_tokens - 1) / M.bin_size;
-      M.out_bin[g] = (uint8_t)(b > M.nbins - 1 ? M.nbins - 1 : b);
-      M.out_part[g] = p;
-      if (g == total - 1) M.out_tok_off[total] = off + r.num_tokens;
-    }
-    copy_segment(M, r.fs0, r.n0, r.lo0, r.hi0, out + 1, lane);
-    copy_segment(M, r.fs1, r.n1, r.lo1, r.hi1, out + 1 + l0 + (seg0 ? 1 : 0), lane);
+// ------------------------------------------------ dense id compaction ----
+constexpr int SCAN_ITEMS = 4096;  // ntok entries per scan block (256 x 16)
+
+int64_t scan_blocks(int64_t n) { return (n + SCAN_ITEMS - 1) / SCAN_ITEMS; }
+
+__device__ __forceinline__ int64_t block_excl_scan256(int64_t v, int64_t* red, int64_t* total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int64_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int64_t y = __shfl_up(x, o);
+    if (lane >= o) x += y;
   }
+  if (lane == 63) red[w] = x;
+  __syncthreads();
+  int64_t pre = 0, tot = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if (k < w) pre += red[k];
+    tot += red[k];
+  }
+  __syncthreads();
+  *total = tot;
+  return pre + x - v;
+}
+
+__global__ __launch_bounds__(256) void scan_reduce_kernel(const int32_t* ntok, int64_t n, int64_t* bsum) {
+  __shared__ int64_t red[4];
+  const int64_t b0 = (int64_t)blockIdx.x * SCAN_ITEMS;
+  int64_t sum = 0;
+  for (int k = threadIdx.x; k < SCAN_ITEMS; k += 256)
+    if (b0 + k < n) sum += ntok[b0 + k];
+  int64_t tot;
+  block_excl_scan256(sum, red, &tot);
+  if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
+}
+
+// exclusive scan of the block sums in place (one block), bsum[nb] = total
+__global__ __launch_bounds__(256) void scan_bsum_kernel(int64_t* bsum, int64_t nb) {
+  __shared__ int64_t red[4];
+  int64_t carry = 0;
+  for (int64_t c = 0; c < nb; c += 256) {
+    const int64_t i = c + threadIdx.x;
+    const int64_t v = i < nb ? bsum[i] : 0;
+    int64_t tot;
+    const int64_t ex = block_excl_scan256(v, red, &tot);
+    if (i < nb) bsum[i] = carry + ex;
+    carry += tot;
+  }
+  if (threadIdx.x == 0) bsum[nb] = carry;
+}
+
+__global__ __launch_bounds__(256) void scan_write_kernel(const int32_t* ntok, int64_t n, const int64_t* bsum,
+                                                         int64_t* tokoff) {
+  __shared__ int64_t red[4];
+  const int64_t b0 = (int64_t)blockIdx.x * SCAN_ITEMS + threadIdx.x * 16;
+  int32_t v[16];
+  int64_t sum = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    v[k] = b0 + k < n ? ntok[b0 + k] : 0;
+    sum += v[k];
+  }
+  int64_t tot;
+  int64_t run = bsum[blockIdx.x] + block_excl_scan256(sum, red, &tot);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    if (b0 + k < n) tokoff[b0 + k] = run;
+    run += v[k];
+  }
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) tokoff[n] = bsum[gridDim.x];
+}
+
+hipError_t launch_scan_ntok(const int32_t* ntok, int64_t n, int64_t* tokoff, int64_t* blocksums, hipStream_t s) {
+  const int64_t nb = scan_blocks(n);
+  if (nb == 0) return hipMemsetAsync(tokoff, 0, sizeof(int64_t), s);
+  hipLaunchKernelGGL(scan_reduce_kernel, dim3((unsigned)nb), dim3(256), 0, s, ntok, n, blocksums);
+  hipLaunchKernelGGL(scan_bsum_kernel, dim3(1), dim3(256), 0, s, blocksums, nb);
+  hipLaunchKernelGGL(scan_write_kernel, dim3((unsigned)nb), dim3(256), 0, s, ntok, n, (const int64_t*)blocksums, tokoff);
+  return hipGetLastError();
+}
+
+// wave per 64 sentences, 8 sentences' copies in flight per step
+__global__ __launch_bounds__(256) void compact_ids_kernel(const uint16_t* ids, const int64_t* sent_off,
+                                                          const int32_t* ntok, const int64_t* tokoff, int64_t n_sent,
+                                                          uint16_t* dense) {
+  const int lane = threadIdx.x & 63;
+  const int64_t base = sent_off[0];
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t s0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64; s0 < n_sent; s0 += nw * 64) {
+    const int64_t s = s0 + lane;
+    int64_t so = 0, to = 0;
+    int nt = 0;
+    if (s < n_sent) {
+      so = sent_off[s] - base;
+      to = tokoff[s];
+      nt = ntok[s];
+    }
+    for (int j0 = 0; j0 < 64; j0 += 8) {
+      uint16_t v[8];
+      int64_t dst[8];
+      int n[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int64_t sq = __shfl(so, j0 + q), tq = __shfl(to, j0 + q);
+        n[q] = __shfl(nt, j0 + q);
+        dst[q] = tq;
+        v[q] = lane < n[q] ? ids[sq + lane] : (uint16_t)0;
+        for (int t = 64 + lane; t < n[q]; t += 64) dense[tq + t] = ids[sq + t];  // long sentences
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        if (lane < n[q]) dense[dst[q] + lane] = v[q];
+    }
+  }
+}
+
+hipError_t launch_compact_ids(const uint16_t* ids, const int64_t* sent_off, const int32_t* ntok,
+                              const int64_t* tokoff, int64_t n_sent, uint16_t* dense, hipStream_t s) {
+  if (n_sent <= 0) return hipSuccess;
+  int64_t grid = (n_sent + 255) / 256;
+  if (grid > 8192) grid = 8192;
+  hipLaunchKernelGGL(compact_ids_kernel, dim3((unsigned)grid), dim3(256), 0, s, ids, sent_off, ntok, tokoff, n_sent,
+                     dense);
+  return hipGetLastError();
 }
 
 hipError_t launch_pack_bert(const PackParams& P, hipStream_t s) {
@@ -464,7 +624,8 @@ hipError_t launch_masked_lm(const MlmParams& M, hipStream_t s) {
 }
 
 hipError_t launch_materialize(const MatParams& M, hipStream_t s) {
-  hipLaunchKernelGGL(materialize_kernel, dim3(2048), dim3(256), 0, s, M);
+  const int64_t grid = (M.n_part + 3) / 4;  // one wave per partition
+  hipLaunchKernelGGL(materialize_kernel, dim3((unsigned)grid), dim3(256), 0, s, M);
   return hipGetLastError();
 }
 

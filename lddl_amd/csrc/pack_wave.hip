@@ -225,6 +225,7 @@ __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
         if (keep) {
           P.fs_ntok[s0 + slot] = n;
           P.fs_base[s0 + slot] = P.sent_off[s0 + kk] - base;
+          P.fs_dense[s0 + slot] = P.tokoff[s0 + kk];
           if (MASK) P.fs_spec[s0 + slot] = P.sent_spec[s0 + kk];
         }
       }
