@@ -11,6 +11,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -565,6 +566,27 @@ static int pack_common(lddl_ctx* c, int codebert, const int32_t* d_ntok, const i
   }
   const char* palgo = getenv("LDDL_PACK_ALGO");
   const bool lane_packer = !masking && palgo && palgo[0] == '1';
+  if (!codebert && !lane_packer) {
+    // wave packer LDS: size the per-partition arrays from the largest
+    // partition, within ~53 KiB per workgroup (3 resident per CU)
+    int32_t* dims;
+    if ((rc = ws_get(c, 35, 2, &dims))) return rc;
+    HIP_TRY(launch_part_max(d_part_doc_off, d_doc_sent_off, n_part, dims, st));
+    HIP_TRY(hipMemcpyAsync(c->h_tot + 6, dims, 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    const int32_t* hd = reinterpret_cast<const int32_t*>(c->h_tot + 6);
+    auto up64 = [](int64_t x) { return (int32_t)((x + 63) / 64 * 64); };
+    const int64_t budget = 53 * 1024 - 5248 - (masking ? 4 * MLM_MAX_SEQ * 2 : 0);
+    P.cap_lens = up64(hd[0]);
+    P.cap_docs = up64(hd[1]);
+    int64_t rest = budget - (int64_t)pack_dyn_bytes(P.cap_lens, P.cap_docs, 0, masking != 0);
+    if (rest < 4096) {  // huge partitions: sentence arrays stay in global memory
+      P.cap_lens = 0;
+      P.cap_docs = 0;
+      rest = budget - (int64_t)pack_dyn_bytes(0, 0, 0, masking != 0);
+    }
+    P.cap_pairs = (int32_t)std::min<int64_t>(rest / 4 / 64 * 64, 65472);
+  }
   for (int attempt = 0;; ++attempt) {
     if (masking) {
       if ((rc = ws_get(c, 30, c->mlm_cap, &P.marena))) return rc;

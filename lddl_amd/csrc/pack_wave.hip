@@ -25,20 +25,23 @@
 
 namespace lddl {
 
-constexpr int PW_LENS = 4096;   // filtered sentences resident in LDS
-constexpr int PW_DOCS = 1024;   // filtered documents resident in LDS
-constexpr int PW_PAIRS = 4096;  // pairs resident in LDS (order + num_tokens)
-
+// Per-partition arrays live in dynamic LDS sized by the host from the largest
+// partition (PackParams cap_*); a partition that does not fit runs the same
+// code on global memory (wave-uniform branch).
 struct PackWaveLds {
   uint32_t mt[MT_N];
   uint32_t tw[MT_N];            // tempered outputs of the current state
-  uint16_t lens[PW_LENS];
-  uint16_t dfirst[PW_DOCS];     // relative to the partition's first slot
-  uint16_t dn[PW_DOCS];
-  uint16_t order[PW_PAIRS];
-  uint16_t ntk[PW_PAIRS];       // num_tokens per pair record
   int32_t red[64];
 };
+struct PackDyn {                // views into the dynamic LDS region
+  uint16_t* lens;               // [cap_lens] filtered sentence lengths
+  uint16_t* dfirst;             // [cap_docs] relative to the partition's first slot
+  uint16_t* dn;                 // [cap_docs]
+  uint16_t* order;              // [cap_pairs] shuffle order
+  uint16_t* ntk;                // [cap_pairs] num_tokens per pair record
+  uint32_t* spec;               // [cap_lens / 32 + 2] (masking) slot holds a [CLS]/[SEP] token
+};
+extern __shared__ __attribute__((aligned(16))) uint8_t pw_dyn[];
 
 // static masking lists (MASK instantiation only)
 struct MaskLds {
@@ -46,9 +49,12 @@ struct MaskLds {
   uint16_t jb[MLM_MAX_SEQ];     // shuffle draws: swap x[i] <-> x[jb[i]]
   uint16_t mpos[MLM_MAX_SEQ];   // picked positions in pick order
   uint16_t mid[MLM_MAX_SEQ];    // their replacement ids (MLM_KEEP = unchanged)
-  uint32_t spec[PW_LENS / 32];  // filtered slot holds a [CLS]/[SEP] token
 };
 struct NoMaskLds {};
+
+size_t pack_dyn_bytes(int cap_lens, int cap_docs, int cap_pairs, bool mask) {
+  return 2 * (size_t)cap_lens + 4 * (size_t)cap_docs + 4 * (size_t)cap_pairs + (mask ? 4 * (size_t)(cap_lens / 32 + 2) : 0);
+}
 
 __device__ __forceinline__ void wsync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -199,6 +205,13 @@ template <bool MASK>
 __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
   __shared__ PackWaveLds L;
   __shared__ typename std::conditional<MASK, MaskLds, NoMaskLds>::type ML;
+  PackDyn D;
+  D.lens = reinterpret_cast<uint16_t*>(pw_dyn);
+  D.dfirst = D.lens + P.cap_lens;
+  D.dn = D.dfirst + P.cap_docs;
+  D.order = D.dn + P.cap_docs;
+  D.ntk = D.order + P.cap_pairs;
+  D.spec = reinterpret_cast<uint32_t*>(D.ntk + P.cap_pairs);
   const int lane = threadIdx.x;
   const int64_t p = blockIdx.x;
   if (p >= P.n_part) return;
@@ -260,25 +273,25 @@ __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __builtin_amdgcn_s_waitcnt(0);
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-  const bool lres = nfs <= PW_LENS && nd <= PW_DOCS;
+  const bool lres = nfs <= P.cap_lens && nd <= P.cap_docs;
   if (lres) {
-    for (int k = lane; k < nfs; k += 64) L.lens[k] = (uint16_t)P.fs_ntok[s0 + k];
+    for (int k = lane; k < nfs; k += 64) D.lens[k] = (uint16_t)P.fs_ntok[s0 + k];
     for (int k = lane; k < nd; k += 64) {
-      L.dfirst[k] = (uint16_t)(P.fd_first[d0 + k] - s0);
-      L.dn[k] = (uint16_t)P.fd_n[d0 + k];
+      D.dfirst[k] = (uint16_t)(P.fd_first[d0 + k] - s0);
+      D.dn[k] = (uint16_t)P.fd_n[d0 + k];
     }
     if constexpr (MASK) {
       for (int k = 0; k < nfs; k += 64) {
         const uint64_t m = __ballot(k + lane < nfs && P.fs_spec[s0 + k + lane] != 0);
-        if (lane == 0) { ML.spec[k >> 5] = (uint32_t)m; if ((k >> 5) + 1 < PW_LENS / 32) ML.spec[(k >> 5) + 1] = (uint32_t)(m >> 32); }
+        if (lane == 0) { D.spec[k >> 5] = (uint32_t)m; D.spec[(k >> 5) + 1] = (uint32_t)(m >> 32); }
       }
     }
   }
   wsync();
   // slot-relative accessors
-  auto len_at = [&](int k) -> int { return lres ? (int)L.lens[k] : P.fs_ntok[s0 + k]; };
-  auto doc_first = [&](int d) -> int { return lres ? (int)L.dfirst[d] : (int)(P.fd_first[d0 + d] - s0); };
-  auto doc_n = [&](int d) -> int { return lres ? (int)L.dn[d] : P.fd_n[d0 + d]; };
+  auto len_at = [&](int k) -> int { return lres ? (int)D.lens[k] : P.fs_ntok[s0 + k]; };
+  auto doc_first = [&](int d) -> int { return lres ? (int)D.dfirst[d] : (int)(P.fd_first[d0 + d] - s0); };
+  auto doc_n = [&](int d) -> int { return lres ? (int)D.dn[d] : P.fd_n[d0 + d]; };
 
   WaveRng rng{L, lane, MT_N};
   rng.seed(P.seed + (uint64_t)p);
@@ -286,7 +299,7 @@ __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
   PairRec* out = P.pairs + pb;
   int np = 0;
   int err = PACK_OK;
-  const int pcap = PW_PAIRS;
+  const int pcap = P.cap_pairs;
   int64_t mcur = 0, mend = 0;  // this partition's current arena chunk
   int nmask_part = 0;
   (void)mcur; (void)mend; (void)nmask_part;
@@ -297,7 +310,7 @@ __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
       for (int k = 0; k < n; k += 64) {
         const int kk = k0 + k + lane;
         bool x = false;
-        if (k + lane < n) x = lres ? ((ML.spec[kk >> 5] >> (kk & 31)) & 1u) != 0 : P.fs_spec[s0 + kk] != 0;
+        if (k + lane < n) x = lres ? ((D.spec[kk >> 5] >> (kk & 31)) & 1u) != 0 : P.fs_spec[s0 + kk] != 0;
         if (__ballot(x)) { f = true; break; }
       }
     }
@@ -463,7 +476,7 @@ __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
         }
         if (lane == 0) {
           out[np] = r;
-          if (np < pcap) L.ntk[np] = r.num_tokens;
+          if (np < pcap) D.ntk[np] = r.num_tokens;
           if (MASK) P.mref[pb + np] = mref;
         }
         ++np;
@@ -480,24 +493,24 @@ __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
   // ---- random.shuffle(partition_pairs) -----------------------------------
   const bool ores = np <= pcap;
   int32_t* gorder = P.order + pb;
-  if (ores) for (int k = lane; k < np; k += 64) L.order[k] = (uint16_t)k;
+  if (ores) for (int k = lane; k < np; k += 64) D.order[k] = (uint16_t)k;
   else for (int k = lane; k < np; k += 64) gorder[k] = k;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __builtin_amdgcn_s_waitcnt(0);
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  // lane 0 alone touches the order array here (program order suffices)
   for (int k = np - 1; k >= 1; --k) {
     const int j = (int)rng.randbelow((uint32_t)(k + 1));
     if (lane == 0) {
-      if (ores) { const uint16_t t = L.order[k]; L.order[k] = L.order[j]; L.order[j] = t; }
+      if (ores) { const uint16_t t = D.order[k]; D.order[k] = D.order[j]; D.order[j] = t; }
       else { const int32_t t = gorder[k]; gorder[k] = gorder[j]; gorder[j] = t; }
     }
-    wsync();
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __builtin_amdgcn_s_waitcnt(0);
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-  auto ord_at = [&](int k) -> int { return ores ? (int)L.order[k] : gorder[k]; };
-  auto ntk_at = [&](int rec) -> int { return ores ? (int)L.ntk[rec] : (int)out[rec].num_tokens; };
+  auto ord_at = [&](int k) -> int { return ores ? (int)D.order[k] : gorder[k]; };
+  auto ntk_at = [&](int rec) -> int { return ores ? (int)D.ntk[rec] : (int)out[rec].num_tokens; };
   // ---- stable bin partition + token offsets -------------------------------
   const int nb = P.nbins;
   int32_t* binned = P.binned + pb;
@@ -543,11 +556,33 @@ __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
   }
 }
 
+// largest partition (sentences, documents) -> dims[0..1] (atomicMax)
+__global__ void part_max_kernel(const int64_t* part_doc_off, const int64_t* doc_sent_off, int64_t n_part,
+                                int32_t* dims) {
+  int32_t ms = 0, md = 0;
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n_part; p += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t d0 = part_doc_off[p], d1 = part_doc_off[p + 1];
+    ms = max(ms, (int32_t)min(doc_sent_off[d1] - doc_sent_off[d0], (int64_t)INT32_MAX));
+    md = max(md, (int32_t)min(d1 - d0, (int64_t)INT32_MAX));
+  }
+  atomicMax(&dims[0], ms);
+  atomicMax(&dims[1], md);
+}
+
+hipError_t launch_part_max(const int64_t* part_doc_off, const int64_t* doc_sent_off, int64_t n_part, int32_t* dims,
+                           hipStream_t s) {
+  hipError_t e = hipMemsetAsync(dims, 0, 8, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(part_max_kernel, dim3(256), dim3(256), 0, s, part_doc_off, doc_sent_off, n_part, dims);
+  return hipGetLastError();
+}
+
 hipError_t launch_pack_bert_wave(const PackParams& P, hipStream_t s) {
+  const size_t dyn = pack_dyn_bytes(P.cap_lens, P.cap_docs, P.cap_pairs, P.masking != 0);
   if (P.masking)
-    hipLaunchKernelGGL(pack_bert_wave_kernel<true>, dim3((unsigned)P.n_part), dim3(64), 0, s, P);
+    hipLaunchKernelGGL(pack_bert_wave_kernel<true>, dim3((unsigned)P.n_part), dim3(64), dyn, s, P);
   else
-    hipLaunchKernelGGL(pack_bert_wave_kernel<false>, dim3((unsigned)P.n_part), dim3(64), 0, s, P);
+    hipLaunchKernelGGL(pack_bert_wave_kernel<false>, dim3((unsigned)P.n_part), dim3(64), dyn, s, P);
   return hipGetLastError();
 }
 
