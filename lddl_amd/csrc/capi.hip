@@ -586,6 +586,15 @@ static int pack_common(lddl_ctx* c, int codebert, const int32_t* d_ntok, const i
       rest = budget - (int64_t)pack_dyn_bytes(0, 0, 0, masking != 0);
     }
     P.cap_pairs = (int32_t)std::min<int64_t>(rest / 4 / 64 * 64, 65472);
+    const char* caps = getenv("LDDL_PACK_CAPS");  // "lens,docs,pairs" override (tuning)
+    if (caps) {
+      int a = 0, b = 0, d = 0;
+      if (sscanf(caps, "%d,%d,%d", &a, &b, &d) == 3) {
+        P.cap_lens = a / 64 * 64;
+        P.cap_docs = b / 64 * 64;
+        P.cap_pairs = std::min(d / 64 * 64, 65472);
+      }
+    }
   }
   for (int attempt = 0;; ++attempt) {
     if (masking) {
