@@ -567,25 +567,14 @@ static int pack_common(lddl_ctx* c, int codebert, const int32_t* d_ntok, const i
   const char* palgo = getenv("LDDL_PACK_ALGO");
   const bool lane_packer = !masking && palgo && palgo[0] == '1';
   if (!codebert && !lane_packer) {
-    // wave packer LDS: size the per-partition arrays from the largest
-    // partition, within ~53 KiB per workgroup (3 resident per CU)
-    int32_t* dims;
-    if ((rc = ws_get(c, 35, 2, &dims))) return rc;
-    HIP_TRY(launch_part_max(d_part_doc_off, d_doc_sent_off, n_part, dims, st));
-    HIP_TRY(hipMemcpyAsync(c->h_tot + 6, dims, 8, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
-    const int32_t* hd = reinterpret_cast<const int32_t*>(c->h_tot + 6);
-    auto up64 = [](int64_t x) { return (int32_t)((x + 63) / 64 * 64); };
-    const int64_t budget = 53 * 1024 - 5248 - (masking ? 4 * MLM_MAX_SEQ * 2 : 0);
-    P.cap_lens = up64(hd[0]);
-    P.cap_docs = up64(hd[1]);
-    int64_t rest = budget - (int64_t)pack_dyn_bytes(P.cap_lens, P.cap_docs, 0, masking != 0);
-    if (rest < 4096) {  // huge partitions: sentence arrays stay in global memory
-      P.cap_lens = 0;
-      P.cap_docs = 0;
-      rest = budget - (int64_t)pack_dyn_bytes(0, 0, 0, masking != 0);
-    }
-    P.cap_pairs = (int32_t)std::min<int64_t>(rest / 4 / 64 * 64, 65472);
+    // Wave packer: one 64-lane workgroup per partition runs a serial chain, so
+    // throughput is partitions in flight; measured on the bench workload the
+    // per-partition arrays are best left in global memory (L2), keeping the
+    // workgroup at ~5 KiB of LDS (~30 partitions per CU): 65 ms against 250 ms
+    // with 4 partitions per CU.  LDDL_PACK_CAPS=lens,docs,pairs puts them in LDS.
+    P.cap_lens = 0;
+    P.cap_docs = 0;
+    P.cap_pairs = 0;
     const char* caps = getenv("LDDL_PACK_CAPS");  // "lens,docs,pairs" override (tuning)
     if (caps) {
       int a = 0, b = 0, d = 0;

@@ -126,8 +126,6 @@ struct MatParams {
 hipError_t launch_pack_bert(const PackParams& P, hipStream_t s);
 hipError_t launch_pack_bert_wave(const PackParams& P, hipStream_t s);
 size_t pack_dyn_bytes(int cap_lens, int cap_docs, int cap_pairs, bool mask);
-hipError_t launch_part_max(const int64_t* part_doc_off, const int64_t* doc_sent_off, int64_t n_part, int32_t* dims,
-                           hipStream_t s);
 hipError_t launch_pack_codebert(const PackParams& P, hipStream_t s);
 hipError_t launch_scan_parts(const int64_t* a, const int64_t* b, int64_t n, int64_t* sa, int64_t* sb,
                              const int32_t* err, int32_t* err_any, hipStream_t s);

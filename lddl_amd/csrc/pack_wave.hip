@@ -556,27 +556,6 @@ __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
   }
 }
 
-// largest partition (sentences, documents) -> dims[0..1] (atomicMax)
-__global__ void part_max_kernel(const int64_t* part_doc_off, const int64_t* doc_sent_off, int64_t n_part,
-                                int32_t* dims) {
-  int32_t ms = 0, md = 0;
-  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n_part; p += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t d0 = part_doc_off[p], d1 = part_doc_off[p + 1];
-    ms = max(ms, (int32_t)min(doc_sent_off[d1] - doc_sent_off[d0], (int64_t)INT32_MAX));
-    md = max(md, (int32_t)min(d1 - d0, (int64_t)INT32_MAX));
-  }
-  atomicMax(&dims[0], ms);
-  atomicMax(&dims[1], md);
-}
-
-hipError_t launch_part_max(const int64_t* part_doc_off, const int64_t* doc_sent_off, int64_t n_part, int32_t* dims,
-                           hipStream_t s) {
-  hipError_t e = hipMemsetAsync(dims, 0, 8, s);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(part_max_kernel, dim3(256), dim3(256), 0, s, part_doc_off, doc_sent_off, n_part, dims);
-  return hipGetLastError();
-}
-
 hipError_t launch_pack_bert_wave(const PackParams& P, hipStream_t s) {
   const size_t dyn = pack_dyn_bytes(P.cap_lens, P.cap_docs, P.cap_pairs, P.masking != 0);
   if (P.masking)

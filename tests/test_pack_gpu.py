@@ -86,9 +86,15 @@ def test_codebert_golden(cpacker, k):
     assert (a, b, len(tok)) == (e['doc'], e['code'], e['num_tokens'])
 
 
+@pytest.mark.parametrize('caps', [None, '8192,512,8192', '0,0,256'])
 @pytest.mark.parametrize('seq,bin_size,nparts', [(128, 32, 7), (512, 64, 3), (128, None, 1)])
-def test_bert_end_to_end_vs_oracle(gpu, seq, bin_size, nparts):
+def test_bert_end_to_end_vs_oracle(gpu, monkeypatch, seq, bin_size, nparts, caps):
+  """caps: the wave packer's per-partition arrays in global memory (default),
+  all in LDS, and order/num_tokens in LDS with a capacity some partitions
+  exceed (mixed paths in one launch)."""
   from lddl_amd import synth, pipeline
+  if caps:
+    monkeypatch.setenv('LDDL_PACK_CAPS', caps)
   c = synth.make_wiki(600_000, seed=seq + nparts)
   res = pipeline.run_bert(c, target_seq_length=seq, bin_size=bin_size, n_partitions=nparts, seed=999,
                           check_host=True)
