@@ -47,13 +47,25 @@ constexpr int NBUF = CAP + DCAP + 64; // + over-read pad of the candidate loads
 constexpr int UCAP = 256;             // units per tile
 constexpr int NSCAP = 64;             // sentences per tile
 constexpr int XCAP = 32;              // expansion markers per tile
+constexpr int MPCAP = CAP / 2 - UCAP * 2;  // multi-piece buffer entries (u16) per round
 constexpr uint32_t BF = 0xFFu, BX = 0xFDu, BS = 0xF8u;  // filler, expansion, special k = BS+k
 
 // class byte per input byte value
 enum : uint32_t { C_W = 1, C_I = 2, C_S = 4, C_D = 8, C_UP = 16, C_X = 32, C_CS = 64 };
 
 struct WaveLds {
-  uint32_t rp[CAP / 2 + 4];  // raw bytes (step 1), then u16 pieces by raw position
+  // raw bytes (step 1); afterwards the same bytes hold the pieces: uid[u] =
+  // the id of a unit done with one piece (specials, [UNK], first-probe hits),
+  // upo[u] = offset of a WordPiece unit's pieces in mp (bump-allocated, <=
+  // its byte length each), 0xFFFF = uid
+  union {
+    uint32_t rp[CAP / 4 + 4];
+    struct {
+      uint16_t uid[UCAP];
+      uint16_t upo[UCAP];
+      uint16_t mp[MPCAP];
+    } pcs;
+  };
   uint32_t nb[NBUF / 4];     // normalised bytes in window coordinates; side buffer at [CAP, CAP+DCAP)
   uint32_t brk[64];          // break bits: unit starts, spaces, sentence starts
   uint32_t dm[64];           // dirty bits: filler / expansion marker bytes
@@ -65,7 +77,7 @@ struct WaveLds {
   uint16_t stot[NSCAP];      // tokens per sentence
   uint32_t xent[XCAP];       // table entry of each expansion marker
   uint8_t xlen[XCAP];        // its normalised byte length
-  int32_t misc[4];           // 0 side-buffer cursor, 1 #markers, 2 overflow
+  int32_t misc[4];           // 0 side-buffer cursor, 1 #markers, 2 overflow, 3 mp cursor
 };
 
 __device__ __forceinline__ void wsync() {
@@ -271,7 +283,6 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   WaveLds& L = Ls[wv];
-  uint16_t* pc = reinterpret_cast<uint16_t*>(L.rp);
   const int64_t base = P.sent_off[0];
   const int64_t nwaves = (int64_t)gridDim.x * WAVES;
   constexpr bool dbg = DBG;
@@ -480,7 +491,10 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
     int prev_sent = -1;
     for (int rb = 0; rb < n; rb += UCAP) {
       const int nr = min(UCAP, n - rb);
-      if (lane == 0) L.misc[0] = 0;
+      if (lane == 0) {
+        L.misc[0] = 0;
+        L.misc[3] = 0;
+      }
       {
         int u = ub;
         for (uint32_t m = U; m; m &= m - 1, ++u) {
@@ -507,7 +521,7 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
         const uint32_t b0 = nbyte(L, p);
         int cnt = -1;
         if (b0 >= BS && b0 < BS + 5) {
-          pc[p] = (uint16_t)P.special[b0 - BS];
+          L.pcs.uid[u] = (uint16_t)P.special[b0 - BS];
           cnt = 1;
         } else {
           const int q = span_end(L, p, nb);
@@ -516,7 +530,7 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
           if (len == 0) {
             cnt = 0;
           } else if (len > 100 && count_chars(L, src, len) > 100) {
-            pc[p] = (uint16_t)P.unk;
+            L.pcs.uid[u] = (uint16_t)P.unk;
             cnt = 1;
           } else {
             need = true;
@@ -524,6 +538,7 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
           }
         }
         if (cnt >= 0) L.ucnt[u] = (uint8_t)cnt;
+        L.pcs.upo[u] = 0xFFFFu;
         if (!need) L.uwp[u] = 0;
       }
       const uint64_t bm = __ballot(need);
@@ -564,7 +579,7 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
     const int len = (int)(w >> 20);                                            \
     const Key6 key = load_key(L, (int)((w >> 8) & 0xFFFu), len);               \
     if (slot_eq(fa##k, fb##k, key, ((uint32_t)len << 16) | 0x80000000u)) {      \
-      pc[L.urec[u] & 0xFFFFu] = (uint16_t)(fb##k.z & 0xFFFFu);                 \
+      L.pcs.uid[u] = (uint16_t)(fb##k.z & 0xFFFFu);                            \
       L.ucnt[u] = 1;                                                           \
       L.uwp[u] = 0;                                                            \
       if (dbg) acc[6] += 1;                                                    \
@@ -670,8 +685,16 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
       auto begin = [&](uint32_t w) {
         u = (int)(w & 0xFFu);
         s = (int)((w >> 8) & 0xFFFu);
-        we = s + (int)(w >> 20);
-        pb = (int)(L.urec[u] & 0xFFFFu);
+        const int len = (int)(w >> 20);
+        we = s + len;
+        pb = atomicAdd(&L.misc[3], len);  // #pieces <= #bytes
+        if (pb + len > MPCAP) {           // piece buffer exhausted: the tile falls back
+          L.misc[2] = 1;
+          L.ucnt[u] = 0;
+          u = -1;
+          return;
+        }
+        L.pcs.upo[u] = (uint16_t)pb;
         np = 0;
         cont = 0;
         start_piece(mb0);
@@ -731,7 +754,7 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
           }
           STAMP(12);
           if (fail) {
-            pc[pb] = (uint16_t)P.unk;
+            L.pcs.mp[pb] = (uint16_t)P.unk;
             L.ucnt[u] = 1;
             u = -1;
           } else {
@@ -753,7 +776,7 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
             if (m0 && len > 24) m0 = long_eq(L, P, s, len, a1.w);
             if (m1 && len > 24) m1 = long_eq(L, P, s, len, b1.w);
             if (m0 || m1) {
-              pc[pb + np] = (uint16_t)((m0 ? a1.z : b1.z) & 0xFFFFu);
+              L.pcs.mp[pb + np] = (uint16_t)((m0 ? a1.z : b1.z) & 0xFFFFu);
               ++np;
               s = e;
               if (s >= we) {
@@ -830,12 +853,17 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
         const int uu = u0 + k;
         if (k < per && uu < nr) {
           const uint32_t rec = L.urec[uu];
-          const int sj = (int)(rec >> 16), p = (int)(rec & 0xFFFFu);
+          const int sj = (int)(rec >> 16);
           if (is_head(uu, sj)) before = false;
           const int pos = lpre[k] + (before ? ex : 0);
           const int c = L.ucnt[uu];
           uint16_t* out = P.out_ids + (obase + (int64_t)L.sst[sj] + pos);
-          for (int q = 0; q < c && pos + q < P.max_tok; ++q) out[q] = pc[p + q];
+          const int po = L.pcs.upo[uu];
+          if (po == 0xFFFF) {
+            if (c > 0 && pos < P.max_tok) out[0] = L.pcs.uid[uu];
+          } else {
+            for (int q = 0; q < c && pos + q < P.max_tok; ++q) out[q] = L.pcs.mp[po + q];
+          }
           if (uu == nr - 1 || (int)(L.urec[uu + 1] >> 16) != sj) L.stot[sj] = (uint16_t)(pos + c);
         }
       }
@@ -893,6 +921,7 @@ hipError_t launch_tokenize_stream(const TokParams& P, int64_t nbytes, int64_t* t
       case 1: e = tok4::launch_cfg<4, false, false>(P, n_tiles, tile_sent, fb_list, fb_count, n_cu, s); break;
       case 2: e = tok4::launch_cfg<12, true, false>(P, n_tiles, tile_sent, fb_list, fb_count, n_cu, s); break;
       case 3: e = tok4::launch_cfg<8, true, false>(P, n_tiles, tile_sent, fb_list, fb_count, n_cu, s); break;
+      case 4: e = tok4::launch_cfg<16, true, false>(P, n_tiles, tile_sent, fb_list, fb_count, n_cu, s); break;
       default: e = tok4::launch_cfg<4, true, false>(P, n_tiles, tile_sent, fb_list, fb_count, n_cu, s); break;
     }
   }
