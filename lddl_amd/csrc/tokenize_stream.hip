@@ -682,19 +682,58 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
         if (e < we && !(asc && e - s < 24))
           while (e > s && (nbyte(L, e) & 0xC0u) == 0x80u) --e;
       };
+      // pieces: the first 8 in registers (u16 pairs), allocated exactly in mp
+      // when the word ends; a word reaching 8 pieces spills to a block of its
+      // byte length (#pieces <= #bytes)
+      uint32_t pr0 = 0, pr1 = 0, pr2 = 0, pr3 = 0;
+      int ulen = 0;
+      auto mp_alloc = [&](int n) {
+        const int at = atomicAdd(&L.misc[3], n);
+        if (at + n > MPCAP) {  // piece buffer exhausted: the tile falls back
+          L.misc[2] = 1;
+          return -1;
+        }
+        return at;
+      };
+      auto reg_piece = [&](int q) {
+        const uint32_t w = q < 2 ? pr0 : q < 4 ? pr1 : q < 6 ? pr2 : pr3;
+        return (uint16_t)(w >> ((q & 1) * 16));
+      };
+      auto put_piece = [&](uint32_t id) {
+        if (pb >= 0) {
+          L.pcs.mp[pb + np] = (uint16_t)id;
+        } else if (np < 8) {
+          const uint32_t sh = (uint32_t)(np & 1) * 16u, keep = ~(0xFFFFu << sh), v = id << sh;
+          const int w = np >> 1;
+          pr0 = w == 0 ? (pr0 & keep) | v : pr0;
+          pr1 = w == 1 ? (pr1 & keep) | v : pr1;
+          pr2 = w == 2 ? (pr2 & keep) | v : pr2;
+          pr3 = w == 3 ? (pr3 & keep) | v : pr3;
+        } else {
+          pb = mp_alloc(ulen);
+          if (pb >= 0) {
+            for (int q = 0; q < 8; ++q) L.pcs.mp[pb + q] = reg_piece(q);
+            L.pcs.mp[pb + 8] = (uint16_t)id;
+          }
+        }
+        ++np;
+      };
+      auto finish = [&]() {  // the word's pieces are complete
+        if (pb < 0 && np <= 8) {
+          pb = mp_alloc(np);
+          if (pb >= 0)
+            for (int q = 0; q < np; ++q) L.pcs.mp[pb + q] = reg_piece(q);
+        }
+        L.pcs.upo[u] = (uint16_t)(pb >= 0 ? pb : 0);
+        L.ucnt[u] = (uint8_t)(pb >= 0 ? np : 0);
+        u = -1;
+      };
       auto begin = [&](uint32_t w) {
         u = (int)(w & 0xFFu);
         s = (int)((w >> 8) & 0xFFFu);
-        const int len = (int)(w >> 20);
-        we = s + len;
-        pb = atomicAdd(&L.misc[3], len);  // #pieces <= #bytes
-        if (pb + len > MPCAP) {           // piece buffer exhausted: the tile falls back
-          L.misc[2] = 1;
-          L.ucnt[u] = 0;
-          u = -1;
-          return;
-        }
-        L.pcs.upo[u] = (uint16_t)pb;
+        ulen = (int)(w >> 20);
+        we = s + ulen;
+        pb = -1;
         np = 0;
         cont = 0;
         start_piece(mb0);
@@ -753,10 +792,10 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
             else fail = true;
           }
           STAMP(12);
-          if (fail) {
-            L.pcs.mp[pb] = (uint16_t)P.unk;
-            L.ucnt[u] = 1;
-            u = -1;
+          if (fail) {  // some position has no match: the whole word is [UNK]
+            np = 0;
+            put_piece(P.unk);
+            finish();
           } else {
             if (dbg) acc[6] += 1;
             const int len = e - s;
@@ -776,12 +815,10 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
             if (m0 && len > 24) m0 = long_eq(L, P, s, len, a1.w);
             if (m1 && len > 24) m1 = long_eq(L, P, s, len, b1.w);
             if (m0 || m1) {
-              L.pcs.mp[pb + np] = (uint16_t)((m0 ? a1.z : b1.z) & 0xFFFFu);
-              ++np;
+              put_piece((m0 ? a1.z : b1.z) & 0xFFFFu);
               s = e;
               if (s >= we) {
-                L.ucnt[u] = (uint8_t)np;
-                u = -1;
+                finish();
               } else {
                 cont = 1;
                 start_piece(mb1);
