@@ -314,7 +314,7 @@ extern "C" int lddl_create(const char* vocab_path, const char* table_path, int d
   c->tok_algo = (algo && algo[0] >= '1' && algo[0] <= '4') ? algo[0] - '0' : 4;
   if (c->tok_algo == 4 && !c->tok4_ok) c->tok_algo = 3;
   const char* cfg = getenv("LDDL_TOK4_CFG");  // waves per workgroup / Bloom (tokenize.h)
-  c->tok4_cfg = cfg ? atoi(cfg) : 2;
+  c->tok4_cfg = cfg ? atoi(cfg) : 4;
   const char* tchunk = getenv("LDDL_TILE_CHUNK");  // tiles per launch (tests force several launches)
   c->tile_chunk = tchunk ? atoll(tchunk) : 0;
   const char* mcap = getenv("LDDL_MLM_CAP");  // initial masking arena (tests force the regrow path)

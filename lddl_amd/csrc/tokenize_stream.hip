@@ -479,8 +479,13 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
     L.brk[lane] = U | (S & CS) | SB;
     L.dm[lane] = D;
     uint32_t tot;
-    const int ub = (int)wave_excl((uint32_t)__popc(U), lane, &tot);
-    const int n = (int)tot;
+    // one scan for both: units (low 16 bits) and sentence starts (high)
+    const uint32_t ex = wave_excl((uint32_t)__popc(U) | ((uint32_t)__popc(SB) << 16), lane, &tot);
+    const int ub = (int)(ex & 0xFFFFu), sb_before = (int)(ex >> 16);
+    const int n = (int)(tot & 0xFFFFu);
+    // every sentence start distinct (no empty sentence shares one): a unit's
+    // sentence is the number of starts at or before it, minus one
+    const bool starts_distinct = (int)(tot >> 16) == ns;
     if (wbad) {
       if (lane == 0) fb_list[atomicAdd(fb_count, 1)] = (int32_t)t;
       if (dbg) acc[11] += 1;
@@ -499,12 +504,18 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
         int u = ub;
         for (uint32_t m = U; m; m &= m - 1, ++u) {
           if (u < rb || u >= rb + nr) continue;
-          const int p = p0 + __ffs(m) - 1;
-          int lo = 0, hi = ns - 1;  // last sentence starting at or before p
-          while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if ((int)L.sst[mid] <= p) lo = mid;
-            else hi = mid - 1;
+          const int b = __ffs(m) - 1, p = p0 + b;
+          int lo;
+          if (starts_distinct) {
+            lo = sb_before + __popc(SB & ((2u << b) - 1u)) - 1;
+          } else {
+            lo = 0;  // last sentence starting at or before p
+            int hi = ns - 1;
+            while (lo < hi) {
+              const int mid = (lo + hi + 1) >> 1;
+              if ((int)L.sst[mid] <= p) lo = mid;
+              else hi = mid - 1;
+            }
           }
           L.urec[u - rb] = (uint32_t)p | ((uint32_t)lo << 16);
         }
