@@ -256,11 +256,12 @@ static int load_vocab(lddl_ctx* c, const char* path) {
     bloom[(uint32_t)(key >> 40) & (BLOOM_WORDS - 1)] |= (1u << (key & 31)) | (1u << ((key >> 5) & 31));
   }
   if ((rc0 = upload(&c->d_bloom, bloom.data(), bloom.size() * 4))) return rc0;
-  // v4 table: >= V buckets of two 32-B slots (load <= 1/2), linear probing
-  // over buckets; Bloom filter over the same hashes (common.h vhash)
+  // v4 table: >= 2V buckets of two 32-B slots (load <= 1/4: a key outside
+  // its home bucket costs the WordPiece loop a dependent probe; tools/wp_sim.py),
+  // linear probing over buckets; Bloom filter over the same hashes (common.h vhash)
   {
     uint32_t nbk = 1;
-    while (nbk < V) nbk <<= 1;
+    while (nbk < 2 * V) nbk <<= 1;
     std::vector<uint32_t> vt((size_t)nbk * 16, 0u);
     std::vector<uint32_t> vbl(BLOOM_WORDS, 0u);
     for (size_t i = 0; i < V; ++i) {
