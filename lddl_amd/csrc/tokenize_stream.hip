@@ -303,7 +303,8 @@ __device__ __forceinline__ bool bloom_ok(const uint32_t* bloom, uint32_t h) {
   const uint32_t bb = vbloom_bits(h);
   return (bloom[vbloom_word(h)] & bb) == bb;
 }
-// The two longest candidates <= C.e - C.s the Bloom filter does not rule out:
+// The longest candidate <= C.e - C.s the Bloom filter does not rule out, and
+// the next one if it lies in the same dword group (hashed already, free):
 // lengths *l1 > *l2 (0 = none) with hashes; C.e is left at s + *l1.
 template <bool BLOOM>
 __device__ __forceinline__ void cand_scan2(const WaveLds& L, const uint32_t* bloom, Cand& C, uint32_t cont, int* l1,
@@ -328,7 +329,7 @@ __device__ __forceinline__ void cand_scan2(const WaveLds& L, const uint32_t* blo
     }                        \
   }
 #define TOK4_GROUP(k, Hk, Hk1, ck)                                                                   \
-  if (f2 == 0 && 4 * (k) < len) {                                                                    \
+  if (f1 == 0 && 4 * (k) < len) {                                                                    \
     const uint32_t g4 = vfinal(Hk1, 4 * (k) + 4, cont), g3 = vfinal(vmix(Hk, (ck) & 0xFFFFFFu), 4 * (k) + 3, cont), \
                    g2 = vfinal(vmix(Hk, (ck) & 0xFFFFu), 4 * (k) + 2, cont),                         \
                    g1 = vfinal(vmix(Hk, (ck) & 0xFFu), 4 * (k) + 1, cont);                           \
@@ -349,16 +350,12 @@ __device__ __forceinline__ void cand_scan2(const WaveLds& L, const uint32_t* blo
 #undef TOK4_GROUP
 #undef TOK4_TAKE
   } else {
-    while (C.e > C.s && f2 == 0) {
+    while (C.e > C.s) {  // (no second candidate here: rare non-ASCII / long words)
       const uint32_t hh = cand_hash(C, C.e - C.s, cont);
       if (bloom_ok<BLOOM>(bloom, hh)) {
-        if (f1 == 0) {
-          f1 = C.e - C.s;
-          g1h = hh;
-        } else {
-          f2 = C.e - C.s;
-          g2h = hh;
-        }
+        f1 = C.e - C.s;
+        g1h = hh;
+        break;
       }
       cand_shrink(L, C);
     }
