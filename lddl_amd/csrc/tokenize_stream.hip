@@ -247,126 +247,6 @@ __device__ __forceinline__ bool slot_eq(const uint4& a, const uint4& b, const Ke
          b.y == k.d5;
 }
 
-// ---- WordPiece candidate (named scalars: no dynamic register indexing, so
-//      nothing is demoted to scratch)
-struct Cand {
-  uint32_t c0, c1, c2, c3, c4, c5;  // bytes [s, s+24) as dwords
-  int s, e;                         // piece start, candidate end
-  bool asc;                         // those 24 bytes are ASCII
-};
-__device__ __forceinline__ void cand_load(const WaveLds& L, Cand& C, int s) {
-  const int a = s >> 2;
-  const uint32_t sh = (uint32_t)(s & 3);
-  const uint32_t x0 = L.nb[a], x1 = L.nb[a + 1], x2 = L.nb[a + 2], x3 = L.nb[a + 3], x4 = L.nb[a + 4],
-                 x5 = L.nb[a + 5], x6 = L.nb[a + 6];
-  C.s = s;
-  C.c0 = __builtin_amdgcn_alignbyte(x1, x0, sh);
-  C.c1 = __builtin_amdgcn_alignbyte(x2, x1, sh);
-  C.c2 = __builtin_amdgcn_alignbyte(x3, x2, sh);
-  C.c3 = __builtin_amdgcn_alignbyte(x4, x3, sh);
-  C.c4 = __builtin_amdgcn_alignbyte(x5, x4, sh);
-  C.c5 = __builtin_amdgcn_alignbyte(x6, x5, sh);
-  C.asc = ((C.c0 | C.c1 | C.c2 | C.c3 | C.c4 | C.c5) & 0x80808080u) == 0;
-}
-// == vhash of the candidate [s, s+l): full dwords, then the masked tail
-__device__ __forceinline__ uint32_t cand_hash(const Cand& C, int l, uint32_t cont) {
-  const int lc = min(l, 24);
-  auto m = [&](int i, uint32_t c) {
-    const int rem = lc - 4 * i;
-    return rem >= 4 ? c : (c & ((1u << (8 * rem)) - 1u));
-  };
-  uint32_t h = VSEED;
-  if (lc > 0) h = vmix(h, m(0, C.c0));
-  if (lc > 4) h = vmix(h, m(1, C.c1));
-  if (lc > 8) h = vmix(h, m(2, C.c2));
-  if (lc > 12) h = vmix(h, m(3, C.c3));
-  if (lc > 16) h = vmix(h, m(4, C.c4));
-  if (lc > 20) h = vmix(h, m(5, C.c5));
-  return vfinal(h, (uint32_t)l, cont);
-}
-__device__ __forceinline__ void cand_backoff(const WaveLds& L, Cand& C) {  // to a char boundary
-  if (!(C.asc && C.e - C.s < 24))
-    while (C.e > C.s && (nbyte(L, C.e) & 0xC0u) == 0x80u) --C.e;
-}
-__device__ __forceinline__ void cand_start(const WaveLds& L, Cand& C, int s, int we, int maxb) {
-  cand_load(L, C, s);
-  C.e = min(we, s + maxb);
-  if (C.e < we) cand_backoff(L, C);
-}
-__device__ __forceinline__ void cand_shrink(const WaveLds& L, Cand& C) {  // previous char boundary
-  --C.e;
-  cand_backoff(L, C);
-}
-template <bool BLOOM>
-__device__ __forceinline__ bool bloom_ok(const uint32_t* bloom, uint32_t h) {
-  if (!BLOOM) return true;
-  const uint32_t bb = vbloom_bits(h);
-  return (bloom[vbloom_word(h)] & bb) == bb;
-}
-// The longest candidate <= C.e - C.s the Bloom filter does not rule out, and
-// the next one if it lies in the same dword group (hashed already, free):
-// lengths *l1 > *l2 (0 = none) with hashes; C.e is left at s + *l1.
-template <bool BLOOM>
-__device__ __forceinline__ void cand_scan2(const WaveLds& L, const uint32_t* bloom, Cand& C, uint32_t cont, int* l1,
-                                           uint32_t* h1, int* l2, uint32_t* h2) {
-  int len = C.e - C.s;
-  int f1 = 0, f2 = 0;
-  uint32_t g1h = 0, g2h = 0;
-  if (C.asc && len <= 24) {
-    // ASCII: every length is a char boundary.  Dword group k holds lengths
-    // 4k+1..4k+4, hashed from Hk / H(k+1) with constant register indices;
-    // groups from the top down, four Bloom reads in flight per group.
-    const uint32_t H0 = VSEED, H1 = vmix(H0, C.c0), H2 = vmix(H1, C.c1), H3 = vmix(H2, C.c2), H4 = vmix(H3, C.c3),
-                   H5 = vmix(H4, C.c4), H6 = vmix(H5, C.c5);
-#define TOK4_TAKE(ok, l, g)  \
-  if (ok) {                  \
-    if (f1 == 0) {           \
-      f1 = (l);              \
-      g1h = (g);             \
-    } else if (f2 == 0) {    \
-      f2 = (l);              \
-      g2h = (g);             \
-    }                        \
-  }
-#define TOK4_GROUP(k, Hk, Hk1, ck)                                                                   \
-  if (f1 == 0 && 4 * (k) < len) {                                                                    \
-    const uint32_t g4 = vfinal(Hk1, 4 * (k) + 4, cont), g3 = vfinal(vmix(Hk, (ck) & 0xFFFFFFu), 4 * (k) + 3, cont), \
-                   g2 = vfinal(vmix(Hk, (ck) & 0xFFFFu), 4 * (k) + 2, cont),                         \
-                   g1 = vfinal(vmix(Hk, (ck) & 0xFFu), 4 * (k) + 1, cont);                           \
-    const bool o4 = 4 * (k) + 4 <= len && bloom_ok<BLOOM>(bloom, g4),                                \
-               o3 = 4 * (k) + 3 <= len && bloom_ok<BLOOM>(bloom, g3),                                \
-               o2 = 4 * (k) + 2 <= len && bloom_ok<BLOOM>(bloom, g2), o1 = bloom_ok<BLOOM>(bloom, g1); \
-    TOK4_TAKE(o4, 4 * (k) + 4, g4)                                                                   \
-    TOK4_TAKE(o3, 4 * (k) + 3, g3)                                                                   \
-    TOK4_TAKE(o2, 4 * (k) + 2, g2)                                                                   \
-    TOK4_TAKE(o1, 4 * (k) + 1, g1)                                                                   \
-  }
-    TOK4_GROUP(5, H5, H6, C.c5)
-    TOK4_GROUP(4, H4, H5, C.c4)
-    TOK4_GROUP(3, H3, H4, C.c3)
-    TOK4_GROUP(2, H2, H3, C.c2)
-    TOK4_GROUP(1, H1, H2, C.c1)
-    TOK4_GROUP(0, H0, H1, C.c0)
-#undef TOK4_GROUP
-#undef TOK4_TAKE
-  } else {
-    while (C.e > C.s) {  // (no second candidate here: rare non-ASCII / long words)
-      const uint32_t hh = cand_hash(C, C.e - C.s, cont);
-      if (bloom_ok<BLOOM>(bloom, hh)) {
-        f1 = C.e - C.s;
-        g1h = hh;
-        break;
-      }
-      cand_shrink(L, C);
-    }
-  }
-  C.e = C.s + f1;
-  *l1 = f1;
-  *h1 = g1h;
-  *l2 = f2;
-  *h2 = g2h;
-}
-
 template <int WAVES, bool BLOOM, bool DBG>
 __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int64_t* tile_sent, int64_t n_tiles,
                                                           int32_t* fb_list, int32_t* fb_count) {
@@ -754,15 +634,65 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
     STAMP(3);
     if (dbg) acc[8] += nr;
     // ---- 4: WordPiece on the work queue --------------------------------------
-    // Every active lane owns one word: per step one bucket probe of the
-    // current candidate plus a home-slot probe of the next shorter
-    // Bloom-positive one, so a false positive costs no extra step.
     {
       const int mb0 = (int)P.maxb[0], mb1 = (int)P.maxb[1];
       const uint32_t vmask = P.vt_mask;
-      int u = -1, we = 0, pb = -1, np = 0, slot = -1;  // slot -1: scan first, -2: no candidate left
-      uint32_t cont = 0;
-      Cand C;
+      int u = -1, s = 0, we = 0, e = 0, pb = 0, np = 0, slot = -1;
+      uint32_t cont = 0, hcur = 0;
+      bool asc = false;
+      // candidate bytes [s, s+24) as dwords c0..c5 and the prefix mixes
+      // H0..H6 (H(k+1) = vmix(Hk, ck)): named scalars, never an indexed
+      // array, so nothing is demoted to scratch by dynamic indexing
+      uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0, c4 = 0, c5 = 0;
+      uint32_t H0 = VSEED, H1 = 0, H2 = 0, H3 = 0, H4 = 0, H5 = 0, H6 = 0;
+      auto load_cand = [&]() {
+        const int a = s >> 2;
+        const uint32_t sh = (uint32_t)(s & 3);
+        const uint32_t x0 = L.nb[a], x1 = L.nb[a + 1], x2 = L.nb[a + 2], x3 = L.nb[a + 3], x4 = L.nb[a + 4],
+                       x5 = L.nb[a + 5], x6 = L.nb[a + 6];
+        c0 = __builtin_amdgcn_alignbyte(x1, x0, sh);
+        c1 = __builtin_amdgcn_alignbyte(x2, x1, sh);
+        c2 = __builtin_amdgcn_alignbyte(x3, x2, sh);
+        c3 = __builtin_amdgcn_alignbyte(x4, x3, sh);
+        c4 = __builtin_amdgcn_alignbyte(x5, x4, sh);
+        c5 = __builtin_amdgcn_alignbyte(x6, x5, sh);
+        H1 = vmix(H0, c0);
+        H2 = vmix(H1, c1);
+        H3 = vmix(H2, c2);
+        H4 = vmix(H3, c3);
+        H5 = vmix(H4, c4);
+        H6 = vmix(H5, c5);
+        asc = ((c0 | c1 | c2 | c3 | c4 | c5) & 0x80808080u) == 0;
+      };
+      auto selH = [&](int q) {
+        return q <= 0 ? H0 : q == 1 ? H1 : q == 2 ? H2 : q == 3 ? H3 : q == 4 ? H4 : q == 5 ? H5 : H6;
+      };
+      auto selD = [&](int q) {
+        return q <= 0 ? c0 : q == 1 ? c1 : q == 2 ? c2 : q == 3 ? c3 : q == 4 ? c4 : c5;
+      };
+      auto hash_len = [&](int l) {  // == vhash of the candidate [s, s+l)
+        const int lc = min(l, 24), q = lc >> 2, r = lc & 3;
+        uint32_t h = selH(q);
+        if (r) h = vmix(h, selD(q) & ((1u << (8 * r)) - 1u));
+        return vfinal(h, (uint32_t)l, cont);
+      };
+      auto bloom_ok = [&](uint32_t h) {
+        if (!BLOOM) return true;
+        const uint32_t bb = vbloom_bits(h);
+        return (bloom[vbloom_word(h)] & bb) == bb;
+      };
+      auto shrink = [&]() {  // previous char boundary
+        --e;
+        if (!(asc && e - s < 24))
+          while (e > s && (nbyte(L, e) & 0xC0u) == 0x80u) --e;
+      };
+      auto start_piece = [&](int maxb) {
+        slot = -1;
+        load_cand();
+        e = min(we, s + maxb);
+        if (e < we && !(asc && e - s < 24))
+          while (e > s && (nbyte(L, e) & 0xC0u) == 0x80u) --e;
+      };
       // pieces: the first 8 in registers (u16 pairs), allocated exactly in mp
       // when the word ends; a word reaching 8 pieces spills to a block of its
       // byte length (#pieces <= #bytes)
@@ -811,28 +741,13 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
       };
       auto begin = [&](uint32_t w) {
         u = (int)(w & 0xFFu);
+        s = (int)((w >> 8) & 0xFFFu);
         ulen = (int)(w >> 20);
-        const int s0w = (int)((w >> 8) & 0xFFFu);
-        we = s0w + ulen;
+        we = s + ulen;
         pb = -1;
         np = 0;
         cont = 0;
-        slot = -1;
-        cand_start(L, C, s0w, we, mb0);
-      };
-      // second candidate of the current piece (shorter, Bloom-positive),
-      // probed on its home slot alongside the current one: e2 / slot2
-      int e2 = 0, slot2 = -1;
-      auto take = [&](uint32_t id) {  // candidate [C.s, C.e) matched
-        put_piece(id);
-        slot = -1;
-        slot2 = -1;
-        if (C.e >= we) {
-          finish();
-        } else {
-          cont = 1;
-          cand_start(L, C, C.e, we, mb1);
-        }
+        start_piece(mb0);
       };
       if (lane < nwl) begin(L.uwp[lane]);
       int next = 64;
@@ -840,65 +755,88 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
         if (__ballot(u >= 0) == 0 && next >= nwl) break;
         if (dbg) acc[9] += 1;
         STAMP(4);
-        if (u >= 0 && slot == -1) {
-          int l1, l2;
-          uint32_t h1, h2;
-          cand_scan2<BLOOM>(L, bloom, C, cont, &l1, &h1, &l2, &h2);
-          slot = l1 > 0 ? (int)(h1 & vmask) : -2;
-          e2 = C.s + l2;
-          slot2 = l2 > 0 ? (int)(h2 & vmask) : -1;
-        }
-        STAMP(12);
         if (u >= 0) {
-          if (slot == -2) {  // some position has no match: the whole word is [UNK]
+          bool fail = false;
+          if (slot < 0) {
+            // longest candidate <= e - s the Bloom filter does not rule out
+            int len = e - s;
+            bool found = false;
+            if (asc && len <= 24) {
+              // ASCII: every length is a char boundary.  Dword group k holds
+              // lengths 4k+1..4k+4, hashed from Hk / H(k+1) with constant
+              // register indices; groups from the top down.
+              int fl = 0;
+#define TOK4_GROUP(k, Hk, Hk1, ck)                                                                  \
+  if (fl == 0 && 4 * (k) < len) {                                                                   \
+    const uint32_t g4 = vfinal(Hk1, 4 * (k) + 4, cont), g3 = vfinal(vmix(Hk, (ck) & 0xFFFFFFu), 4 * (k) + 3, cont), \
+                   g2 = vfinal(vmix(Hk, (ck) & 0xFFFFu), 4 * (k) + 2, cont),                        \
+                   g1 = vfinal(vmix(Hk, (ck) & 0xFFu), 4 * (k) + 1, cont);                          \
+    const bool o4 = 4 * (k) + 4 <= len && bloom_ok(g4), o3 = 4 * (k) + 3 <= len && bloom_ok(g3),   \
+               o2 = 4 * (k) + 2 <= len && bloom_ok(g2), o1 = bloom_ok(g1);                          \
+    if (o4 | o3 | o2 | o1) {                                                                        \
+      fl = o4 ? 4 * (k) + 4 : o3 ? 4 * (k) + 3 : o2 ? 4 * (k) + 2 : 4 * (k) + 1;                    \
+      hcur = o4 ? g4 : o3 ? g3 : o2 ? g2 : g1;                                                      \
+    }                                                                                               \
+  }
+              TOK4_GROUP(5, H5, H6, c5)
+              TOK4_GROUP(4, H4, H5, c4)
+              TOK4_GROUP(3, H3, H4, c3)
+              TOK4_GROUP(2, H2, H3, c2)
+              TOK4_GROUP(1, H1, H2, c1)
+              TOK4_GROUP(0, H0, H1, c0)
+#undef TOK4_GROUP
+              if (dbg) acc[7] += len - fl;
+              found = fl > 0;
+              e = s + fl;
+            } else {
+              while (e > s) {
+                hcur = hash_len(e - s);
+                if (bloom_ok(hcur)) {
+                  found = true;
+                  break;
+                }
+                if (dbg) acc[7] += 1;
+                shrink();
+              }
+            }
+            if (found) slot = (int)(hcur & vmask);
+            else fail = true;
+          }
+          STAMP(12);
+          if (fail) {  // some position has no match: the whole word is [UNK]
             np = 0;
-            pb = -1;
             put_piece(P.unk);
             finish();
           } else {
             if (dbg) acc[6] += 1;
-            const int len = C.e - C.s;
+            const int len = e - s;
+            const int lc = min(len, 24), q = lc >> 2, r = lc & 3;
+            auto msk = [&](int k, uint32_t c) {
+              return k < q ? c : (k == q && r) ? (c & ((1u << (8 * r)) - 1u)) : 0u;
+            };
+            const uint32_t m0c = msk(0, c0), m1c = msk(1, c1), m2c = msk(2, c2), m3c = msk(3, c3), m4c = msk(4, c4),
+                           m5c = msk(5, c5);
             const uint4* bk = P.vt + 4 * (uint32_t)slot;
             const uint4 a0 = bk[0], a1 = bk[1], b0 = bk[2], b1 = bk[3];
-            uint4 z0 = make_uint4(0, 0, 0, 0), z1 = z0;
-            if (slot2 >= 0) {
-              const uint4* bk2 = P.vt + 4 * (uint32_t)slot2;
-              z0 = bk2[0];
-              z1 = bk2[1];
-            }
-            // slot (x, y) holds the masked key of length l?
-            auto eq = [&](const uint4& x, const uint4& y, int l) {
-              const int lc = min(l, 24), q = lc >> 2, r = lc & 3;
-              auto mk = [&](int k, uint32_t c) { return k < q ? c : (k == q && r) ? (c & ((1u << (8 * r)) - 1u)) : 0u; };
-              const uint32_t want = ((uint32_t)l << 16) | (cont << 24) | 0x80000000u;
-              bool m = (y.z & 0xFFFF0000u) == want && x.x == mk(0, C.c0) && x.y == mk(1, C.c1) && x.z == mk(2, C.c2) &&
-                       x.w == mk(3, C.c3) && y.x == mk(4, C.c4) && y.y == mk(5, C.c5);
-              if (m && l > 24) m = long_eq(L, P, C.s, l, y.w);
-              return m;
-            };
-            const bool m0 = eq(a0, a1, len), m1 = eq(b0, b1, len);
+            const uint32_t want = ((uint32_t)len << 16) | (cont << 24) | 0x80000000u;
+            bool m0 = (a1.z & 0xFFFF0000u) == want && a0.x == m0c && a0.y == m1c && a0.z == m2c && a0.w == m3c &&
+                      a1.x == m4c && a1.y == m5c;
+            bool m1 = (b1.z & 0xFFFF0000u) == want && b0.x == m0c && b0.y == m1c && b0.z == m2c && b0.w == m3c &&
+                      b1.x == m4c && b1.y == m5c;
+            if (m0 && len > 24) m0 = long_eq(L, P, s, len, a1.w);
+            if (m1 && len > 24) m1 = long_eq(L, P, s, len, b1.w);
             if (m0 || m1) {
-              take((m0 ? a1.z : b1.z) & 0xFFFFu);
-            } else if (!(a1.z & 0x80000000u) || !(b1.z & 0x80000000u)) {
-              // the current candidate is absent: the second one is next
-              if (slot2 >= 0) {
-                const int l2 = e2 - C.s;
-                const bool h2 = eq(z0, z1, l2);
-                C.e = e2;
-                if (h2) {
-                  take(z1.z & 0xFFFFu);
-                } else if (!(z1.z & 0x80000000u)) {  // empty home bucket: absent too
-                  slot = -1;
-                  slot2 = -1;
-                  cand_shrink(L, C);
-                } else {  // probe it fully next step
-                  slot = slot2;
-                  slot2 = -1;
-                }
+              put_piece((m0 ? a1.z : b1.z) & 0xFFFFu);
+              s = e;
+              if (s >= we) {
+                finish();
               } else {
-                slot = -1;  // an empty slot ends the probe sequence: no such key
-                cand_shrink(L, C);
+                cont = 1;
+                start_piece(mb1);
               }
+            } else if (!(a1.z & 0x80000000u) || !(b1.z & 0x80000000u)) {
+              slot = -1;  // an empty slot ends the probe sequence: no such key
+              shrink();
             } else {
               slot = (int)(((uint32_t)slot + 1u) & vmask);
             }
