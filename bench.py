@@ -163,24 +163,24 @@ def main():
     return res, ntok
 
   for _ in range(args.warmup):
-    res, ntok = step(False)
+    step(False)
   torch.cuda.synchronize()
+  if dist is not None:
+    dist.barrier()
+  torch.cuda.synchronize()
+  t0 = time.perf_counter()
+  for _ in range(args.steps):
+    res, ntok = step(True)
+  torch.cuda.synchronize()
+  if dist is not None:
+    dist.barrier()
+  el = time.perf_counter() - t0
   n_tok = int(ntok[:sh.n_sent].sum().item())
   # full-size property check (outside the timed region): every replica of the
   # unique corpus must tokenize to the same number of tokens
   per_rep = ntok[:reps * base.n_sent].view(reps, base.n_sent).to(torch.int64).sum(1)
   if not bool((per_rep == per_rep[0]).all()):
     raise RuntimeError('tokenize: replicas disagree: %s' % per_rep.tolist()[:16])
-  if dist is not None:
-    dist.barrier()
-  torch.cuda.synchronize()
-  t0 = time.perf_counter()
-  for _ in range(args.steps):
-    res, _ = step(True)
-  torch.cuda.synchronize()
-  if dist is not None:
-    dist.barrier()
-  el = time.perf_counter() - t0
   tk = float(np.mean([a.elapsed_time(b) for a, b in tok_ms]))
   if dist is not None:
     t = torch.tensor([el, float(n_tok)], dtype=torch.float64, device=device)
@@ -223,7 +223,7 @@ def main():
   try:
     with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), 'profiles', 'traffic.json')) as f:
       tr = json.load(f)
-    if tr.get('workload') == line['config']['workload']:
+    if (tr.get('workload'), tr.get('kernel')) == (line['config']['workload'], line['roofline']['kernel']):
       line['roofline']['traffic'] = tr['traffic_bytes_per_call']
       line['roofline']['traffic_source'] = tr['source']
   except (OSError, ValueError, KeyError):

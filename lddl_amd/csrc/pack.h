@@ -129,7 +129,9 @@ size_t pack_dyn_bytes(int cap_lens, int cap_docs, int cap_pairs, bool mask);
 hipError_t launch_pack_codebert(const PackParams& P, hipStream_t s);
 hipError_t launch_scan_parts(const int64_t* a, const int64_t* b, int64_t n, int64_t* sa, int64_t* sb,
                              const int32_t* err, int32_t* err_any, hipStream_t s);
-hipError_t launch_materialize(const MatParams& M, hipStream_t s);
+// algo 1: wave per partition (u16 copies); otherwise wave per 64 pairs with
+// 16-B stores (needs out_tokens 16-B aligned and dense padded by 16 u16)
+hipError_t launch_materialize(const MatParams& M, int64_t total_pairs, int algo, hipStream_t s);
 // tokoff[0..n] = exclusive scan of ntok[0..n) (int64); blocksums: scratch of
 // scan_blocks(n) + 1 entries
 int64_t scan_blocks(int64_t n);

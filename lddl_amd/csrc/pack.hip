@@ -410,6 +410,190 @@ __global__ __launch_bounds__(256) void materialize_kernel(MatParams M) {
   }
 }
 
+// ---- materialize v2: wave per 64 consecutive global pairs ------------------
+// Waves are dispatched in pair order, so the resident waves touch only a few
+// dozen partitions' dense ids at a time: the dup-fold re-reads of a sentence's
+// ids are served on-die (L2 / MALL) rather than from HBM.  The 64 rows of a
+// wave are one contiguous output range [G0, G1), written in aligned 8-token
+// (16-B) chunks.  Phase 1 is branch-free, 4 chunks per lane in flight: a chunk
+// inside one source segment is two aligned 16-B loads funnel-shifted into one
+// 16-B store.  Every other chunk ([CLS]/[SEP], a row boundary, or one of the
+// two chunks shared with the neighbouring waves) goes to a per-wave list that
+// phase 2 drains token-parallel (one token per lane, u16 load + store).
+constexpr int MAT_U = 4;         // chunks per lane per phase-1 iteration
+constexpr int MAT_SLOW = 512;    // slow-chunk list capacity per wave
+struct RowDesc {
+  int64_t src0, src1;       // dense start of segment A / B
+  int32_t l0, b1, l1, nt;   // |A|, first position of B, |B|, row length
+};
+struct MatWave {
+  int32_t roff[64];         // row start relative to G0 (INT_MAX past the last row)
+  RowDesc row[64];
+  uint32_t slow[MAT_SLOW];  // chunk start (relative to G0, + 8) | row << 20
+};
+
+// u16 window [m, m + 8) of the 16 u16 held in A:B
+__device__ __forceinline__ uint4 funnel8(const uint4 A, const uint4 B, uint32_t m) {
+  const uint32_t h = m >> 1, sh = (m & 1u) * 16u;
+  const bool h0 = h == 0, h1 = h == 1, h2 = h == 2;
+  const uint32_t e0 = h0 ? A.x : h1 ? A.y : h2 ? A.z : A.w;
+  const uint32_t e1 = h0 ? A.y : h1 ? A.z : h2 ? A.w : B.x;
+  const uint32_t e2 = h0 ? A.z : h1 ? A.w : h2 ? B.x : B.y;
+  const uint32_t e3 = h0 ? A.w : h1 ? B.x : h2 ? B.y : B.z;
+  const uint32_t e4 = h0 ? B.x : h1 ? B.y : h2 ? B.z : B.w;
+  return make_uint4(__builtin_amdgcn_alignbit(e1, e0, sh), __builtin_amdgcn_alignbit(e2, e1, sh),
+                    __builtin_amdgcn_alignbit(e3, e2, sh), __builtin_amdgcn_alignbit(e4, e3, sh));
+}
+
+__device__ __forceinline__ void mat_wsync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// phase 2: the ns listed chunks, one token per lane
+__device__ __forceinline__ void mat_drain(const MatParams& M, const MatWave& W, int ns, int nr, int64_t G0,
+                                          int32_t G1r, int lane) {
+  mat_wsync();
+  const int ntok = ns * 8;
+  const uint16_t cls = (uint16_t)M.cls_id, sep = (uint16_t)M.sep_id;
+  for (int j0 = 0; j0 < ntok; j0 += 4 * 64) {
+    uint32_t y[4];
+    int32_t pos[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int j = j0 + m * 64 + lane;
+      pos[m] = -1;
+      y[m] = sep;
+      int64_t src = 0;
+      bool ld = false;
+      if (j < ntok) {
+        const uint32_t e = W.slow[j >> 3];
+        const int32_t p = (int32_t)(e & 0xFFFFFu) - 8 + (j & 7);
+        int r = (int)(e >> 20);
+        if (p >= 0 && p < G1r) {
+          // 8 tokens span at most 4 rows (a row holds >= 3 tokens)
+#pragma unroll
+          for (int k = 0; k < 3; ++k)
+            if (r + 1 < nr && p >= W.roff[r + 1]) ++r;
+          const RowDesc x = W.row[r];
+          const int32_t t = p - W.roff[r];
+          pos[m] = p;
+          if (t == 0) y[m] = cls;
+          else if (t <= x.l0) { src = x.src0 + (t - 1); ld = true; }
+          else if (t >= x.b1 && t < x.b1 + x.l1) { src = x.src1 + (t - x.b1); ld = true; }
+        }
+      }
+      if (ld) y[m] = M.dense[src];
+    }
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+      if (pos[m] >= 0) M.out_tokens[G0 + pos[m]] = (uint16_t)y[m];
+  }
+  mat_wsync();
+}
+
+__global__ __launch_bounds__(256) void materialize2_kernel(MatParams M, int64_t total) {
+  __shared__ MatWave mw[4];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t item = (int64_t)blockIdx.x * 4 + wv;
+  const int64_t gbase = item * 64;
+  if (gbase >= total) return;
+  const int nr = (int)min((int64_t)64, total - gbase);
+  MatWave& W = mw[wv];
+  // partition of the item's first pair (uniform binary search over pair_base)
+  int64_t plo = 0, phi = M.n_part - 1;
+  while (plo < phi) {
+    const int64_t mid = (plo + phi + 1) >> 1;
+    if (M.pair_base[mid] <= gbase) plo = mid;
+    else phi = mid - 1;
+  }
+  // ---- row metadata + per-pair outputs ----
+  int64_t off = 0, rend = 0;
+  RowDesc x{};
+  if (lane < nr) {
+    const int64_t g = gbase + lane;
+    int64_t p = plo;
+    while (M.pair_base[p + 1] <= g) ++p;  // partitions of < 64 pairs
+    const int64_t i = g - M.pair_base[p];
+    const int64_t pb = (int64_t)M.dup * M.doc_sent_off[M.part_doc_off[p]];
+    const PairRec r = M.pairs[pb + M.binned[pb + i]];
+    off = M.tok_base[p] + M.tok_local[pb + i];
+    const int32_t l0 = r.hi0 - r.lo0, l1 = r.hi1 - r.lo1;
+    x.src0 = l0 > 0 ? M.fs_dense[r.fs0] + r.lo0 : 0;
+    x.src1 = l1 > 0 ? M.fs_dense[r.fs1] + r.lo1 : 0;
+    x.l0 = l0;
+    x.l1 = l1;
+    x.b1 = 1 + l0 + ((r.flags & 2) != 0);
+    x.nt = r.num_tokens;
+    rend = off + r.num_tokens;
+    M.out_tok_off[g] = off;
+    M.out_len0[g] = (uint16_t)l0;
+    M.out_len1[g] = (uint16_t)l1;
+    M.out_flags[g] = (uint8_t)r.flags;
+    const int32_t b = ((int32_t)r.num_tokens - 1) / M.bin_size;
+    M.out_bin[g] = (uint8_t)(b > M.nbins - 1 ? M.nbins - 1 : b);
+    M.out_part[g] = p;
+    if (g == total - 1) M.out_tok_off[total] = rend;
+  }
+  const int64_t G0 = __shfl(off, 0), G1 = __shfl(rend, nr - 1);
+  const int32_t G1r = (int32_t)(G1 - G0);
+  W.roff[lane] = lane < nr ? (int32_t)(off - G0) : 0x7FFFFFFF;
+  W.row[lane] = x;
+  mat_wsync();
+  // ---- phase 1 ----
+  const int64_t q0 = G0 >> 3, q1 = (G1 + 7) >> 3;
+  uint4* out4 = reinterpret_cast<uint4*>(M.out_tokens);
+  const uint4* d4 = reinterpret_cast<const uint4*>(M.dense);
+  int ns = 0;  // listed slow chunks (wave-uniform)
+  for (int64_t qb = q0; qb < q1; qb += MAT_U * 64) {
+    int64_t src[MAT_U];
+    bool fast[MAT_U], slow[MAT_U];
+    int rw[MAT_U];
+#pragma unroll
+    for (int u = 0; u < MAT_U; ++u) {
+      const int64_t q = qb + u * 64 + lane;
+      const int32_t p0 = (int32_t)((q << 3) - G0), ps = p0 < 0 ? 0 : p0;
+      int r = 0;
+#pragma unroll
+      for (int st = 32; st >= 1; st >>= 1)
+        if (W.roff[r + st] <= ps) r += st;
+      rw[u] = r;
+      const RowDesc y = W.row[r];
+      const int32_t t0 = p0 - W.roff[r];
+      const bool inA = t0 >= 1 && t0 + 8 <= 1 + y.l0, inB = t0 >= y.b1 && t0 + 8 <= y.b1 + y.l1;
+      fast[u] = q < q1 && (inA || inB);
+      slow[u] = q < q1 && !(inA || inB);
+      src[u] = fast[u] ? (inA ? y.src0 + (t0 - 1) : y.src1 + (t0 - y.b1)) : 0;
+    }
+    uint4 va[MAT_U], vb[MAT_U];
+#pragma unroll
+    for (int u = 0; u < MAT_U; ++u) {
+      const int64_t a = src[u] >> 3;
+      va[u] = d4[a];
+      vb[u] = d4[a + 1];
+    }
+#pragma unroll
+    for (int u = 0; u < MAT_U; ++u)
+      if (fast[u]) out4[qb + u * 64 + lane] = funnel8(va[u], vb[u], (uint32_t)(src[u] & 7));
+    // slow chunks to the list (ballot-compacted)
+#pragma unroll
+    for (int u = 0; u < MAT_U; ++u) {
+      const uint64_t m = __ballot(slow[u]);
+      if (slow[u]) {
+        const int32_t p0 = (int32_t)(((qb + u * 64 + lane) << 3) - G0);
+        W.slow[ns + __popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)(p0 + 8) | ((uint32_t)rw[u] << 20);
+      }
+      ns += __popcll(m);
+    }
+    if (ns > MAT_SLOW - MAT_U * 64) {
+      mat_drain(M, W, ns, nr, G0, G1r, lane);
+      ns = 0;
+    }
+  }
+  if (ns > 0) mat_drain(M, W, ns, nr, G0, G1r, lane);
+}
+
 // ------------------------------------------------ dense id compaction ----
 constexpr int SCAN_ITEMS = 4096;  // ntok entries per scan block (256 x 16)
 
@@ -623,9 +807,15 @@ hipError_t launch_masked_lm(const MlmParams& M, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_materialize(const MatParams& M, hipStream_t s) {
-  const int64_t grid = (M.n_part + 3) / 4;  // one wave per partition
-  hipLaunchKernelGGL(materialize_kernel, dim3((unsigned)grid), dim3(256), 0, s, M);
+hipError_t launch_materialize(const MatParams& M, int64_t total_pairs, int algo, hipStream_t s) {
+  // v2 needs a 16-B aligned output and 16 u16 of slack after the dense ids
+  if (algo != 1 && (reinterpret_cast<uintptr_t>(M.out_tokens) & 15u) == 0) {
+    const int64_t items = (total_pairs + 63) / 64;  // one wave per 64 pairs
+    hipLaunchKernelGGL(materialize2_kernel, dim3((unsigned)((items + 3) / 4)), dim3(256), 0, s, M, total_pairs);
+  } else {
+    const int64_t grid = (M.n_part + 3) / 4;  // one wave per partition
+    hipLaunchKernelGGL(materialize_kernel, dim3((unsigned)grid), dim3(256), 0, s, M);
+  }
   return hipGetLastError();
 }
 
