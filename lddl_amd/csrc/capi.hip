@@ -664,8 +664,11 @@ extern "C" int lddl_materialize(lddl_ctx* c, const uint16_t* d_ids, uint16_t* d_
   M.ids = d_ids;
   uint16_t* dense;
   int rc;
+  // LDDL_MAT_ALGO=1: the wave-per-partition materialize and per-sentence
+  // compaction kernels; otherwise the chunked v2 kernels
+  const int mat_algo = getenv("LDDL_MAT_ALGO") ? atoi(getenv("LDDL_MAT_ALGO")) : 2;
   if ((rc = ws_get(c, 34, (size_t)c->last_ndense + 16, &dense))) return rc;
-  HIP_TRY(launch_compact_ids(d_ids, P.sent_off, P.ntok, P.tokoff, c->last_nsent, dense, st));
+  HIP_TRY(launch_compact_ids(d_ids, P.sent_off, P.ntok, P.tokoff, c->last_nsent, dense, mat_algo, st));
   M.dense = dense;
   M.fs_dense = P.fs_dense;
   M.sent_off = P.sent_off;
@@ -696,8 +699,7 @@ extern "C" int lddl_materialize(lddl_ctx* c, const uint16_t* d_ids, uint16_t* d_
   if (c->last_npairs == 0) {
     HIP_TRY(hipMemsetAsync(d_out_tok_off, 0, 8, st));
   } else {
-    static const int mat_algo = getenv("LDDL_MAT_ALGO") ? atoi(getenv("LDDL_MAT_ALGO")) : 2;
-    HIP_TRY(launch_materialize(M, c->last_npairs, mat_algo, st));
+    HIP_TRY(launch_materialize(M, c->last_npairs, c->last_ndense + 16, mat_algo, st));
   }
   if (d_bin_count)
     HIP_TRY(hipMemcpyAsync(d_bin_count, P.bin_count, (size_t)P.n_part * P.nbins * 8, hipMemcpyDeviceToDevice, st));

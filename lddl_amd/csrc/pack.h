@@ -131,14 +131,14 @@ hipError_t launch_scan_parts(const int64_t* a, const int64_t* b, int64_t n, int6
                              const int32_t* err, int32_t* err_any, hipStream_t s);
 // algo 1: wave per partition (u16 copies); otherwise wave per 64 pairs with
 // 16-B stores (needs out_tokens 16-B aligned and dense padded by 16 u16)
-hipError_t launch_materialize(const MatParams& M, int64_t total_pairs, int algo, hipStream_t s);
+hipError_t launch_materialize(const MatParams& M, int64_t total_pairs, int64_t n_dense, int algo, hipStream_t s);
 // tokoff[0..n] = exclusive scan of ntok[0..n) (int64); blocksums: scratch of
 // scan_blocks(n) + 1 entries
 int64_t scan_blocks(int64_t n);
 hipError_t launch_scan_ntok(const int32_t* ntok, int64_t n, int64_t* tokoff, int64_t* blocksums, hipStream_t s);
 // dense[tokoff[s] + k] = ids[sent_off[s] - sent_off[0] + k], k < ntok[s]
 hipError_t launch_compact_ids(const uint16_t* ids, const int64_t* sent_off, const int32_t* ntok,
-                              const int64_t* tokoff, int64_t n_sent, uint16_t* dense, hipStream_t s);
+                              const int64_t* tokoff, int64_t n_sent, uint16_t* dense, int algo, hipStream_t s);
 hipError_t launch_sent_special(const uint16_t* ids, const int64_t* sent_off, const int32_t* ntok, int64_t n_sent,
                                uint32_t cls, uint32_t sep, uint8_t* out, hipStream_t s);
 hipError_t launch_masked_lm(const MlmParams& M, hipStream_t s);

@@ -410,26 +410,29 @@ __global__ __launch_bounds__(256) void materialize_kernel(MatParams M) {
   }
 }
 
-// ---- materialize v2: wave per 64 consecutive global pairs ------------------
-// Waves are dispatched in pair order, so the resident waves touch only a few
-// dozen partitions' dense ids at a time: the dup-fold re-reads of a sentence's
-// ids are served on-die (L2 / MALL) rather than from HBM.  The 64 rows of a
-// wave are one contiguous output range [G0, G1), written in aligned 8-token
-// (16-B) chunks.  Phase 1 is branch-free, 4 chunks per lane in flight: a chunk
-// inside one source segment is two aligned 16-B loads funnel-shifted into one
-// 16-B store.  Every other chunk ([CLS]/[SEP], a row boundary, or one of the
-// two chunks shared with the neighbouring waves) goes to a per-wave list that
-// phase 2 drains token-parallel (one token per lane, u16 load + store).
+// ---- chunked row copy (materialize v2, dense compaction v2) ----------------
+// A wave owns 64 consecutive rows whose outputs form one contiguous range
+// [G0, G1).  Materialize: a row is [CLS] A [SEP] (B [SEP]) from the dense ids
+// (LEAD); compaction: a row is one sentence's ids.  Waves are dispatched in
+// row order, so the resident waves touch only a narrow window of the source
+// (the dup-fold re-reads of a sentence's ids in materialize stay on-die).
+// The range is written in aligned 8-token (16-B) chunks.  Phase 1 is
+// branch-free, MAT_U chunks per lane in flight: a chunk inside one source
+// segment is two aligned 16-B loads funnel-shifted into one 16-B store.
+// Every other chunk ([CLS]/[SEP], a row boundary, or one of the two chunks
+// shared with the neighbouring waves) goes to a per-wave list that phase 2
+// drains token-parallel (one token per lane, u16 load + store).
 constexpr int MAT_U = 4;         // chunks per lane per phase-1 iteration
 constexpr int MAT_SLOW = 512;    // slow-chunk list capacity per wave
+constexpr int MAT_PBITS = 26;    // slow entry: chunk start + 8 (26 bits) | row << 26
 struct RowDesc {
-  int64_t src0, src1;       // dense start of segment A / B
+  int64_t src0, src1;       // source start of segment A / B
   int32_t l0, b1, l1, nt;   // |A|, first position of B, |B|, row length
 };
 struct MatWave {
   int32_t roff[64];         // row start relative to G0 (INT_MAX past the last row)
   RowDesc row[64];
-  uint32_t slow[MAT_SLOW];  // chunk start (relative to G0, + 8) | row << 20
+  uint32_t slow[MAT_SLOW];
 };
 
 // u16 window [m, m + 8) of the 16 u16 held in A:B
@@ -451,12 +454,36 @@ __device__ __forceinline__ void mat_wsync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// phase 2: the ns listed chunks, one token per lane
-__device__ __forceinline__ void mat_drain(const MatParams& M, const MatWave& W, int ns, int nr, int64_t G0,
-                                          int32_t G1r, int lane) {
+// last row starting at or before p (rows may be empty: the last of equals)
+__device__ __forceinline__ int mat_row(const MatWave& W, int32_t p) {
+  int r = 0;
+#pragma unroll
+  for (int st = 32; st >= 1; st >>= 1)
+    if (W.roff[r + st] <= p) r += st;
+  return r;
+}
+
+// token t of row x: the special it is (false) or its source index (true)
+template <bool LEAD>
+__device__ __forceinline__ bool mat_tok(const RowDesc& x, int32_t t, uint32_t cls, uint32_t& y, int64_t& src) {
+  if constexpr (LEAD) {
+    if (t == 0) { y = cls; return false; }
+    if (t <= x.l0) { src = x.src0 + (t - 1); return true; }
+    if (t >= x.b1 && t < x.b1 + x.l1) { src = x.src1 + (t - x.b1); return true; }
+    return false;  // [SEP]
+  } else {
+    src = x.src0 + t;
+    return true;
+  }
+}
+
+// phase 2: tokens [0, ntok) of the listed chunks (or, with W == nullptr
+// semantics via plain, every position of the range), one token per lane
+template <bool LEAD>
+__device__ __forceinline__ void mat_drain(const MatWave& W, int ntok, bool listed, int64_t G0, int32_t G1r,
+                                          const uint16_t* src, uint16_t* out, uint32_t cls, uint32_t sep,
+                                          int lane) {
   mat_wsync();
-  const int ntok = ns * 8;
-  const uint16_t cls = (uint16_t)M.cls_id, sep = (uint16_t)M.sep_id;
   for (int j0 = 0; j0 < ntok; j0 += 4 * 64) {
     uint32_t y[4];
     int32_t pos[4];
@@ -465,39 +492,101 @@ __device__ __forceinline__ void mat_drain(const MatParams& M, const MatWave& W, 
       const int j = j0 + m * 64 + lane;
       pos[m] = -1;
       y[m] = sep;
-      int64_t src = 0;
+      int64_t s = 0;
       bool ld = false;
       if (j < ntok) {
-        const uint32_t e = W.slow[j >> 3];
-        const int32_t p = (int32_t)(e & 0xFFFFFu) - 8 + (j & 7);
-        int r = (int)(e >> 20);
+        const int32_t p = listed ? (int32_t)(W.slow[j >> 3] & ((1u << MAT_PBITS) - 1u)) - 8 + (j & 7) : j;
         if (p >= 0 && p < G1r) {
-          // 8 tokens span at most 4 rows (a row holds >= 3 tokens)
-#pragma unroll
-          for (int k = 0; k < 3; ++k)
-            if (r + 1 < nr && p >= W.roff[r + 1]) ++r;
-          const RowDesc x = W.row[r];
-          const int32_t t = p - W.roff[r];
+          const int r = mat_row(W, p);
           pos[m] = p;
-          if (t == 0) y[m] = cls;
-          else if (t <= x.l0) { src = x.src0 + (t - 1); ld = true; }
-          else if (t >= x.b1 && t < x.b1 + x.l1) { src = x.src1 + (t - x.b1); ld = true; }
+          ld = mat_tok<LEAD>(W.row[r], p - W.roff[r], cls, y[m], s);
         }
       }
-      if (ld) y[m] = M.dense[src];
+      if (ld) y[m] = src[s];
     }
 #pragma unroll
     for (int m = 0; m < 4; ++m)
-      if (pos[m] >= 0) M.out_tokens[G0 + pos[m]] = (uint16_t)y[m];
+      if (pos[m] >= 0) out[G0 + pos[m]] = (uint16_t)y[m];
   }
   mat_wsync();
 }
 
-__global__ __launch_bounds__(256) void materialize2_kernel(MatParams M, int64_t total) {
+// rows published in W (roff, row) for nr rows spanning [G0, G1) of out;
+// src readable for n_src entries
+template <bool LEAD>
+__device__ __forceinline__ void mat_copy(MatWave& W, int64_t G0, int64_t G1, const uint16_t* src, int64_t n_src,
+                                         uint16_t* out, uint32_t cls, uint32_t sep, int lane) {
+  const int32_t G1r = (int32_t)(G1 - G0);
+  if (G1 - G0 >= (1 << MAT_PBITS) - 16) {  // (rows beyond any real max_tok) token by token
+    mat_drain<LEAD>(W, G1r, false, G0, G1r, src, out, cls, sep, lane);
+    return;
+  }
+  const int64_t q0 = G0 >> 3, q1 = (G1 + 7) >> 3;
+  uint4* out4 = reinterpret_cast<uint4*>(out);
+  const uint4* s4 = reinterpret_cast<const uint4*>(src);
+  const int64_t amax = (n_src >> 3) - 2;  // last 16-B pair fully inside src
+  int ns = 0;  // listed slow chunks (wave-uniform)
+  for (int64_t qb = q0; qb < q1; qb += MAT_U * 64) {
+    int64_t sv[MAT_U];
+    bool fast[MAT_U], slow[MAT_U];
+    int rw[MAT_U];
+#pragma unroll
+    for (int u = 0; u < MAT_U; ++u) {
+      const int64_t q = qb + u * 64 + lane;
+      const int32_t p0 = (int32_t)((q << 3) - G0);
+      const int r = mat_row(W, p0 < 0 ? 0 : p0);
+      rw[u] = r;
+      const RowDesc y = W.row[r];
+      const int32_t t0 = p0 - W.roff[r];
+      bool inA, inB;
+      int64_t v;
+      if constexpr (LEAD) {
+        inA = t0 >= 1 && t0 + 8 <= 1 + y.l0;
+        inB = t0 >= y.b1 && t0 + 8 <= y.b1 + y.l1;
+        v = inA ? y.src0 + (t0 - 1) : y.src1 + (t0 - y.b1);
+      } else {
+        inA = t0 >= 0 && t0 + 8 <= y.l0;
+        inB = false;
+        v = y.src0 + t0;
+      }
+      fast[u] = q < q1 && (inA || inB) && (v >> 3) <= amax;
+      slow[u] = q < q1 && !fast[u];
+      sv[u] = fast[u] ? v : 0;
+    }
+    uint4 va[MAT_U], vb[MAT_U];
+#pragma unroll
+    for (int u = 0; u < MAT_U; ++u) {
+      const int64_t a = sv[u] >> 3;
+      va[u] = vb[u] = make_uint4(0, 0, 0, 0);
+      if (fast[u]) {  // exec-masked: no load past a short source
+        va[u] = s4[a];
+        vb[u] = s4[a + 1];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < MAT_U; ++u)
+      if (fast[u]) out4[qb + u * 64 + lane] = funnel8(va[u], vb[u], (uint32_t)(sv[u] & 7));
+#pragma unroll
+    for (int u = 0; u < MAT_U; ++u) {
+      const uint64_t m = __ballot(slow[u]);
+      if (slow[u]) {
+        const int32_t p0 = (int32_t)(((qb + u * 64 + lane) << 3) - G0);
+        W.slow[ns + __popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)(p0 + 8) | ((uint32_t)rw[u] << MAT_PBITS);
+      }
+      ns += __popcll(m);
+    }
+    if (ns > MAT_SLOW - MAT_U * 64) {
+      mat_drain<LEAD>(W, ns * 8, true, G0, G1r, src, out, cls, sep, lane);
+      ns = 0;
+    }
+  }
+  if (ns > 0) mat_drain<LEAD>(W, ns * 8, true, G0, G1r, src, out, cls, sep, lane);
+}
+
+__global__ __launch_bounds__(256) void materialize2_kernel(MatParams M, int64_t total, int64_t n_src) {
   __shared__ MatWave mw[4];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int64_t item = (int64_t)blockIdx.x * 4 + wv;
-  const int64_t gbase = item * 64;
+  const int64_t gbase = ((int64_t)blockIdx.x * 4 + wv) * 64;
   if (gbase >= total) return;
   const int nr = (int)min((int64_t)64, total - gbase);
   MatWave& W = mw[wv];
@@ -537,61 +626,37 @@ __global__ __launch_bounds__(256) void materialize2_kernel(MatParams M, int64_t 
     if (g == total - 1) M.out_tok_off[total] = rend;
   }
   const int64_t G0 = __shfl(off, 0), G1 = __shfl(rend, nr - 1);
-  const int32_t G1r = (int32_t)(G1 - G0);
   W.roff[lane] = lane < nr ? (int32_t)(off - G0) : 0x7FFFFFFF;
   W.row[lane] = x;
   mat_wsync();
-  // ---- phase 1 ----
-  const int64_t q0 = G0 >> 3, q1 = (G1 + 7) >> 3;
-  uint4* out4 = reinterpret_cast<uint4*>(M.out_tokens);
-  const uint4* d4 = reinterpret_cast<const uint4*>(M.dense);
-  int ns = 0;  // listed slow chunks (wave-uniform)
-  for (int64_t qb = q0; qb < q1; qb += MAT_U * 64) {
-    int64_t src[MAT_U];
-    bool fast[MAT_U], slow[MAT_U];
-    int rw[MAT_U];
-#pragma unroll
-    for (int u = 0; u < MAT_U; ++u) {
-      const int64_t q = qb + u * 64 + lane;
-      const int32_t p0 = (int32_t)((q << 3) - G0), ps = p0 < 0 ? 0 : p0;
-      int r = 0;
-#pragma unroll
-      for (int st = 32; st >= 1; st >>= 1)
-        if (W.roff[r + st] <= ps) r += st;
-      rw[u] = r;
-      const RowDesc y = W.row[r];
-      const int32_t t0 = p0 - W.roff[r];
-      const bool inA = t0 >= 1 && t0 + 8 <= 1 + y.l0, inB = t0 >= y.b1 && t0 + 8 <= y.b1 + y.l1;
-      fast[u] = q < q1 && (inA || inB);
-      slow[u] = q < q1 && !(inA || inB);
-      src[u] = fast[u] ? (inA ? y.src0 + (t0 - 1) : y.src1 + (t0 - y.b1)) : 0;
-    }
-    uint4 va[MAT_U], vb[MAT_U];
-#pragma unroll
-    for (int u = 0; u < MAT_U; ++u) {
-      const int64_t a = src[u] >> 3;
-      va[u] = d4[a];
-      vb[u] = d4[a + 1];
-    }
-#pragma unroll
-    for (int u = 0; u < MAT_U; ++u)
-      if (fast[u]) out4[qb + u * 64 + lane] = funnel8(va[u], vb[u], (uint32_t)(src[u] & 7));
-    // slow chunks to the list (ballot-compacted)
-#pragma unroll
-    for (int u = 0; u < MAT_U; ++u) {
-      const uint64_t m = __ballot(slow[u]);
-      if (slow[u]) {
-        const int32_t p0 = (int32_t)(((qb + u * 64 + lane) << 3) - G0);
-        W.slow[ns + __popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)(p0 + 8) | ((uint32_t)rw[u] << 20);
-      }
-      ns += __popcll(m);
-    }
-    if (ns > MAT_SLOW - MAT_U * 64) {
-      mat_drain(M, W, ns, nr, G0, G1r, lane);
-      ns = 0;
-    }
+  mat_copy<true>(W, G0, G1, M.dense, n_src, M.out_tokens, M.cls_id, M.sep_id, lane);
+}
+
+// dense[tokoff[s] + k] = ids[sent_off[s] - sent_off[0] + k]: wave per 64 sentences
+__global__ __launch_bounds__(256) void compact2_kernel(const uint16_t* ids, const int64_t* sent_off,
+                                                       const int32_t* ntok, const int64_t* tokoff, int64_t n_sent,
+                                                       uint16_t* dense) {
+  __shared__ MatWave mw[4];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t sbase = ((int64_t)blockIdx.x * 4 + wv) * 64;
+  if (sbase >= n_sent) return;
+  const int nr = (int)min((int64_t)64, n_sent - sbase);
+  MatWave& W = mw[wv];
+  const int64_t base = sent_off[0], n_ids = sent_off[n_sent] - base;
+  int64_t off = 0, rend = 0;
+  RowDesc x{};
+  if (lane < nr) {
+    const int64_t s = sbase + lane;
+    off = tokoff[s];
+    x.l0 = x.nt = ntok[s];
+    x.src0 = sent_off[s] - base;
+    rend = off + x.nt;
   }
-  if (ns > 0) mat_drain(M, W, ns, nr, G0, G1r, lane);
+  const int64_t G0 = __shfl(off, 0), G1 = __shfl(rend, nr - 1);
+  W.roff[lane] = lane < nr ? (int32_t)(off - G0) : 0x7FFFFFFF;
+  W.row[lane] = x;
+  mat_wsync();
+  mat_copy<false>(W, G0, G1, ids, n_ids, dense, 0, 0, lane);
 }
 
 // ------------------------------------------------ dense id compaction ----
@@ -712,8 +777,14 @@ __global__ __launch_bounds__(256) void compact_ids_kernel(const uint16_t* ids, c
 }
 
 hipError_t launch_compact_ids(const uint16_t* ids, const int64_t* sent_off, const int32_t* ntok,
-                              const int64_t* tokoff, int64_t n_sent, uint16_t* dense, hipStream_t s) {
+                              const int64_t* tokoff, int64_t n_sent, uint16_t* dense, int algo, hipStream_t s) {
   if (n_sent <= 0) return hipSuccess;
+  if (algo != 1 && ((reinterpret_cast<uintptr_t>(ids) | reinterpret_cast<uintptr_t>(dense)) & 15u) == 0) {
+    const int64_t items = (n_sent + 63) / 64;  // one wave per 64 sentences
+    hipLaunchKernelGGL(compact2_kernel, dim3((unsigned)((items + 3) / 4)), dim3(256), 0, s, ids, sent_off, ntok, tokoff,
+                       n_sent, dense);
+    return hipGetLastError();
+  }
   int64_t grid = (n_sent + 255) / 256;
   if (grid > 8192) grid = 8192;
   hipLaunchKernelGGL(compact_ids_kernel, dim3((unsigned)grid), dim3(256), 0, s, ids, sent_off, ntok, tokoff, n_sent,
@@ -807,11 +878,12 @@ hipError_t launch_masked_lm(const MlmParams& M, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_materialize(const MatParams& M, int64_t total_pairs, int algo, hipStream_t s) {
-  // v2 needs a 16-B aligned output and 16 u16 of slack after the dense ids
-  if (algo != 1 && (reinterpret_cast<uintptr_t>(M.out_tokens) & 15u) == 0) {
+hipError_t launch_materialize(const MatParams& M, int64_t total_pairs, int64_t n_dense, int algo, hipStream_t s) {
+  // v2 needs 16-B aligned output and dense ids
+  if (algo != 1 && ((reinterpret_cast<uintptr_t>(M.out_tokens) | reinterpret_cast<uintptr_t>(M.dense)) & 15u) == 0) {
     const int64_t items = (total_pairs + 63) / 64;  // one wave per 64 pairs
-    hipLaunchKernelGGL(materialize2_kernel, dim3((unsigned)((items + 3) / 4)), dim3(256), 0, s, M, total_pairs);
+    hipLaunchKernelGGL(materialize2_kernel, dim3((unsigned)((items + 3) / 4)), dim3(256), 0, s, M, total_pairs,
+                       n_dense);
   } else {
     const int64_t grid = (M.n_part + 3) / 4;  // one wave per partition
     hipLaunchKernelGGL(materialize_kernel, dim3((unsigned)grid), dim3(256), 0, s, M);

@@ -86,15 +86,18 @@ def test_codebert_golden(cpacker, k):
     assert (a, b, len(tok)) == (e['doc'], e['code'], e['num_tokens'])
 
 
-@pytest.mark.parametrize('caps', [None, '8192,512,8192', '0,0,256'])
+@pytest.mark.parametrize('caps,mat', [(None, None), ('8192,512,8192', None), ('0,0,256', None), (None, '1')])
 @pytest.mark.parametrize('seq,bin_size,nparts', [(128, 32, 7), (512, 64, 3), (128, None, 1)])
-def test_bert_end_to_end_vs_oracle(gpu, monkeypatch, seq, bin_size, nparts, caps):
+def test_bert_end_to_end_vs_oracle(gpu, monkeypatch, seq, bin_size, nparts, caps, mat):
   """caps: the wave packer's per-partition arrays in global memory (default),
   all in LDS, and order/num_tokens in LDS with a capacity some partitions
-  exceed (mixed paths in one launch)."""
+  exceed (mixed paths in one launch).  mat: the chunked materialize and
+  compaction kernels (default) or the per-partition / per-sentence ones (1)."""
   from lddl_amd import synth, pipeline
   if caps:
     monkeypatch.setenv('LDDL_PACK_CAPS', caps)
+  if mat:
+    monkeypatch.setenv('LDDL_MAT_ALGO', mat)
   c = synth.make_wiki(600_000, seed=seq + nparts)
   res = pipeline.run_bert(c, target_seq_length=seq, bin_size=bin_size, n_partitions=nparts, seed=999,
                           check_host=True)
@@ -110,8 +113,11 @@ def test_bert_end_to_end_vs_oracle(gpu, monkeypatch, seq, bin_size, nparts, caps
     assert np.array_equal(bc[p], cnt)
 
 
-def test_codebert_end_to_end_vs_oracle(gpu):
+@pytest.mark.parametrize('mat', [None, '1'])
+def test_codebert_end_to_end_vs_oracle(gpu, monkeypatch, mat):
   from lddl_amd import synth, pipeline
+  if mat:
+    monkeypatch.setenv('LDDL_MAT_ALGO', mat)
   c = synth.make_code(400, seed=31)
   pdo = pipeline.partition_by_bytes(c, 3)
   res = pipeline.run_bert(c, vocab_file=pipeline.VOCAB_CODEBERT, target_seq_length=512, bin_size=64,
