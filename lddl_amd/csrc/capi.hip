@@ -592,7 +592,24 @@ static int pack_common(lddl_ctx* c, int codebert, const int32_t* d_ntok, const i
       P.mcap = c->mlm_cap;
       HIP_TRY(hipMemsetAsync(P.mcounter, 0, 8, st));
     }
+    static uint64_t* d_pdbg = nullptr;
+    const char* pdbg = getenv("LDDL_PACK_DEBUG");
+    P.dbg = nullptr;
+    if (pdbg && pdbg[0] == '1') {
+      if (!d_pdbg) HIP_TRY(hipMalloc((void**)&d_pdbg, 8 * 8));
+      HIP_TRY(hipMemsetAsync(d_pdbg, 0, 8 * 8, st));
+      P.dbg = d_pdbg;
+    }
     HIP_TRY(codebert ? launch_pack_codebert(P, st) : lane_packer ? launch_pack_bert(P, st) : launch_pack_bert_wave(P, st));
+    if (P.dbg && !codebert && !lane_packer) {
+      uint64_t h[8];
+      HIP_TRY(hipMemcpyAsync(h, P.dbg, sizeof h, hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipStreamSynchronize(st));
+      const char* nm[8] = {"filter", "ldsfill", "seed", "generate", "shuffle", "bin", "pairs", "parts"};
+      fprintf(stderr, "[lddl pack dbg]");
+      for (int k = 0; k < 8; ++k) fprintf(stderr, " %s=%llu", nm[k], (unsigned long long)h[k]);
+      fprintf(stderr, "\n");
+    }
     HIP_TRY(launch_scan_parts(P.part_npairs, P.part_ntok, n_part, pair_base, tok_base, P.part_err, err_any, st));
     HIP_TRY(hipMemcpyAsync(c->h_tot, pair_base + n_part, 8, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipMemcpyAsync(c->h_tot + 1, tok_base + n_part, 8, hipMemcpyDeviceToHost, st));

@@ -55,6 +55,7 @@ struct PackParams {
   int32_t* part_err;            // [n_part]
   int32_t* kept;                // [n_sent + n_part] wave packer scratch
   int32_t cap_lens, cap_docs, cap_pairs;  // wave packer: dynamic LDS capacities (per partition)
+  uint64_t* dbg;                // wave packer phase cycles (LDDL_PACK_DEBUG=1), else null
   // static masking (create_masked_lm_predictions, pretrain.py:182-238)
   int32_t masking;
   double mlm_ratio;             // --masked-lm-ratio

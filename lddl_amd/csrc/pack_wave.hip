@@ -20,6 +20,7 @@
 // arrays in global memory (wave-uniform branch).
 #include "common.h"
 #include "pack.h"
+#include "wave.h"
 
 #include <type_traits>
 
@@ -63,19 +64,11 @@ __device__ __forceinline__ void wsync() {
 }
 
 __device__ __forceinline__ int wscan_incl(int v, int lane) {
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int y = __shfl_up(v, o);
-    if (lane >= o) v += y;
-  }
-  return v;
+  (void)lane;
+  return wave_incl_add(v);
 }
 
-__device__ __forceinline__ int wsum(int v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
-}
+__device__ __forceinline__ int wsum(int v) { return lane_get(wave_incl_add(v), 63); }
 
 // ---- CPython MT19937 with the state in LDS -----------------------------
 struct WaveRng {
@@ -185,10 +178,10 @@ __device__ __forceinline__ int find_fill(const GET& len_at, int k0, int n, int t
     const uint64_t m = __ballot(cond);
     if (m) {
       const int j = __ffsll((unsigned long long)m) - 1;
-      *sum_out = __shfl(ps, j);
+      *sum_out = lane_get(ps, j);
       return k + j;
     }
-    base = __shfl(ps, 63);
+    base = lane_get(ps, 63);
   }
   *sum_out = base;
   return n - 1;  // unreachable for n > 0
@@ -220,6 +213,15 @@ __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
   const int64_t pb = (int64_t)P.dup * s0;
   const int64_t base = P.sent_off[0];
   const int nsent = (int)(s1 - s0), ndoc = (int)(d1 - d0);
+  // optional phase stamps (wave-uniform branch): filter, LDS fill, seed,
+  // pair generation, shuffle, binning
+  uint64_t ph[6] = {0, 0, 0, 0, 0, 0}, tprev = P.dbg ? __builtin_amdgcn_s_memtime() : 0;
+#define PW_STAMP(k)                                     \
+  if (P.dbg) {                                          \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime();   \
+    ph[k] += t_ - tprev;                                \
+    tprev = t_;                                         \
+  }
 
   // ---- filter: kept sentence slots via a running wave scan ---------------
   // kept_before[k] = #kept sentences before sentence s0 + k (k <= nsent)
@@ -242,7 +244,7 @@ __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
           if (MASK) P.fs_spec[s0 + slot] = P.sent_spec[s0 + kk];
         }
       }
-      run += __shfl(incl, 63);
+      run += lane_get(incl, 63);
     }
     if (lane == 0) kept_before[nsent] = run;
   }
@@ -267,12 +269,13 @@ __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
       P.fd_first[d0 + di] = s0 + first;
       P.fd_n[d0 + di] = cnt;
     }
-    nd += __shfl(incl, 63);
+    nd += lane_get(incl, 63);
   }
   const int nfs = kept_before[nsent];
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __builtin_amdgcn_s_waitcnt(0);
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  PW_STAMP(0)
   const bool lres = nfs <= P.cap_lens && nd <= P.cap_docs;
   if (lres) {
     for (int k = lane; k < nfs; k += 64) D.lens[k] = (uint16_t)P.fs_ntok[s0 + k];
@@ -288,6 +291,7 @@ __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
     }
   }
   wsync();
+  PW_STAMP(1)
   // slot-relative accessors
   auto len_at = [&](int k) -> int { return lres ? (int)D.lens[k] : P.fs_ntok[s0 + k]; };
   auto doc_first = [&](int d) -> int { return lres ? (int)D.dfirst[d] : (int)(P.fd_first[d0 + d] - s0); };
@@ -295,6 +299,7 @@ __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
 
   WaveRng rng{L, lane, MT_N};
   rng.seed(P.seed + (uint64_t)p);
+  PW_STAMP(2)
   const int max_num = P.max_seq - 3;
   PairRec* out = P.pairs + pb;
   int np = 0;
@@ -484,6 +489,7 @@ __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
       }
     }
   }
+  PW_STAMP(3)
   if (lane == 0) P.part_err[p] = err;
   if (err) {
     if (lane == 0) { P.part_npairs[p] = 0; P.part_ntok[p] = 0; if (MASK) P.part_nmask[p] = 0; }
@@ -509,6 +515,7 @@ __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __builtin_amdgcn_s_waitcnt(0);
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  PW_STAMP(4)
   auto ord_at = [&](int k) -> int { return ores ? (int)D.order[k] : gorder[k]; };
   auto ntk_at = [&](int rec) -> int { return ores ? (int)D.ntk[rec] : (int)out[rec].num_tokens; };
   // ---- stable bin partition + token offsets -------------------------------
@@ -541,11 +548,11 @@ __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
         const int nmk = in ? (int)((uint64_t)P.mref[pb + rec] >> 48) : 0;
         const int minc = wscan_incl(nmk, lane);
         if (in) P.mloc[pb + pos + before] = macc + minc - nmk;
-        macc += __shfl(minc, 63);
+        macc += lane_get(minc, 63);
       }
       pos += __popcll(m);
       cnt += __popcll(m);
-      acc += __shfl(tinc, 63);
+      acc += lane_get(tinc, 63);
     }
     if (lane == 0) P.bin_count[p * nb + b] = cnt;
   }
@@ -554,6 +561,13 @@ __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
     P.part_ntok[p] = acc;
     if (MASK) P.part_nmask[p] = macc;
   }
+  PW_STAMP(5)
+  if (P.dbg && lane == 0) {
+    for (int k = 0; k < 6; ++k) atomicAdd((unsigned long long*)&P.dbg[k], (unsigned long long)ph[k]);
+    atomicAdd((unsigned long long*)&P.dbg[6], (unsigned long long)np);
+    atomicAdd((unsigned long long*)&P.dbg[7], 1ull);
+  }
+#undef PW_STAMP
 }
 
 hipError_t launch_pack_bert_wave(const PackParams& P, hipStream_t s) {
