@@ -36,6 +36,7 @@
 // are listed and re-run by tokenize_fallback_kernel (exact serial path).
 #include "common.h"
 #include "tokenize.h"
+#include "wave.h"
 #include "tokenize_serial.h"
 
 namespace lddl {
@@ -103,13 +104,9 @@ __device__ __forceinline__ int lane_rank(uint64_t m) {
 }
 
 __device__ __forceinline__ uint32_t wave_excl(uint32_t v, int lane, uint32_t* total) {
-  uint32_t x = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t y = __shfl_up(x, o);
-    if (lane >= o) x += y;
-  }
-  *total = __shfl(x, 63);
+  (void)lane;
+  const uint32_t x = wave_incl_add(v);
+  *total = lane_get(x, 63);
   return x - v;
 }
 
@@ -460,8 +457,7 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
       }
     }
     {
-      uint32_t im = __shfl_up(sp_m, 1), iw = __shfl_up(sp_w, 1), id = __shfl_up(sp_d, 1);
-      if (lane == 0) im = iw = id = 0;
+      const uint32_t im = wave_shr1(sp_m), iw = wave_shr1(sp_w), id = wave_shr1(sp_d);  // lane 0: 0
       W = ((W & ~im) | iw) & inwin;
       I &= ~im & inwin;
       S &= ~im & inwin;
@@ -473,7 +469,7 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
     STAMP(1);
     // ---- 2: units -----------------------------------------------------------
     const uint32_t SB = L.sb[lane];
-    const uint32_t carry = __shfl_up(W, 1) >> 31;
+    const uint32_t carry = wave_shr1(W) >> 31;
     const uint32_t pw = (W << 1) | (lane ? carry : 0u);
     const uint32_t U = CS & (I | (W & (~pw | SB)));
     L.brk[lane] = U | (S & CS) | SB;
@@ -882,17 +878,9 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
           run += L.ucnt[uu];
         }
       }
-      int hv = head, sv = run;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const int ph = __shfl_up(hv, o), ps = __shfl_up(sv, o);
-        if (lane >= o && !hv) {
-          sv += ps;
-          hv = ph;
-        }
-      }
-      int ex = __shfl_up(sv, 1), exh = __shfl_up(hv, 1);
-      if (lane == 0) ex = exh = 0;
+      uint32_t hv = (uint32_t)head, sv = (uint32_t)run;
+      wave_seg_incl_add(hv, sv);
+      int ex = (int)wave_shr1(sv), exh = (int)wave_shr1(hv);  // lane 0: 0
       if (!exh) ex += carry0;  // units before any head continue the previous round's sentence
       bool before = true;
       const int64_t obase = (A - base) - aoff;
