@@ -7,7 +7,7 @@ import ctypes
 import os
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_PKG, 'liblddl_amd.so')
+LIB_PATH = os.environ.get('LDDL_LIB') or os.path.join(_PKG, 'liblddl_amd.so')  # LDDL_LIB: A/B tools
 TABLE_PATH = os.path.join(_PKG, 'data', 'unicode_table.bin')
 VOCAB_BERT = os.path.join(_PKG, 'data', 'bert_vocab.txt')
 VOCAB_CODEBERT = os.path.join(_PKG, 'data', 'codebert_52000_vocab.txt')

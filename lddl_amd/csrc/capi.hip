@@ -268,8 +268,8 @@ static int load_vocab(lddl_ctx* c, const char* path) {
       if (vlen[i] == 0) continue;
       uint32_t d[VKEY_DW] = {0, 0, 0, 0, 0, 0};
       memcpy(d, &pool[voff[i]], vlen[i] < 24 ? vlen[i] : 24);
-      const uint32_t h = vhash(d, vlen[i], vcont[i]);
-      vbl[vbloom_word(h)] |= vbloom_bits(h);
+      const uint32_t h = vhash(d, vlen[i], vcont[i]), bk = vbkey_of(d, vlen[i], vcont[i]);
+      vbl[vbloom_word(bk)] |= vbloom_bits(bk);
       bool done = false;
       for (uint32_t b = h & (nbk - 1); !done; b = (b + 1) & (nbk - 1)) {
         for (int sl = 0; sl < 2 && !done; ++sl) {

@@ -84,11 +84,33 @@ LDDL_HD uint32_t vhash(const uint32_t* d, uint32_t len, uint32_t cont) {
   if (r) h = vmix(h, d[q] & ((1u << (8 * r)) - 1u));
   return vfinal(h, len, cont);
 }
-// blocked Bloom filter over the same keys (BLOOM_WORDS dwords, 2 bits/key),
-// indexed straight from the (finalised) hash: word = top 13 bits, bits = the
-// two low 5-bit fields (the bucket index reuses the low bits; harmless)
-LDDL_HD uint32_t vbloom_word(uint32_t h) { return h >> 19; }
-LDDL_HD uint32_t vbloom_bits(uint32_t h) { return (1u << (h & 31u)) | (1u << ((h >> 5) & 31u)); }
+// low 32 bits of the product of the low 24 bits of a and b (v_mul_u32_u24,
+// full rate; a 32-bit v_mul_lo_u32 is quarter rate)
+LDDL_HD uint32_t mul24(uint32_t a, uint32_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __umul24(a, b);
+#else
+  return (a & 0xFFFFFFu) * (b & 0xFFFFFFu);
+#endif
+}
+// Bloom key of a candidate from the mixes hq of its full dwords (first 24
+// bytes), its masked partial dword (0 if none), byte length and "##" flag.
+// The WordPiece scan evaluates it for every candidate length, so it avoids
+// the 32-bit multiplies of vfinal; the bucket index keeps vhash.
+LDDL_HD uint32_t vbkey(uint32_t hq, uint32_t tail, uint32_t len, uint32_t cont) {
+  uint32_t x = hq ^ mul24(tail, 0xB5297Au) ^ mul24(len, 0x9E3779u) ^ (cont ? 0x7F4A7C15u : 0u);
+  return x ^ (x >> 16);
+}
+LDDL_HD uint32_t vbkey_of(const uint32_t* d, uint32_t len, uint32_t cont) {
+  const uint32_t l = len < 24u ? len : 24u, q = l >> 2, r = l & 3u;
+  uint32_t h = VSEED;
+  for (uint32_t k = 0; k < q; ++k) h = vmix(h, d[k]);
+  return vbkey(h, r ? d[q] & ((1u << (8 * r)) - 1u) : 0u, len, cont);
+}
+// blocked Bloom filter over the Bloom keys (BLOOM_WORDS dwords, 2 bits/key):
+// word = top 13 bits, bits = two 5-bit fields below them
+LDDL_HD uint32_t vbloom_word(uint32_t x) { return x >> 19; }
+LDDL_HD uint32_t vbloom_bits(uint32_t x) { return (1u << ((x >> 9) & 31u)) | (1u << ((x >> 14) & 31u)); }
 
 // ---- MT19937 (CPython random) ----------------------------------------------
 constexpr int MT_N = 624;

@@ -227,16 +227,27 @@ __device__ __forceinline__ Key6 load_key(const WaveLds& L, int s, int len) {
   k.d5 = m(5, __builtin_amdgcn_alignbyte(x6, x5, sh));
   return k;
 }
-// == vhash (common.h) of a loaded key
-__device__ __forceinline__ uint32_t key_hash(const Key6& k, int len, uint32_t cont) {
+// == vhash (common.h) of a loaded key; *bk = its Bloom key (vbkey)
+__device__ __forceinline__ uint32_t key_hash(const Key6& k, int len, uint32_t cont, uint32_t* bk) {
   const int lc = min(len, 24);
-  uint32_t h = VSEED;
-  if (lc > 0) h = vmix(h, k.d0);
-  if (lc > 4) h = vmix(h, k.d1);
-  if (lc > 8) h = vmix(h, k.d2);
-  if (lc > 12) h = vmix(h, k.d3);
-  if (lc > 16) h = vmix(h, k.d4);
-  if (lc > 20) h = vmix(h, k.d5);
+  uint32_t h = VSEED, hq = VSEED, tail = 0;
+#define TOK4_KH(i, di)            \
+  if (lc > 4 * (i)) {             \
+    if (lc < 4 * (i) + 4) {       \
+      hq = h;                     \
+      tail = di;                  \
+    }                             \
+    h = vmix(h, di);              \
+  }
+  TOK4_KH(0, k.d0)
+  TOK4_KH(1, k.d1)
+  TOK4_KH(2, k.d2)
+  TOK4_KH(3, k.d3)
+  TOK4_KH(4, k.d4)
+  TOK4_KH(5, k.d5)
+#undef TOK4_KH
+  if ((lc & 3) == 0) hq = h;
+  *bk = vbkey(hq, tail, (uint32_t)len, cont);
   return vfinal(h, (uint32_t)len, cont);
 }
 __device__ __forceinline__ bool slot_eq(const uint4& a, const uint4& b, const Key6& k, uint32_t want) {
@@ -570,8 +581,9 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
     const uint32_t w = u < nr ? L.uwp[u] : 0u;                                 \
     const int len = (int)(w >> 20);                                            \
     if (w != 0 && len <= 24 && len <= mb0) {                                   \
-      const uint32_t h = key_hash(load_key(L, (int)((w >> 8) & 0xFFFu), len), len, 0u); \
-      if (bl_ok(h)) {                                                          \
+      uint32_t bk;                                                             \
+      const uint32_t h = key_hash(load_key(L, (int)((w >> 8) & 0xFFFu), len), len, 0u, &bk); \
+      if (bl_ok(bk)) {                                                         \
         const uint4* bk = P.vt + 4 * (h & vmask);                              \
         fa##k = bk[0];                                                         \
         fb##k = bk[1];                                                         \
@@ -672,6 +684,10 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
         if (r) h = vmix(h, selD(q) & ((1u << (8 * r)) - 1u));
         return vfinal(h, (uint32_t)l, cont);
       };
+      auto bkey_len = [&](int l) {  // == vbkey of the candidate [s, s+l)
+        const int lc = min(l, 24), q = lc >> 2, r = lc & 3;
+        return vbkey(selH(q), r ? selD(q) & ((1u << (8 * r)) - 1u) : 0u, (uint32_t)l, cont);
+      };
       auto bloom_ok = [&](uint32_t h) {
         if (!BLOOM) return true;
         const uint32_t bb = vbloom_bits(h);
@@ -764,15 +780,12 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
               int fl = 0;
 #define TOK4_GROUP(k, Hk, Hk1, ck)                                                                  \
   if (fl == 0 && 4 * (k) < len) {                                                                   \
-    const uint32_t g4 = vfinal(Hk1, 4 * (k) + 4, cont), g3 = vfinal(vmix(Hk, (ck) & 0xFFFFFFu), 4 * (k) + 3, cont), \
-                   g2 = vfinal(vmix(Hk, (ck) & 0xFFFFu), 4 * (k) + 2, cont),                        \
-                   g1 = vfinal(vmix(Hk, (ck) & 0xFFu), 4 * (k) + 1, cont);                          \
+    const uint32_t g4 = vbkey(Hk1, 0u, 4 * (k) + 4, cont), g3 = vbkey(Hk, (ck) & 0xFFFFFFu, 4 * (k) + 3, cont), \
+                   g2 = vbkey(Hk, (ck) & 0xFFFFu, 4 * (k) + 2, cont),                               \
+                   g1 = vbkey(Hk, (ck) & 0xFFu, 4 * (k) + 1, cont);                                 \
     const bool o4 = 4 * (k) + 4 <= len && bloom_ok(g4), o3 = 4 * (k) + 3 <= len && bloom_ok(g3),   \
                o2 = 4 * (k) + 2 <= len && bloom_ok(g2), o1 = bloom_ok(g1);                          \
-    if (o4 | o3 | o2 | o1) {                                                                        \
-      fl = o4 ? 4 * (k) + 4 : o3 ? 4 * (k) + 3 : o2 ? 4 * (k) + 2 : 4 * (k) + 1;                    \
-      hcur = o4 ? g4 : o3 ? g3 : o2 ? g2 : g1;                                                      \
-    }                                                                                               \
+    if (o4 | o3 | o2 | o1) fl = o4 ? 4 * (k) + 4 : o3 ? 4 * (k) + 3 : o2 ? 4 * (k) + 2 : 4 * (k) + 1; \
   }
               TOK4_GROUP(5, H5, H6, c5)
               TOK4_GROUP(4, H4, H5, c4)
@@ -784,10 +797,11 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
               if (dbg) acc[7] += len - fl;
               found = fl > 0;
               e = s + fl;
+              if (found) hcur = hash_len(fl);  // bucket hash of the survivor only
             } else {
               while (e > s) {
-                hcur = hash_len(e - s);
-                if (bloom_ok(hcur)) {
+                if (bloom_ok(bkey_len(e - s))) {
+                  hcur = hash_len(e - s);
                   found = true;
                   break;
                 }
@@ -895,10 +909,11 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
           const int c = L.ucnt[uu];
           uint16_t* out = P.out_ids + (obase + (int64_t)L.sst[sj] + pos);
           const int po = L.pcs.upo[uu];
+          // streamed out non-temporally: keep L2 for the vocab table
           if (po == 0xFFFF) {
-            if (c > 0 && pos < P.max_tok) out[0] = L.pcs.uid[uu];
+            if (c > 0 && pos < P.max_tok) __builtin_nontemporal_store(L.pcs.uid[uu], out);
           } else {
-            for (int q = 0; q < c && pos + q < P.max_tok; ++q) out[q] = L.pcs.mp[po + q];
+            for (int q = 0; q < c && pos + q < P.max_tok; ++q) __builtin_nontemporal_store(L.pcs.mp[po + q], out + q);
           }
           if (uu == nr - 1 || (int)(L.urec[uu + 1] >> 16) != sj) L.stot[sj] = (uint16_t)(pos + c);
         }
@@ -913,7 +928,7 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
       if (dbg) { acc[11] += 1; acc[15] += 1; }
       continue;
     }
-    if (lane < ns) P.out_ntok[sa + lane] = min((int)L.stot[lane], P.max_tok);
+    if (lane < ns) __builtin_nontemporal_store(min((int)L.stot[lane], P.max_tok), P.out_ntok + sa + lane);
     STAMP(5);
   }
   if (dbg && lane == 0)
