@@ -270,6 +270,14 @@ static int load_vocab(lddl_ctx* c, const char* path) {
       memcpy(d, &pool[voff[i]], vlen[i] < 24 ? vlen[i] : 24);
       const uint32_t h = vhash(d, vlen[i], vcont[i]), bk = vbkey_of(d, vlen[i], vcont[i]);
       vbl[vbloom_word(bk)] |= vbloom_bits(bk);
+      {  // extension keys of its 4-, 8-, .. 24-byte prefixes shorter than it
+        uint32_t hp = VSEED;
+        for (uint32_t j = 0; j < VKEY_DW && 4 * (j + 1) < vlen[i]; ++j) {
+          hp = vmix(hp, d[j]);
+          const uint32_t ek = vbkey_ext(hp, 4 * (j + 1), vcont[i]);
+          vbl[vbloom_word(ek)] |= vbloom_bits(ek);
+        }
+      }
       bool done = false;
       for (uint32_t b = h & (nbk - 1); !done; b = (b + 1) & (nbk - 1)) {
         for (int sl = 0; sl < 2 && !done; ++sl) {

@@ -107,6 +107,12 @@ LDDL_HD uint32_t vbkey_of(const uint32_t* d, uint32_t len, uint32_t cont) {
   for (uint32_t k = 0; k < q; ++k) h = vmix(h, d[k]);
   return vbkey(h, r ? d[q] & ((1u << (8 * r)) - 1u) : 0u, len, cont);
 }
+// "extension" key of a prefix of 4(j+1) bytes (hq = mixes of its j+1
+// dwords): in the Bloom filter iff some vocab key longer than 4(j+1) bytes
+// starts with it, so the WordPiece scan never needs lengths > 4(j+1) when
+// it is absent.  Tagged length (bit 23): never equal to a real key's.
+constexpr uint32_t VEXT_TAG = 0x800000u;
+LDDL_HD uint32_t vbkey_ext(uint32_t hq, uint32_t plen, uint32_t cont) { return vbkey(hq, 0u, VEXT_TAG | plen, cont); }
 // blocked Bloom filter over the Bloom keys (BLOOM_WORDS dwords, 2 bits/key):
 // word = top 13 bits, bits = two 5-bit fields below them
 LDDL_HD uint32_t vbloom_word(uint32_t x) { return x >> 19; }

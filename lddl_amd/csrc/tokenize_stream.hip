@@ -778,8 +778,19 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
               // lengths 4k+1..4k+4, hashed from Hk / H(k+1) with constant
               // register indices; groups from the top down.
               int fl = 0;
+              // highest reachable group: k+1 only if some vocab key longer
+              // than 4(k+1) bytes starts with the candidate's first 4(k+1)
+              int ga = 0;
+#define TOK4_EXT(j, Hj1) \
+  if (ga == (j) && 4 * ((j) + 1) < len && bloom_ok(vbkey_ext(Hj1, 4 * ((j) + 1), cont))) ga = (j) + 1;
+              TOK4_EXT(0, H1)
+              TOK4_EXT(1, H2)
+              TOK4_EXT(2, H3)
+              TOK4_EXT(3, H4)
+              TOK4_EXT(4, H5)
+#undef TOK4_EXT
 #define TOK4_GROUP(k, Hk, Hk1, ck)                                                                  \
-  if (fl == 0 && 4 * (k) < len) {                                                                   \
+  if (fl == 0 && 4 * (k) < len && (k) <= ga) {                                                      \
     const uint32_t g4 = vbkey(Hk1, 0u, 4 * (k) + 4, cont), g3 = vbkey(Hk, (ck) & 0xFFFFFFu, 4 * (k) + 3, cont), \
                    g2 = vbkey(Hk, (ck) & 0xFFFFu, 4 * (k) + 2, cont),                               \
                    g1 = vbkey(Hk, (ck) & 0xFFu, 4 * (k) + 1, cont);                                 \
