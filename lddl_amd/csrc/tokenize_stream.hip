@@ -920,11 +920,12 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
           const int c = L.ucnt[uu];
           uint16_t* out = P.out_ids + (obase + (int64_t)L.sst[sj] + pos);
           const int po = L.pcs.upo[uu];
-          // streamed out non-temporally: keep L2 for the vocab table
+          // plain stores: L2 merges the partial lines (non-temporal u16
+          // stores measured 1 % faster but 7.6x the HBM write bytes)
           if (po == 0xFFFF) {
-            if (c > 0 && pos < P.max_tok) __builtin_nontemporal_store(L.pcs.uid[uu], out);
+            if (c > 0 && pos < P.max_tok) out[0] = L.pcs.uid[uu];
           } else {
-            for (int q = 0; q < c && pos + q < P.max_tok; ++q) __builtin_nontemporal_store(L.pcs.mp[po + q], out + q);
+            for (int q = 0; q < c && pos + q < P.max_tok; ++q) out[q] = L.pcs.mp[po + q];
           }
           if (uu == nr - 1 || (int)(L.urec[uu + 1] >> 16) != sj) L.stot[sj] = (uint16_t)(pos + c);
         }
@@ -939,7 +940,7 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
       if (dbg) { acc[11] += 1; acc[15] += 1; }
       continue;
     }
-    if (lane < ns) __builtin_nontemporal_store(min((int)L.stot[lane], P.max_tok), P.out_ntok + sa + lane);
+    if (lane < ns) P.out_ntok[sa + lane] = min((int)L.stot[lane], P.max_tok);
     STAMP(5);
   }
   if (dbg && lane == 0)
