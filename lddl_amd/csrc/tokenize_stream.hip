@@ -250,9 +250,11 @@ __device__ __forceinline__ uint32_t key_hash(const Key6& k, int len, uint32_t co
   *bk = vbkey(hq, tail, (uint32_t)len, cont);
   return vfinal(h, (uint32_t)len, cont);
 }
+// branch-free (an && chain lets the compiler sink the slot's other loads
+// behind the first compare: a second dependent round trip on every hit)
 __device__ __forceinline__ bool slot_eq(const uint4& a, const uint4& b, const Key6& k, uint32_t want) {
-  return (b.z & 0xFFFF0000u) == want && a.x == k.d0 && a.y == k.d1 && a.z == k.d2 && a.w == k.d3 && b.x == k.d4 &&
-         b.y == k.d5;
+  return (((b.z & 0xFFFF0000u) ^ want) | (a.x ^ k.d0) | (a.y ^ k.d1) | (a.z ^ k.d2) | (a.w ^ k.d3) | (b.x ^ k.d4) |
+          (b.y ^ k.d5)) == 0u;
 }
 
 template <int WAVES, bool BLOOM, bool DBG>
@@ -638,6 +640,15 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
       nwl = at;  // first-probe hits have left the queue
     }
     wsync();
+    if (P.dbg_mode == 1) {  // ablation (LDDL_TOK_ABLATE=1, diagnostics only): no WordPiece loop
+      for (int i = lane; i < nwl; i += 64) {
+        const int u = (int)(L.uwp[i] & 0xFFu);
+        L.pcs.uid[u] = (uint16_t)P.unk;
+        L.ucnt[u] = 1;
+      }
+      nwl = 0;
+      wsync();
+    }
     if (L.misc[2]) break;  // side buffer overflow: the whole tile falls back
     STAMP(3);
     if (dbg) acc[8] += nr;
@@ -780,9 +791,10 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
               int fl = 0;
               // highest reachable group: k+1 only if some vocab key longer
               // than 4(k+1) bytes starts with the candidate's first 4(k+1)
+              // (branch-free: the Bloom words are always in range)
               int ga = 0;
 #define TOK4_EXT(j, Hj1) \
-  if (ga == (j) && 4 * ((j) + 1) < len && bloom_ok(vbkey_ext(Hj1, 4 * ((j) + 1), cont))) ga = (j) + 1;
+  ga = ((ga == (j)) & (4 * ((j) + 1) < len) & bloom_ok(vbkey_ext(Hj1, 4 * ((j) + 1), cont))) ? (j) + 1 : ga;
               TOK4_EXT(0, H1)
               TOK4_EXT(1, H2)
               TOK4_EXT(2, H3)
@@ -794,8 +806,8 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
     const uint32_t g4 = vbkey(Hk1, 0u, 4 * (k) + 4, cont), g3 = vbkey(Hk, (ck) & 0xFFFFFFu, 4 * (k) + 3, cont), \
                    g2 = vbkey(Hk, (ck) & 0xFFFFu, 4 * (k) + 2, cont),                               \
                    g1 = vbkey(Hk, (ck) & 0xFFu, 4 * (k) + 1, cont);                                 \
-    const bool o4 = 4 * (k) + 4 <= len && bloom_ok(g4), o3 = 4 * (k) + 3 <= len && bloom_ok(g3),   \
-               o2 = 4 * (k) + 2 <= len && bloom_ok(g2), o1 = bloom_ok(g1);                          \
+    const bool o4 = (4 * (k) + 4 <= len) & bloom_ok(g4), o3 = (4 * (k) + 3 <= len) & bloom_ok(g3),  \
+               o2 = (4 * (k) + 2 <= len) & bloom_ok(g2), o1 = bloom_ok(g1);                         \
     if (o4 | o3 | o2 | o1) fl = o4 ? 4 * (k) + 4 : o3 ? 4 * (k) + 3 : o2 ? 4 * (k) + 2 : 4 * (k) + 1; \
   }
               TOK4_GROUP(5, H5, H6, c5)
@@ -832,18 +844,21 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
             if (dbg) acc[6] += 1;
             const int len = e - s;
             const int lc = min(len, 24), q = lc >> 2, r = lc & 3;
-            auto msk = [&](int k, uint32_t c) {
-              return k < q ? c : (k == q && r) ? (c & ((1u << (8 * r)) - 1u)) : 0u;
+            auto msk = [&](int k, uint32_t c) {  // the key's bytes of dword k, branch-free
+              const int nbk = min(max(lc - 4 * k, 0), 4);
+              return c & (nbk >= 4 ? 0xFFFFFFFFu : ((1u << (8 * nbk)) - 1u));
             };
+            (void)q;
+            (void)r;
             const uint32_t m0c = msk(0, c0), m1c = msk(1, c1), m2c = msk(2, c2), m3c = msk(3, c3), m4c = msk(4, c4),
                            m5c = msk(5, c5);
             const uint4* bk = P.vt + 4 * (uint32_t)slot;
             const uint4 a0 = bk[0], a1 = bk[1], b0 = bk[2], b1 = bk[3];
             const uint32_t want = ((uint32_t)len << 16) | (cont << 24) | 0x80000000u;
-            bool m0 = (a1.z & 0xFFFF0000u) == want && a0.x == m0c && a0.y == m1c && a0.z == m2c && a0.w == m3c &&
-                      a1.x == m4c && a1.y == m5c;
-            bool m1 = (b1.z & 0xFFFF0000u) == want && b0.x == m0c && b0.y == m1c && b0.z == m2c && b0.w == m3c &&
-                      b1.x == m4c && b1.y == m5c;
+            bool m0 = (((a1.z & 0xFFFF0000u) ^ want) | (a0.x ^ m0c) | (a0.y ^ m1c) | (a0.z ^ m2c) | (a0.w ^ m3c) |
+                       (a1.x ^ m4c) | (a1.y ^ m5c)) == 0u;
+            bool m1 = (((b1.z & 0xFFFF0000u) ^ want) | (b0.x ^ m0c) | (b0.y ^ m1c) | (b0.z ^ m2c) | (b0.w ^ m3c) |
+                       (b1.x ^ m4c) | (b1.y ^ m5c)) == 0u;
             if (m0 && len > 24) m0 = long_eq(L, P, s, len, a1.w);
             if (m1 && len > 24) m1 = long_eq(L, P, s, len, b1.w);
             if (m0 || m1) {
