@@ -70,6 +70,37 @@ __device__ __forceinline__ int wscan_incl(int v, int lane) {
 
 __device__ __forceinline__ int wsum(int v) { return lane_get(wave_incl_add(v), 63); }
 
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+
+// MT19937 twist (64-word chunks, ascending: the in-place dependences of the
+// sequential generator hold chunk-wise) + temper into tw, all lanes.  Out of
+// line: every draw site would otherwise inline its own copy (code size, SGPR
+// spills); LDS-qualified pointers keep it on ds_* instructions.
+__device__ __attribute__((noinline)) void pack_mt_refill(lds_u32* mt, lds_u32* tw, int lane) {
+  for (int c = 0; c < MT_N; c += 64) {
+    const int i = c + lane;
+    uint32_t v = 0;
+    if (i < MT_N) {
+      const uint32_t a = mt[i], b = mt[i + 1 == MT_N ? 0 : i + 1];
+      const uint32_t m = mt[i + MT_M >= MT_N ? i + MT_M - MT_N : i + MT_M];
+      const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
+      v = m ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+    }
+    wsync();
+    if (i < MT_N) mt[i] = v;
+    wsync();
+  }
+  for (int i = lane; i < MT_N; i += 64) {
+    uint32_t y = mt[i];
+    y ^= y >> 11;
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= y >> 18;
+    tw[i] = y;
+  }
+  wsync();
+}
+
 // ---- CPython MT19937 with the state in LDS -----------------------------
 struct WaveRng {
   PackWaveLds& L;
@@ -111,24 +142,9 @@ struct WaveRng {
     return y;
   }
 
-  // twist + temper on all lanes
+  // twist + temper on all lanes (out of line: pack_mt_refill)
   __device__ __forceinline__ void refill() {
-    uint32_t* mt = L.mt;
-    for (int c = 0; c < MT_N; c += 64) {
-      const int i = c + lane;
-      uint32_t v = 0;
-      if (i < MT_N) {
-        const uint32_t a = mt[i], b = mt[i + 1 == MT_N ? 0 : i + 1];
-        const uint32_t m = mt[i + MT_M >= MT_N ? i + MT_M - MT_N : i + MT_M];
-        const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
-        v = m ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
-      }
-      wsync();
-      if (i < MT_N) mt[i] = v;
-      wsync();
-    }
-    for (int i = lane; i < MT_N; i += 64) L.tw[i] = temper(mt[i]);
-    wsync();
+    pack_mt_refill((lds_u32*)L.mt, (lds_u32*)L.tw, lane);
     idx = 0;
     wbase = -1024;
   }
@@ -194,7 +210,9 @@ __device__ __forceinline__ int range_sum(const GET& len_at, int k0, int k1, int 
   return wsum(s);
 }
 
-template <bool MASK>
+// LDSOK = false: every LDS capacity is 0 (the default), the arrays are in
+// global memory and the LDS/global branches compile away
+template <bool MASK, bool LDSOK>
 __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
   __shared__ PackWaveLds L;
   __shared__ typename std::conditional<MASK, MaskLds, NoMaskLds>::type ML;
@@ -276,7 +294,7 @@ __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
   __builtin_amdgcn_s_waitcnt(0);
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   PW_STAMP(0)
-  const bool lres = nfs <= P.cap_lens && nd <= P.cap_docs;
+  const bool lres = LDSOK && nfs <= P.cap_lens && nd <= P.cap_docs;
   if (lres) {
     for (int k = lane; k < nfs; k += 64) D.lens[k] = (uint16_t)P.fs_ntok[s0 + k];
     for (int k = lane; k < nd; k += 64) {
@@ -497,7 +515,7 @@ __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
   }
   wsync();
   // ---- random.shuffle(partition_pairs) -----------------------------------
-  const bool ores = np <= pcap;
+  const bool ores = LDSOK && np <= pcap;
   int32_t* gorder = P.order + pb;
   if (ores) for (int k = lane; k < np; k += 64) D.order[k] = (uint16_t)k;
   else for (int k = lane; k < np; k += 64) gorder[k] = k;
@@ -572,10 +590,15 @@ __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
 
 hipError_t launch_pack_bert_wave(const PackParams& P, hipStream_t s) {
   const size_t dyn = pack_dyn_bytes(P.cap_lens, P.cap_docs, P.cap_pairs, P.masking != 0);
-  if (P.masking)
-    hipLaunchKernelGGL(pack_bert_wave_kernel<true>, dim3((unsigned)P.n_part), dim3(64), dyn, s, P);
-  else
-    hipLaunchKernelGGL(pack_bert_wave_kernel<false>, dim3((unsigned)P.n_part), dim3(64), dyn, s, P);
+  const bool lds = P.cap_lens > 0 || P.cap_docs > 0 || P.cap_pairs > 0;
+  const dim3 g((unsigned)P.n_part), b(64);
+  if (P.masking) {
+    if (lds) hipLaunchKernelGGL((pack_bert_wave_kernel<true, true>), g, b, dyn, s, P);
+    else hipLaunchKernelGGL((pack_bert_wave_kernel<true, false>), g, b, dyn, s, P);
+  } else {
+    if (lds) hipLaunchKernelGGL((pack_bert_wave_kernel<false, true>), g, b, dyn, s, P);
+    else hipLaunchKernelGGL((pack_bert_wave_kernel<false, false>), g, b, dyn, s, P);
+  }
   return hipGetLastError();
 }
 
