@@ -29,10 +29,11 @@ namespace lddl {
 // Per-partition arrays live in dynamic LDS sized by the host from the largest
 // partition (PackParams cap_*); a partition that does not fit runs the same
 // code on global memory (wave-uniform branch).
+constexpr int PW_DOCS = 512;    // documents held in static LDS by the global-only variant
 struct PackWaveLds {
-  uint32_t mt[MT_N];
-  uint32_t tw[MT_N];            // tempered outputs of the current state
-  int32_t red[64];
+  uint32_t mt[MT_N];            // MT19937 state; draws temper on the fly
+  uint16_t dfirst[PW_DOCS];     // global-only variant: the partition's documents
+  uint16_t dn[PW_DOCS];         //   (first kept slot relative to s0, #kept sentences)
 };
 struct PackDyn {                // views into the dynamic LDS region
   uint16_t* lens;               // [cap_lens] filtered sentence lengths
@@ -73,10 +74,10 @@ __device__ __forceinline__ int wsum(int v) { return lane_get(wave_incl_add(v), 6
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 
 // MT19937 twist (64-word chunks, ascending: the in-place dependences of the
-// sequential generator hold chunk-wise) + temper into tw, all lanes.  Out of
+// sequential generator hold chunk-wise), all lanes.  Out of
 // line: every draw site would otherwise inline its own copy (code size, SGPR
 // spills); LDS-qualified pointers keep it on ds_* instructions.
-__device__ __attribute__((noinline)) void pack_mt_refill(lds_u32* mt, lds_u32* tw, int lane) {
+__device__ __attribute__((noinline)) void pack_mt_refill(lds_u32* mt, int lane) {
   for (int c = 0; c < MT_N; c += 64) {
     const int i = c + lane;
     uint32_t v = 0;
@@ -90,15 +91,6 @@ __device__ __attribute__((noinline)) void pack_mt_refill(lds_u32* mt, lds_u32* t
     if (i < MT_N) mt[i] = v;
     wsync();
   }
-  for (int i = lane; i < MT_N; i += 64) {
-    uint32_t y = mt[i];
-    y ^= y >> 11;
-    y ^= (y << 7) & 0x9d2c5680u;
-    y ^= (y << 15) & 0xefc60000u;
-    y ^= y >> 18;
-    tw[i] = y;
-  }
-  wsync();
 }
 
 // ---- CPython MT19937 with the state in LDS -----------------------------
@@ -144,7 +136,7 @@ struct WaveRng {
 
   // twist + temper on all lanes (out of line: pack_mt_refill)
   __device__ __forceinline__ void refill() {
-    pack_mt_refill((lds_u32*)L.mt, (lds_u32*)L.tw, lane);
+    pack_mt_refill((lds_u32*)L.mt, lane);
     idx = 0;
     wbase = -1024;
   }
@@ -154,7 +146,7 @@ struct WaveRng {
     int o = idx - wbase;
     if (o < 0 || o >= 64) {
       wbase = idx;
-      win = L.tw[idx + lane < MT_N ? idx + lane : MT_N - 1];
+      win = temper(L.mt[idx + lane < MT_N ? idx + lane : MT_N - 1]);
       o = 0;
     }
     ++idx;
@@ -311,9 +303,20 @@ __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
   wsync();
   PW_STAMP(1)
   // slot-relative accessors
+  // global-only variant: the documents (the random-next lookups) in static LDS
+  const bool dres = !LDSOK && nd <= PW_DOCS && nfs < 65536;
+  if (dres) {
+    for (int k = lane; k < nd; k += 64) {
+      L.dfirst[k] = (uint16_t)(P.fd_first[d0 + k] - s0);
+      L.dn[k] = (uint16_t)P.fd_n[d0 + k];
+    }
+    wsync();
+  }
   auto len_at = [&](int k) -> int { return lres ? (int)D.lens[k] : P.fs_ntok[s0 + k]; };
-  auto doc_first = [&](int d) -> int { return lres ? (int)D.dfirst[d] : (int)(P.fd_first[d0 + d] - s0); };
-  auto doc_n = [&](int d) -> int { return lres ? (int)D.dn[d] : P.fd_n[d0 + d]; };
+  auto doc_first = [&](int d) -> int {
+    return lres ? (int)D.dfirst[d] : dres ? (int)L.dfirst[d] : (int)(P.fd_first[d0 + d] - s0);
+  };
+  auto doc_n = [&](int d) -> int { return lres ? (int)D.dn[d] : dres ? (int)L.dn[d] : P.fd_n[d0 + d]; };
 
   WaveRng rng{L, lane, MT_N};
   rng.seed(P.seed + (uint64_t)p);
@@ -401,7 +404,7 @@ __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
           const int n = min(min(E, 64), avail);
           const int t = t0 + lane;
           bool sideA = d0l > 0 ? (t < d0l ? true : ((t - d0l) & 1) != 0) : (t < nb0 ? false : ((t - nb0) & 1) == 0);
-          const bool front = lane < n ? (L.tw[rng.idx + 2 * lane] >> 31) == 0 : false;
+          const bool front = lane < n ? (WaveRng::temper(L.mt[rng.idx + 2 * lane]) >> 31) == 0 : false;
           const bool act = lane < n;
           alo += __popcll(__ballot(act && sideA && front));
           ahi -= __popcll(__ballot(act && sideA && !front));
