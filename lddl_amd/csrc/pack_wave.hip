@@ -202,6 +202,20 @@ __device__ __forceinline__ int range_sum(const GET& len_at, int k0, int k1, int 
   return wsum(s);
 }
 
+// find_fill / range_sum over a document of <= 64 sentences whose lengths are
+// held one per lane in dl (lane k = sentence k, 0 beyond): no memory access
+__device__ __forceinline__ int find_fill_reg(int dl, int k0, int n, int target, int lane, int* sum_out) {
+  const bool in = lane >= k0 && lane < n;
+  const int ps = wscan_incl(in ? dl : 0, lane);
+  const uint64_t m = __ballot(in && (lane == n - 1 || ps >= target));  // lane n-1 always qualifies
+  const int j = __ffsll((unsigned long long)m) - 1;
+  *sum_out = lane_get(ps, j);
+  return j;
+}
+__device__ __forceinline__ int range_sum_reg(int dl, int k0, int k1, int lane) {
+  return wsum(lane >= k0 && lane < k1 ? dl : 0);
+}
+
 // LDSOK = false: every LDS capacity is 0 (the default), the arrays are in
 // global memory and the LDS/global branches compile away
 template <bool MASK, bool LDSOK>
@@ -345,17 +359,23 @@ __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
   for (int dup = 0; dup < P.dup && !err; ++dup) {
     for (int di = 0; di < nd && !err; ++di) {
       const int first = doc_first(di), len = doc_n(di);
+      // a document of <= 64 sentences keeps its lengths in a register
+      const bool dreg = len <= 64;
+      const int dl = dreg && lane < len ? len_at(first + lane) : 0;
       int target = max_num;
       if (rng.random() < P.short_seq_prob) target = (int)rng.randint(2, max_num);
       int i = 0;
       while (i < len) {
         const int cs = i;
         int cur;
-        const int j = find_fill([&](int k) { return len_at(first + k); }, cs, len, target, lane, &cur);
+        const int j = dreg ? find_fill_reg(dl, cs, len, target, lane, &cur)
+                           : find_fill([&](int k) { return len_at(first + k); }, cs, len, target, lane, &cur);
         const int nchunk = j - cs + 1;
         int a_end = 1;
         if (nchunk >= 2) a_end = (int)rng.randint(1, nchunk - 1);
-        const int la = a_end == nchunk ? cur : range_sum([&](int k) { return len_at(first + k); }, cs, cs + a_end, lane);
+        const int la = a_end == nchunk ? cur
+                       : dreg ? range_sum_reg(dl, cs, cs + a_end, lane)
+                              : range_sum([&](int k) { return len_at(first + k); }, cs, cs + a_end, lane);
         PairRec r;
         r.fs0 = s0 + first + cs;
         r.n0 = (uint16_t)a_end;
