@@ -714,6 +714,7 @@ extern "C" int lddl_materialize(lddl_ctx* c, const uint16_t* d_ids, uint16_t* d_
   M.cls_id = c->special[2];
   M.sep_id = c->special[3];
   M.codebert = c->pack_codebert;
+  M.ablate = getenv("LDDL_MAT_ABLATE") ? atoi(getenv("LDDL_MAT_ABLATE")) : 0;
   M.out_tokens = d_out_tokens;
   M.out_tok_off = d_out_tok_off;
   M.out_len0 = d_out_len0;

@@ -515,7 +515,7 @@ __device__ __forceinline__ void mat_drain(const MatWave& W, int ntok, bool liste
 // src readable for n_src entries
 template <bool LEAD>
 __device__ __forceinline__ void mat_copy(MatWave& W, int64_t G0, int64_t G1, const uint16_t* src, int64_t n_src,
-                                         uint16_t* out, uint32_t cls, uint32_t sep, int lane) {
+                                         uint16_t* out, uint32_t cls, uint32_t sep, int lane, bool no_drain = false) {
   const int32_t G1r = (int32_t)(G1 - G0);
   if (G1 - G0 >= (1 << MAT_PBITS) - 16) {  // (rows beyond any real max_tok) token by token
     mat_drain<LEAD>(W, G1r, false, G0, G1r, src, out, cls, sep, lane);
@@ -576,17 +576,27 @@ __device__ __forceinline__ void mat_copy(MatWave& W, int64_t G0, int64_t G1, con
       ns += __popcll(m);
     }
     if (ns > MAT_SLOW - MAT_U * 64) {
-      mat_drain<LEAD>(W, ns * 8, true, G0, G1r, src, out, cls, sep, lane);
+      if (!no_drain) mat_drain<LEAD>(W, ns * 8, true, G0, G1r, src, out, cls, sep, lane);
       ns = 0;
     }
   }
-  if (ns > 0) mat_drain<LEAD>(W, ns * 8, true, G0, G1r, src, out, cls, sep, lane);
+  if (ns > 0 && !no_drain) mat_drain<LEAD>(W, ns * 8, true, G0, G1r, src, out, cls, sep, lane);
+}
+
+// workgroups are dealt round-robin to the 8 XCDs (one L2 each): block b runs
+// on XCD b % 8, so map it to item range (b % 8) of 8 contiguous ranges --
+// each XCD's L2 then holds the dense ids of a few partitions, not all of the
+// ones in flight (the dup-fold re-reads hit L2 instead of the MALL / HBM)
+__device__ __forceinline__ int64_t xcd_block(int64_t b, int64_t nblk) {
+  if (nblk < 64) return b;
+  const int64_t per = (nblk + 7) >> 3;
+  return (b & 7) * per + (b >> 3);
 }
 
 __global__ __launch_bounds__(256) void materialize2_kernel(MatParams M, int64_t total, int64_t n_src) {
   __shared__ MatWave mw[4];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int64_t gbase = ((int64_t)blockIdx.x * 4 + wv) * 64;
+  const int64_t gbase = (xcd_block(blockIdx.x, gridDim.x) * 4 + wv) * 64;
   if (gbase >= total) return;
   const int nr = (int)min((int64_t)64, total - gbase);
   MatWave& W = mw[wv];
@@ -629,7 +639,7 @@ __global__ __launch_bounds__(256) void materialize2_kernel(MatParams M, int64_t 
   W.roff[lane] = lane < nr ? (int32_t)(off - G0) : 0x7FFFFFFF;
   W.row[lane] = x;
   mat_wsync();
-  mat_copy<true>(W, G0, G1, M.dense, n_src, M.out_tokens, M.cls_id, M.sep_id, lane);
+  mat_copy<true>(W, G0, G1, M.dense, n_src, M.out_tokens, M.cls_id, M.sep_id, lane, M.ablate == 1);
 }
 
 // dense[tokoff[s] + k] = ids[sent_off[s] - sent_off[0] + k]: wave per 64 sentences
@@ -882,8 +892,9 @@ hipError_t launch_materialize(const MatParams& M, int64_t total_pairs, int64_t n
   // v2 needs 16-B aligned output and dense ids
   if (algo != 1 && ((reinterpret_cast<uintptr_t>(M.out_tokens) | reinterpret_cast<uintptr_t>(M.dense)) & 15u) == 0) {
     const int64_t items = (total_pairs + 63) / 64;  // one wave per 64 pairs
-    hipLaunchKernelGGL(materialize2_kernel, dim3((unsigned)((items + 3) / 4)), dim3(256), 0, s, M, total_pairs,
-                       n_dense);
+    int64_t nblk = (items + 3) / 4;
+    if (nblk >= 64) nblk = (nblk + 7) & ~(int64_t)7;  // xcd_block: 8 equal ranges (extra blocks exit)
+    hipLaunchKernelGGL(materialize2_kernel, dim3((unsigned)nblk), dim3(256), 0, s, M, total_pairs, n_dense);
   } else {
     const int64_t grid = (M.n_part + 3) / 4;  // one wave per partition
     hipLaunchKernelGGL(materialize_kernel, dim3((unsigned)grid), dim3(256), 0, s, M);
