@@ -118,6 +118,29 @@ int lddl_materialize(lddl_ctx *ctx, const uint16_t *d_ids, uint16_t *d_out_token
 int lddl_masked_lm(lddl_ctx *ctx, int64_t *d_out_mlm_off, uint16_t *d_out_mlm_pos, uint16_t *d_out_mlm_label,
                    void *stream);
 
+/* Render one string column of rows [row0, row0 + n_rows) as Arrow string
+ * data: d_out_off[0..n_rows] (int64, d_out_off[0] = 0) and the UTF-8 bytes of
+ * ' '.join(vocab[t] for t in segment) per row -- the reference's
+ * 'A'/'B' (pretrain.py:348-353), 'masked_lm_labels' (:356-360),
+ * 'doc'/'code' (pretrain_codebert.py:425-432) columns, which to_parquet
+ * writes as pa.string() (pretrain.py:457-471).  segment: 0 = first segment
+ * (A / doc: row tokens [1, 1 + len0)), 1 = second (B / code, after the [SEP];
+ * codebert != 0: a [SEP] follows the doc segment only when flags bit1),
+ * 2 = the whole row (d_row_off only; masked_lm labels from lddl_masked_lm).
+ * Two-phase: *out_nbytes receives the byte count (the stream is synchronised
+ * once); with d_out_bytes == NULL that is all (size query), else out_cap
+ * must be >= it (LDDL_ECAPACITY) and the bytes are written asynchronously. */
+int lddl_render_strings(lddl_ctx *ctx, const uint16_t *d_tokens, const int64_t *d_row_off, const uint16_t *d_len0,
+                        const uint16_t *d_len1, const uint8_t *d_flags, int64_t row0, int64_t n_rows,
+                        int32_t segment, int32_t codebert, int64_t *d_out_off, uint8_t *d_out_bytes,
+                        int64_t out_cap, int64_t *out_nbytes, void *stream);
+
+/* Document index (into the corpus' documents) of every row of the last pack
+ * call, in lddl_materialize's row order: the row's own document (seg0's; a
+ * CodeBERT row without docstring: its code's) -- feeds CodeBERT's 'id'
+ * column = document._id (pretrain_codebert.py:425-426). */
+int lddl_row_docs(lddl_ctx *ctx, int64_t *d_out_doc, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -35,6 +35,10 @@ SIGNATURES = {
     'lddl_materialize': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                  c_void_p, c_void_p, c_void_p, c_void_p]),
     'lddl_masked_lm': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    'lddl_render_strings': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64,
+                                    c_int32, c_int32, c_void_p, c_void_p, c_int64, ctypes.POINTER(c_int64),
+                                    c_void_p]),
+    'lddl_row_docs': (c_int, [c_void_p, c_void_p, c_void_p]),
 }
 
 _lib = None

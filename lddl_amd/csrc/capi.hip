@@ -18,6 +18,7 @@
 #include "../../include/lddl_amd.h"
 #include "common.h"
 #include "pack.h"
+#include "render.h"
 #include "tokenize.h"
 
 using namespace lddl;
@@ -53,6 +54,8 @@ struct lddl_ctx {
   uint32_t slot_mask = 0;
   uint8_t* d_pool = nullptr;
   uint32_t* d_voff = nullptr;
+  uint8_t* d_rpool = nullptr;    // full vocab strings (incl. "##"), 4-aligned: rendering
+  uint32_t* d_rinfo = nullptr;   // [V] offset << 8 | length into d_rpool
   uint32_t maxb[2] = {0, 0};
   uint4* d_vt = nullptr;         // v4 bucketed vocab table
   uint32_t vt_mask = 0;
@@ -110,6 +113,8 @@ static void free_ctx(lddl_ctx* c) {
   (void)hipFree(c->d_bloom);
   (void)hipFree(c->d_pool);
   (void)hipFree(c->d_voff);
+  (void)hipFree(c->d_rpool);
+  (void)hipFree(c->d_rinfo);
   (void)hipFree(c->d_vt);
   (void)hipFree(c->d_vbloom);
   (void)hipFree(c->d_ovf);
@@ -302,6 +307,20 @@ static int load_vocab(lddl_ctx* c, const char* path) {
   if ((rc = upload(&c->d_slots, slots.data(), slots.size() * sizeof(uint4)))) return rc;
   if ((rc = upload(&c->d_pool, pool.data(), pool.size()))) return rc;
   if ((rc = upload(&c->d_voff, voff.data(), voff.size() * 4))) return rc;
+  {  // rendering tables: the vocab entries verbatim (pretrain.py:348-353 joins them)
+    std::vector<uint8_t> rpool;
+    std::vector<uint32_t> rinfo(V);
+    for (size_t i = 0; i < V; ++i) {
+      const std::string& w = c->vocab[i];
+      if (rpool.size() >= (1u << 24)) return set_err(LDDL_EFORMAT, "vocab text larger than 16 MiB");
+      rinfo[i] = (uint32_t)rpool.size() << 8 | (uint32_t)w.size();  // size <= 255, checked above
+      rpool.insert(rpool.end(), w.begin(), w.end());
+      rpool.resize((rpool.size() + 3) & ~(size_t)3, 0);
+    }
+    rpool.resize(rpool.size() + 16, 0);
+    if ((rc = upload(&c->d_rpool, rpool.data(), rpool.size()))) return rc;
+    if ((rc = upload(&c->d_rinfo, rinfo.data(), rinfo.size() * 4))) return rc;
+  }
   return 0;
 }
 
@@ -766,5 +785,71 @@ extern "C" int lddl_masked_lm(lddl_ctx* c, int64_t* d_out_mlm_off, uint16_t* d_o
     HIP_TRY(launch_masked_lm(M, st));
   }
   c->last_nmask = -1;  // the rows are masked in place exactly once
+  return 0;
+}
+
+// --------------------------------------------------------------- render --
+extern "C" int lddl_render_strings(lddl_ctx* c, const uint16_t* d_tokens, const int64_t* d_row_off,
+                                   const uint16_t* d_len0, const uint16_t* d_len1, const uint8_t* d_flags,
+                                   int64_t row0, int64_t n_rows, int32_t segment, int32_t codebert,
+                                   int64_t* d_out_off, uint8_t* d_out_bytes, int64_t out_cap, int64_t* out_nbytes,
+                                   void* stream) {
+  if (!c) return set_err(LDDL_EINVAL, "null ctx");
+  if (segment < RENDER_SEG0 || segment > RENDER_ROW) return set_err(LDDL_EINVAL, "segment %d not in 0..2", segment);
+  if (row0 < 0 || n_rows < 0) return set_err(LDDL_EINVAL, "negative row range");
+  if (!d_tokens || !d_row_off || !d_out_off || !out_nbytes) return set_err(LDDL_EINVAL, "null pointer");
+  if (segment != RENDER_ROW && (!d_len0 || (segment == RENDER_SEG1 && (!d_len1 || (codebert && !d_flags)))))
+    return set_err(LDDL_EINVAL, "segment %d needs len0/len1%s", segment, codebert ? "/flags" : "");
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t st = (hipStream_t)stream;
+  RenderParams R{};
+  R.tokens = d_tokens;
+  R.row_off = d_row_off;
+  R.len0 = d_len0;
+  R.len1 = d_len1;
+  R.flags = d_flags;
+  R.row0 = row0;
+  R.n_rows = n_rows;
+  R.segment = segment;
+  R.codebert = codebert;
+  R.vinfo = c->d_rinfo;
+  R.vpool = c->d_rpool;
+  int64_t* bsum;
+  int rc;
+  if ((rc = ws_get(c, 35, (size_t)n_rows, &R.lens))) return rc;
+  if ((rc = ws_get(c, 36, (size_t)scan_blocks(n_rows) + 1, &bsum))) return rc;
+  HIP_TRY(launch_render_len(R, c->n_cu, st));
+  HIP_TRY(launch_scan_ntok(R.lens, n_rows, d_out_off, bsum, st));
+  HIP_TRY(hipMemcpyAsync(&c->h_tot[6], d_out_off + n_rows, 8, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  *out_nbytes = c->h_tot[6];
+  if (!d_out_bytes) return 0;  // size query
+  if (out_cap < c->h_tot[6])
+    return set_err(LDDL_ECAPACITY, "render needs %lld bytes, out_cap %lld", (long long)c->h_tot[6], (long long)out_cap);
+  R.out_off = d_out_off;
+  R.out = d_out_bytes;
+  HIP_TRY(launch_render_bytes(R, c->n_cu, st));
+  return 0;
+}
+
+extern "C" int lddl_row_docs(lddl_ctx* c, int64_t* d_out_doc, void* stream) {
+  if (!c) return set_err(LDDL_EINVAL, "null ctx");
+  if (c->last_npairs < 0) return set_err(LDDL_EINVAL, "no successful lddl_pack_* call");
+  if (!d_out_doc) return set_err(LDDL_EINVAL, "null pointer");
+  HIP_TRY(hipSetDevice(c->device));
+  const PackParams& P = c->pp;
+  RowDocParams D{};
+  D.pairs = P.pairs;
+  D.binned = P.binned;
+  D.pair_base = (const int64_t*)c->ws[15].p;
+  D.fs_base = P.fs_base;
+  D.sent_off = P.sent_off;
+  D.doc_sent_off = P.doc_sent_off;
+  D.part_doc_off = P.part_doc_off;
+  D.n_part = P.n_part;
+  D.n_rows = c->last_npairs;
+  D.dup = P.dup;
+  D.out_doc = d_out_doc;
+  HIP_TRY(launch_row_docs(D, c->n_cu, (hipStream_t)stream));
   return 0;
 }

@@ -1,0 +1,191 @@
+"""Parquet shards in the reference's schema, from GPU-rendered string columns.
+
+The reference turns every packed instance into a dict of strings
+(pretrain.py:348-360, pretrain_codebert.py:425-432) and writes them with
+``to_parquet`` (unbinned: ``part.{i}.parquet``, pretrain.py:472-478) or
+``to_parquet_binned`` (one file per bin, ``part.{i}.parquet_{b}``, every bin
+written even when empty, binning.py:353-431):
+
+  BERT      A string, B string, is_random_next bool, num_tokens uint16
+            [, masked_lm_positions binary (np.save bytes of uint16[k],
+               lddl/utils.py:98-102), masked_lm_labels string]
+            [, bin_id int64]                               pretrain.py:450-498
+  CodeBERT  id string, doc string, code string, num_tokens uint16
+            [, bin_id int64]                       pretrain_codebert.py:495-537
+
+Here the rows of a pack call are already in file order on the device
+(partition-major, bin-major, shuffled order within a bin), so a file is a
+contiguous row range.  The string columns are rendered on the GPU by
+``lddl_render_strings`` (Arrow layout: offsets + UTF-8 bytes) in row batches,
+copied to the host once and wrapped zero-copy into Arrow arrays; the host only
+slices offsets per file and runs the parquet encoder.
+"""
+import ctypes
+import io
+import os
+
+import numpy as np
+import pyarrow as pa
+import pyarrow.parquet as pq
+import torch
+
+from . import _lib
+from .tokenizer import _ptr, _stream
+
+SEG0, SEG1, ROW = 0, 1, 2
+
+BERT_SCHEMA = [('A', pa.string()), ('B', pa.string()), ('is_random_next', pa.bool_()),
+               ('num_tokens', pa.uint16())]
+MLM_SCHEMA = [('masked_lm_positions', pa.binary()), ('masked_lm_labels', pa.string())]
+CODEBERT_SCHEMA = [('id', pa.string()), ('doc', pa.string()), ('code', pa.string()), ('num_tokens', pa.uint16())]
+
+
+def schema(codebert=False, masking=False, binned=False):
+  f = list(CODEBERT_SCHEMA if codebert else BERT_SCHEMA)
+  if masking and not codebert:
+    f += MLM_SCHEMA
+  if binned:
+    f.append(('bin_id', pa.int64()))
+  return pa.schema(f)
+
+
+def render(packer, tokens, row_off, row0, n_rows, segment, len0=None, len1=None, flags=None, codebert=False,
+           stream=None):
+  """One string column of rows [row0, row0 + n_rows) on the GPU.
+
+  Returns (offsets int64[n_rows + 1] starting at 0, bytes uint8) on the host.
+  """
+  L = _lib.lib()
+  dev = packer.device
+  off = torch.empty(n_rows + 1, dtype=torch.int64, device=dev)
+  nb = ctypes.c_int64(0)
+  s = _stream(stream)
+  args = (packer.tok.handle, _ptr(tokens), _ptr(row_off), _ptr(len0), _ptr(len1), _ptr(flags), row0, n_rows,
+          segment, 1 if codebert else 0, _ptr(off))
+  _lib.check(L.lddl_render_strings(*args, None, 0, ctypes.byref(nb), s))
+  data = torch.empty(max(nb.value, 1), dtype=torch.uint8, device=dev)
+  _lib.check(L.lddl_render_strings(*args, _ptr(data), nb.value, ctypes.byref(nb), s))
+  return off.cpu().numpy(), data[:nb.value].cpu().numpy()
+
+
+def row_docs(packer, n_rows, stream=None):
+  """document index of every row of the last pack call (lddl_row_docs)"""
+  out = torch.empty(max(n_rows, 1), dtype=torch.int64, device=packer.device)
+  _lib.check(_lib.lib().lddl_row_docs(packer.tok.handle, _ptr(out), _stream(stream)))
+  return out[:n_rows].cpu().numpy()
+
+
+def _npy_header(k):
+  b = io.BytesIO()
+  np.save(b, np.zeros(k, dtype=np.uint16))  # serialize_np_array, lddl/utils.py:98-102
+  return np.frombuffer(b.getvalue()[:len(b.getvalue()) - 2 * k], dtype=np.uint8)
+
+
+def npy_positions(mlm_off, mlm_pos):
+  """masked_lm_positions column: per row the np.save bytes of uint16[k]
+  (header + 2k bytes), built vectorised.  mlm_off: int64[n+1] (from 0),
+  mlm_pos: uint16[mlm_off[-1]].  Returns (int64 offsets, uint8 data)."""
+  k = np.diff(mlm_off)
+  hdr = {int(v): _npy_header(int(v)) for v in np.unique(k)} if len(k) else {}
+  hlen = np.array([len(hdr[int(v)]) for v in k], dtype=np.int64) if len(k) else np.zeros(0, np.int64)
+  sizes = hlen + 2 * k
+  off = np.zeros(len(k) + 1, dtype=np.int64)
+  np.cumsum(sizes, out=off[1:])
+  data = np.empty(int(off[-1]), dtype=np.uint8)
+  for v, h in hdr.items():
+    rows = np.nonzero(k == v)[0]
+    data[(off[rows][:, None] + np.arange(len(h))[None, :]).ravel()] = np.tile(h, len(rows))
+  # position bytes: row r's 2k bytes start at off[r] + hlen[r]
+  if len(mlm_pos):
+    rix = np.repeat(np.arange(len(k)), 2 * k)
+    within = np.arange(int(2 * k.sum())) - np.repeat(2 * mlm_off[:-1], 2 * k)
+    data[off[rix] + hlen[rix] + within] = np.ascontiguousarray(mlm_pos, dtype='<u2').view(np.uint8)
+  return off, data
+
+
+def _arrow(typ, off, data, lo, hi):
+  """rows [lo, hi) of a (int64 offsets, bytes) column as an Arrow array"""
+  o = off[lo:hi + 1] - off[lo]
+  d = data[off[lo]:off[hi]]
+  if o[-1] < 2**31:
+    return pa.Array.from_buffers(typ, hi - lo, [None, pa.py_buffer(o.astype(np.int32)), pa.py_buffer(d)])
+  big = pa.large_string() if typ == pa.string() else pa.large_binary()
+  return pa.Array.from_buffers(big, hi - lo, [None, pa.py_buffer(o), pa.py_buffer(d)]).cast(typ)
+
+
+def write_shards(packer, res, out_dir, bin_size=None, codebert=False, masking=False, doc_ids=None,
+                 part_base=0, compression='snappy', batch_rows=1 << 20, stream=None):
+  """Write the rows of ``res`` (a pipeline.PackResult) as the reference's
+  parquet files under out_dir.  Partition p of this pack call is file
+  ``part.{part_base + p}.parquet`` (unbinned) or ``part.{..}.parquet_{b}``
+  for every bin b (binned).  doc_ids: CodeBERT 'id' strings per document of
+  the packed corpus.  Returns the list of files written."""
+  os.makedirs(out_dir, exist_ok=True)
+  binned = bin_size is not None
+  nbins = res.nbins if binned else 1
+  n_part = res.bin_count.shape[0]
+  counts = res.bin_count.cpu().numpy().reshape(n_part, res.nbins)
+  if not binned:
+    counts = counts.sum(axis=1, keepdims=True)
+  file_rows = counts.ravel()  # (partition, bin) major order == row order
+  file_start = np.zeros(len(file_rows) + 1, dtype=np.int64)
+  np.cumsum(file_rows, out=file_start[1:])
+  assert file_start[-1] == res.n_pairs, (file_start[-1], res.n_pairs)
+  sch = schema(codebert, masking and not codebert, binned)
+  tok_off = res.tok_off[:res.n_pairs + 1]
+  num_tokens = np.diff(tok_off.cpu().numpy()).astype(np.uint16)
+  flags = res.flags[:res.n_pairs].cpu().numpy()
+  bins = res.bins[:res.n_pairs].cpu().numpy().astype(np.int64)
+  docs = None
+  if codebert:
+    if doc_ids is None:
+      raise ValueError('CodeBERT shards need doc_ids (the id column)')
+    docs = pa.array(row_docs(packer, res.n_pairs, stream))
+    ids_col = pa.array(doc_ids, type=pa.string()).take(docs) if res.n_pairs else pa.array([], pa.string())
+  if masking and not codebert:
+    moff_all = res.mlm_off[:res.n_pairs + 1].cpu().numpy()
+    mpos_all = res.mlm_pos[:res.n_masked].cpu().numpy().view(np.uint16)
+  files = []
+  f = 0
+  nfiles = len(file_rows)
+  # render in batches of whole files (>= batch_rows rows, or one big file)
+  while f < nfiles:
+    g = f + 1
+    while g < nfiles and file_start[g + 1] - file_start[f] <= batch_rows:
+      g += 1
+    r0, r1 = int(file_start[f]), int(file_start[g])
+    n = r1 - r0
+    kw = dict(len0=res.len0, len1=res.len1, flags=res.flags, codebert=codebert, stream=stream)
+    c0 = render(packer, res.tokens, res.tok_off, r0, n, SEG0, **kw)
+    c1 = render(packer, res.tokens, res.tok_off, r0, n, SEG1, **kw)
+    if masking and not codebert:
+      m0 = int(moff_all[r0])
+      lab = render(packer, res.mlm_label, res.mlm_off, r0, n, ROW, stream=stream)
+      pos = npy_positions(moff_all[r0:r1 + 1] - m0, mpos_all[m0:int(moff_all[r1])])
+    for fi in range(f, g):
+      lo, hi = int(file_start[fi] - r0), int(file_start[fi + 1] - r0)
+      p, b = divmod(fi, nbins)
+      cols = {}
+      if codebert:
+        cols['id'] = ids_col.slice(r0 + lo, hi - lo)
+        cols['doc'] = _arrow(pa.string(), *c0, lo, hi)
+        cols['code'] = _arrow(pa.string(), *c1, lo, hi)
+      else:
+        cols['A'] = _arrow(pa.string(), *c0, lo, hi)
+        cols['B'] = _arrow(pa.string(), *c1, lo, hi)
+        cols['is_random_next'] = pa.array((flags[r0 + lo:r0 + hi] & 1).astype(bool))
+      cols['num_tokens'] = pa.array(num_tokens[r0 + lo:r0 + hi])
+      if masking and not codebert:
+        cols['masked_lm_positions'] = _arrow(pa.binary(), *pos, lo, hi)
+        cols['masked_lm_labels'] = _arrow(pa.string(), *lab, lo, hi)
+      if binned:
+        cols['bin_id'] = pa.array(bins[r0 + lo:r0 + hi])
+      t = pa.Table.from_arrays([cols[name] for name in sch.names], schema=sch)
+      name = 'part.%d.parquet' % (part_base + p)
+      if binned:
+        name += '_%d' % b
+      path = os.path.join(out_dir, name)
+      pq.write_table(t, path, compression=compression)
+      files.append(path)
+    f = g
+  return files
