@@ -1,0 +1,340 @@
+"""Load balancer for the parquet shards (reference: lddl/dask/load_balance.py).
+
+The reference balances the preprocessor's files ``part.{i}.parquet[_b]`` into
+``--num-shards`` files ``shard-{k}.parquet[_b]`` whose sample counts differ
+by at most one, per bin, and writes ``.num_samples.json``
+(load_balance.py:372-378).  It counts rows by reading every file under MPI
+(``_build_files`` + Allreduce, :222-233), then moves rows in pairwise steps
+(``Shard.balance`` :129-140, ``Progress.report`` :190-203) that re-read and
+re-write intermediate shard files on every step.
+
+Here the same pairwise procedure runs on *row runs* instead of tables:
+``plan()`` replays it exactly -- same file order (lexicographic paths, then a
+stable sort by count), same pops from the back, same split of partially
+consumed files, same pairing order -- and yields, per output shard, the list
+of (file, first row, row count) runs it ends up holding.  Each shard is then
+written once, by rank ``k % world``, from slices of the source files.  The
+row counts need no file reads: on the GPU path they are the packer's
+per-(partition, bin) counts, gathered over ranks with one all-gather
+(RCCL on the GPUs, ``gather_bin_counts``) in place of the MPI Allreduce.
+
+Where the reference cannot finish, this raises instead:
+  * more shards than files: Shard._input_files is None (:240-242) and
+    flush()/_load() raise TypeError -> ValueError here;
+  * a total divisible by --num-shards keeps a zero-count target (:163-167);
+    a shard passing through exactly base+1 samples is then taken as ready and
+    the loop never ends (or ends with a shard never flushed).  By default the
+    zero-count target is dropped, which changes nothing in any run the
+    reference finishes correctly (the key only matters once a shard reaches
+    it, which is exactly the failure) and finishes the others balanced;
+    strict=True keeps it and raises RuntimeError at the first iteration that
+    can pair no shards.
+"""
+import argparse
+import json
+import os
+import time
+
+import numpy as np
+
+__all__ = ['plan', 'plan_files', 'write_shards', 'gather_bin_counts', 'balance_counts', 'main']
+
+
+class _Shard:
+  """load_balance.py:42-157 Shard, holding runs [file, first_row, n] instead of tables."""
+
+  def __init__(self, idx, inputs, counts, postfix):
+    self.idx = idx
+    self.inputs = inputs  # list of file indices (popped from the back) or None
+    self.counts = counts
+    self.postfix = postfix
+    self.out = None       # runs of the output file, or None (no file yet)
+    self.out_n = 0
+
+  @property
+  def num_samples(self):
+    n = sum(self.counts[f] for f in self.inputs) if self.inputs is not None else 0
+    return n + (self.out_n if self.out is not None else 0)
+
+  @property
+  def name(self):
+    return 'shard-{}.parquet{}'.format(self.idx, self.postfix)
+
+  def _store(self, n, runs):
+    if self.out is None:
+      self.out, self.out_n = [], 0
+    self.out.extend(r for r in runs if r[2] > 0)
+    self.out_n += n
+
+  def _load(self, n):
+    if self.inputs is None:
+      raise ValueError('more shards than files (the reference fails here: load_balance.py:240-242)')
+    taken = []
+    while n > 0:
+      if self.inputs:
+        f = self.inputs.pop()
+        runs, fn = [[f, 0, self.counts[f]]], self.counts[f]
+      else:
+        runs, fn = self.out, self.out_n
+        self.out, self.out_n = None, 0
+      k = min(fn, n)
+      head, tail = _split(runs, k)
+      taken.extend(head)
+      if k < fn:
+        self._store(fn - k, tail)
+      n -= k
+    return taken
+
+  def balance(self, smaller):
+    n = self.num_samples - (self.num_samples + smaller.num_samples) // 2
+    smaller._store(n, self._load(n))
+
+  def flush(self):
+    if self.inputs is None:
+      raise ValueError('more shards than files (the reference fails here: load_balance.py:143-148)')
+    runs, n = [], 0
+    while self.inputs:
+      f = self.inputs.pop()
+      n += self.counts[f]
+      runs.append([f, 0, self.counts[f]])
+    if n > 0:
+      self._store(n, runs)
+
+
+def _split(runs, k):
+  head, tail = [], []
+  for f, r0, n in runs:
+    if k >= n:
+      head.append([f, r0, n])
+      k -= n
+    elif k > 0:
+      head.append([f, r0, k])
+      tail.append([f, r0 + k, n - k])
+      k = 0
+    else:
+      tail.append([f, r0, n])
+  return head, tail
+
+
+class _Progress:
+  """load_balance.py:160-207 Progress (targets dict kept verbatim)."""
+
+  def __init__(self, shards, strict):
+    n = len(shards)
+    total = sum(s.num_samples for s in shards)
+    base = total // n
+    self.targets = {base: n - total % n, base + 1: total % n}
+    if not strict:
+      self.targets = {k: v for k, v in self.targets.items() if v > 0}
+    self.ready = []
+
+  def completed(self):
+    return sum(self.targets.values()) == 0
+
+  def report(self, shards):
+    smaller, larger = [], []
+    for s in shards:
+      ns = s.num_samples
+      if ns in self.targets:
+        self.targets[ns] -= 1
+        self.ready.append(s)
+        if self.targets[ns] == 0:
+          del self.targets[ns]
+      elif ns < min(self.targets.keys()):
+        smaller.append(s)
+      else:
+        larger.append(s)
+    return smaller, larger
+
+
+def plan(counts, num_shards, postfix='', strict=False):
+  """Replay load_balance.py:_balance (:281-322) over files with the given row
+  counts (in the reference's path order).  Returns the ready shards in the
+  reference's order as (shard file name, runs, num_samples); runs are
+  [file index, first row, n] in row order."""
+  counts = [int(c) for c in counts]
+  if num_shards < 1:
+    raise ValueError('--num-shards must be >= 1')
+  order = sorted(range(len(counts)), key=lambda i: counts[i])  # _build_files: stable sort by count
+  shards = [_Shard(k, order[k::num_shards] if k < len(order) else None, counts, postfix)
+            for k in range(num_shards)]
+  progress = _Progress(shards, strict)
+  while not progress.completed():
+    smaller, larger = progress.report(shards)
+    smaller = sorted(smaller, key=lambda s: s.num_samples)
+    larger = sorted(larger, key=lambda s: s.num_samples, reverse=True)
+    npairs = min(len(smaller), len(larger))
+    for s, l in zip(smaller[:npairs], larger[:npairs]):
+      l.balance(s)
+    if npairs == 0 and not progress.completed():
+      raise RuntimeError('load balance cannot finish: %d samples over %d shards leaves shards it can no longer '
+                         'pair (the reference loops forever here, load_balance.py:163-167,302-322)'
+                         % (sum(counts), num_shards))
+    shards = smaller + larger
+  for s in progress.ready:
+    s.flush()
+  out = []
+  for s in progress.ready:
+    if s.out is None:
+      raise ValueError('shard %d ends with no samples (the reference fails here: load_balance.py:327-330)' % s.idx)
+    out.append((s.name, _merge(s.out), s.out_n))
+  return out
+
+
+def _merge(runs):
+  """adjacent runs of the same file back to back -> one run"""
+  out = []
+  for f, r0, n in runs:
+    if out and out[-1][0] == f and out[-1][1] + out[-1][2] == r0:
+      out[-1][2] += n
+    else:
+      out.append([f, r0, n])
+  return out
+
+
+def _bin_of(name):
+  ext = os.path.splitext(name)[1]
+  return int(ext.split('_')[-1]) if '_' in ext else None
+
+
+def plan_files(names, counts, num_shards, bin_ids=None, strict=False):
+  """load_balance.py:main (:333-369) over (file path, row count) pairs:
+  per bin (or unbinned) the files in sorted path order, then plan().
+  Returns (list of (shard name, [(path, first_row, n)], num_samples),
+  num_samples dict in the reference's .num_samples.json order)."""
+  by_name = dict(zip(names, counts))
+  paths = sorted(p for p in names if '.parquet' in os.path.splitext(p)[1])  # get_all_parquets_under
+  if bin_ids is None:
+    found = sorted({_bin_of(p) for p in paths if _bin_of(p) is not None})
+    if found != list(range(len(found))):
+      raise ValueError('bin id must be contiguous integers starting from 0!')
+    bin_ids = found or None
+  groups = [(paths, '')] if bin_ids is None else [
+      ([p for p in paths if os.path.splitext(p)[1] == '.parquet_{}'.format(b)], '_{}'.format(b)) for b in bin_ids]
+  shards = []
+  for gp, postfix in groups:
+    for name, runs, n in plan([by_name[p] for p in gp], num_shards, postfix, strict):
+      shards.append((name, [(gp[f], r0, k) for f, r0, k in runs], n))
+  return shards, {name: n for name, _, n in shards}
+
+
+def write_shards(shards, outdir, rank=0, world=1, compression='snappy'):
+  """Write every planned shard owned by this rank (shard k -> rank k % world,
+  the reference's idx % world ownership) from slices of its source files.
+  Returns the written paths."""
+  import pyarrow as pa
+  import pyarrow.parquet as pq
+  os.makedirs(outdir, exist_ok=True)
+  written = []
+  cache = {}
+  for name, runs, n in shards:
+    k = int(name.split('-')[1].split('.')[0])
+    if k % world != rank:
+      continue
+    parts = []
+    for path, r0, cnt in runs:
+      if path not in cache:
+        cache.clear()  # runs of a shard mostly come from few files: keep the last one
+        cache[path] = pq.read_table(path)
+      parts.append(cache[path].slice(r0, cnt))
+    t = pa.concat_tables(parts) if parts else None
+    if t is None:
+      raise ValueError('shard %s has no rows' % name)
+    assert t.num_rows == n, (name, t.num_rows, n)
+    path = os.path.join(outdir, name)
+    pq.write_table(t, path, compression=compression)
+    written.append(path)
+  return written
+
+
+def gather_bin_counts(bin_count, part_base, group=None):
+  """All-gather every rank's per-(partition, bin) row counts.
+
+  bin_count: int64 tensor [n_part_local, nbins] (PackResult.bin_count, on
+  the GPU under the nccl=RCCL backend, on the CPU under gloo); part_base: the
+  global index of this rank's first partition.  One all_gather_into_tensor of
+  a padded [max_parts, nbins + 1] block per rank (row 0 carries part_base and
+  n_part) replaces the MPI Allreduce of _build_files (load_balance.py:222-233).
+  Returns a numpy int64 [n_part_total, nbins] array in global partition order."""
+  import torch
+  import torch.distributed as dist
+  world = dist.get_world_size(group)
+  n_part, nbins = bin_count.shape
+  n = torch.tensor([n_part], dtype=torch.int64, device=bin_count.device)
+  ns = torch.empty(world, dtype=torch.int64, device=bin_count.device)
+  dist.all_gather_into_tensor(ns, n, group=group)
+  mx = int(ns.max().item())
+  blk = torch.zeros(mx + 1, nbins + 1, dtype=torch.int64, device=bin_count.device)
+  blk[0, 0], blk[0, 1] = part_base, n_part
+  blk[1:n_part + 1, :nbins] = bin_count.to(torch.int64)
+  allb = torch.empty(world * (mx + 1), nbins + 1, dtype=torch.int64, device=bin_count.device)
+  dist.all_gather_into_tensor(allb, blk, group=group)
+  allb = allb.cpu().numpy().reshape(world, mx + 1, nbins + 1)
+  total = max([int(allb[r, 0, 0] + allb[r, 0, 1]) for r in range(world)] + [0])
+  out = np.zeros((total, nbins), dtype=np.int64)
+  for r in range(world):
+    b, k = int(allb[r, 0, 0]), int(allb[r, 0, 1])
+    out[b:b + k] = allb[r, 1:k + 1, :nbins]
+  return out
+
+
+def balance_counts(counts, num_shards, binned, outdir=None, strict=False):
+  """Plan from a [n_part, nbins] count array (no file reads): the files are
+  part.{p}.parquet (unbinned, nbins == 1) or part.{p}.parquet_{b}."""
+  counts = np.asarray(counts)
+  base = outdir or ''
+  if binned:
+    names = [os.path.join(base, 'part.%d.parquet_%d' % (p, b)) for p in range(counts.shape[0])
+             for b in range(counts.shape[1])]
+  else:
+    names = [os.path.join(base, 'part.%d.parquet' % p) for p in range(counts.shape[0])]
+    counts = counts.sum(axis=1)
+  return plan_files(names, counts.ravel().tolist(), num_shards, strict=strict)
+
+
+def store_num_samples(num_samples, outdir):
+  """load_balance.py:372-378 .num_samples.json"""
+  with open(os.path.join(outdir, '.num_samples.json'), 'w') as f:
+    json.dump(num_samples, f)
+
+
+def attach_args(parser=None):
+  """The reference's balance_dask_output flags (load_balance.py:265-306)."""
+  parser = parser or argparse.ArgumentParser('lddl_amd load balancer for the preprocessor\'s parquet shards')
+  parser.add_argument('--indir', type=str, required=True)
+  parser.add_argument('--outdir', type=str, default=None)
+  parser.add_argument('--num-shards', type=int, required=True)
+  parser.add_argument('--bin-ids', type=int, nargs='*', default=None)
+  parser.add_argument('--keep-orig', dest='keep_orig', action='store_true')
+  parser.add_argument('--no-keep-orig', dest='keep_orig', action='store_false')
+  parser.set_defaults(keep_orig=False)
+  return parser
+
+
+def main(args, rank=0, world=1):
+  """Counts from the parquet footers (no table reads), plan, write, and
+  .num_samples.json (rank 0)."""
+  import pyarrow.parquet as pq
+  outdir = args.indir if args.outdir is None else os.path.abspath(os.path.expanduser(args.outdir))
+  os.makedirs(outdir, exist_ok=True)
+  paths = sorted(os.path.join(r, f) for r, _, fs in os.walk(args.indir) for f in fs
+                 if '.parquet' in os.path.splitext(f)[1])
+  counts = [pq.ParquetFile(p).metadata.num_rows for p in paths]
+  shards, ns = plan_files(paths, counts, args.num_shards, args.bin_ids)
+  written = write_shards(shards, outdir, rank, world)
+  if not args.keep_orig and world == 1:
+    for p in paths:
+      os.remove(p)
+  if rank == 0:
+    store_num_samples(ns, outdir)
+  return written, ns
+
+
+def console_script():
+  tic = time.perf_counter()
+  main(attach_args().parse_args())
+  print('Load balancing took {} s!'.format(time.perf_counter() - tic))
+
+
+if __name__ == '__main__':
+  console_script()

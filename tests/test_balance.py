@@ -1,0 +1,127 @@
+"""Load balancer (lddl_amd.balance) vs the reference's own load_balance.py
+outputs (tests/golden/balance.json.gz, tools/gen_golden_balance.py), and the
+multi-rank count gather / shard ownership over gloo (world size 2)."""
+import gzip
+import json
+import os
+
+import numpy as np
+import pyarrow as pa
+import pyarrow.parquet as pq
+import pytest
+import torch.multiprocessing as mp
+
+from lddl_amd import balance
+
+GOLD = json.load(gzip.open(os.path.join(os.path.dirname(__file__), 'golden', 'balance.json.gz'), 'rt'))
+CASES = GOLD['cases']
+
+
+@pytest.mark.parametrize('k', range(len(CASES)))
+@pytest.mark.parametrize('strict', [False, True])
+def test_plan_matches_reference(k, strict):
+  c = CASES[k]
+  if c['error'] == 'TypeError':  # more shards than files
+    with pytest.raises(ValueError):
+      balance.plan_files(c['files'], c['counts'], c['num_shards'], c['bin_ids'], strict)
+    return
+  if c['error'] == 'TimeoutError':  # the reference never finishes
+    if strict:
+      with pytest.raises(RuntimeError):
+        balance.plan_files(c['files'], c['counts'], c['num_shards'], c['bin_ids'], strict)
+      return
+    shards, ns = balance.plan_files(c['files'], c['counts'], c['num_shards'], c['bin_ids'], strict)
+    for b in sorted({n.split('.parquet')[1] for n in ns}):
+      v = [n for name, n in ns.items() if name.split('.parquet')[1] == b]
+      assert len(v) == c['num_shards'] and max(v) - min(v) <= 1
+    assert sum(ns.values()) == sum(c['counts'])
+    return
+  shards, ns = balance.plan_files(c['files'], c['counts'], c['num_shards'], c['bin_ids'], strict)
+  idx = {n: i for i, n in enumerate(c['files'])}
+  got = {name: [[idx[p], r0, n] for p, r0, n in runs] for name, runs, _ in shards}
+  assert got == c['shards']
+  assert list(ns.items()) == list(c['num_samples'].items())  # .num_samples.json incl. key order
+  if len(shards):
+    assert max(ns.values()) - min(ns.values()) <= 1 or c['bin_ids'] is not None or any(
+        '_' in os.path.splitext(f)[1] for f in c['files'])
+
+
+def _write_inputs(d, c):
+  for i, (nm, n) in enumerate(zip(c['files'], c['counts'])):
+    pq.write_table(pa.table({'rid': (np.int64(i) << 32) + np.arange(n, dtype=np.int64)}), os.path.join(d, nm))
+
+
+def _runs_of(path):
+  out = []
+  for v in pq.read_table(path).column('rid').to_numpy():
+    f, r = int(v) >> 32, int(v) & 0xFFFFFFFF
+    if out and out[-1][0] == f and out[-1][1] + out[-1][2] == r:
+      out[-1][2] += 1
+    else:
+      out.append([f, r, 1])
+  return out
+
+
+@pytest.mark.parametrize('k', [i for i, c in enumerate(CASES) if not c['error']][:12])
+def test_cli_writes_reference_shards(tmp_path, k):
+  c = CASES[k]
+  ind, outd = tmp_path / 'in', tmp_path / 'out'
+  ind.mkdir()
+  _write_inputs(str(ind), c)
+  args = balance.attach_args().parse_args(['--indir', str(ind), '--outdir', str(outd), '--num-shards',
+                                           str(c['num_shards']), '--keep-orig'])
+  balance.main(args)
+  for name, runs in c['shards'].items():
+    assert _runs_of(str(outd / name)) == runs
+  with open(str(outd / '.num_samples.json')) as f:
+    assert list(json.load(f).items()) == list(c['num_samples'].items())
+
+
+def test_balance_counts_names():
+  counts = np.array([[3, 1], [0, 5], [7, 2]])
+  shards, ns = balance.balance_counts(counts, 2, binned=True)
+  assert sorted(ns) == ['shard-0.parquet_0', 'shard-0.parquet_1', 'shard-1.parquet_0', 'shard-1.parquet_1']
+  assert ns['shard-0.parquet_0'] + ns['shard-1.parquet_0'] == 10
+  shards, ns = balance.balance_counts(counts, 3, binned=False)
+  assert sorted(ns.values()) == [6, 6, 6]
+
+
+def _rank(rank, world, port, d, counts, parts, q):
+  import torch
+  import torch.distributed as dist
+  os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+  dist.init_process_group('gloo', rank=rank, world_size=world)
+  lo, hi = parts[rank]
+  got = balance.gather_bin_counts(torch.from_numpy(counts[lo:hi]), lo)
+  shards, ns = balance.balance_counts(got, 3, binned=True, outdir=d)
+  written = balance.write_shards(shards, os.path.join(d, 'out'), rank, world)
+  q.put((rank, got.tolist(), sorted(os.path.basename(w) for w in written)))
+  dist.barrier()
+  dist.destroy_process_group()
+
+
+def test_gather_and_ownership_gloo(tmp_path):
+  """world size 2: counts of unequal partition ranges gathered, every rank
+  computes the same plan, shard k written by rank k % 2, union = 1-rank run"""
+  rng = np.random.default_rng(5)
+  counts = rng.integers(0, 30, (7, 4)).astype(np.int64)
+  d = str(tmp_path)
+  names = ['part.%d.parquet_%d' % (p, b) for p in range(7) for b in range(4)]
+  _write_inputs(d, {'files': names, 'counts': counts.ravel().tolist()})
+  ctx = mp.get_context('spawn')
+  q = ctx.Queue()
+  port = 29500 + os.getpid() % 1000
+  procs = [ctx.Process(target=_rank, args=(r, 2, port, d, counts, [(0, 3), (3, 7)], q)) for r in range(2)]
+  for p in procs:
+    p.start()
+  res = sorted(q.get(timeout=120) for _ in range(2))
+  for p in procs:
+    p.join(60)
+    assert p.exitcode == 0
+  assert res[0][1] == counts.tolist() and res[1][1] == counts.tolist()
+  assert all(int(n.split('-')[1].split('.')[0]) % 2 == r for r, _, ws in res for n in ws)
+  shards, ns = balance.balance_counts(counts, 3, binned=True, outdir=d)
+  assert sorted(res[0][2] + res[1][2]) == sorted(ns)
+  for name, runs, n in shards:
+    t = pq.read_table(os.path.join(d, 'out', name))
+    assert t.num_rows == n
