@@ -47,6 +47,9 @@ def parse():
   ap.add_argument('--masking', action='store_true', help='static masking (--masking of the reference)')
   ap.add_argument('--no-cpu-baseline', action='store_true')
   ap.add_argument('--cpu-seconds', type=float, default=12.0)
+  ap.add_argument('--parquet-parts', type=int, default=64,
+                  help='after timing: write this many partitions as parquet shards and report the writer rate '
+                       '(GPU string rendering + host Arrow/parquet encode; 0 = skip)')
   return ap.parse_args()
 
 
@@ -127,6 +130,28 @@ def cpu_baseline(args, base, pdo, seconds):
           'tokenize_tokens_per_s': tok_rate, 'pack_tokens_per_s_per_thread': pack_rate}
 
 
+def parquet_sample(args, pk, res):
+  """Writer throughput on the first --parquet-parts partitions (outside the
+  timed step; the reference's to_parquet_binned stage, reported separately)"""
+  import shutil
+  import tempfile
+  from lddl_amd import writer
+  d = tempfile.mkdtemp(prefix='lddl_bench_pq_')
+  try:
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    files = writer.write_shards(pk, res, d, bin_size=args.bin_size, masking=args.masking,
+                                max_parts=args.parquet_parts)
+    el = time.perf_counter() - t
+    nbytes = sum(os.path.getsize(f) for f in files)
+    nb = res.nbins
+    rows = int(res.bin_count[:args.parquet_parts].sum().item())
+    return {'partitions': args.parquet_parts, 'files': len(files), 'rows': rows, 'seconds': el,
+            'rows_per_s': rows / el, 'parquet_mb': nbytes / 1e6, 'compression': 'snappy', 'nbins': nb}
+  finally:
+    shutil.rmtree(d, ignore_errors=True)
+
+
 def main():
   args = parse()
   rank = int(os.environ.get('RANK', 0))
@@ -155,9 +180,10 @@ def main():
     e1.record(s)
     res = pk.pack(sh, ids, ntok, **kw)
     if dist is not None:
-      bc = res.bin_count.reshape(-1)
-      allc = torch.empty(bc.numel() * world, dtype=bc.dtype, device=device)
-      dist.all_gather_into_tensor(allc, bc)
+      # per-(partition, bin) row counts of every rank: the load balancer's
+      # input (lddl_amd/balance.py), one RCCL all-gather per step
+      from lddl_amd.balance import gather_bin_counts
+      gather_bin_counts(res.bin_count, rank * sh.n_part)
     if timed:
       tok_ms.append((e0, e1))
     return res, ntok
@@ -228,6 +254,8 @@ def main():
       line['roofline']['traffic_source'] = tr['source']
   except (OSError, ValueError, KeyError):
     pass
+  if args.parquet_parts > 0:
+    line['parquet_writer'] = parquet_sample(args, pk, res)
   if not args.no_cpu_baseline:
     line['cpu_baseline'] = cpu_baseline(args, base, pdo, args.cpu_seconds)
   print(json.dumps(line), flush=True)

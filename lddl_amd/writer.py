@@ -114,12 +114,13 @@ def _arrow(typ, off, data, lo, hi):
 
 
 def write_shards(packer, res, out_dir, bin_size=None, codebert=False, masking=False, doc_ids=None,
-                 part_base=0, compression='snappy', batch_rows=1 << 20, stream=None):
+                 part_base=0, compression='snappy', batch_rows=1 << 20, max_parts=None, stream=None):
   """Write the rows of ``res`` (a pipeline.PackResult) as the reference's
   parquet files under out_dir.  Partition p of this pack call is file
   ``part.{part_base + p}.parquet`` (unbinned) or ``part.{..}.parquet_{b}``
   for every bin b (binned).  doc_ids: CodeBERT 'id' strings per document of
-  the packed corpus.  Returns the list of files written."""
+  the packed corpus.  max_parts: only the first max_parts partitions.
+  Returns the list of files written."""
   os.makedirs(out_dir, exist_ok=True)
   binned = bin_size is not None
   nbins = res.nbins if binned else 1
@@ -132,22 +133,22 @@ def write_shards(packer, res, out_dir, bin_size=None, codebert=False, masking=Fa
   np.cumsum(file_rows, out=file_start[1:])
   assert file_start[-1] == res.n_pairs, (file_start[-1], res.n_pairs)
   sch = schema(codebert, masking and not codebert, binned)
-  tok_off = res.tok_off[:res.n_pairs + 1]
-  num_tokens = np.diff(tok_off.cpu().numpy()).astype(np.uint16)
-  flags = res.flags[:res.n_pairs].cpu().numpy()
-  bins = res.bins[:res.n_pairs].cpu().numpy().astype(np.int64)
+  nfiles = len(file_rows) if max_parts is None else min(len(file_rows), max_parts * nbins)
+  n_rows = int(file_start[nfiles])  # rows of the files written
+  num_tokens = np.diff(res.tok_off[:n_rows + 1].cpu().numpy()).astype(np.uint16)
+  flags = res.flags[:n_rows].cpu().numpy()
+  bins = res.bins[:n_rows].cpu().numpy().astype(np.int64)
   docs = None
   if codebert:
     if doc_ids is None:
       raise ValueError('CodeBERT shards need doc_ids (the id column)')
-    docs = pa.array(row_docs(packer, res.n_pairs, stream))
-    ids_col = pa.array(doc_ids, type=pa.string()).take(docs) if res.n_pairs else pa.array([], pa.string())
+    docs = pa.array(row_docs(packer, res.n_pairs, stream)[:n_rows])
+    ids_col = pa.array(doc_ids, type=pa.string()).take(docs) if n_rows else pa.array([], pa.string())
   if masking and not codebert:
-    moff_all = res.mlm_off[:res.n_pairs + 1].cpu().numpy()
-    mpos_all = res.mlm_pos[:res.n_masked].cpu().numpy().view(np.uint16)
+    moff_all = res.mlm_off[:n_rows + 1].cpu().numpy()
+    mpos_all = res.mlm_pos[:int(moff_all[-1])].cpu().numpy().view(np.uint16)
   files = []
   f = 0
-  nfiles = len(file_rows)
   # render in batches of whole files (>= batch_rows rows, or one big file)
   while f < nfiles:
     g = f + 1

@@ -121,3 +121,92 @@ def test_end_to_end_parquet_vs_oracle(gpu, tmp_path):
       assert got['B'] == [_join(vocab, r[1]) for r in want]
       assert got['is_random_next'] == [bool(r[2]) for r in want]
       assert got['num_tokens'] == [r[3] for r in want]
+
+
+def _bin_rows(rows, bin_size, nbins):
+  return [[r for r in rows if po.bin_of(r[-1], bin_size, nbins) == b] for b in range(nbins)]
+
+
+def test_cli_bert_end_to_end(gpu, tmp_path):
+  """preprocess_bert_pretrain drop-in: text files -> part.{i}.parquet_{b},
+  rows equal to the oracle pipeline on the same sampled / shuffled /
+  sentence-split corpus; then the load balancer over the written files"""
+  from lddl_amd import synth, preprocess, pipeline, balance
+  from oracle.oracle import OracleTokenizer
+  c = synth.make_wiki(300_000, seed=123)
+  docs = c.documents()
+  src = tmp_path / 'wiki' / 'en'
+  src.mkdir(parents=True)
+  for k in range(2):
+    with open(str(src / ('wiki_%d.txt' % k)), 'w', encoding='utf-8') as f:
+      for d in range(k, len(docs), 2):
+        f.write('wiki-%d %s\n' % (d, ' '.join(docs[d])))
+  sink = tmp_path / 'out'
+  args = preprocess.attach_args().parse_args(
+      ['--wikipedia', str(tmp_path / 'wiki'), '--sink', str(sink), '--target-seq-length', '128', '--bin-size', '32',
+       '--num-blocks', '4', '--sentence-splitter', 'rules', '--seed', '5'])
+  files, t = preprocess.main(args)
+  assert sorted(os.path.basename(f) for f in files) == sorted(
+      'part.%d.parquet_%d' % (p, b) for p in range(4) for b in range(4))
+  recs = preprocess.read_records(preprocess.find_files_under(str(src)))
+  corpus, ids = preprocess.build_corpus(recs, 5, 0.9, splitter=preprocess._rule_split)
+  pdo = preprocess.partition_docs(corpus, num_blocks=4)
+  oids, ontok = OracleTokenizer(pipeline.VOCAB_BERT).run(corpus.data, corpus.sent_off, 512, nthreads=8)
+  exp = po.run_bert_shards(corpus, oids, ontok, pdo, 128, 0.1, 5, 5, 32)
+  vocab = _vocab(pipeline.VOCAB_BERT)
+  for p, rows in enumerate(exp):
+    for b, want in enumerate(_bin_rows(rows, 32, 4)):
+      got = _read(str(sink / ('part.%d.parquet_%d' % (p, b))))
+      assert got['A'] == [_join(vocab, r[0]) for r in want]
+      assert got['B'] == [_join(vocab, r[1]) for r in want]
+      assert got['num_tokens'] == [r[3] for r in want]
+  # load balancer over the written shards: every row lands exactly once
+  bargs = balance.attach_args().parse_args(['--indir', str(sink), '--outdir', str(tmp_path / 'bal'),
+                                            '--num-shards', '3', '--keep-orig'])
+  try:
+    written, ns = balance.main(bargs)
+  except RuntimeError:
+    pytest.skip('counts hit the reference load balancer non-termination case')
+  for b in range(4):
+    n_in = sum(len(_bin_rows(rows, 32, 4)[b]) for rows in exp)
+    assert sum(v for k, v in ns.items() if k.endswith('_%d' % b)) == n_in
+    got = sorted(a for k in range(3) for a in _read(str(tmp_path / 'bal' / ('shard-%d.parquet_%d' % (k, b))))['A'])
+    assert got == sorted(_join(vocab, r[0]) for rows in exp for r in _bin_rows(rows, 32, 4)[b])
+
+
+def test_cli_codebert_end_to_end(gpu, tmp_path):
+  from lddl_amd import synth, preprocess, pipeline
+  from oracle.oracle import OracleTokenizer
+  lines = synth.make_code_lines(300, seed=9)
+  (tmp_path / 'code').mkdir()
+  (tmp_path / 'code' / 'a.txt').write_bytes('\r\n'.join(lines).encode('utf-8'))
+  sink = tmp_path / 'out'
+  args = preprocess.attach_args(codebert=True).parse_args(
+      ['--code', str(tmp_path / 'code'), '--sink', str(sink), '--target-seq-length', '128', '--num-blocks', '2',
+       '--seed', '8', '--sample-ratio', '1.0'])
+  files, t = preprocess.main(args, codebert=True)
+  assert sorted(os.path.basename(f) for f in files) == ['part.0.parquet', 'part.1.parquet']
+  recs = preprocess.read_records([str(tmp_path / 'code' / 'a.txt')], linedelimiter='\r\n')
+  c, ids = preprocess.build_corpus(recs, 8, 1.0, codebert=True)
+  pdo = preprocess.partition_docs(c, num_blocks=2)
+  oids, ontok = OracleTokenizer(pipeline.VOCAB_CODEBERT).run(c.data, c.sent_off, 512, nthreads=8)
+  vocab = _vocab(pipeline.VOCAB_CODEBERT)
+  for p in range(2):
+    docs, nd, dmap = [], [], []
+    for d in range(pdo[p], pdo[p + 1]):
+      ss = [list(map(int, oids[c.sent_off[s]:c.sent_off[s] + ontok[s]]))
+            for s in range(c.doc_sent_off[d], c.doc_sent_off[d + 1])]
+      k = int(c.doc_nseg_doc[d])
+      ds, cs = [s for s in ss[:k] if s], [s for s in ss[k:] if s]
+      if cs:
+        docs.append(ds + cs)
+        nd.append(len(ds))
+        dmap.append(d)
+    pairs = po.partition_pairs(docs, 8 + p, lambda D, di, r: po.codebert_pairs(D, nd, di, 128, 0.1, r), 1)
+    got = _read(str(sink / ('part.%d.parquet' % p)))
+    want_id, want_doc, want_code = [], [], []
+    for (doc_s, code_s, dw, cw) in pairs:
+      want_doc.append(_join(vocab, [t for (d, s) in doc_s for t in docs[d][s]][dw[0]:dw[1]]))
+      want_code.append(_join(vocab, [t for (d, s) in code_s for t in docs[d][s]][cw[0]:cw[1]]))
+      want_id.append(ids[dmap[code_s[0][0]]])
+    assert got['doc'] == want_doc and got['code'] == want_code and got['id'] == want_id
