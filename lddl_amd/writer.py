@@ -20,6 +20,7 @@ contiguous row range.  The string columns are rendered on the GPU by
 copied to the host once and wrapped zero-copy into Arrow arrays; the host only
 slices offsets per file and runs the parquet encoder.
 """
+import concurrent.futures
 import ctypes
 import io
 import os
@@ -149,6 +150,9 @@ def write_shards(packer, res, out_dir, bin_size=None, codebert=False, masking=Fa
     mpos_all = res.mlm_pos[:int(moff_all[-1])].cpu().numpy().view(np.uint16)
   files = []
   f = 0
+  workers = max(1, min(16, os.cpu_count() or 1))
+  pool = concurrent.futures.ThreadPoolExecutor(workers)
+  pending = []
   # render in batches of whole files (>= batch_rows rows, or one big file)
   while f < nfiles:
     g = f + 1
@@ -186,7 +190,14 @@ def write_shards(packer, res, out_dir, bin_size=None, codebert=False, masking=Fa
       if binned:
         name += '_%d' % b
       path = os.path.join(out_dir, name)
-      pq.write_table(t, path, compression=compression)
+      pending.append(pool.submit(pq.write_table, t, path, compression=compression))
       files.append(path)
+    # the parquet encoder releases the GIL: files of a batch encode in
+    # parallel on the host cores while the next batch renders on the GPU
+    while len(pending) > 4 * workers:
+      pending.pop(0).result()
     f = g
+  for fu in pending:
+    fu.result()
+  pool.shutdown()
   return files
