@@ -38,10 +38,14 @@ def parse():
   ap.add_argument('--steps', type=int, default=3)
   ap.add_argument('--warmup', type=int, default=1)
   ap.add_argument('--corpus-gb', type=float, default=20.0)
-  ap.add_argument('--unique-mb', type=int, default=256)
+  ap.add_argument('--corpus', choices=('wiki', 'code'), default='wiki',
+                  help='wiki: BERT on Wikipedia-style text (configs[1]); code: CodeBERT codebert_52000 vocab on '
+                       'code-style CodeSearchNet lines (configs[2], one GPU of it)')
+  ap.add_argument('--unique-mb', type=int, default=None, help='unique synthetic MB (default 256 wiki / 16 code)')
   ap.add_argument('--target-seq-length', type=int, default=512)
   ap.add_argument('--bin-size', type=int, default=64)
-  ap.add_argument('--duplicate-factor', type=int, default=5)
+  ap.add_argument('--duplicate-factor', type=int, default=None,
+                  help='default 5 for BERT (pretrain.py:693), 1 for CodeBERT (pretrain_codebert.py:725)')
   ap.add_argument('--partition-mb', type=float, default=1.0, help='bytes per partition (--block-size)')
   ap.add_argument('--seed', type=int, default=12345)
   ap.add_argument('--masking', action='store_true', help='static masking (--masking of the reference)')
@@ -50,14 +54,24 @@ def parse():
   ap.add_argument('--parquet-parts', type=int, default=64,
                   help='after timing: write this many partitions as parquet shards and report the writer rate '
                        '(GPU string rendering + host Arrow/parquet encode; 0 = skip)')
-  return ap.parse_args()
+  args = ap.parse_args()
+  code = args.corpus == 'code'
+  if args.unique_mb is None:
+    args.unique_mb = 16 if code else 256
+  if args.duplicate_factor is None:
+    args.duplicate_factor = 1 if code else 5
+  return args
 
 
 def build_shards(args, rank, device):
   from lddl_amd import synth
   from lddl_amd.pipeline import ShardSet, partition_by_bytes
   t0 = time.time()
-  base = synth.make_wiki(args.unique_mb << 20, seed=20261015 + rank)
+  if args.corpus == 'code':
+    # ~1.7 KB per CodeSearchNet-style line (docstring + code segments)
+    base = synth.make_code(max(1, (args.unique_mb << 20) // 1700), seed=20261015 + rank)
+  else:
+    base = synth.make_wiki(args.unique_mb << 20, seed=20261015 + rank)
   gen_s = time.time() - t0
   nb = base.nbytes
   reps = max(1, int(round(args.corpus_gb * (1 << 30) / nb)))
@@ -76,21 +90,42 @@ def build_shards(args, rank, device):
   doc_sent_off = torch.empty(nd * reps + 1, dtype=torch.int64, device=device)
   pd = torch.from_numpy(pdo).to(device)
   part_doc_off = torch.empty(npb * reps + 1, dtype=torch.int64, device=device)
+  nseg = None
+  if base.doc_nseg_doc is not None:
+    nseg = torch.from_numpy(np.tile(base.doc_nseg_doc, reps)).to(device)
   for r in range(reps):
     sent_off[r * ns:(r + 1) * ns + 1] = so + r * nb
     doc_sent_off[r * nd:(r + 1) * nd + 1] = dso + r * ns
     part_doc_off[r * npb:(r + 1) * npb + 1] = pd + r * nd
-  sh = ShardSet(data, sent_off, doc_sent_off, part_doc_off, None, nb * reps)
+  sh = ShardSet(data, sent_off, doc_sent_off, part_doc_off, nseg, nb * reps)
   return sh, base, pdo, reps, gen_s
+
+
+def _code_docs(base, ids, ntok, d0, d1):
+  """CodeBERT documents of docs [d0, d1): (docstring + code segments, #docstring
+  segments), empty segments dropped, docs without code dropped
+  (pretrain_codebert.py:126-161)"""
+  docs, nd = [], []
+  for d in range(d0, d1):
+    ss = [list(map(int, ids[base.sent_off[s] - base.sent_off[0]:base.sent_off[s] - base.sent_off[0] + ntok[s]]))
+          for s in range(base.doc_sent_off[d], base.doc_sent_off[d + 1])]
+    k = int(base.doc_nseg_doc[d])
+    ds = [s for s in ss[:k] if s]
+    cs = [s for s in ss[k:] if s]
+    if cs:
+      docs.append(ds + cs)
+      nd.append(len(ds))
+  return docs, nd
 
 
 def cpu_baseline(args, base, pdo, seconds):
   """oracle/ restatement timed on the host cores on a bounded sample."""
   from oracle.oracle import OracleTokenizer
   from oracle import pack_oracle as po
-  from lddl_amd.pipeline import VOCAB_BERT
+  from lddl_amd.pipeline import VOCAB_BERT, VOCAB_CODEBERT
+  code = args.corpus == 'code'
   threads = min(os.cpu_count() or 1, 16)
-  ot = OracleTokenizer(VOCAB_BERT)
+  ot = OracleTokenizer(VOCAB_CODEBERT if code else VOCAB_BERT)
   # calibrate on ~1 MB, then size the sample to ~seconds of work
   ns = int(np.searchsorted(base.sent_off, base.sent_off[0] + (1 << 20)))
   t = time.time()
@@ -107,12 +142,22 @@ def cpu_baseline(args, base, pdo, seconds):
   t = time.time()
   ptoks, p = 0, 0
   while time.time() - t < seconds * 0.3 and p < len(pdo) - 1 and base.doc_sent_off[pdo[p + 1]] <= ns:
-    docs = po.filtered_docs(ids, ntok, base.sent_off, base.doc_sent_off, int(pdo[p]), int(pdo[p + 1]))
-    pairs = po.partition_pairs(docs, args.seed + p, lambda D, di, r: po.bert_pairs(
-        D, di, args.target_seq_length, 0.1, r), args.duplicate_factor)
-    rows = [po.pair_tokens(docs, pr) for pr in pairs]
-    po.binned_order([len(a) + len(b) + 3 for a, b, _ in rows], args.bin_size,
-                    args.target_seq_length // args.bin_size)
+    if code:
+      docs, nd = _code_docs(base, ids, ntok, int(pdo[p]), int(pdo[p + 1]))
+      pairs = po.partition_pairs(docs, args.seed + p, lambda D, di, r: po.codebert_pairs(
+          D, nd, di, args.target_seq_length, 0.1, r), args.duplicate_factor)
+      nt = []
+      for (doc_s, code_s, dw, cw) in pairs:
+        dt = [t for (d, s) in doc_s for t in docs[d][s]][dw[0]:dw[1]]
+        ct = [t for (d, s) in code_s for t in docs[d][s]][cw[0]:cw[1]]
+        nt.append(len(dt) + len(ct) + (3 if nd[code_s[0][0]] else 2))
+    else:
+      docs = po.filtered_docs(ids, ntok, base.sent_off, base.doc_sent_off, int(pdo[p]), int(pdo[p + 1]))
+      pairs = po.partition_pairs(docs, args.seed + p, lambda D, di, r: po.bert_pairs(
+          D, di, args.target_seq_length, 0.1, r), args.duplicate_factor)
+      rows = [po.pair_tokens(docs, pr) for pr in pairs]
+      nt = [len(a) + len(b) + 3 for a, b, _ in rows]
+    po.binned_order(nt, args.bin_size, args.target_seq_length // args.bin_size)
     ptoks += int(sum(ntok[base.doc_sent_off[pdo[p]]:base.doc_sent_off[pdo[p + 1]]]))
     p += 1
   pack_s = time.time() - t
@@ -130,17 +175,22 @@ def cpu_baseline(args, base, pdo, seconds):
           'tokenize_tokens_per_s': tok_rate, 'pack_tokens_per_s_per_thread': pack_rate}
 
 
-def parquet_sample(args, pk, res):
+def parquet_sample(args, pk, res, sh):
   """Writer throughput on the first --parquet-parts partitions (outside the
   timed step; the reference's to_parquet_binned stage, reported separately)"""
   import shutil
   import tempfile
   from lddl_amd import writer
   d = tempfile.mkdtemp(prefix='lddl_bench_pq_')
+  doc_ids = None
+  if args.corpus == 'code':  # the CodeBERT 'id' column of the documents written
+    nd = int(sh.part_doc_off[min(args.parquet_parts, sh.n_part)].item())
+    doc_ids = ['python_%d' % i for i in range(nd)]
   try:
     torch.cuda.synchronize()
     t = time.perf_counter()
     files = writer.write_shards(pk, res, d, bin_size=args.bin_size, masking=args.masking,
+                                codebert=args.corpus == 'code', doc_ids=doc_ids,
                                 max_parts=args.parquet_parts)
     el = time.perf_counter() - t
     nbytes = sum(os.path.getsize(f) for f in files)
@@ -167,9 +217,11 @@ def main():
   from lddl_amd import build
   build.build_hip()
   sh, base, pdo, reps, gen_s = build_shards(args, rank, device)
-  pk = Packer(device=local)
+  from lddl_amd.pipeline import VOCAB_BERT, VOCAB_CODEBERT
+  code = args.corpus == 'code'
+  pk = Packer(VOCAB_CODEBERT if code else VOCAB_BERT, device=local)
   kw = dict(target_seq_length=args.target_seq_length, short_seq_prob=0.1, duplicate_factor=args.duplicate_factor,
-            seed=args.seed + rank * 10_000_000, bin_size=args.bin_size, masking=args.masking)
+            seed=args.seed + rank * 10_000_000, bin_size=args.bin_size, masking=args.masking, codebert=code)
   tok_ms = []
 
   def step(timed):
@@ -228,12 +280,15 @@ def main():
       'metric': METRIC, 'value': value, 'unit': 'tokens/s', 'n_gpus': world, 'steps': args.steps,
       'warmup': args.warmup, 'ms_per_step': el * 1e3 / args.steps, 'higher_is_better': True,
       'scaling': 'weak', 'vs_baseline': None, 'dtype': 'u8',
-      'data': 'synthetic (Wikipedia-style, %d MB unique tiled x%d per GPU)' % (args.unique_mb, reps),
-      'config': {'workload': 'bert_seq%d_bin%d_%dGB_per_gpu%s' % (args.target_seq_length, args.bin_size,
+      'data': 'synthetic (%s, %d MB unique tiled x%d per GPU)' % (
+          'CodeSearchNet-style code' if code else 'Wikipedia-style', args.unique_mb, reps),
+      'config': {'workload': '%s_seq%d_bin%d_%dGB_per_gpu%s' % ('codebert' if code else 'bert',
+                                                                 args.target_seq_length, args.bin_size,
                                                                    round(sh.nbytes / (1 << 30)),
                                                                    '_masking' if args.masking else ''),
                  'target_seq_length': args.target_seq_length, 'bin_size': args.bin_size,
-                 'duplicate_factor': args.duplicate_factor, 'vocab': 'bert-base-uncased (lddl/dask/bert/vocab)',
+                 'duplicate_factor': args.duplicate_factor, 'vocab': ('codebert_52000/vocab.txt' if code else
+                                                                   'bert-base-uncased (lddl/dask/bert/vocab)'),
                  'corpus_bytes_per_gpu': sh.nbytes, 'sentences_per_gpu': sh.n_sent,
                  'partitions_per_gpu': sh.n_part, 'wordpiece_tokens_per_gpu': n_tok,
                  'pairs_per_gpu': res.n_pairs, 'packed_tokens_per_gpu': res.n_tokens,
@@ -255,7 +310,7 @@ def main():
   except (OSError, ValueError, KeyError):
     pass
   if args.parquet_parts > 0:
-    line['parquet_writer'] = parquet_sample(args, pk, res)
+    line['parquet_writer'] = parquet_sample(args, pk, res, sh)
   if not args.no_cpu_baseline:
     line['cpu_baseline'] = cpu_baseline(args, base, pdo, args.cpu_seconds)
   print(json.dumps(line), flush=True)

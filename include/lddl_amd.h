@@ -141,6 +141,51 @@ int lddl_render_strings(lddl_ctx *ctx, const uint16_t *d_tokens, const int64_t *
  * column = document._id (pretrain_codebert.py:425-426). */
 int lddl_row_docs(lddl_ctx *ctx, int64_t *d_out_doc, void *stream);
 
+/* ---- training-time collate -------------------------
+ * Replaces lddl/torch/bert.py:69-153 `_to_encoded_inputs` (+ :156-196
+ * `_mask_tokens`) for a batch of parquet rows.  Columns arrive as Arrow-style
+ * string columns on the device: bytes + int64 offsets[n_rows + 1].
+ *
+ * lddl_collate_seq_len: the batch's padded length = max over rows of
+ * len(A.split()) + len(B.split()) + 3, rounded up to seq_align
+ * (bert.py:94-101).  Synchronises the stream (the length shapes the outputs). */
+int lddl_collate_seq_len(lddl_ctx *ctx, const uint8_t *d_a, const int64_t *d_a_off, const uint8_t *d_b,
+                         const int64_t *d_b_off, int64_t n_rows, int32_t seq_align, int64_t *out_seq_len,
+                         void *stream);
+
+/* Fill the [n_rows, seq_len] int64 outputs (bert.py:102-152): input_ids
+ * ([CLS] A [SEP] B [SEP], tokens -> ids via the vocab, [UNK] for a miss, 0
+ * padding), token_type_ids, attention_mask, next_sentence_labels[n_rows] and
+ * d_labels by mode:
+ *   0  special_tokens_mask (bert.py:117-122; dynamic masking left to
+ *      lddl_mask_tokens);
+ *   1  static masking labels: ignore_index except labels[positions] =
+ *      ids(labels.split()), positions = the row's np.save uint16 bytes
+ *      (d_pos / d_pos_off, d_lab / d_lab_off required);
+ *   2  dynamic masking fused: mode 0 then lddl_mask_tokens with the same seed
+ *      and counter (identical result).
+ * Errors: LDDL_ECAPACITY (a row longer than seq_len, seq_len > 2048),
+ * LDDL_EINDEX (a masked position >= seq_len: bert.py:113's IndexError),
+ * LDDL_EFORMAT (positions not np.save bytes, or count != label count). */
+int lddl_collate_bert(lddl_ctx *ctx, const uint8_t *d_a, const int64_t *d_a_off, const uint8_t *d_b,
+                      const int64_t *d_b_off, const uint8_t *d_is_random_next, const uint8_t *d_pos,
+                      const int64_t *d_pos_off, const uint8_t *d_lab, const int64_t *d_lab_off, int64_t n_rows,
+                      int64_t seq_len, int32_t mode, int64_t ignore_index, double mlm_probability, uint64_t seed,
+                      uint64_t counter, int64_t *d_input_ids, int64_t *d_token_type_ids,
+                      int64_t *d_attention_mask, int64_t *d_labels, int64_t *d_next_sentence_labels,
+                      void *stream);
+
+/* Dynamic MLM masking in place (bert.py:156-196 `_mask_tokens`): a column
+ * with special_tokens_mask == 0 is selected with probability
+ * mlm_probability; selected -> [MASK] (p 0.8), else a uniform id in
+ * [0, vocab size) (p 0.5), else kept; labels = the original id where
+ * selected, ignore_index elsewhere.  Draws are a counter-based hash of
+ * (seed, counter, row, column): the reference's distribution, not torch's
+ * CPU generator stream. */
+int lddl_mask_tokens(lddl_ctx *ctx, int64_t *d_inputs, const int64_t *d_special_tokens_mask, int64_t *d_labels,
+                     int64_t n_rows, int64_t seq_len, double mlm_probability, int64_t ignore_index, uint64_t seed,
+                     uint64_t counter, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

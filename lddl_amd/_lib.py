@@ -39,6 +39,13 @@ SIGNATURES = {
                                     c_int32, c_int32, c_void_p, c_void_p, c_int64, ctypes.POINTER(c_int64),
                                     c_void_p]),
     'lddl_row_docs': (c_int, [c_void_p, c_void_p, c_void_p]),
+    'lddl_collate_seq_len': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int32,
+                                     ctypes.POINTER(c_int64), c_void_p]),
+    'lddl_collate_bert': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                  c_void_p, c_void_p, c_int64, c_int64, c_int32, c_int64, c_double, c_uint64,
+                                  c_uint64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    'lddl_mask_tokens': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_double, c_int64,
+                                 c_uint64, c_uint64, c_void_p]),
 }
 
 _lib = None

@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "../../include/lddl_amd.h"
+#include "collate.h"
 #include "common.h"
 #include "pack.h"
 #include "render.h"
@@ -83,6 +84,9 @@ struct lddl_ctx {
   int64_t tile_chunk = 0;  // tiles per tile-kernel launch (0 = default)
   uint8_t* d_ovf = nullptr;
   uint32_t* d_counter = nullptr;
+  // collate: whole-token vocab table (built on first use)
+  uint2* d_ctab = nullptr;
+  uint32_t ctab_mask = 0;
 };
 
 // ------------------------------------------------------------------ pack --
@@ -119,6 +123,7 @@ static void free_ctx(lddl_ctx* c) {
   (void)hipFree(c->d_vbloom);
   (void)hipFree(c->d_ovf);
   (void)hipFree(c->d_counter);
+  (void)hipFree(c->d_ctab);
   for (auto& b : c->ws) (void)hipFree(b.p);
   if (c->h_tot) (void)hipHostFree(c->h_tot);
   delete c;
@@ -851,5 +856,164 @@ extern "C" int lddl_row_docs(lddl_ctx* c, int64_t* d_out_doc, void* stream) {
   D.dup = P.dup;
   D.out_doc = d_out_doc;
   HIP_TRY(launch_row_docs(D, c->n_cu, (hipStream_t)stream));
+  return 0;
+}
+
+// -------------------------------------------------------------- collate --
+static int collate_vocab(lddl_ctx* c, CollateVocab* V) {
+  if (!c->d_ctab) {
+    const size_t n = c->vocab.size();
+    uint32_t sz = 1024;
+    while (sz < 4 * n) sz <<= 1;
+    std::vector<uint2> tab(sz, make_uint2(0u, 0xFFFFFFFFu));
+    for (size_t i = 0; i < n; ++i) {
+      const std::string& w = c->vocab[i];
+      const uint32_t h = collate_hash_host((const uint8_t*)w.data(), (int)w.size());
+      for (uint32_t s = h & (sz - 1);; s = (s + 1) & (sz - 1)) {
+        if (tab[s].y == 0xFFFFFFFFu) {
+          tab[s] = make_uint2(h, (uint32_t)i);
+          break;
+        }
+        if (tab[s].x == h && c->vocab[tab[s].y] == w) {  // duplicate line: last id wins
+          tab[s].y = (uint32_t)i;
+          break;
+        }
+      }
+    }
+    int rc;
+    if ((rc = upload(&c->d_ctab, tab.data(), tab.size() * sizeof(uint2)))) return rc;
+    c->ctab_mask = sz - 1;
+  }
+  V->slots = c->d_ctab;
+  V->mask = c->ctab_mask;
+  V->vinfo = c->d_rinfo;
+  V->vpool = c->d_rpool;
+  V->unk = (int32_t)c->special[1];
+  V->cls = (int32_t)c->special[2];
+  V->sep = (int32_t)c->special[3];
+  V->mask_id = (int32_t)c->special[4];
+  V->n_random = c->vocab_size;
+  return 0;
+}
+
+extern "C" int lddl_collate_seq_len(lddl_ctx* c, const uint8_t* d_a, const int64_t* d_a_off, const uint8_t* d_b,
+                                    const int64_t* d_b_off, int64_t n_rows, int32_t seq_align, int64_t* out_seq_len,
+                                    void* stream) {
+  if (!c) return set_err(LDDL_EINVAL, "null ctx");
+  if (n_rows < 0 || seq_align < 1 || !out_seq_len) return set_err(LDDL_EINVAL, "bad n_rows / seq_align / out");
+  if (n_rows > 0 && (!d_a || !d_a_off || !d_b || !d_b_off)) return set_err(LDDL_EINVAL, "null column pointer");
+  if (n_rows == 0) return set_err(LDDL_EINVAL, "empty batch (max() of an empty sequence)");
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t st = (hipStream_t)stream;
+  CollateParams P{};
+  int rc;
+  if ((rc = collate_vocab(c, &P.V))) return rc;
+  P.a = d_a;
+  P.a_off = d_a_off;
+  P.b = d_b;
+  P.b_off = d_b_off;
+  P.n_rows = n_rows;
+  if ((rc = ws_get(c, 37, 1, &P.max_len))) return rc;
+  if (!c->h_tot) HIP_TRY(hipHostMalloc((void**)&c->h_tot, 8 * sizeof(int64_t)));
+  HIP_TRY(hipMemsetAsync(P.max_len, 0, 4, st));
+  HIP_TRY(launch_collate_len(P, c->n_cu, st));
+  HIP_TRY(hipMemcpyAsync(&c->h_tot[7], P.max_len, 4, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  const int64_t m = *(const int32_t*)&c->h_tot[7];
+  *out_seq_len = ((m - 1) / seq_align + 1) * seq_align;
+  return 0;
+}
+
+extern "C" int lddl_collate_bert(lddl_ctx* c, const uint8_t* d_a, const int64_t* d_a_off, const uint8_t* d_b,
+                                 const int64_t* d_b_off, const uint8_t* d_is_random_next, const uint8_t* d_pos,
+                                 const int64_t* d_pos_off, const uint8_t* d_lab, const int64_t* d_lab_off,
+                                 int64_t n_rows, int64_t seq_len, int32_t mode, int64_t ignore_index,
+                                 double mlm_probability, uint64_t seed, uint64_t counter, int64_t* d_input_ids,
+                                 int64_t* d_token_type_ids, int64_t* d_attention_mask, int64_t* d_labels,
+                                 int64_t* d_next_sentence_labels, void* stream) {
+  if (!c) return set_err(LDDL_EINVAL, "null ctx");
+  if (n_rows < 0) return set_err(LDDL_EINVAL, "negative n_rows");
+  if (mode < COLLATE_SPECIAL_MASK || mode > COLLATE_DYNAMIC) return set_err(LDDL_EINVAL, "mode %d not in 0..2", mode);
+  if (seq_len < 3 || seq_len > COLLATE_MAX_LEN)
+    return set_err(LDDL_ECAPACITY, "seq_len %lld not in [3, %d]", (long long)seq_len, COLLATE_MAX_LEN);
+  if (ignore_index < INT32_MIN || ignore_index > INT32_MAX) return set_err(LDDL_EINVAL, "ignore_index out of int32");
+  if (!(mlm_probability >= 0.0 && mlm_probability <= 1.0)) return set_err(LDDL_EINVAL, "mlm_probability not in [0, 1]");
+  if (n_rows > 0 && (!d_a || !d_a_off || !d_b || !d_b_off || !d_is_random_next || !d_input_ids ||
+                     !d_token_type_ids || !d_attention_mask || !d_labels || !d_next_sentence_labels))
+    return set_err(LDDL_EINVAL, "null pointer");
+  if (mode == COLLATE_STATIC && n_rows > 0 && (!d_pos || !d_pos_off || !d_lab || !d_lab_off))
+    return set_err(LDDL_EINVAL, "static masking needs positions and labels");
+  if (n_rows == 0) return 0;
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t st = (hipStream_t)stream;
+  CollateParams P{};
+  int rc;
+  if ((rc = collate_vocab(c, &P.V))) return rc;
+  P.a = d_a;
+  P.a_off = d_a_off;
+  P.b = d_b;
+  P.b_off = d_b_off;
+  P.is_random_next = d_is_random_next;
+  P.pos = d_pos;
+  P.pos_off = d_pos_off;
+  P.lab = d_lab;
+  P.lab_off = d_lab_off;
+  P.n_rows = n_rows;
+  P.seq_len = (int32_t)seq_len;
+  P.mode = mode;
+  P.ignore_index = ignore_index;
+  P.mlm_probability = mlm_probability;
+  P.seed = seed;
+  P.counter = counter;
+  P.input_ids = d_input_ids;
+  P.token_type_ids = d_token_type_ids;
+  P.attention_mask = d_attention_mask;
+  P.labels = d_labels;
+  P.next_sentence_labels = d_next_sentence_labels;
+  if ((rc = ws_get(c, 39, 1, &P.err))) return rc;
+  if (!c->h_tot) HIP_TRY(hipHostMalloc((void**)&c->h_tot, 8 * sizeof(int64_t)));
+  HIP_TRY(hipMemsetAsync(P.err, 0, 4, st));
+  HIP_TRY(launch_collate_fill(P, c->n_cu, st));
+  uint32_t* h_err = (uint32_t*)&c->h_tot[7];
+  HIP_TRY(hipMemcpyAsync(h_err, P.err, 4, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  const uint32_t e = *h_err;
+  if (e) {
+    const unsigned long long row = e >> 4;
+    switch (e & 15u) {
+      case CERR_LONG: return set_err(LDDL_ECAPACITY, "row %llu longer than seq_len %lld", row, (long long)seq_len);
+      case CERR_POS_RANGE:
+        return set_err(LDDL_EINDEX, "row %llu: masked_lm_positions index out of range for seq_len %lld", row,
+                       (long long)seq_len);
+      case CERR_NPY: return set_err(LDDL_EFORMAT, "row %llu: masked_lm_positions is not np.save bytes", row);
+      default:
+        return set_err(LDDL_EFORMAT, "row %llu: masked_lm_positions and masked_lm_labels differ in length", row);
+    }
+  }
+  return 0;
+}
+
+extern "C" int lddl_mask_tokens(lddl_ctx* c, int64_t* d_inputs, const int64_t* d_special_tokens_mask,
+                                int64_t* d_labels, int64_t n_rows, int64_t seq_len, double mlm_probability,
+                                int64_t ignore_index, uint64_t seed, uint64_t counter, void* stream) {
+  if (!c) return set_err(LDDL_EINVAL, "null ctx");
+  if (n_rows < 0 || seq_len < 0 || seq_len >= (1 << 20)) return set_err(LDDL_EINVAL, "bad shape");
+  if (!(mlm_probability >= 0.0 && mlm_probability <= 1.0)) return set_err(LDDL_EINVAL, "mlm_probability not in [0, 1]");
+  if (n_rows * seq_len > 0 && (!d_inputs || !d_special_tokens_mask || !d_labels))
+    return set_err(LDDL_EINVAL, "null pointer");
+  HIP_TRY(hipSetDevice(c->device));
+  MaskParams M{};
+  M.inputs = d_inputs;
+  M.special = d_special_tokens_mask;
+  M.labels = d_labels;
+  M.n_rows = n_rows;
+  M.seq_len = (int32_t)seq_len;
+  M.mask_id = (int32_t)c->special[4];
+  M.n_random = c->vocab_size;
+  M.ignore_index = ignore_index;
+  M.mlm_probability = mlm_probability;
+  M.seed = seed;
+  M.counter = counter;
+  HIP_TRY(launch_mask_tokens(M, c->n_cu, (hipStream_t)stream));
   return 0;
 }
