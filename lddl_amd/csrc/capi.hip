@@ -632,7 +632,9 @@ static int pack_common(lddl_ctx* c, int codebert, const int32_t* d_ntok, const i
       HIP_TRY(hipMemsetAsync(d_pdbg, 0, 8 * 8, st));
       P.dbg = d_pdbg;
     }
-    HIP_TRY(codebert ? launch_pack_codebert(P, st) : lane_packer ? launch_pack_bert(P, st) : launch_pack_bert_wave(P, st));
+    const bool lane_cb = palgo && palgo[0] == '1';  // LDDL_PACK_ALGO=1: the lane-serial packers
+    HIP_TRY(codebert ? (lane_cb ? launch_pack_codebert(P, st) : launch_pack_codebert_wave(P, st))
+                     : lane_packer ? launch_pack_bert(P, st) : launch_pack_bert_wave(P, st));
     if (P.dbg && !codebert && !lane_packer) {
       uint64_t h[8];
       HIP_TRY(hipMemcpyAsync(h, P.dbg, sizeof h, hipMemcpyDeviceToHost, st));

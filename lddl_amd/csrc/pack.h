@@ -129,6 +129,7 @@ hipError_t launch_pack_bert(const PackParams& P, hipStream_t s);
 hipError_t launch_pack_bert_wave(const PackParams& P, hipStream_t s);
 size_t pack_dyn_bytes(int cap_lens, int cap_docs, int cap_pairs, bool mask);
 hipError_t launch_pack_codebert(const PackParams& P, hipStream_t s);
+hipError_t launch_pack_codebert_wave(const PackParams& P, hipStream_t s);
 hipError_t launch_scan_parts(const int64_t* a, const int64_t* b, int64_t n, int64_t* sa, int64_t* sb,
                              const int32_t* err, int32_t* err_any, hipStream_t s);
 // algo 1: wave per partition (u16 copies); otherwise wave per 64 pairs with

@@ -625,4 +625,245 @@ hipError_t launch_pack_bert_wave(const PackParams& P, hipStream_t s) {
   return hipGetLastError();
 }
 
+// ------------------------------------------------------------- CodeBERT ----
+// pretrain_codebert.py:343-442 create_pairs_from_document + :236-247
+// _truncate_seq, one wave per partition (same contract and results as
+// pack_codebert_kernel in pack.hip, the lane-serial variant).  The serial
+// "accumulate segments until the chunk overflows" loops become wave prefix
+// sums + ballots, _truncate_seq decides 64 coins per round, the shuffle /
+// binning are the BERT wave packer's (global-memory arrays).
+
+// smallest k in [k0, n) with (k == stop) or (base + sum lens[k0..k] > limit);
+// returns -1 (and the total in *sum_out) when there is none
+template <class GET>
+__device__ __forceinline__ int find_over(const GET& len_at, int k0, int n, int stop, int base, int limit, int lane,
+                                         int* sum_out) {
+  for (int k = k0; k < n; k += 64) {
+    const int kk = k + lane;
+    const int l = kk < n ? len_at(kk) : 0;
+    const int ps = base + wscan_incl(l, lane);
+    const uint64_t m = __ballot(kk < n && (kk == stop || ps > limit));
+    if (m) {
+      const int j = __ffsll((unsigned long long)m) - 1;
+      *sum_out = lane_get(ps, j);
+      return k + j;
+    }
+    base = lane_get(ps, 63);
+  }
+  *sum_out = base;
+  return -1;
+}
+
+// _truncate_seq on [lo, hi) down to max_n tokens: one coin (= one random()
+// call, 2 MT words) per excess token, MSB of the first word decides
+__device__ __forceinline__ void trunc_seq_wave(WaveRng& rng, PackWaveLds& L, int lane, int& lo, int& hi, int max_n) {
+  int E = (hi - lo) - max_n;
+  while (E > 0) {
+    const int avail = (MT_N - rng.idx) >> 1;
+    if (avail == 0) {  // a coin straddles the twist: one serial step
+      if (rng.coin_lt_half()) ++lo; else --hi;
+      --E;
+      continue;
+    }
+    const int n = min(min(E, 64), avail);
+    const bool act = lane < n;
+    const bool front = act ? (WaveRng::temper(L.mt[rng.idx + 2 * lane]) >> 31) == 0 : false;
+    lo += __popcll(__ballot(act && front));
+    hi -= __popcll(__ballot(act && !front));
+    rng.idx += 2 * n;
+    E -= n;
+  }
+}
+
+__global__ __launch_bounds__(64) void pack_codebert_wave_kernel(PackParams P) {
+  __shared__ PackWaveLds L;
+  const int lane = threadIdx.x;
+  const int64_t p = blockIdx.x;
+  if (p >= P.n_part) return;
+  const int64_t d0 = P.part_doc_off[p], d1 = P.part_doc_off[p + 1];
+  const int64_t s0 = P.doc_sent_off[d0], s1 = P.doc_sent_off[d1];
+  const int64_t pb = (int64_t)P.dup * s0;
+  const int64_t base = P.sent_off[0];
+  const int nsent = (int)(s1 - s0), ndoc = (int)(d1 - d0);
+  // ---- filter: kept segment slots (wave scan), kept documents ------------
+  int32_t* kept_before = P.kept + s0 + p;
+  {
+    int run = 0;
+    for (int k = 0; k < nsent; k += 64) {
+      const int kk = k + lane;
+      const int n = kk < nsent ? P.ntok[s0 + kk] : 0;
+      const int keep = (kk < nsent && n > 0) ? 1 : 0;
+      const int incl = wscan_incl(keep, lane);
+      if (kk < nsent) {
+        const int slot = run + incl - keep;
+        kept_before[kk] = slot;
+        if (keep) {
+          P.fs_ntok[s0 + slot] = n;
+          P.fs_base[s0 + slot] = P.sent_off[s0 + kk] - base;
+          P.fs_dense[s0 + slot] = P.tokoff[s0 + kk];
+        }
+      }
+      run += lane_get(incl, 63);
+    }
+    if (lane == 0) kept_before[nsent] = run;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  // a document is kept when it has a kept code segment (len(CodePair) > 0,
+  // pretrain_codebert.py:161); its first fd_nd kept slots are docstring
+  int nd_docs = 0;
+  for (int k = 0; k < ndoc; k += 64) {
+    const int kk = k + lane;
+    int first = 0, cnt = 0, ndseg = 0;
+    if (kk < ndoc) {
+      const int a = (int)(P.doc_sent_off[d0 + kk] - s0), b = (int)(P.doc_sent_off[d0 + kk + 1] - s0);
+      const int c = min(a + P.doc_nseg_doc[d0 + kk], b);
+      first = kept_before[a];
+      cnt = kept_before[b] - first;
+      ndseg = kept_before[c] - first;
+    }
+    const int keep = (kk < ndoc && cnt - ndseg > 0) ? 1 : 0;
+    const int incl = wscan_incl(keep, lane);
+    if (keep) {
+      const int di = nd_docs + incl - 1;
+      P.fd_first[d0 + di] = s0 + first;
+      P.fd_n[d0 + di] = cnt;
+      P.fd_nd[d0 + di] = ndseg;
+    }
+    nd_docs += lane_get(incl, 63);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  auto len_abs = [&](int64_t slot) -> int { return P.fs_ntok[slot]; };
+
+  WaveRng rng{L, lane, MT_N};
+  rng.seed(P.seed + (uint64_t)p);
+  const int max_doc = P.max_seq >= 512 ? 64 : 32;
+  PairRec* out = P.pairs + pb;
+  int np = 0;
+  int err = PACK_OK;
+  for (int dup = 0; dup < P.dup && !err; ++dup) {
+    for (int di = 0; di < nd_docs && !err; ++di) {
+      const int64_t first = P.fd_first[d0 + di];
+      const int nd = P.fd_nd[d0 + di];
+      const int nc = P.fd_n[d0 + di] - nd;
+      const int64_t cfirst = first + nd;
+      const int special = nd ? 3 : 2;
+      const int max_num = P.max_seq - special;
+      const double sp = rng.random();
+      // docstring part (pretrain_codebert.py:375-396)
+      int dn = 0, dlo = 0, dhi = 0;
+      if (nd && sp < P.short_seq_prob) {
+        dn = 1;
+        dhi = len_abs(first);
+      } else if (nd) {
+        int cur;
+        // flush at i == nc - 1 (the quirk: the code-segment count) or cur > max_doc
+        const int i = find_over([&](int k) { return len_abs(first + k); }, 0, nd, nc - 1, 0, max_doc, lane, &cur);
+        if (i >= 0) {
+          const int cn = i + 1;
+          dn = (cur > max_doc && cn > 1) ? cn - 1 : cn;
+          dhi = dn == cn ? cur : cur - len_abs(first + i);
+          trunc_seq_wave(rng, L, lane, dlo, dhi, max_doc);
+        }
+      }
+      const int doc_len = dhi - dlo;
+      // code part (:400-440): chunks [cs, i], the overflowing segment carried
+      int cs = 0, k0 = 0, carried = 0;  // carried: the chunk already holds segment cs (stay)
+      int nout = 0;
+      while (k0 < nc && !err) {
+        const int b0 = doc_len + carried;
+        int cur;
+        const int i = find_over([&](int k) { return len_abs(cfirst + k); }, k0, nc, nc - 1, b0, max_num, lane, &cur);
+        const int cn = i - cs + 1;
+        const bool stay = cur > max_num && cn > 1;
+        int clo = 0, chi = cur - doc_len;
+        const int lim = max_num - doc_len;
+        if (lim < 0) { err = PACK_EINDEX; break; }  // del from an empty list: IndexError
+        trunc_seq_wave(rng, L, lane, clo, chi, lim);
+        if (chi - clo < 1) { err = PACK_EASSERT; break; }
+        if (nout == 0 || chi - clo >= 16) {
+          if (lane == 0) {
+            PairRec r;
+            r.fs0 = first; r.n0 = (uint16_t)dn; r.lo0 = (uint16_t)dlo; r.hi0 = (uint16_t)dhi;
+            r.fs1 = cfirst + cs; r.n1 = (uint16_t)cn; r.lo1 = (uint16_t)clo; r.hi1 = (uint16_t)chi;
+            r.flags = (uint16_t)(special == 3 ? 2 : 0);
+            r.num_tokens = (uint16_t)(doc_len + (chi - clo) + special);
+            out[np] = r;
+          }
+          ++np;
+          ++nout;
+        }
+        if (stay) { cs = i; carried = len_abs(cfirst + i); }
+        else { cs = i + 1; carried = 0; }
+        k0 = i + 1;
+      }
+    }
+  }
+  if (lane == 0) P.part_err[p] = err;
+  if (err) {
+    if (lane == 0) { P.part_npairs[p] = 0; P.part_ntok[p] = 0; }
+    return;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  // ---- random.shuffle(partition_pairs) (:476) ------------------------------
+  int32_t* gorder = P.order + pb;
+  for (int k = lane; k < np; k += 64) gorder[k] = k;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  for (int k = np - 1; k >= 1; --k) {
+    const int j = (int)rng.randbelow((uint32_t)(k + 1));
+    if (lane == 0) { const int32_t t = gorder[k]; gorder[k] = gorder[j]; gorder[j] = t; }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  // ---- stable bin partition + token offsets ---------------------------------
+  const int nb = P.nbins;
+  int32_t* binned = P.binned + pb;
+  int64_t* tl = P.tok_local + pb;
+  int pos = 0;
+  int64_t acc = 0;
+  for (int b = 0; b < nb; ++b) {
+    int cnt = 0;
+    for (int k = 0; k < np; k += 64) {
+      const int kk = k + lane;
+      int rec = 0, nt = 0;
+      bool in = false;
+      if (kk < np) {
+        rec = gorder[kk];
+        nt = out[rec].num_tokens;
+        int bb = (nt - 1) / P.bin_size;
+        bb = bb > nb - 1 ? nb - 1 : bb;
+        in = bb == b;
+      }
+      const uint64_t m = __ballot(in);
+      const int before = __popcll(m & ((1ull << lane) - 1ull));
+      const int tinc = wscan_incl(in ? nt : 0, lane);
+      if (in) {
+        binned[pos + before] = rec;
+        tl[pos + before] = acc + tinc - nt;
+      }
+      pos += __popcll(m);
+      cnt += __popcll(m);
+      acc += lane_get(tinc, 63);
+    }
+    if (lane == 0) P.bin_count[p * nb + b] = cnt;
+  }
+  if (lane == 0) {
+    P.part_npairs[p] = np;
+    P.part_ntok[p] = acc;
+  }
+}
+
+hipError_t launch_pack_codebert_wave(const PackParams& P, hipStream_t s) {
+  hipLaunchKernelGGL(pack_codebert_wave_kernel, dim3((unsigned)P.n_part), dim3(64), 0, s, P);
+  return hipGetLastError();
+}
+
 }  // namespace lddl

@@ -68,8 +68,12 @@ def test_bert_golden(packer, k, binned):
       assert bn == po.bin_of(e['num_tokens'], case['bin_size'], case['nbins'])
 
 
+@pytest.mark.parametrize('algo', [None, '1'])
 @pytest.mark.parametrize('k', range(len(CODE['cases'])))
-def test_codebert_golden(cpacker, k):
+def test_codebert_golden(cpacker, monkeypatch, k, algo):
+  """algo: the wave-per-partition packer (default) or the lane-serial one (1)"""
+  if algo:
+    monkeypatch.setenv('LDDL_PACK_ALGO', algo)
   case = CODE['cases'][k]
   c = case['cfg']
   sh, ids, ntok = shards_from_docs(case['docs'], case['ndoc'])
@@ -113,11 +117,13 @@ def test_bert_end_to_end_vs_oracle(gpu, monkeypatch, seq, bin_size, nparts, caps
     assert np.array_equal(bc[p], cnt)
 
 
-@pytest.mark.parametrize('mat', [None, '1'])
-def test_codebert_end_to_end_vs_oracle(gpu, monkeypatch, mat):
+@pytest.mark.parametrize('mat,algo', [(None, None), ('1', None), (None, '1')])
+def test_codebert_end_to_end_vs_oracle(gpu, monkeypatch, mat, algo):
   from lddl_amd import synth, pipeline
   if mat:
     monkeypatch.setenv('LDDL_MAT_ALGO', mat)
+  if algo:
+    monkeypatch.setenv('LDDL_PACK_ALGO', algo)
   c = synth.make_code(400, seed=31)
   pdo = pipeline.partition_by_bytes(c, 3)
   res = pipeline.run_bert(c, vocab_file=pipeline.VOCAB_CODEBERT, target_seq_length=512, bin_size=64,
@@ -251,3 +257,35 @@ def test_bert_masked_special_tokens_and_arena_regrow(gpu, monkeypatch):
     exp.append([rr[i] for i in order])
   from lddl_amd.pipeline import assert_same_pairs
   assert_same_pairs(res, exp)
+
+
+@pytest.mark.parametrize('seq,ssp,dup', [(512, 0.1, 1), (128, 0.0, 2), (512, 1.0, 1), (128, 0.3, 3)])
+def test_codebert_wave_vs_lane_long_documents(cpacker, monkeypatch, seq, ssp, dup):
+  """Documents with > 64 code and docstring segments (multi-window scans),
+  long segments (truncation rounds across MT twists), empty segments: the
+  wave packer against the lane-serial one (itself pinned by the goldens)."""
+  rng = np.random.default_rng(seq + dup)
+  docs, ndoc = [], []
+  for d in range(60):
+    nds = int(rng.choice([0, 1, 3, 70]))
+    ncs = int(rng.choice([1, 2, 40, 130]))
+    segs = []
+    for q in range(nds + ncs):
+      n = int(rng.choice([0, 1, 5, 12, 40, 90])) if q < nds else int(rng.choice([0, 2, 9, 30, 200]))
+      segs.append([int(x) for x in rng.integers(1000, 2000, n)])
+    if not any(segs[nds:]):
+      segs[-1] = [1500] * 7
+    docs.append(segs)
+    ndoc.append(nds)
+  pdo = [0, 13, 13, 40, 60]
+  out = {}
+  for algo in ('', '1'):
+    monkeypatch.setenv('LDDL_PACK_ALGO', algo)
+    sh, ids, ntok = shards_from_docs(docs, ndoc, part_doc_off=pdo)
+    try:
+      res = cpacker.pack(sh, ids, ntok, target_seq_length=seq, short_seq_prob=ssp, duplicate_factor=dup,
+                         seed=77, codebert=True, bin_size=seq // 4)
+      out[algo] = (res.rows(), res.bin_count.cpu().numpy().tolist())
+    except IndexError:
+      out[algo] = 'IndexError'
+  assert out[''] == out['1']
