@@ -304,9 +304,10 @@ def main():
   try:
     with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), 'profiles', 'traffic.json')) as f:
       tr = json.load(f)
-    if (tr.get('workload'), tr.get('kernel')) == (line['config']['workload'], line['roofline']['kernel']):
-      line['roofline']['traffic'] = tr['traffic_bytes_per_call']
-      line['roofline']['traffic_source'] = tr['source']
+    for e in tr.get('entries', [tr]):
+      if (e.get('workload'), e.get('kernel')) == (line['config']['workload'], line['roofline']['kernel']):
+        line['roofline']['traffic'] = e['traffic_bytes_per_call']
+        line['roofline']['traffic_source'] = e['source']
   except (OSError, ValueError, KeyError):
     pass
   if args.parquet_parts > 0:
