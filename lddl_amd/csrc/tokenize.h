@@ -53,7 +53,8 @@ hipError_t launch_tile_bounds(const int64_t* sent_off, int64_t n_sent, int64_t n
 hipError_t launch_tokenize_fallback(const TokParams& P, const int64_t* tile_sent, const int32_t* fb_list,
                                     const int32_t* fb_count, int grid, hipStream_t s);
 // v4 (tokenize_stream.hip): wave per 1 KiB tile, persistent; cfg selects
-// waves per workgroup / Bloom filter (0: 4+Bloom, 1: 4, 2: 12+Bloom, 3: 8+Bloom)
+// waves per workgroup / Bloom filter (0: 4+Bloom, 1: 4, 2: 12+Bloom, 3: 8+Bloom,
+// 4: 16+Bloom = default), 5 / 6: two 1 KiB tiles per wave (8 / 4 waves + Bloom)
 hipError_t launch_tokenize_stream(const TokParams& P, int64_t nbytes, int64_t* tile_sent, int32_t* fb_list,
                                   int32_t* fb_count, int fb_grid, int n_cu, int cfg, hipStream_t s);
 

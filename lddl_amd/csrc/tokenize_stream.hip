@@ -42,42 +42,59 @@
 namespace lddl {
 namespace tok4 {
 
-constexpr int CAP = 2048;             // window bytes (32 per lane)
-constexpr int DCAP = 256;             // side buffer for dirty words
-constexpr int NBUF = CAP + DCAP + 64; // + over-read pad of the candidate loads
-constexpr int UCAP = 256;             // units per tile
-constexpr int NSCAP = 64;             // sentences per tile
-constexpr int XCAP = 32;              // expansion markers per tile
-constexpr int MPCAP = CAP / 2 - UCAP * 2;  // multi-piece buffer entries (u16) per round
+// Geometry of one wave's tile: H = 1 (1 KiB of sentence starts, 2 KiB
+// window, 32 B per lane) or H = 2 (two 1 KiB tiles as one: 4 KiB window as two
+// 2 KiB halves, twice the units per WordPiece pass -- the pass's serial
+// chain is the longest word's, so its lanes fill up; half the waves per CU)
+template <int H>
+struct Geo {
+  static constexpr int CAP = 2048 * H;              // window bytes (32 per lane per half)
+  static constexpr int DCAP = 256 * H;              // side buffer for dirty words
+  static constexpr int NBUF = CAP + DCAP + 64;      // + over-read pad of the candidate loads
+  static constexpr int UCAP = 256 * H;              // units per round
+  static constexpr int NSCAP = 64 * H;              // sentences per tile
+  static constexpr int XCAP = 32 * H;               // expansion markers per tile
+  static constexpr int MPCAP = CAP / 2 - UCAP * 2;  // multi-piece buffer entries (u16) per round
+  // work entry: unit | window position << UB | byte length << LSH
+  static constexpr int UB = 7 + H, SB = 11 + H, LSH = UB + SB;
+  __device__ static __forceinline__ uint32_t wmake(int u, int src, int len) {
+    return (uint32_t)u | ((uint32_t)src << UB) | ((uint32_t)len << LSH);
+  }
+  __device__ static __forceinline__ int wunit(uint32_t w) { return (int)(w & ((1u << UB) - 1u)); }
+  __device__ static __forceinline__ int wsrc(uint32_t w) { return (int)((w >> UB) & ((1u << SB) - 1u)); }
+  __device__ static __forceinline__ int wlen(uint32_t w) { return (int)(w >> LSH); }
+};
 constexpr uint32_t BF = 0xFFu, BX = 0xFDu, BS = 0xF8u;  // filler, expansion, special k = BS+k
 
 // class byte per input byte value
 enum : uint32_t { C_W = 1, C_I = 2, C_S = 4, C_D = 8, C_UP = 16, C_X = 32, C_CS = 64 };
 
+template <int H>
 struct WaveLds {
+  using G = Geo<H>;
   // raw bytes (step 1); afterwards the same bytes hold the pieces: uid[u] =
   // the id of a unit done with one piece (specials, [UNK], first-probe hits),
   // upo[u] = offset of a WordPiece unit's pieces in mp (bump-allocated, <=
   // its byte length each), 0xFFFF = uid
   union {
-    uint32_t rp[CAP / 4 + 4];
+    uint32_t rp[G::CAP / 4 + 4];
     struct {
-      uint16_t uid[UCAP];
-      uint16_t upo[UCAP];
-      uint16_t mp[MPCAP];
+      uint16_t uid[G::UCAP];
+      uint16_t upo[G::UCAP];
+      uint16_t mp[G::MPCAP];
     } pcs;
   };
-  uint32_t nb[NBUF / 4];     // normalised bytes in window coordinates; side buffer at [CAP, CAP+DCAP)
-  uint32_t brk[64];          // break bits: unit starts, spaces, sentence starts
-  uint32_t dm[64];           // dirty bits: filler / expansion marker bytes
-  uint32_t sb[64];           // sentence-start bits
-  uint32_t urec[UCAP];       // window position | sentence << 16
-  uint32_t uwp[UCAP];        // WordPiece unit | source << 8 | length << 20 (0: none), then the work list in place
-  uint8_t ucnt[UCAP];        // pieces per unit
-  uint16_t sst[NSCAP + 2];   // sentence starts (window coordinates)
-  uint16_t stot[NSCAP];      // tokens per sentence
-  uint32_t xent[XCAP];       // table entry of each expansion marker
-  uint8_t xlen[XCAP];        // its normalised byte length
+  uint32_t nb[G::NBUF / 4];     // normalised bytes in window coordinates; side buffer at [CAP, CAP+DCAP)
+  uint32_t brk[64 * H];          // break bits: unit starts, spaces, sentence starts
+  uint32_t dm[64 * H];           // dirty bits: filler / expansion marker bytes
+  uint32_t sb[64 * H];           // sentence-start bits
+  uint32_t urec[G::UCAP];       // window position | sentence << 16
+  uint32_t uwp[G::UCAP];        // WordPiece entry (Geo::wmake; 0: none), then the work list in place
+  uint8_t ucnt[G::UCAP];        // pieces per unit
+  uint16_t sst[G::NSCAP + 2];   // sentence starts (window coordinates)
+  uint16_t stot[G::NSCAP];      // tokens per sentence
+  uint32_t xent[G::XCAP];       // table entry of each expansion marker
+  uint8_t xlen[G::XCAP];        // its normalised byte length
   int32_t misc[4];           // 0 side-buffer cursor, 1 #markers, 2 overflow, 3 mp cursor
 };
 
@@ -86,9 +103,12 @@ __device__ __forceinline__ void wsync() {
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
-__device__ __forceinline__ uint32_t rawb(const WaveLds& L, int p) { return reinterpret_cast<const uint8_t*>(L.rp)[p]; }
-__device__ __forceinline__ uint32_t nbyte(const WaveLds& L, int p) { return reinterpret_cast<const uint8_t*>(L.nb)[p]; }
-__device__ __forceinline__ void nput(WaveLds& L, int p, uint32_t v) { reinterpret_cast<uint8_t*>(L.nb)[p] = (uint8_t)v; }
+template <int H>
+__device__ __forceinline__ uint32_t rawb(const WaveLds<H>& L, int p) { return reinterpret_cast<const uint8_t*>(L.rp)[p]; }
+template <int H>
+__device__ __forceinline__ uint32_t nbyte(const WaveLds<H>& L, int p) { return reinterpret_cast<const uint8_t*>(L.nb)[p]; }
+template <int H>
+__device__ __forceinline__ void nput(WaveLds<H>& L, int p, uint32_t v) { reinterpret_cast<uint8_t*>(L.nb)[p] = (uint8_t)v; }
 
 // bit q of each byte of c -> 4 bits (byte 0 -> bit 0)
 __device__ __forceinline__ uint32_t gather4(uint32_t c, int q) { return (((c >> q) & 0x01010101u) * 0x01020408u) >> 24; }
@@ -110,7 +130,8 @@ __device__ __forceinline__ uint32_t wave_excl(uint32_t v, int lane, uint32_t* to
   return x - v;
 }
 
-__device__ __forceinline__ int utf8_put(WaveLds& L, int p, uint32_t c) {
+template <int H>
+__device__ __forceinline__ int utf8_put(WaveLds<H>& L, int p, uint32_t c) {
   if (c < 0x80) { nput(L, p, c); return 1; }
   if (c < 0x800) { nput(L, p, 0xC0 | (c >> 6)); nput(L, p + 1, 0x80 | (c & 0x3F)); return 2; }
   if (c < 0x10000) {
@@ -123,7 +144,8 @@ __device__ __forceinline__ int utf8_put(WaveLds& L, int p, uint32_t c) {
 }
 
 // first break position > p (a unit's span end), at most nb
-__device__ __forceinline__ int span_end(const WaveLds& L, int p, int nb) {
+template <int H>
+__device__ __forceinline__ int span_end(const WaveLds<H>& L, int p, int nb) {
   int w = p >> 5;
   uint32_t m = L.brk[w] & ~((2u << (p & 31)) - 1u);
   while (m == 0) {
@@ -134,7 +156,8 @@ __device__ __forceinline__ int span_end(const WaveLds& L, int p, int nb) {
   return min((w << 5) + __ffs(m) - 1, nb);
 }
 
-__device__ __forceinline__ bool span_dirty(const WaveLds& L, int p, int q) {
+template <int H>
+__device__ __forceinline__ bool span_dirty(const WaveLds<H>& L, int p, int q) {
   for (int w = p >> 5; (w << 5) < q; ++w) {
     const int lo = max(p - (w << 5), 0), hi = min(q - (w << 5), 32);
     const uint32_t m = (hi >= 32 ? ~0u : ((1u << hi) - 1u)) & ~((1u << lo) - 1u);
@@ -145,7 +168,8 @@ __device__ __forceinline__ bool span_dirty(const WaveLds& L, int p, int q) {
 
 // Compact / expand the dirty span [p, q) into the side buffer.  Returns its
 // normalised length (source in *src), -1 on overflow (flagged in misc[2]).
-__device__ int dirty_normalize(WaveLds& L, const TokParams& P, int p, int q, int* src) {
+template <int H>
+__device__ int dirty_normalize(WaveLds<H>& L, const TokParams& P, int p, int q, int* src) {
   int len = 0;
   for (int i = p; i < q;) {
     const uint32_t b = nbyte(L, i);
@@ -161,11 +185,11 @@ __device__ int dirty_normalize(WaveLds& L, const TokParams& P, int p, int q, int
   }
   if (len == 0) return 0;
   const int off = atomicAdd(&L.misc[0], len);
-  if (off + len > DCAP) {
+  if (off + len > Geo<H>::DCAP) {
     L.misc[2] = 1;
     return -1;
   }
-  int o = CAP + off;
+  int o = Geo<H>::CAP + off;
   *src = o;
   for (int i = p; i < q;) {
     const uint32_t b = nbyte(L, i);
@@ -190,14 +214,16 @@ __device__ int dirty_normalize(WaveLds& L, const TokParams& P, int p, int q, int
   return len;
 }
 
-__device__ __forceinline__ int count_chars(const WaveLds& L, int src, int len) {
+template <int H>
+__device__ __forceinline__ int count_chars(const WaveLds<H>& L, int src, int len) {
   int n = 0;
   for (int i = 0; i < len; ++i) n += (nbyte(L, src + i) & 0xC0u) != 0x80u;
   return n;
 }
 
 // bytes [24, len) of a candidate against the vocab pool
-__device__ __forceinline__ bool long_eq(const WaveLds& L, const TokParams& P, int s, int len, uint32_t off) {
+template <int H>
+__device__ __forceinline__ bool long_eq(const WaveLds<H>& L, const TokParams& P, int s, int len, uint32_t off) {
   for (int k = 24; k < len; ++k)
     if (nbyte(L, s + k) != P.pool[off + k]) return false;
   return true;
@@ -208,7 +234,8 @@ __device__ __forceinline__ bool long_eq(const WaveLds& L, const TokParams& P, in
 struct Key6 {
   uint32_t d0, d1, d2, d3, d4, d5;
 };
-__device__ __forceinline__ Key6 load_key(const WaveLds& L, int s, int len) {
+template <int H>
+__device__ __forceinline__ Key6 load_key(const WaveLds<H>& L, int s, int len) {
   const int a = s >> 2;
   const uint32_t sh = (uint32_t)(s & 3);
   const uint32_t x0 = L.nb[a], x1 = L.nb[a + 1], x2 = L.nb[a + 2], x3 = L.nb[a + 3], x4 = L.nb[a + 4],
@@ -257,10 +284,12 @@ __device__ __forceinline__ bool slot_eq(const uint4& a, const uint4& b, const Ke
           (b.y ^ k.d5)) == 0u;
 }
 
-template <int WAVES, bool BLOOM, bool DBG>
+template <int WAVES, bool BLOOM, bool DBG, int H>
 __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int64_t* tile_sent, int64_t n_tiles,
                                                           int32_t* fb_list, int32_t* fb_count) {
-  __shared__ WaveLds Ls[WAVES];
+  using G = Geo<H>;
+  constexpr int CAP = G::CAP, UCAP = G::UCAP, NSCAP = G::NSCAP, XCAP = G::XCAP, MPCAP = G::MPCAP;
+  __shared__ WaveLds<H> Ls[WAVES];
   __shared__ uint32_t ctab32[64];
   __shared__ uint32_t bloom[BLOOM ? BLOOM_WORDS : 1];
   // ---- prologue: class table (from the unicode table's ASCII page), Bloom --
@@ -292,9 +321,10 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
   const uint8_t* ctab = reinterpret_cast<const uint8_t*>(ctab32);
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  WaveLds& L = Ls[wv];
+  WaveLds<H>& L = Ls[wv];
   const int64_t base = P.sent_off[0];
   const int64_t nwaves = (int64_t)gridDim.x * WAVES;
+  const int64_t n_work = (n_tiles + H - 1) / H;  // a wave's tile = H consecutive 1 KiB tiles
   constexpr bool dbg = DBG;
   uint64_t acc[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t tprev = 0;
@@ -304,10 +334,18 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
     acc[k] += t_ - tprev;                             \
     tprev = t_;                                       \
   }
-  for (int64_t t = (int64_t)blockIdx.x * WAVES + wv; t < n_tiles; t += nwaves) {
+  for (int64_t t = (int64_t)blockIdx.x * WAVES + wv; t < n_work; t += nwaves) {
     wsync();
     if (dbg) tprev = __builtin_amdgcn_s_memtime();
-    const int64_t sa = uni64(tile_sent[t]), sb = uni64(tile_sent[t + 1]);
+    const int64_t t0 = t * H, t1 = min(t0 + H, n_tiles);
+    // the fallback kernel re-runs listed 1 KiB tiles
+    auto fallback = [&]() {
+      if (lane == 0) {
+        const int at = atomicAdd(fb_count, (int)(t1 - t0));
+        for (int64_t q = t0; q < t1; ++q) fb_list[at + (q - t0)] = (int32_t)q;
+      }
+    };
+    const int64_t sa = uni64(tile_sent[t0]), sb = uni64(tile_sent[t1]);
     if (sa >= sb) continue;
     const int64_t A = uni64(P.sent_off[sa]), B = uni64(P.sent_off[sb]);
     const int aoff = (int)(reinterpret_cast<uintptr_t>(P.bytes + A) & 15u);
@@ -316,67 +354,79 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
     const int ns = (int)(sb - sa);
     if (dbg) acc[10] += 1;
     if (nb64 > CAP || ns > NSCAP) {
-      if (lane == 0) fb_list[atomicAdd(fb_count, 1)] = (int32_t)t;
+      fallback();
       if (dbg) acc[11] += 1;
       continue;
     }
     const int nb = (int)nb64;
     // ---- sentence starts ----------------------------------------------------
-    L.sb[lane] = 0;
+#pragma unroll
+    for (int h = 0; h < H; ++h) L.sb[h * 64 + lane] = 0;
     if (lane == 0) {
       L.misc[0] = 0;
       L.misc[1] = 0;
       L.misc[2] = 0;
     }
-    if (lane < ns) L.stot[lane] = 0;
+    for (int j = lane; j < ns; j += 64) L.stot[j] = 0;
     wsync();
-    if (lane < ns) {
-      const int pos = (int)(P.sent_off[sa + lane] - A) + aoff;
-      L.sst[lane] = (uint16_t)pos;
+    for (int j = lane; j < ns; j += 64) {
+      const int pos = (int)(P.sent_off[sa + j] - A) + aoff;
+      L.sst[j] = (uint16_t)pos;
       if (pos < nb) atomicOr(&L.sb[pos >> 5], 1u << (pos & 31));
     }
     // ---- 1: raw bytes -> masks + normalised bytes in place ------------------
-    const int p0 = lane * 32;
-    uint4 v0 = make_uint4(0, 0, 0, 0), v1 = v0;
-    {
-      // 16-B aligned blocks holding >= 1 window byte: never past a page
-      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-      const u32x4* gp = reinterpret_cast<const u32x4*>(wbase) + 2 * lane;
-      if (p0 < nb) {  // streamed once: non-temporal, keep L2 for the vocab table
-        const u32x4 a = __builtin_nontemporal_load(gp);
-        v0 = make_uint4(a.x, a.y, a.z, a.w);
-      }
-      if (p0 + 16 < nb) {
-        const u32x4 a = __builtin_nontemporal_load(gp + 1);
-        v1 = make_uint4(a.x, a.y, a.z, a.w);
-      }
-    }
-    *reinterpret_cast<uint4*>(&L.rp[lane * 8]) = v0;
-    *reinterpret_cast<uint4*>(&L.rp[lane * 8 + 4]) = v1;
-    const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-    uint32_t W = 0, I = 0, S = 0, CS = 0, D = 0, X = 0;
+    // half h covers window bytes [2048 h, 2048 (h + 1)), lane l its 32 bytes
+    // from 2048 h + 32 l; masks per half in registers (constant indices)
+    uint32_t W[H], I[H], S[H], CS[H], D[H], X[H], inwin[H];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const uint32_t x = w[k];
-      const uint32_t c = (uint32_t)ctab[x & 0xFFu] | ((uint32_t)ctab[(x >> 8) & 0xFFu] << 8) |
-                         ((uint32_t)ctab[(x >> 16) & 0xFFu] << 16) | ((uint32_t)ctab[x >> 24] << 24);
-      L.nb[lane * 8 + k] = (x + ((c & 0x10101010u) << 1)) | (((c >> 3) & 0x01010101u) * 0xFFu);
-      const int sh = 4 * k;
-      W |= gather4(c, 0) << sh;
-      I |= gather4(c, 1) << sh;
-      S |= gather4(c, 2) << sh;
-      D |= gather4(c, 3) << sh;
-      X |= gather4(c, 5) << sh;
-      CS |= gather4(c, 6) << sh;
+    for (int h = 0; h < H; ++h) {
+      const int p0 = h * 2048 + lane * 32;
+      uint4 v0 = make_uint4(0, 0, 0, 0), v1 = v0;
+      {
+        // 16-B aligned blocks holding >= 1 window byte: never past a page
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4* gp = reinterpret_cast<const u32x4*>(wbase) + 2 * (h * 64 + lane);
+        if (p0 < nb) {  // streamed once: non-temporal, keep L2 for the vocab table
+          const u32x4 a = __builtin_nontemporal_load(gp);
+          v0 = make_uint4(a.x, a.y, a.z, a.w);
+        }
+        if (p0 + 16 < nb) {
+          const u32x4 a = __builtin_nontemporal_load(gp + 1);
+          v1 = make_uint4(a.x, a.y, a.z, a.w);
+        }
+      }
+      *reinterpret_cast<uint4*>(&L.rp[(h * 64 + lane) * 8]) = v0;
+      *reinterpret_cast<uint4*>(&L.rp[(h * 64 + lane) * 8 + 4]) = v1;
+      const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+      uint32_t Wh = 0, Ih = 0, Sh = 0, CSh = 0, Dh = 0, Xh = 0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint32_t x = w[k];
+        const uint32_t c = (uint32_t)ctab[x & 0xFFu] | ((uint32_t)ctab[(x >> 8) & 0xFFu] << 8) |
+                           ((uint32_t)ctab[(x >> 16) & 0xFFu] << 16) | ((uint32_t)ctab[x >> 24] << 24);
+        L.nb[(h * 64 + lane) * 8 + k] = (x + ((c & 0x10101010u) << 1)) | (((c >> 3) & 0x01010101u) * 0xFFu);
+        const int sh = 4 * k;
+        Wh |= gather4(c, 0) << sh;
+        Ih |= gather4(c, 1) << sh;
+        Sh |= gather4(c, 2) << sh;
+        Dh |= gather4(c, 3) << sh;
+        Xh |= gather4(c, 5) << sh;
+        CSh |= gather4(c, 6) << sh;
+      }
+      const int wlo = min(max(aoff - p0, 0), 32), whi = min(max(nb - p0, 0), 32);
+      inwin[h] = (whi >= 32 ? ~0u : ((1u << whi) - 1u)) & (wlo >= 32 ? 0u : ~((1u << wlo) - 1u));
+      W[h] = Wh; I[h] = Ih; S[h] = Sh; CS[h] = CSh; D[h] = Dh; X[h] = Xh & inwin[h];
     }
-    const int wlo = min(max(aoff - p0, 0), 32), whi = min(max(nb - p0, 0), 32);
-    const uint32_t inwin = (whi >= 32 ? ~0u : ((1u << whi) - 1u)) & (wlo >= 32 ? 0u : ~((1u << wlo) - 1u));
-    X &= inwin;
     wsync();
     STAMP(0);
-    uint32_t sp_m = 0, sp_w = 0, sp_d = 0;  // this lane's last char / special running into the next lane
     bool bad = false;
-    for (uint32_t xm = X; xm;) {
+    uint32_t spm[H], spw[H], spd[H];  // per half: this lane's last char / special running into the next lane
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+    const int p0 = h * 2048 + lane * 32;
+    uint32_t sp_m = 0, sp_w = 0, sp_d = 0;
+    uint32_t Wh = W[h], Ih = I[h], Sh = S[h], CSh = CS[h], Dh = D[h];
+    for (uint32_t xm = X[h]; xm;) {
       const int i = __ffs(xm) - 1;
       xm &= xm - 1;
       const int p = p0 + i;
@@ -398,11 +448,11 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
           nput(L, p, BS + (uint32_t)sk);
           const uint64_t cov = ((1ull << (len - 1)) - 1ull) << (i + 1);
           const uint32_t cl = (uint32_t)cov;
-          W &= ~cl;
-          I &= ~cl;
-          S &= ~cl;
-          CS &= ~cl;
-          D &= ~cl;
+          Wh &= ~cl;
+          Ih &= ~cl;
+          Sh &= ~cl;
+          CSh &= ~cl;
+          Dh &= ~cl;
           sp_m |= (uint32_t)(cov >> 32);
         }
       } else {
@@ -420,9 +470,9 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
           dirty = true;
           wordc = true;
         } else if (cls == CLS_SPACE) {
-          S |= 1u << i;
+          Sh |= 1u << i;
         } else {
-          if (cls == CLS_ISOLATE) I |= 1u << i;
+          if (cls == CLS_ISOLATE) Ih |= 1u << i;
           else wordc = true;
           if (kind != KIND_IDENT) {
             uint32_t c0 = ent_payload(e), c1 = 0, c2 = 0;
@@ -459,44 +509,72 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
         }
         const uint32_t slo = (uint32_t)span, shi = (uint32_t)(span >> 32);
         if (wordc) {
-          W |= slo;
+          Wh |= slo;
           sp_w |= shi;
         }
         if (dirty) {
-          D |= slo;
+          Dh |= slo;
           sp_d |= shi;
         }
         sp_m |= shi;
       }
     }
-    {
-      const uint32_t im = wave_shr1(sp_m), iw = wave_shr1(sp_w), id = wave_shr1(sp_d);  // lane 0: 0
-      W = ((W & ~im) | iw) & inwin;
-      I &= ~im & inwin;
-      S &= ~im & inwin;
-      CS &= ~im & inwin;
-      D = ((D & ~im) | id) & inwin;
+    W[h] = Wh; I[h] = Ih; S[h] = Sh; CS[h] = CSh; D[h] = Dh;
+    spm[h] = sp_m; spw[h] = sp_w; spd[h] = sp_d;
+    }  // halves
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      // carry into lane 0 of half h > 0 from lane 63 of half h - 1
+      uint32_t im = wave_shr1(spm[h]), iw = wave_shr1(spw[h]), id = wave_shr1(spd[h]);  // lane 0: 0
+      if (h > 0) {
+        const uint32_t pm = lane_get(spm[h > 0 ? h - 1 : 0], 63), pw_ = lane_get(spw[h > 0 ? h - 1 : 0], 63),
+                       pd = lane_get(spd[h > 0 ? h - 1 : 0], 63);
+        if (lane == 0) {
+          im = pm;
+          iw = pw_;
+          id = pd;
+        }
+      }
+      W[h] = ((W[h] & ~im) | iw) & inwin[h];
+      I[h] &= ~im & inwin[h];
+      S[h] &= ~im & inwin[h];
+      CS[h] &= ~im & inwin[h];
+      D[h] = ((D[h] & ~im) | id) & inwin[h];
     }
     const bool wbad = __any(bad);
     wsync();
     STAMP(1);
     // ---- 2: units -----------------------------------------------------------
-    const uint32_t SB = L.sb[lane];
-    const uint32_t carry = wave_shr1(W) >> 31;
-    const uint32_t pw = (W << 1) | (lane ? carry : 0u);
-    const uint32_t U = CS & (I | (W & (~pw | SB)));
-    L.brk[lane] = U | (S & CS) | SB;
-    L.dm[lane] = D;
-    uint32_t tot;
-    // one scan for both: units (low 16 bits) and sentence starts (high)
-    const uint32_t ex = wave_excl((uint32_t)__popc(U) | ((uint32_t)__popc(SB) << 16), lane, &tot);
-    const int ub = (int)(ex & 0xFFFFu), sb_before = (int)(ex >> 16);
-    const int n = (int)(tot & 0xFFFFu);
+    uint32_t U[H], SBm[H];
+    int ub[H], sbb[H];
+    int n = 0, nstarts = 0;
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      const uint32_t SBh = L.sb[h * 64 + lane];
+      uint32_t carry = wave_shr1(W[h]) >> 31;
+      if (h > 0) {
+        const uint32_t pc = lane_get(W[h > 0 ? h - 1 : 0], 63) >> 31;
+        if (lane == 0) carry = pc;
+      }
+      const uint32_t pw = (W[h] << 1) | ((lane || h) ? carry : 0u);
+      const uint32_t Uh = CS[h] & (I[h] | (W[h] & (~pw | SBh)));
+      L.brk[h * 64 + lane] = Uh | (S[h] & CS[h]) | SBh;
+      L.dm[h * 64 + lane] = D[h];
+      uint32_t tot;
+      // one scan for both: units (low 16 bits) and sentence starts (high)
+      const uint32_t ex = wave_excl((uint32_t)__popc(Uh) | ((uint32_t)__popc(SBh) << 16), lane, &tot);
+      ub[h] = n + (int)(ex & 0xFFFFu);
+      sbb[h] = nstarts + (int)(ex >> 16);
+      n += (int)(tot & 0xFFFFu);
+      nstarts += (int)(tot >> 16);
+      U[h] = Uh;
+      SBm[h] = SBh;
+    }
     // every sentence start distinct (no empty sentence shares one): a unit's
     // sentence is the number of starts at or before it, minus one
-    const bool starts_distinct = (int)(tot >> 16) == ns;
+    const bool starts_distinct = nstarts == ns;
     if (wbad) {
-      if (lane == 0) fb_list[atomicAdd(fb_count, 1)] = (int32_t)t;
+      fallback();
       if (dbg) acc[11] += 1;
       continue;
     }
@@ -509,14 +587,16 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
         L.misc[0] = 0;
         L.misc[3] = 0;
       }
-      {
-        int u = ub;
-        for (uint32_t m = U; m; m &= m - 1, ++u) {
+#pragma unroll
+      for (int h = 0; h < H; ++h) {
+        const int p0 = h * 2048 + lane * 32;
+        int u = ub[h];
+        for (uint32_t m = U[h]; m; m &= m - 1, ++u) {
           if (u < rb || u >= rb + nr) continue;
           const int b = __ffs(m) - 1, p = p0 + b;
           int lo;
           if (starts_distinct) {
-            lo = sb_before + __popc(SB & ((2u << b) - 1u)) - 1;
+            lo = sbb[h] + __popc(SBm[h] & ((2u << b) - 1u)) - 1;
           } else {
             lo = 0;  // last sentence starting at or before p
             int hi = ns - 1;
@@ -554,7 +634,7 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
             cnt = 1;
           } else {
             need = true;
-            L.uwp[u] = (uint32_t)u | ((uint32_t)src << 8) | ((uint32_t)len << 20);
+            L.uwp[u] = G::wmake(u, src, len);
           }
         }
         if (cnt >= 0) L.ucnt[u] = (uint8_t)cnt;
@@ -581,10 +661,10 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
   {                                                                            \
     const int u = (k) * 64 + lane;                                             \
     const uint32_t w = u < nr ? L.uwp[u] : 0u;                                 \
-    const int len = (int)(w >> 20);                                            \
+    const int len = G::wlen(w);                                                \
     if (w != 0 && len <= 24 && len <= mb0) {                                   \
       uint32_t bk;                                                             \
-      const uint32_t h = key_hash(load_key(L, (int)((w >> 8) & 0xFFFu), len), len, 0u, &bk); \
+      const uint32_t h = key_hash(load_key(L, G::wsrc(w), len), len, 0u, &bk); \
       if (bl_ok(bk)) {                                                         \
         const uint4* bk = P.vt + 4 * (h & vmask);                              \
         fa##k = bk[0];                                                         \
@@ -597,8 +677,8 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
   if (fact##k) {                                                               \
     const int u = (k) * 64 + lane;                                             \
     const uint32_t w = L.uwp[u];                                               \
-    const int len = (int)(w >> 20);                                            \
-    const Key6 key = load_key(L, (int)((w >> 8) & 0xFFFu), len);               \
+    const int len = G::wlen(w);                                                \
+    const Key6 key = load_key(L, G::wsrc(w), len);                             \
     if (slot_eq(fa##k, fb##k, key, ((uint32_t)len << 16) | 0x80000000u)) {      \
       L.pcs.uid[u] = (uint16_t)(fb##k.z & 0xFFFFu);                            \
       L.ucnt[u] = 1;                                                           \
@@ -606,17 +686,29 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
       if (dbg) acc[6] += 1;                                                    \
     }                                                                          \
   }
-      TOK4_FP_ISSUE(0)
-      TOK4_FP_ISSUE(1)
-      TOK4_FP_ISSUE(2)
-      TOK4_FP_ISSUE(3)
-      TOK4_FP_CHECK(0)
-      TOK4_FP_CHECK(1)
-      TOK4_FP_CHECK(2)
-      TOK4_FP_CHECK(3)
+      {
+        TOK4_FP_ISSUE(0)
+        TOK4_FP_ISSUE(1)
+        TOK4_FP_ISSUE(2)
+        TOK4_FP_ISSUE(3)
+        TOK4_FP_CHECK(0)
+        TOK4_FP_CHECK(1)
+        TOK4_FP_CHECK(2)
+        TOK4_FP_CHECK(3)
+      }
+      if constexpr (H == 2) {  // units 256..511: a second batch of 4 per lane
+        TOK4_FP_ISSUE(4)
+        TOK4_FP_ISSUE(5)
+        TOK4_FP_ISSUE(6)
+        TOK4_FP_ISSUE(7)
+        TOK4_FP_CHECK(4)
+        TOK4_FP_CHECK(5)
+        TOK4_FP_CHECK(6)
+        TOK4_FP_CHECK(7)
+      }
 #undef TOK4_FP_ISSUE
 #undef TOK4_FP_CHECK
-      static_assert(UCAP == 256, "first-probe batch is unrolled for 4 units per lane");
+      static_assert(UCAP == 256 * H && H <= 2, "first-probe batches are unrolled for 4 units per lane");
     }
     wsync();
     // work list (in place over uwp), longest first: long words are the OOV
@@ -632,7 +724,7 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
       for (int pass = 0; pass < 2; ++pass)
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-          const bool take = ent[k] != 0 && ((ent[k] >> 20) >= 10u) == (pass == 0);
+          const bool take = ent[k] != 0 && (G::wlen(ent[k]) >= 10) == (pass == 0);
           const uint64_t bm = __ballot(take);
           if (take) L.uwp[at + lane_rank(bm)] = ent[k];
           at += __popcll(bm);
@@ -642,7 +734,7 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
     wsync();
     if (P.dbg_mode == 1) {  // ablation (LDDL_TOK_ABLATE=1, diagnostics only): no WordPiece loop
       for (int i = lane; i < nwl; i += 64) {
-        const int u = (int)(L.uwp[i] & 0xFFu);
+        const int u = G::wunit(L.uwp[i]);
         L.pcs.uid[u] = (uint16_t)P.unk;
         L.ucnt[u] = 1;
       }
@@ -763,9 +855,9 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
         u = -1;
       };
       auto begin = [&](uint32_t w) {
-        u = (int)(w & 0xFFu);
-        s = (int)((w >> 8) & 0xFFFu);
-        ulen = (int)(w >> 20);
+        u = G::wunit(w);
+        s = G::wsrc(w);
+        ulen = G::wlen(w);
         we = s + ulen;
         pb = -1;
         np = 0;
@@ -951,11 +1043,11 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
     }
     }  // rounds
     if (L.misc[2]) {
-      if (lane == 0) fb_list[atomicAdd(fb_count, 1)] = (int32_t)t;
+      fallback();
       if (dbg) { acc[11] += 1; acc[15] += 1; }
       continue;
     }
-    if (lane < ns) P.out_ntok[sa + lane] = min((int)L.stot[lane], P.max_tok);
+    for (int j = lane; j < ns; j += 64) P.out_ntok[sa + j] = min((int)L.stot[j], P.max_tok);
     STAMP(5);
   }
   if (dbg && lane == 0)
@@ -963,22 +1055,22 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
 #undef STAMP
 }
 
-template <int WAVES, bool BLOOM, bool DBG>
+template <int WAVES, bool BLOOM, bool DBG, int H = 1>
 hipError_t launch_cfg(const TokParams& P, int64_t n_tiles, const int64_t* tile_sent, int32_t* fb_list,
                       int32_t* fb_count, int n_cu, hipStream_t s) {
   static int per_cu = 0;
   if (per_cu == 0) {
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, tok4_kernel<WAVES, BLOOM, DBG>, 64 * WAVES, 0) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, tok4_kernel<WAVES, BLOOM, DBG, H>, 64 * WAVES, 0) !=
             hipSuccess ||
         per_cu < 1)
       per_cu = 1;
   }
   int64_t grid = (int64_t)n_cu * per_cu;
-  const int64_t need = (n_tiles + WAVES - 1) / WAVES;
+  const int64_t need = ((n_tiles + H - 1) / H + WAVES - 1) / WAVES;
   if (grid > need) grid = need;
   if (grid < 1) grid = 1;
-  hipLaunchKernelGGL((tok4_kernel<WAVES, BLOOM, DBG>), dim3((unsigned)grid), dim3(64 * WAVES), 0, s, P, tile_sent,
-                     n_tiles, fb_list, fb_count);
+  hipLaunchKernelGGL((tok4_kernel<WAVES, BLOOM, DBG, H>), dim3((unsigned)grid), dim3(64 * WAVES), 0, s, P,
+                     tile_sent, n_tiles, fb_list, fb_count);
   return hipGetLastError();
 }
 
@@ -1000,6 +1092,8 @@ hipError_t launch_tokenize_stream(const TokParams& P, int64_t nbytes, int64_t* t
       case 2: e = tok4::launch_cfg<12, true, false>(P, n_tiles, tile_sent, fb_list, fb_count, n_cu, s); break;
       case 3: e = tok4::launch_cfg<8, true, false>(P, n_tiles, tile_sent, fb_list, fb_count, n_cu, s); break;
       case 4: e = tok4::launch_cfg<16, true, false>(P, n_tiles, tile_sent, fb_list, fb_count, n_cu, s); break;
+      case 5: e = tok4::launch_cfg<8, true, false, 2>(P, n_tiles, tile_sent, fb_list, fb_count, n_cu, s); break;
+      case 6: e = tok4::launch_cfg<4, true, false, 2>(P, n_tiles, tile_sent, fb_list, fb_count, n_cu, s); break;
       default: e = tok4::launch_cfg<4, true, false>(P, n_tiles, tile_sent, fb_list, fb_count, n_cu, s); break;
     }
   }
