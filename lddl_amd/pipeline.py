@@ -70,16 +70,21 @@ def upload(corpus, part_doc_off, device):
     raise ValueError('part_doc_off must be a non-decreasing cover of [0, n_doc]')
   if np.any(np.diff(corpus.doc_sent_off) < 0) or np.any(np.diff(corpus.sent_off) < 0):
     raise ValueError('offsets must be non-decreasing')
+  # pinned staging + async H2D on the current stream (ordered before the
+  # tokenize launch; the caching host allocator keeps the staging buffers
+  # until the copies have run)
+  def h2d(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).pin_memory().to(device, non_blocking=True)
+
   data = torch.empty(corpus.nbytes + 16, dtype=torch.uint8, device=device)
-  data[:corpus.nbytes].copy_(torch.from_numpy(np.ascontiguousarray(corpus.data[:corpus.nbytes])))
+  data[:corpus.nbytes].copy_(torch.from_numpy(np.ascontiguousarray(corpus.data[:corpus.nbytes])).pin_memory(),
+                             non_blocking=True)
   data[corpus.nbytes:].zero_()
   nseg = None
   if corpus.doc_nseg_doc is not None:
-    nseg = torch.from_numpy(np.ascontiguousarray(corpus.doc_nseg_doc, dtype=np.int32)).to(device)
-  return ShardSet(data,
-                  torch.from_numpy(np.ascontiguousarray(corpus.sent_off - corpus.sent_off[0])).to(device),
-                  torch.from_numpy(np.ascontiguousarray(corpus.doc_sent_off)).to(device),
-                  torch.from_numpy(part_doc_off).to(device), nseg, corpus.nbytes)
+    nseg = h2d(np.asarray(corpus.doc_nseg_doc, dtype=np.int32))
+  return ShardSet(data, h2d(corpus.sent_off - corpus.sent_off[0]), h2d(corpus.doc_sent_off), h2d(part_doc_off), nseg,
+                  corpus.nbytes)
 
 
 @dataclasses.dataclass

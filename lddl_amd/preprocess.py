@@ -15,12 +15,19 @@ Same flags, same input layout, same output files:
   (``python -m lddl_amd.balance``, load_balance.py).
 
 What runs where:
-  host   read + --sample-ratio sampling + document shuffle + sentence split
-         (NLTK Punkt when importable, pretrain.py:86; else a rule-based
-         stand-in, see ``split_sentences``) + partitioning into
-         --num-blocks / --block-size byte blocks (readers.py:48-57);
+  host   read + --sample-ratio sampling + document shuffle + partitioning of
+         the shuffled raw documents into --num-blocks / --block-size byte
+         blocks (readers.py:48-57; like the reference's partitions they are
+         fixed before the split) + sentence split (NLTK Punkt when
+         importable, pretrain.py:86; else a rule-based stand-in, see
+         ``_rule_split``);
   GPU    tokenize -> pair packing -> binning -> materialisation -> string
          rendering (liblddl_amd.so), then the host parquet encoder.
+  The rank's partitions stream through in chunks of --chunk-mb raw MB: a
+  host thread splits chunk k+1 while chunk k is uploaded (pinned staging,
+  async H2D), tokenised, packed and written (the GPU calls and the parquet
+  encoder release the GIL).  The split time is reported separately
+  (``host_split_s``) together with how much of it the GPU/writer hid.
 
 Determinism: the reference draws the sample, the document shuffle and every
 partition's pairs from unseeded / dask-internal RNGs (pretrain.py:101-112,
@@ -117,22 +124,28 @@ def sentence_splitter(kind='auto'):
   return _rule_split, 'rules'
 
 
-def build_corpus(records, seed, sample_ratio, codebert=False, splitter=None):
-  """Documents (sampled, shuffled) -> sentence-split synth.Corpus + doc ids.
-
-  BERT: _to_document (pretrain.py:82-97): sentences = split(body), each
-  stripped, empty ones dropped.  CodeBERT: _to_code_pair
-  (pretrain_codebert.py:126-159): docstring / code lines stripped, empty
-  dropped; the doc's first doc_nseg_doc segments are its docstring."""
+def sample_shuffle(records, seed, sample_ratio):
+  """--sample-ratio sampling (readers.py:67-68) and the document shuffle
+  (pretrain.py:101-112), both from PCG64(seed)."""
   rng = np.random.Generator(np.random.PCG64(seed))
   records = list(records)
   if sample_ratio < 1.0:
     keep = rng.random(len(records)) < sample_ratio
     records = [r for r, k in zip(records, keep) if k]
   order = rng.permutation(len(records))
+  return [records[i] for i in order]
+
+
+def split_records(records, codebert=False, splitter=None):
+  """Documents (in order) -> sentence-split synth.Corpus + doc ids; document
+  i of the corpus is record i.
+
+  BERT: _to_document (pretrain.py:82-97): sentences = split(body), each
+  stripped, empty ones dropped.  CodeBERT: _to_code_pair
+  (pretrain_codebert.py:126-159): docstring / code lines stripped, empty
+  dropped; the doc's first doc_nseg_doc segments are its docstring."""
   sents, doc_off, nseg, ids = [], [0], [], []
-  for i in order:
-    r = records[i]
+  for r in records:
     if codebert:
       parts = r.split('<CODESPLIT>')
       if len(parts) != 3:
@@ -147,6 +160,28 @@ def build_corpus(records, seed, sample_ratio, codebert=False, splitter=None):
     ids.append(doc_id)
     doc_off.append(len(sents))
   return synth.corpus_from_sentences(sents, doc_off, nseg if codebert else None), ids
+
+
+def build_corpus(records, seed, sample_ratio, codebert=False, splitter=None):
+  """sample_shuffle + split_records over the whole input (tests, tools)."""
+  return split_records(sample_shuffle(records, seed, sample_ratio), codebert, splitter)
+
+
+def partition_records(records, block_size=None, num_blocks=None):
+  """--block-size / --num-blocks (readers.py:43-57) over the shuffled raw
+  documents: record offsets of partitions of ~equal raw size, documents
+  kept whole (= document offsets of split_records' corpus)."""
+  if num_blocks is not None and block_size is not None:
+    raise ValueError('Only one of num_blocks or blocksize needs to be set!')
+  sizes = np.fromiter((len(r) for r in records), dtype=np.int64, count=len(records))
+  total = int(sizes.sum())
+  if num_blocks is None:
+    num_blocks = max(1, int(round(total / block_size))) if block_size else 1
+  n = max(1, min(num_blocks, max(1, len(records))))
+  cum = np.concatenate([[0], np.cumsum(sizes)])
+  cuts = np.searchsorted(cum, np.linspace(0, cum[-1], n + 1)[1:-1])
+  off = np.concatenate([[0], cuts, [len(records)]]).astype(np.int64)
+  return np.maximum.accumulate(off)
 
 
 def partition_docs(corpus, block_size=None, num_blocks=None):
@@ -193,6 +228,9 @@ def attach_args(parser=None, codebert=False):
   p.add_argument('--masking', action='store_true')
   p.add_argument('--masked-lm-ratio', type=float, default=0.15)
   p.add_argument('--sentence-splitter', type=str, default='auto', choices=['auto', 'punkt', 'rules'])
+  p.add_argument('--chunk-mb', type=float, default=256.0,
+                 help='raw MB of partitions per pipeline chunk (host split of chunk k+1 overlaps the GPU and the '
+                      'writer on chunk k)')
   return p
 
 
@@ -207,6 +245,7 @@ def _check(args):
 def main(args, codebert=False):
   """Returns (files written by this rank, timings dict)."""
   import torch
+  from concurrent.futures import ThreadPoolExecutor
   from . import pipeline, writer
   _check(args)
   rank = int(os.environ.get('RANK', 0))
@@ -216,7 +255,7 @@ def main(args, codebert=False):
   if not os.path.isfile(vocab):
     raise ValueError('--vocab-file must be a local vocab.txt (no hub access): %s' % vocab)
   t = {}
-  t0 = time.perf_counter()
+  wall0 = t0 = time.perf_counter()
   if codebert:
     if not args.code:
       raise ValueError('--code is required')
@@ -231,35 +270,64 @@ def main(args, codebert=False):
     files = [f for s in srcs if s for f in find_files_under(s)]
     recs = read_records(files)
     split, how = sentence_splitter(args.sentence_splitter)
-  corpus, doc_ids = build_corpus(recs, args.seed, args.sample_ratio, codebert, split)
-  pdo = partition_docs(corpus, args.block_size, args.num_blocks)
-  n_part = len(pdo) - 1
+  recs = sample_shuffle(recs, args.seed, args.sample_ratio)
+  pro = partition_records(recs, args.block_size, args.num_blocks)
+  n_part = len(pro) - 1
   lo, hi = rank * n_part // world, (rank + 1) * n_part // world
-  t['host_read_split_s'] = time.perf_counter() - t0
-  # this rank's partitions as their own shard set (global partition ids kept)
-  d0, d1 = int(pdo[lo]), int(pdo[hi])
-  s0, s1 = int(corpus.doc_sent_off[d0]), int(corpus.doc_sent_off[d1])
-  sub = synth.Corpus(corpus.data[corpus.sent_off[s0]:corpus.sent_off[s1]],
-                     corpus.sent_off[s0:s1 + 1] - corpus.sent_off[s0], corpus.doc_sent_off[d0:d1 + 1] - s0,
-                     None if corpus.doc_nseg_doc is None else corpus.doc_nseg_doc[d0:d1])
+  t['host_read_s'] = time.perf_counter() - t0
+  # chunks of this rank's partitions, ~--chunk-mb raw MB each
+  sizes = np.fromiter((len(r) for r in recs[pro[lo]:pro[hi]]), dtype=np.int64, count=int(pro[hi] - pro[lo]))
+  cum = np.concatenate([[0], np.cumsum(sizes)])
+  part_end = cum[pro[lo + 1:hi + 1] - pro[lo]]
+  chunk_b = max(1, int(args.chunk_mb * (1 << 20)))
+  bounds = [lo]
+  acc0 = 0
+  for p in range(lo, hi):
+    if part_end[p - lo] - acc0 >= chunk_b and p + 1 < hi:
+      bounds.append(p + 1)
+      acc0 = part_end[p - lo]
+  bounds.append(hi)
+  chunks = [(a, b) for a, b in zip(bounds[:-1], bounds[1:]) if b > a]
+
+  def split_chunk(c):
+    a, b = chunks[c]
+    ts = time.perf_counter()
+    corpus, ids = split_records(recs[pro[a]:pro[b]], codebert, split)
+    return corpus, ids, time.perf_counter() - ts
+
   device = torch.device('cuda', local)
   torch.cuda.set_device(device)
-  t0 = time.perf_counter()
   pk = pipeline.Packer(vocab, local)
-  sh = pipeline.upload(sub, pdo[lo:hi + 1] - d0, device)
-  ids, ntok = pk.tokenize(sh)
-  # partition p of this rank packs after random.seed(args.seed + global p)
-  res = pk.pack(sh, ids, ntok, target_seq_length=args.target_seq_length, short_seq_prob=args.short_seq_prob,
-                duplicate_factor=args.duplicate_factor, seed=args.seed + lo, bin_size=args.bin_size,
-                codebert=codebert, masking=args.masking and not codebert, masked_lm_ratio=args.masked_lm_ratio)
-  torch.cuda.synchronize()
-  t['gpu_s'] = time.perf_counter() - t0
-  t0 = time.perf_counter()
   sink = os.path.abspath(os.path.expanduser(args.sink))
-  out = writer.write_shards(pk, res, sink, bin_size=args.bin_size, codebert=codebert,
-                            masking=args.masking and not codebert, doc_ids=doc_ids[d0:d1], part_base=lo)
-  t['write_s'] = time.perf_counter() - t0
-  t.update(rank=rank, world=world, partitions=[lo, hi], documents=d1 - d0, pairs=res.n_pairs,
+  out = []
+  t.update(host_split_s=0.0, split_wait_s=0.0, gpu_s=0.0, write_s=0.0, pairs=0)
+  with ThreadPoolExecutor(1) as ex:
+    fut = ex.submit(split_chunk, 0) if chunks else None
+    for c, (a, b) in enumerate(chunks):
+      tw = time.perf_counter()
+      corpus, ids, ts = fut.result()
+      t['split_wait_s'] += time.perf_counter() - tw
+      t['host_split_s'] += ts
+      if c + 1 < len(chunks):
+        fut = ex.submit(split_chunk, c + 1)  # overlaps this chunk's GPU work and parquet writes
+      t0 = time.perf_counter()
+      sh = pipeline.upload(corpus, pro[a:b + 1] - pro[a], device)
+      ids_d, ntok = pk.tokenize(sh)
+      # partition p packs after random.seed(args.seed + global p)
+      res = pk.pack(sh, ids_d, ntok, target_seq_length=args.target_seq_length, short_seq_prob=args.short_seq_prob,
+                    duplicate_factor=args.duplicate_factor, seed=args.seed + a, bin_size=args.bin_size,
+                    codebert=codebert, masking=args.masking and not codebert, masked_lm_ratio=args.masked_lm_ratio)
+      torch.cuda.synchronize()
+      t['gpu_s'] += time.perf_counter() - t0
+      t0 = time.perf_counter()
+      out += writer.write_shards(pk, res, sink, bin_size=args.bin_size, codebert=codebert,
+                                 masking=args.masking and not codebert, doc_ids=ids, part_base=a)
+      t['write_s'] += time.perf_counter() - t0
+      t['pairs'] += res.n_pairs
+  t['wall_s'] = time.perf_counter() - wall0
+  # the part of the host split hidden behind the GPU and the writer
+  t['host_split_hidden_s'] = max(0.0, t['host_split_s'] - t['split_wait_s'])
+  t.update(rank=rank, world=world, partitions=[lo, hi], documents=int(pro[hi] - pro[lo]), chunks=len(chunks),
            sentence_splitter=how)
   return out, t
 

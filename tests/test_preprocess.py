@@ -4,6 +4,7 @@ sentence split / sampling / partitioning and the reference's flag defaults
 import os
 
 import numpy as np
+import pytest
 
 from lddl_amd import preprocess
 
@@ -75,3 +76,23 @@ def test_partition_docs():
   assert len(pdo) == 8 and pdo[0] == 0 and pdo[-1] == c.n_doc
   pdo = preprocess.partition_docs(c, block_size=50_000)
   assert len(pdo) - 1 == round(c.nbytes / 50_000)
+
+
+def test_partition_records():
+  recs = ['x' * (10 + (i * 37) % 200) for i in range(500)]
+  pro = preprocess.partition_records(recs, num_blocks=7)
+  assert len(pro) == 8 and pro[0] == 0 and pro[-1] == 500 and np.all(np.diff(pro) > 0)
+  sizes = np.array([len(r) for r in recs])
+  part = [sizes[pro[k]:pro[k + 1]].sum() for k in range(7)]
+  assert max(part) - min(part) <= 2 * sizes.max()
+  assert len(preprocess.partition_records(recs, block_size=10_000)) - 1 == round(sizes.sum() / 10_000)
+  assert list(preprocess.partition_records(['a', 'b'], num_blocks=5)) == [0, 1, 2]
+  with pytest.raises(ValueError):
+    preprocess.partition_records(recs, block_size=10, num_blocks=2)
+
+
+def test_build_corpus_is_shuffle_then_split():
+  recs = ['wiki-%d Body %d here. Second one.' % (i, i) for i in range(50)]
+  c, ids = preprocess.build_corpus(recs, 4, 0.8, splitter=preprocess._rule_split)
+  c2, ids2 = preprocess.split_records(preprocess.sample_shuffle(recs, 4, 0.8), splitter=preprocess._rule_split)
+  assert ids == ids2 and np.array_equal(c.data, c2.data) and np.array_equal(c.doc_sent_off, c2.doc_sent_off)

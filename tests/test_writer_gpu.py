@@ -148,9 +148,18 @@ def test_cli_bert_end_to_end(gpu, tmp_path):
   files, t = preprocess.main(args)
   assert sorted(os.path.basename(f) for f in files) == sorted(
       'part.%d.parquet_%d' % (p, b) for p in range(4) for b in range(4))
-  recs = preprocess.read_records(preprocess.find_files_under(str(src)))
-  corpus, ids = preprocess.build_corpus(recs, 5, 0.9, splitter=preprocess._rule_split)
-  pdo = preprocess.partition_docs(corpus, num_blocks=4)
+  # several pipeline chunks (host split of chunk k+1 overlapping chunk k) give the same files
+  sink2 = tmp_path / 'out2'
+  args2 = preprocess.attach_args().parse_args(
+      ['--wikipedia', str(tmp_path / 'wiki'), '--sink', str(sink2), '--target-seq-length', '128', '--bin-size', '32',
+       '--num-blocks', '4', '--sentence-splitter', 'rules', '--seed', '5', '--chunk-mb', '0.05'])
+  files2, t2 = preprocess.main(args2)
+  assert t2['chunks'] > 1 and t['chunks'] == 1
+  for f in files:
+    assert _read(f) == _read(str(sink2 / os.path.basename(f)))
+  recs = preprocess.sample_shuffle(preprocess.read_records(preprocess.find_files_under(str(src))), 5, 0.9)
+  pdo = preprocess.partition_records(recs, num_blocks=4)
+  corpus, ids = preprocess.split_records(recs, splitter=preprocess._rule_split)
   oids, ontok = OracleTokenizer(pipeline.VOCAB_BERT).run(corpus.data, corpus.sent_off, 512, nthreads=8)
   exp = po.run_bert_shards(corpus, oids, ontok, pdo, 128, 0.1, 5, 5, 32)
   vocab = _vocab(pipeline.VOCAB_BERT)
@@ -186,9 +195,10 @@ def test_cli_codebert_end_to_end(gpu, tmp_path):
        '--seed', '8', '--sample-ratio', '1.0'])
   files, t = preprocess.main(args, codebert=True)
   assert sorted(os.path.basename(f) for f in files) == ['part.0.parquet', 'part.1.parquet']
-  recs = preprocess.read_records([str(tmp_path / 'code' / 'a.txt')], linedelimiter='\r\n')
-  c, ids = preprocess.build_corpus(recs, 8, 1.0, codebert=True)
-  pdo = preprocess.partition_docs(c, num_blocks=2)
+  recs = preprocess.sample_shuffle(
+      preprocess.read_records([str(tmp_path / 'code' / 'a.txt')], linedelimiter='\r\n'), 8, 1.0)
+  pdo = preprocess.partition_records(recs, num_blocks=2)
+  c, ids = preprocess.split_records(recs, codebert=True)
   oids, ontok = OracleTokenizer(pipeline.VOCAB_CODEBERT).run(c.data, c.sent_off, 512, nthreads=8)
   vocab = _vocab(pipeline.VOCAB_CODEBERT)
   for p in range(2):
