@@ -23,11 +23,14 @@ What runs where:
          ``_rule_split``);
   GPU    tokenize -> pair packing -> binning -> materialisation -> string
          rendering (liblddl_amd.so), then the host parquet encoder.
-  The rank's partitions stream through in chunks of --chunk-mb raw MB: a
-  host thread splits chunk k+1 while chunk k is uploaded (pinned staging,
-  async H2D), tokenised, packed and written (the GPU calls and the parquet
-  encoder release the GIL).  The split time is reported separately
-  (``host_split_s``) together with how much of it the GPU/writer hid.
+  The rank's partitions stream through in chunks of --chunk-mb raw MB:
+  --split-workers host processes (forked before the GPU is touched, so they
+  hold the shuffled records copy-on-write and never see a GPU context) split
+  the next chunks while chunk k is uploaded (pinned staging, async H2D),
+  tokenised, packed and written.  Processes, not threads: the split is
+  GIL-bound Python (Punkt or the stand-in) and would stall the main thread's
+  GPU / writer calls.  The split time is reported separately
+  (``host_split_s``) together with how much of it was hidden.
 
 Determinism: the reference draws the sample, the document shuffle and every
 partition's pairs from unseeded / dask-internal RNGs (pretrain.py:101-112,
@@ -228,9 +231,11 @@ def attach_args(parser=None, codebert=False):
   p.add_argument('--masking', action='store_true')
   p.add_argument('--masked-lm-ratio', type=float, default=0.15)
   p.add_argument('--sentence-splitter', type=str, default='auto', choices=['auto', 'punkt', 'rules'])
-  p.add_argument('--chunk-mb', type=float, default=256.0,
-                 help='raw MB of partitions per pipeline chunk (host split of chunk k+1 overlaps the GPU and the '
-                      'writer on chunk k)')
+  p.add_argument('--chunk-mb', type=float, default=64.0,
+                 help='raw MB of partitions per pipeline chunk (host split of the next chunks overlaps the GPU and '
+                      'the writer on chunk k)')
+  p.add_argument('--split-workers', type=int, default=4,
+                 help='host processes splitting sentences ahead of the GPU (0: split inline)')
   return p
 
 
@@ -240,6 +245,15 @@ def _check(args):
       raise ValueError('Please provide a bin size that is <= target-seq-length')
     if args.target_seq_length % args.bin_size != 0:
       raise ValueError('Please provide a bin size that can divide the target sequence length.')
+
+
+_FE = {}  # the split workers' fork-inherited state (records, mode, splitter)
+
+
+def _split_worker(a, b):
+  ts = time.perf_counter()
+  corpus, ids = split_records(_FE['recs'][a:b], _FE['codebert'], _FE['split'])
+  return corpus, ids, time.perf_counter() - ts
 
 
 def main(args, codebert=False):
@@ -289,27 +303,43 @@ def main(args, codebert=False):
   bounds.append(hi)
   chunks = [(a, b) for a, b in zip(bounds[:-1], bounds[1:]) if b > a]
 
-  def split_chunk(c):
-    a, b = chunks[c]
+  # split workers: forked here, before anything touches the GPU
+  nw = min(max(0, args.split_workers), len(chunks)) if len(chunks) > 1 else 0
+  pool = None
+  if nw > 0:
+    import multiprocessing
+    _FE.update(recs=recs, codebert=codebert, split=split)
+    pool = multiprocessing.get_context('fork').Pool(nw)
+    _FE.clear()
+
+  def submit(c):
+    a, b = int(pro[chunks[c][0]]), int(pro[chunks[c][1]])
+    if pool is not None:
+      return pool.apply_async(_split_worker, (a, b))
     ts = time.perf_counter()
-    corpus, ids = split_records(recs[pro[a]:pro[b]], codebert, split)
-    return corpus, ids, time.perf_counter() - ts
+    corpus, ids = split_records(recs[a:b], codebert, split)
+
+    class Done:
+      def get(self):
+        return corpus, ids, time.perf_counter() - ts
+    return Done()
 
   device = torch.device('cuda', local)
   torch.cuda.set_device(device)
   pk = pipeline.Packer(vocab, local)
   sink = os.path.abspath(os.path.expanduser(args.sink))
   out = []
-  t.update(host_split_s=0.0, split_wait_s=0.0, gpu_s=0.0, write_s=0.0, pairs=0)
-  with ThreadPoolExecutor(1) as ex:
-    fut = ex.submit(split_chunk, 0) if chunks else None
+  t.update(host_split_s=0.0, split_wait_s=0.0, gpu_s=0.0, write_s=0.0, pairs=0, split_workers=nw)
+  try:
+    ahead = max(1, nw)
+    futs = {c: submit(c) for c in range(min(ahead, len(chunks)))} if pool is not None else {}
     for c, (a, b) in enumerate(chunks):
       tw = time.perf_counter()
-      corpus, ids, ts = fut.result()
+      corpus, ids, ts = (futs.pop(c) if c in futs else submit(c)).get()
       t['split_wait_s'] += time.perf_counter() - tw
       t['host_split_s'] += ts
-      if c + 1 < len(chunks):
-        fut = ex.submit(split_chunk, c + 1)  # overlaps this chunk's GPU work and parquet writes
+      if pool is not None and c + ahead < len(chunks):
+        futs[c + ahead] = submit(c + ahead)  # overlaps this chunk's GPU work and parquet writes
       t0 = time.perf_counter()
       sh = pipeline.upload(corpus, pro[a:b + 1] - pro[a], device)
       ids_d, ntok = pk.tokenize(sh)
@@ -324,6 +354,10 @@ def main(args, codebert=False):
                                  masking=args.masking and not codebert, doc_ids=ids, part_base=a)
       t['write_s'] += time.perf_counter() - t0
       t['pairs'] += res.n_pairs
+  finally:
+    if pool is not None:
+      pool.terminate()
+      pool.join()
   t['wall_s'] = time.perf_counter() - wall0
   # the part of the host split hidden behind the GPU and the writer
   t['host_split_hidden_s'] = max(0.0, t['host_split_s'] - t['split_wait_s'])

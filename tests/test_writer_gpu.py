@@ -144,19 +144,28 @@ def test_cli_bert_end_to_end(gpu, tmp_path):
   sink = tmp_path / 'out'
   args = preprocess.attach_args().parse_args(
       ['--wikipedia', str(tmp_path / 'wiki'), '--sink', str(sink), '--target-seq-length', '128', '--bin-size', '32',
-       '--num-blocks', '4', '--sentence-splitter', 'rules', '--seed', '5'])
+       '--num-blocks', '4', '--sentence-splitter', 'rules', '--seed', '5', '--split-workers', '0'])
   files, t = preprocess.main(args)
   assert sorted(os.path.basename(f) for f in files) == sorted(
       'part.%d.parquet_%d' % (p, b) for p in range(4) for b in range(4))
-  # several pipeline chunks (host split of chunk k+1 overlapping chunk k) give the same files
-  sink2 = tmp_path / 'out2'
-  args2 = preprocess.attach_args().parse_args(
-      ['--wikipedia', str(tmp_path / 'wiki'), '--sink', str(sink2), '--target-seq-length', '128', '--bin-size', '32',
-       '--num-blocks', '4', '--sentence-splitter', 'rules', '--seed', '5', '--chunk-mb', '0.05'])
-  files2, t2 = preprocess.main(args2)
-  assert t2['chunks'] > 1 and t['chunks'] == 1
+  # several pipeline chunks split ahead by forked worker processes give the
+  # same files: the CLI in a fresh process (its workers fork before the GPU
+  # is touched, as in production), and inline chunks in this one
+  import subprocess
+  import sys
+  sink2, sink3 = tmp_path / 'out2', tmp_path / 'out3'
+  common = ['--wikipedia', str(tmp_path / 'wiki'), '--target-seq-length', '128', '--bin-size', '32',
+            '--num-blocks', '4', '--sentence-splitter', 'rules', '--seed', '5', '--chunk-mb', '0.05']
+  r = subprocess.run([sys.executable, '-m', 'lddl_amd.preprocess', '--sink', str(sink2), '--split-workers', '2'] +
+                     common, cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))), capture_output=True,
+                     text=True, timeout=300)
+  assert r.returncode == 0, r.stderr[-2000:]
+  assert "'split_workers': 2" in r.stdout and "'chunks': 4" in r.stdout, r.stdout
+  files3, t3 = preprocess.main(preprocess.attach_args().parse_args(['--sink', str(sink3), '--split-workers', '0'] +
+                                                                     common))
+  assert t3['chunks'] > 1 and t['chunks'] == 1
   for f in files:
-    assert _read(f) == _read(str(sink2 / os.path.basename(f)))
+    assert _read(f) == _read(str(sink2 / os.path.basename(f))) == _read(str(sink3 / os.path.basename(f)))
   recs = preprocess.sample_shuffle(preprocess.read_records(preprocess.find_files_under(str(src))), 5, 0.9)
   pdo = preprocess.partition_records(recs, num_blocks=4)
   corpus, ids = preprocess.split_records(recs, splitter=preprocess._rule_split)
@@ -192,7 +201,7 @@ def test_cli_codebert_end_to_end(gpu, tmp_path):
   sink = tmp_path / 'out'
   args = preprocess.attach_args(codebert=True).parse_args(
       ['--code', str(tmp_path / 'code'), '--sink', str(sink), '--target-seq-length', '128', '--num-blocks', '2',
-       '--seed', '8', '--sample-ratio', '1.0'])
+       '--seed', '8', '--sample-ratio', '1.0', '--split-workers', '0', '--chunk-mb', '0.1'])
   files, t = preprocess.main(args, codebert=True)
   assert sorted(os.path.basename(f) for f in files) == ['part.0.parquet', 'part.1.parquet']
   recs = preprocess.sample_shuffle(
