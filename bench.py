@@ -118,6 +118,30 @@ def _code_docs(base, ids, ntok, d0, d1):
   return docs, nd
 
 
+def reference_tokenizer_rate(args, base, seconds):
+  """The reference's own tokenizer call (pretrain.py:79-80: HF
+  BertTokenizerFast(vocab).tokenize(s, max_length=512, truncation=True), one
+  Python call per sentence in each single-threaded Dask worker) on one host
+  core, over the first sentences of the same corpus for ~seconds.  The
+  reference runs one such worker per core, so its node rate is about this x
+  the cores.  None when transformers is not importable."""
+  try:
+    import transformers
+  except Exception:
+    return None
+  from lddl_amd.pipeline import VOCAB_BERT, VOCAB_CODEBERT
+  tok = transformers.BertTokenizerFast(VOCAB_CODEBERT if args.corpus == 'code' else VOCAB_BERT)
+  n = k = 0
+  t = time.perf_counter()
+  while k < base.n_sent and (k & 255 or time.perf_counter() - t < seconds):
+    n += min(512, len(tok.tokenize(base.sentence(k), max_length=512, truncation=True)))
+    k += 1
+  el = time.perf_counter() - t
+  return {'tokens_per_s_per_core': n / el, 'unit': 'tokens/s', 'cores': 1, 'kind': 'reference-library',
+          'sample': 'transformers %s BertTokenizerFast.tokenize per sentence (the call at pretrain.py:79-80) on %d '
+                    'sentences, %.1f s, 1 core' % (transformers.__version__, k, el)}
+
+
 def cpu_baseline(args, base, pdo, seconds):
   """oracle/ restatement timed on the host cores on a bounded sample."""
   from oracle.oracle import OracleTokenizer
@@ -166,7 +190,9 @@ def cpu_baseline(args, base, pdo, seconds):
   e2e = None
   if pack_rate:
     e2e = 1.0 / (1.0 / tok_rate + 1.0 / (pack_rate * threads))
+  ref = reference_tokenizer_rate(args, base, min(3.0, seconds * 0.25))
   return {'value': e2e if e2e else tok_rate, 'unit': 'tokens/s', 'cores': threads, 'kind': 'port',
+          'reference_library': ref,
           'sample': ('oracle/tokenizer_oracle.c on %d sentences (%.1f MB, %.1f s, %.3g tok/s at %d threads) + '
                      'oracle/pack_oracle.py on %d partitions (%.1f s, %.3g input tok/s/thread); value = '
                      'tokenize and pack at %d cores in series' % (
