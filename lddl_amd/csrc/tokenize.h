@@ -38,7 +38,8 @@ struct TokParams {
   uint8_t* ovf;
   uint32_t* work_counter;
   uint64_t* dbg;  // optional phase stamps (LDDL_TOK_DEBUG=1), else null
-  int32_t dbg_mode;  // ablation (LDDL_TOK_ABLATE): 1 = skip WordPiece, 2 = filter-only lookups
+  int32_t dbg_mode;  // ablation (LDDL_TOK_ABLATE): 1 = skip WordPiece, 2 = filter-only lookups,
+                     // 3 = WordPiece without bucket loads (tok4)
 };
 
 hipError_t launch_tokenize(const TokParams& P, int grid, hipStream_t stream);

@@ -945,8 +945,15 @@ __global__ __launch_bounds__(64 * WAVES) void tok4_kernel(TokParams P, const int
             const uint32_t m0c = msk(0, c0), m1c = msk(1, c1), m2c = msk(2, c2), m3c = msk(3, c3), m4c = msk(4, c4),
                            m5c = msk(5, c5);
             const uint4* bk = P.vt + 4 * (uint32_t)slot;
-            const uint4 a0 = bk[0], a1 = bk[1], b0 = bk[2], b1 = bk[3];
             const uint32_t want = ((uint32_t)len << 16) | (cont << 24) | 0x80000000u;
+            uint4 a0, a1, b0, b1;
+            if (P.dbg_mode == 3) {  // ablation: the survivor "hits" without its bucket load
+              a0 = make_uint4(m0c, m1c, m2c, m3c);
+              a1 = make_uint4(m4c, m5c, want | 100u, 0u);
+              b0 = b1 = make_uint4(0, 0, 0, 0);
+            } else {
+              a0 = bk[0]; a1 = bk[1]; b0 = bk[2]; b1 = bk[3];
+            }
             bool m0 = (((a1.z & 0xFFFF0000u) ^ want) | (a0.x ^ m0c) | (a0.y ^ m1c) | (a0.z ^ m2c) | (a0.w ^ m3c) |
                        (a1.x ^ m4c) | (a1.y ^ m5c)) == 0u;
             bool m1 = (((b1.z & 0xFFFF0000u) ^ want) | (b0.x ^ m0c) | (b0.y ^ m1c) | (b0.z ^ m2c) | (b0.w ^ m3c) |
