@@ -338,7 +338,7 @@ def main():
     pass
   if args.parquet_parts > 0:
     line['parquet_writer'] = parquet_sample(args, pk, res, sh)
-  if not args.no_cpu_baseline:
+  if not args.no_cpu_baseline and world == 1:  # the host baseline: rank 0 at N=1 only
     line['cpu_baseline'] = cpu_baseline(args, base, pdo, args.cpu_seconds)
   print(json.dumps(line), flush=True)
   if dist is not None:
