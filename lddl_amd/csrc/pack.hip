@@ -565,7 +565,21 @@ __device__ __forceinline__ void mat_copy(MatWave& W, int64_t G0, int64_t G1, con
     }
 #pragma unroll
     for (int u = 0; u < MAT_U; ++u)
-      if (fast[u]) out4[qb + u * 64 + lane] = funnel8(va[u], vb[u], (uint32_t)(sv[u] & 7));
+      if (fast[u]) {
+        const uint4 v = funnel8(va[u], vb[u], (uint32_t)(sv[u] & 7));
+        if constexpr (LEAD) {
+          // the packed rows are written once and read next by the host copy:
+          // streaming stores keep L2 for the dup-fold re-reads of the dense
+          // ids (materialize 28.3 -> 25.0 ms).  Not for compaction, whose
+          // output materialize reads back (10.9 -> 12.4 ms with them).
+          typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+          u32x4 w;
+          w.x = v.x; w.y = v.y; w.z = v.z; w.w = v.w;
+          __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(out4) + (qb + u * 64 + lane));
+        } else {
+          out4[qb + u * 64 + lane] = v;
+        }
+      }
 #pragma unroll
     for (int u = 0; u < MAT_U; ++u) {
       const uint64_t m = __ballot(slow[u]);
