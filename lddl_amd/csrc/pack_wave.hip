@@ -48,7 +48,7 @@ extern __shared__ __attribute__((aligned(16))) uint8_t pw_dyn[];
 // static masking lists (MASK instantiation only)
 struct MaskLds {
   uint16_t cand[MLM_MAX_SEQ];   // explicit candidate positions (pairs with [CLS]/[SEP] tokens)
-  uint16_t jb[MLM_MAX_SEQ];     // shuffle draws: swap x[i] <-> x[jb[i]]
+  alignas(16) uint16_t jb[MLM_MAX_SEQ + 8];  // shuffle draws: swap x[i] <-> x[jb[i]]
   uint16_t mpos[MLM_MAX_SEQ];   // picked positions in pick order
   uint16_t mid[MLM_MAX_SEQ];    // their replacement ids (MLM_KEEP = unchanged)
 };
@@ -170,6 +170,117 @@ struct WaveRng {
   }
   __device__ __forceinline__ int64_t randint(int64_t a, int64_t b) {
     return a + (int64_t)randbelow((uint32_t)(b - a + 1));
+  }
+
+  // random.shuffle's draws over m items (random.py shuffle: for q = m-1..1,
+  // j = _randbelow(q+1)), recorded as jb[q] = j; the same words consumed as
+  // m-1 sequential randbelow calls.  Wave-parallel over the next <= 64 MT
+  // words: a batch covers the draws whose bounds n share one bit length k and
+  // span <= 64 values [n_lo, n_hi], so each word's test r < n (r = word >> (32-k))
+  // is already decided for every draw the batch could give it (r < n_lo:
+  // accepted, r >= n_hi: rejected); only the words with r in [n_lo, n_hi) are
+  // walked in order, one ballot step each.
+  __device__ __noinline__ void shuffle_draws(int m, uint16_t* jb) {
+    int q = m - 1;
+    while (q >= 1) {
+      if (idx >= MT_N) refill();
+      const int n_hi = q + 1;
+      const int k = 32 - __clz((uint32_t)n_hi);
+      const int n_lo = max(n_hi - 63, 1 << (k - 1));
+      const int dmax = n_hi - n_lo + 1;  // draws this batch may complete (<= q)
+      const int lim = min(MT_N - idx, 64);
+      const bool valid = lane < lim;
+      const uint32_t r = valid ? temper(L.mt[idx + lane]) >> (32 - k) : 0xFFFFFFFFu;
+      uint64_t accm = __ballot(valid && r < (uint32_t)n_lo);
+      const uint64_t ambm = __ballot(valid && r >= (uint32_t)n_lo && r < (uint32_t)n_hi);
+      const uint64_t lt = (1ull << lane) - 1ull;
+      int s = 0, pos = 0, end;
+      for (;;) {
+        const uint64_t rest = pos >= 64 ? 0ull : ambm & (~0ull << pos);
+        const int a = rest ? __ffsll((unsigned long long)rest) - 1 : lim;
+        const uint64_t span = (a >= 64 ? ~0ull : (1ull << a) - 1ull) & (pos >= 64 ? 0ull : ~0ull << pos);
+        const int c = __popcll(accm & span);
+        if (s + c >= dmax) {  // the batch's last draw is accepted inside [pos, a)
+          const uint64_t hit = __ballot(((accm & span) >> lane & 1ull) && __popcll(accm & lt) == dmax - 1);
+          end = __ffsll((unsigned long long)hit) - 1;
+          s = dmax;
+          break;
+        }
+        s += c;
+        if (a >= lim) {
+          end = lim - 1;
+          break;
+        }
+        const uint32_t ra = (uint32_t)__builtin_amdgcn_readlane((int)r, a);
+        if (ra < (uint32_t)(n_hi - s)) {
+          accm |= 1ull << a;
+          if (++s == dmax) {
+            end = a;
+            break;
+          }
+        }
+        pos = a + 1;
+      }
+      if (lane <= end && (accm >> lane & 1ull)) jb[q - __popcll(accm & lt)] = (uint16_t)r;
+      idx += end + 1;
+      q -= s;
+    }
+    wsync();
+  }
+
+  // create_masked_lm_predictions' replacement choices for nm picks
+  // (pretrain.py:224-232: random() < 0.8 -> [MASK]; else random() < 0.5 ->
+  // keep; else vocab_words[randint(0, V-1)]), the same words consumed as the
+  // sequential calls.  Every lane decides the pick that would start at its
+  // word (its length 2 / 4 / 4 + randbelow's words and its id) from the next
+  // <= 64 words; the scalar walk then hops from pick to pick.  A pick that
+  // runs past the window starts the next window; one that cannot fit before
+  // the state's end is drawn sequentially.
+  __device__ __noinline__ void mlm_choices(int nm, uint32_t V, uint32_t mask_id, uint32_t keep_id, uint16_t* mid) {
+    const int kV = 32 - __clz(V);
+    int pk = 0;
+    while (pk < nm) {
+      if (idx >= MT_N) refill();
+      const int lim = min(MT_N - idx, 64);
+      const uint32_t w = lane < lim ? temper(L.mt[idx + lane]) : 0u;
+      const uint32_t w1 = (uint32_t)__shfl((int)w, min(lane + 1, 63)), w2 = (uint32_t)__shfl((int)w, min(lane + 2, 63));
+      const uint64_t accV = __ballot(lane < lim && (w >> (32 - kV)) < V);
+      const double x = ((double)(w >> 5) * 67108864.0 + (double)(w1 >> 6)) * (1.0 / 9007199254740992.0);
+      const uint64_t rest = lane + 4 < 64 ? accV & (~0ull << (lane + 4)) : 0ull;
+      const int p = rest ? __ffsll((unsigned long long)rest) - 1 : 64;
+      const uint32_t rv = (uint32_t)__shfl((int)(w >> (32 - kV)), p < 64 ? p : 63);
+      bool res = false;
+      int len = 0;
+      uint32_t nid = 0;
+      if (lane + 1 < lim && x < 0.8) {
+        res = true; len = 2; nid = mask_id;
+      } else if (lane + 3 < lim && (w2 >> 31) == 0u) {
+        res = true; len = 4; nid = keep_id;
+      } else if (lane + 3 < lim && p < lim) {
+        res = true; len = p - lane + 1; nid = rv;
+      }
+      const uint64_t resm = __ballot(res);
+      uint64_t chosen = 0;
+      int pos = 0;
+      const int pk0 = pk;
+      while (pk < nm && pos < lim && (resm >> pos & 1ull)) {
+        chosen |= 1ull << pos;
+        ++pk;
+        pos += __builtin_amdgcn_readlane(len, pos);
+      }
+      if (chosen >> lane & 1ull) mid[pk0 + __popcll(chosen & ((1ull << lane) - 1ull))] = (uint16_t)nid;
+      if (pos == 0) {  // the pick does not fit before the state's end: sequential
+        uint32_t v;
+        if (random() < 0.8) v = mask_id;
+        else if (random() < 0.5) v = keep_id;
+        else v = randbelow(V);
+        if (lane == 0) mid[pk] = (uint16_t)v;
+        ++pk;
+      } else {
+        idx += pos;
+      }
+    }
+    wsync();
   }
 };
 
@@ -474,32 +585,39 @@ __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
           }
           // random.shuffle(cand_indexes): record the swaps, then undo them
           // per picked slot (lane per pick) instead of permuting the list
-          for (int q = m - 1; q >= 1; --q) {
-            const uint32_t j = rng.randbelow((uint32_t)(q + 1));
-            if (lane == 0) ML.jb[q] = (uint16_t)j;
-          }
-          wsync();
+          rng.shuffle_draws(m, ML.jb);
           const int nm = min(ntp, m);
-          for (int pb0 = 0; pb0 < nm; pb0 += 64) {
-            const int pk = pb0 + lane;
-            if (pk < nm) {
-              int q = pk;
-              for (int i2 = 1; i2 < m; ++i2) {
-                const int j = ML.jb[i2];
-                q = q == i2 ? j : (q == j ? i2 : q);
+          // pick pk's candidate = the slot that the swaps (q, jb[q]), applied
+          // for q = m-1 .. 1, move to pk: traced back over q = 1 .. m-1.
+          // Picks pk, pk + 64 per lane; 8 swaps per 16-B LDS read (measured
+          // against u16 reads / readlane swaps: 2.87 vs 3.82 / 3.23 s per step)
+          auto pick_pos = [&](int q) { return (uint16_t)(expl ? (int)ML.cand[q] : (q < la2 ? 1 + q : 2 + q)); };
+          {
+            // identity swaps pad the list: jb[0] = 0, jb[q] = q for q in [m, m8)
+            const int m8 = (m + 7) & ~7;
+            if (lane == 0) ML.jb[0] = 0;
+            if (m + lane < m8) ML.jb[m + lane] = (uint16_t)(m + lane);
+            wsync();
+            const uint4* jb4 = reinterpret_cast<const uint4*>(ML.jb);
+            for (int pb0 = 0; pb0 < nm; pb0 += 128) {
+              const int pk = pb0 + lane, pk2 = pk + 64;
+              int qa = pk, qb = pk2;
+              for (int c = 0; c < m8; c += 8) {
+                const uint4 w = jb4[c >> 3];
+                const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+                for (int t = 0; t < 8; ++t) {
+                  const int i2 = c + t, j = (int)((ww[t >> 1] >> (16 * (t & 1))) & 0xFFFFu);
+                  qa = qa == i2 ? j : (qa == j ? i2 : qa);
+                  qb = qb == i2 ? j : (qb == j ? i2 : qb);
+                }
               }
-              ML.mpos[pk] = (uint16_t)(expl ? (int)ML.cand[q] : (q < la2 ? 1 + q : 2 + q));
+              if (pk < nm) ML.mpos[pk] = pick_pos(qa);
+              if (pk2 < nm) ML.mpos[pk2] = pick_pos(qb);
             }
           }
           // 80% [MASK], 10% keep, 10% random word, in pick order
-          for (int pk = 0; pk < nm; ++pk) {
-            uint32_t nid;
-            if (rng.random() < 0.8) nid = P.mask_id;
-            else if (rng.random() < 0.5) nid = MLM_KEEP;
-            else nid = rng.randbelow(P.n_vocab);
-            if (lane == 0) ML.mid[pk] = (uint16_t)nid;
-          }
-          wsync();
+          rng.mlm_choices(nm, P.n_vocab, P.mask_id, MLM_KEEP, ML.mid);
           if (mcur + nm > mend) {
             unsigned long long b0 = 0;
             if (lane == 0) b0 = atomicAdd(P.mcounter, (unsigned long long)MLM_CHUNK);
