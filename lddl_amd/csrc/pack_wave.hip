@@ -45,12 +45,15 @@ struct PackDyn {                // views into the dynamic LDS region
 };
 extern __shared__ __attribute__((aligned(16))) uint8_t pw_dyn[];
 
-// static masking lists (MASK instantiation only)
+// static masking lists (MASK instantiations only), sized for target_seq_length
+// <= 512 (MASK = 1) or <= MLM_MAX_SEQ (MASK = 2): the half-size lists leave
+// LDS for more resident waves
+template <int CAP>
 struct MaskLds {
-  uint16_t cand[MLM_MAX_SEQ];   // explicit candidate positions (pairs with [CLS]/[SEP] tokens)
-  alignas(16) uint16_t jb[MLM_MAX_SEQ + 8];  // shuffle draws: swap x[i] <-> x[jb[i]]
-  uint16_t mpos[MLM_MAX_SEQ];   // picked positions in pick order
-  uint16_t mid[MLM_MAX_SEQ];    // their replacement ids (MLM_KEEP = unchanged)
+  uint16_t cand[CAP];   // explicit candidate positions (pairs with [CLS]/[SEP] tokens)
+  alignas(16) uint16_t jb[CAP + 8];  // shuffle draws: swap x[i] <-> x[jb[i]]
+  uint16_t mpos[CAP];           // picked positions in pick order
+  uint16_t mid[CAP];            // their replacement ids (MLM_KEEP = unchanged)
 };
 struct NoMaskLds {};
 
@@ -329,10 +332,10 @@ __device__ __forceinline__ int range_sum_reg(int dl, int k0, int k1, int lane) {
 
 // LDSOK = false: every LDS capacity is 0 (the default), the arrays are in
 // global memory and the LDS/global branches compile away
-template <bool MASK, bool LDSOK>
+template <int MASK, bool LDSOK>
 __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
   __shared__ PackWaveLds L;
-  __shared__ typename std::conditional<MASK, MaskLds, NoMaskLds>::type ML;
+  __shared__ typename std::conditional<MASK != 0, MaskLds<MASK == 1 ? 512 : MLM_MAX_SEQ>, NoMaskLds>::type ML;
   PackDyn D;
   D.lens = reinterpret_cast<uint16_t*>(pw_dyn);
   D.dfirst = D.lens + P.cap_lens;
@@ -733,12 +736,15 @@ hipError_t launch_pack_bert_wave(const PackParams& P, hipStream_t s) {
   const size_t dyn = pack_dyn_bytes(P.cap_lens, P.cap_docs, P.cap_pairs, P.masking != 0);
   const bool lds = P.cap_lens > 0 || P.cap_docs > 0 || P.cap_pairs > 0;
   const dim3 g((unsigned)P.n_part), b(64);
-  if (P.masking) {
-    if (lds) hipLaunchKernelGGL((pack_bert_wave_kernel<true, true>), g, b, dyn, s, P);
-    else hipLaunchKernelGGL((pack_bert_wave_kernel<true, false>), g, b, dyn, s, P);
+  if (P.masking && P.max_seq <= 512) {
+    if (lds) hipLaunchKernelGGL((pack_bert_wave_kernel<1, true>), g, b, dyn, s, P);
+    else hipLaunchKernelGGL((pack_bert_wave_kernel<1, false>), g, b, dyn, s, P);
+  } else if (P.masking) {
+    if (lds) hipLaunchKernelGGL((pack_bert_wave_kernel<2, true>), g, b, dyn, s, P);
+    else hipLaunchKernelGGL((pack_bert_wave_kernel<2, false>), g, b, dyn, s, P);
   } else {
-    if (lds) hipLaunchKernelGGL((pack_bert_wave_kernel<false, true>), g, b, dyn, s, P);
-    else hipLaunchKernelGGL((pack_bert_wave_kernel<false, false>), g, b, dyn, s, P);
+    if (lds) hipLaunchKernelGGL((pack_bert_wave_kernel<0, true>), g, b, dyn, s, P);
+    else hipLaunchKernelGGL((pack_bert_wave_kernel<0, false>), g, b, dyn, s, P);
   }
   return hipGetLastError();
 }
