@@ -605,14 +605,27 @@ __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
             for (int pb0 = 0; pb0 < nm; pb0 += 128) {
               const int pk = pb0 + lane, pk2 = pk + 64;
               int qa = pk, qb = pk2;
-              for (int c = 0; c < m8; c += 8) {
-                const uint4 w = jb4[c >> 3];
-                const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
+              // swaps q < pb0 leave picks >= pb0 in place (j_q <= q)
+              if (nm - pb0 <= 64) {  // one pick per lane (seq 128: always)
+                for (int c = pb0; c < m8; c += 8) {
+                  const uint4 w = jb4[c >> 3];
+                  const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
-                for (int t = 0; t < 8; ++t) {
-                  const int i2 = c + t, j = (int)((ww[t >> 1] >> (16 * (t & 1))) & 0xFFFFu);
-                  qa = qa == i2 ? j : (qa == j ? i2 : qa);
-                  qb = qb == i2 ? j : (qb == j ? i2 : qb);
+                  for (int t = 0; t < 8; ++t) {
+                    const int i2 = c + t, j = (int)((ww[t >> 1] >> (16 * (t & 1))) & 0xFFFFu);
+                    qa = qa == i2 ? j : (qa == j ? i2 : qa);
+                  }
+                }
+              } else {
+                for (int c = pb0; c < m8; c += 8) {
+                  const uint4 w = jb4[c >> 3];
+                  const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+                  for (int t = 0; t < 8; ++t) {
+                    const int i2 = c + t, j = (int)((ww[t >> 1] >> (16 * (t & 1))) & 0xFFFFu);
+                    qa = qa == i2 ? j : (qa == j ? i2 : qa);
+                    qb = qb == i2 ? j : (qb == j ? i2 : qb);
+                  }
                 }
               }
               if (pk < nm) ML.mpos[pk] = pick_pos(qa);
