@@ -628,20 +628,21 @@ static int pack_common(lddl_ctx* c, int codebert, const int32_t* d_ntok, const i
     const char* pdbg = getenv("LDDL_PACK_DEBUG");
     P.dbg = nullptr;
     if (pdbg && pdbg[0] == '1') {
-      if (!d_pdbg) HIP_TRY(hipMalloc((void**)&d_pdbg, 8 * 8));
-      HIP_TRY(hipMemsetAsync(d_pdbg, 0, 8 * 8, st));
+      if (!d_pdbg) HIP_TRY(hipMalloc((void**)&d_pdbg, 16 * 8));
+      HIP_TRY(hipMemsetAsync(d_pdbg, 0, 16 * 8, st));
       P.dbg = d_pdbg;
     }
     const bool lane_cb = palgo && palgo[0] == '1';  // LDDL_PACK_ALGO=1: the lane-serial packers
     HIP_TRY(codebert ? (lane_cb ? launch_pack_codebert(P, st) : launch_pack_codebert_wave(P, st))
                      : lane_packer ? launch_pack_bert(P, st) : launch_pack_bert_wave(P, st));
     if (P.dbg && !codebert && !lane_packer) {
-      uint64_t h[8];
+      uint64_t h[13];
       HIP_TRY(hipMemcpyAsync(h, P.dbg, sizeof h, hipMemcpyDeviceToHost, st));
       HIP_TRY(hipStreamSynchronize(st));
-      const char* nm[8] = {"filter", "ldsfill", "seed", "generate", "shuffle", "bin", "pairs", "parts"};
+      const char* nm[13] = {"filter", "ldsfill", "seed", "generate", "shuffle", "bin", "pairs", "parts",
+                            "m_cand", "m_draws", "m_trace", "m_choices", "m_write"};
       fprintf(stderr, "[lddl pack dbg]");
-      for (int k = 0; k < 8; ++k) fprintf(stderr, " %s=%llu", nm[k], (unsigned long long)h[k]);
+      for (int k = 0; k < (P.masking ? 13 : 8); ++k) fprintf(stderr, " %s=%llu", nm[k], (unsigned long long)h[k]);
       fprintf(stderr, "\n");
     }
     HIP_TRY(launch_scan_parts(P.part_npairs, P.part_ntok, n_part, pair_base, tok_base, P.part_err, err_any, st));

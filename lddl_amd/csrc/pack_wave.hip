@@ -194,37 +194,35 @@ struct WaveRng {
       const int lim = min(MT_N - idx, 64);
       const bool valid = lane < lim;
       const uint32_t r = valid ? temper(L.mt[idx + lane]) >> (32 - k) : 0xFFFFFFFFu;
-      uint64_t accm = __ballot(valid && r < (uint32_t)n_lo);
-      const uint64_t ambm = __ballot(valid && r >= (uint32_t)n_lo && r < (uint32_t)n_hi);
+      const uint64_t defm = __ballot(valid && r < (uint32_t)n_lo);
+      uint64_t ambm = __ballot(valid && r >= (uint32_t)n_lo && r < (uint32_t)n_hi);
       const uint64_t lt = (1ull << lane) - 1ull;
-      int s = 0, pos = 0, end;
-      for (;;) {
-        const uint64_t rest = pos >= 64 ? 0ull : ambm & (~0ull << pos);
-        const int a = rest ? __ffsll((unsigned long long)rest) - 1 : lim;
-        const uint64_t span = (a >= 64 ? ~0ull : (1ull << a) - 1ull) & (pos >= 64 ? 0ull : ~0ull << pos);
-        const int c = __popcll(accm & span);
-        if (s + c >= dmax) {  // the batch's last draw is accepted inside [pos, a)
-          const uint64_t hit = __ballot(((accm & span) >> lane & 1ull) && __popcll(accm & lt) == dmax - 1);
-          end = __ffsll((unsigned long long)hit) - 1;
-          s = dmax;
-          break;
-        }
-        s += c;
-        if (a >= lim) {
-          end = lim - 1;
-          break;
-        }
-        const uint32_t ra = (uint32_t)__builtin_amdgcn_readlane((int)r, a);
-        if (ra < (uint32_t)(n_hi - s)) {
+      // ambiguous word a (in order) is accepted iff the draws before it,
+      // D_a definite + A earlier accepted ambiguous, leave its bound above r:
+      // A < n_hi - r - D_a =: u_a.  Lanes past the batch's last draw are
+      // resolved too and cut below (their outcome never feeds back).
+      const int u = n_hi - (int)r - __popcll(defm & lt);
+      uint64_t accm = defm;
+      int A = 0;
+      while (ambm) {
+        const int a = __ffsll((unsigned long long)ambm) - 1;
+        ambm &= ambm - 1;
+        if (A < __builtin_amdgcn_readlane(u, a)) {
+          ++A;
           accm |= 1ull << a;
-          if (++s == dmax) {
-            end = a;
-            break;
-          }
         }
-        pos = a + 1;
       }
-      if (lane <= end && (accm >> lane & 1ull)) jb[q - __popcll(accm & lt)] = (uint16_t)r;
+      const int pre = __popcll(accm & lt);
+      const uint64_t hit = __ballot((accm >> lane & 1ull) && pre == dmax - 1);
+      int end, s;
+      if (hit) {
+        end = __ffsll((unsigned long long)hit) - 1;
+        s = dmax;
+      } else {
+        end = lim - 1;
+        s = __popcll(accm);
+      }
+      if (lane <= end && (accm >> lane & 1ull)) jb[q - pre] = (uint16_t)r;
       idx += end + 1;
       q -= s;
     }
@@ -352,8 +350,9 @@ __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
   const int64_t base = P.sent_off[0];
   const int nsent = (int)(s1 - s0), ndoc = (int)(d1 - d0);
   // optional phase stamps (wave-uniform branch): filter, LDS fill, seed,
-  // pair generation, shuffle, binning
-  uint64_t ph[6] = {0, 0, 0, 0, 0, 0}, tprev = P.dbg ? __builtin_amdgcn_s_memtime() : 0;
+  // pair generation, shuffle, binning; masking: candidates, shuffle draws,
+  // pick trace, 80/10/10 choices, sorted writes
+  uint64_t ph[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, tprev = P.dbg ? __builtin_amdgcn_s_memtime() : 0;
 #define PW_STAMP(k)                                     \
   if (P.dbg) {                                          \
     const uint64_t t_ = __builtin_amdgcn_s_memtime();   \
@@ -556,6 +555,7 @@ __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
         int64_t mref = 0;
         if constexpr (MASK) {
           // ---- create_masked_lm_predictions (pretrain.py:182-238) ----------
+          PW_STAMP(3)
           const int la2 = ahi - alo, lb2 = bhi - blo;
           const int ntp = max(1, (int)rint((double)(la2 + lb2 + 3) * P.mlm_ratio));
           const int fa = first + cs, fb = (int)(r.fs1 - s0);
@@ -588,7 +588,9 @@ __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
           }
           // random.shuffle(cand_indexes): record the swaps, then undo them
           // per picked slot (lane per pick) instead of permuting the list
+          PW_STAMP(6)
           rng.shuffle_draws(m, ML.jb);
+          PW_STAMP(7)
           const int nm = min(ntp, m);
           // pick pk's candidate = the slot that the swaps (q, jb[q]), applied
           // for q = m-1 .. 1, move to pk: traced back over q = 1 .. m-1.
@@ -633,7 +635,9 @@ __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
             }
           }
           // 80% [MASK], 10% keep, 10% random word, in pick order
+          PW_STAMP(8)
           rng.mlm_choices(nm, P.n_vocab, P.mask_id, MLM_KEEP, ML.mid);
+          PW_STAMP(9)
           if (mcur + nm > mend) {
             unsigned long long b0 = 0;
             if (lane == 0) b0 = atomicAdd(P.mcounter, (unsigned long long)MLM_CHUNK);
@@ -653,6 +657,7 @@ __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
           mref = mcur | ((int64_t)nm << 48);
           mcur += nm;
           wsync();
+          PW_STAMP(10)
         }
         if (lane == 0) {
           out[np] = r;
@@ -741,6 +746,7 @@ __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
     for (int k = 0; k < 6; ++k) atomicAdd((unsigned long long*)&P.dbg[k], (unsigned long long)ph[k]);
     atomicAdd((unsigned long long*)&P.dbg[6], (unsigned long long)np);
     atomicAdd((unsigned long long*)&P.dbg[7], 1ull);
+    for (int k = 6; k < 11; ++k) atomicAdd((unsigned long long*)&P.dbg[k + 2], (unsigned long long)ph[k]);
   }
 #undef PW_STAMP
 }
