@@ -344,7 +344,9 @@ extern "C" int lddl_create(const char* vocab_path, const char* table_path, int d
   c->n_cu = prop.multiProcessorCount;
   if ((rc = load_table(c, table_path)) || (rc = load_vocab(c, vocab_path))) { free_ctx(c); return rc; }
   const char* algo = getenv("LDDL_TOKENIZE_ALGO");
-  c->tok_algo = (algo && algo[0] >= '1' && algo[0] <= '4') ? algo[0] - '0' : 4;
+  c->tok_algo = (algo && algo[0] >= '1' && algo[0] <= '5') ? algo[0] - '0' : 5;
+  // v5 entries keep ids below SPLIT_EDEF; both need tok4's ASCII class table
+  if (c->tok_algo == 5 && (!c->tok4_ok || c->vocab_size > (int)SPLIT_EDEF)) c->tok_algo = 4;
   if (c->tok_algo == 4 && !c->tok4_ok) c->tok_algo = 3;
   const char* cfg = getenv("LDDL_TOK4_CFG");  // waves per workgroup / Bloom (tokenize.h)
   c->tok4_cfg = cfg ? atoi(cfg) : 4;
@@ -438,7 +440,31 @@ extern "C" int lddl_tokenize(lddl_ctx* c, const uint8_t* d_bytes, int64_t nbytes
     P.dbg = d_dbg;
   }
   const int64_t chunks = (n_sent + P.chunk - 1) / P.chunk;
-  if (c->tok_algo == 4) {
+  if (c->tok_algo == 5) {
+    const int64_t nt = tile_count(nbytes);
+    // LDDL_SPLIT_SEG (tiles per segment) / LDDL_SPLIT_CHUNKS (record chunks):
+    // tests force segment seams and record-capacity fallbacks at small sizes
+    const char* eseg = getenv("LDDL_SPLIT_SEG");
+    const char* ech = getenv("LDDL_SPLIT_CHUNKS");
+    const int64_t seg_max = eseg && atoll(eseg) > 0 ? atoll(eseg) : SPLIT_SEG_TILES;
+    const int64_t seg = nt < seg_max ? nt : seg_max;
+    int64_t n_chunks = split_seg_slots(seg) / SPLIT_CHUNK;
+    if (ech && atoll(ech) > 0) n_chunks = atoll(ech);
+    const int64_t slots = n_chunks * SPLIT_CHUNK;
+    int64_t* tile_sent;
+    SplitParams S{};
+    int rc;
+    if ((rc = ws_get(c, 19, nt + 1, &tile_sent)) || (rc = ws_get(c, 20, nt, &S.fb_list)) ||
+        (rc = ws_get(c, 21, 16, &S.fb_count)) || (rc = ws_get(c, 34, (size_t)seg * 1024 + 4096, &S.ent)) ||
+        (rc = ws_get(c, 35, (size_t)slots * 4, &S.rec)) || (rc = ws_get(c, 36, (size_t)n_chunks + 16, &S.chunk_fill)) ||
+        (rc = ws_get(c, 37, n_sent, &S.nent)) || (rc = ws_get(c, 38, n_sent, &S.nslot)) ||
+        (rc = ws_get(c, 39, n_sent, &S.qb)))
+      return rc;
+    S.chunk_ctr = S.chunk_fill + n_chunks;
+    S.n_chunks = (uint32_t)n_chunks;
+    S.seg_tiles = seg;
+    HIP_TRY(launch_tokenize_split(P, nbytes, tile_sent, S, c->n_cu, c->tok_grid, st));
+  } else if (c->tok_algo == 4) {
     const int64_t nt = tile_count(nbytes);
     int64_t* tile_sent;
     int32_t *fb_list, *fb_count;

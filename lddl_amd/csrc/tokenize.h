@@ -59,4 +59,40 @@ hipError_t launch_tokenize_fallback(const TokParams& P, const int64_t* tile_sent
 hipError_t launch_tokenize_stream(const TokParams& P, int64_t nbytes, int64_t* tile_sent, int32_t* fb_list,
                                   int32_t* fb_count, int fb_grid, int n_cu, int cfg, hipStream_t s);
 
+// v5 (tokenize_split.hip): the tile scan resolves whole-word vocab hits and
+// hands every other word to a WordPiece record queue; a full-occupancy
+// WordPiece kernel runs the records, a count pass and an expand pass write
+// the ids.  Scratch per segment of tiles (SPLIT_SEG_TILES):
+//   ent    u16 per byte of the segment: sentence s's entries at
+//          sent_off[s] - sent_off[0] - t0 * 1 KiB + k: a vocab id, or
+//          SPLIT_EDEF | (record slot - qb[s]) for a word of the queue
+//   rec    64-B record slots in chunks of SPLIT_CHUNK, chunk_fill[c] used
+//   nent / nslot / qb per sentence; out_ntok holds the resolved count until
+//   the count pass adds the records' piece counts
+constexpr int64_t SPLIT_SEG_TILES = int64_t(1) << 20;  // 1 GiB of input per segment
+constexpr uint32_t SPLIT_CHUNK = 1024;                 // record slots per allocation chunk (64 KiB)
+constexpr uint32_t SPLIT_EDEF = 0xF000u;               // entry >= EDEF: a queued word
+constexpr uint16_t SPLIT_NENT_FB = 0xFFFFu;            // nent of a sentence of a fallback tile
+
+struct SplitParams {
+  int64_t seg_tiles;       // tiles per segment (SPLIT_SEG_TILES; tests force small ones)
+  int64_t t0, t1;          // the segment's tiles
+  const int64_t* tile_sent;
+  uint16_t* ent;
+  uint4* rec;              // 4 uint4 per slot
+  uint32_t* chunk_fill;
+  uint32_t* chunk_ctr;     // [0] chunks handed out
+  uint32_t n_chunks;
+  uint16_t* nent;
+  uint16_t* nslot;
+  uint32_t* qb;
+  int32_t* fb_list;
+  int32_t* fb_count;
+  uint16_t* dense;         // expand: dense output (null: sparse, the lddl_tokenize layout)
+  const int64_t* tokoff;   // expand: dense offsets
+};
+hipError_t launch_tokenize_split(const TokParams& P, int64_t nbytes, int64_t* tile_sent, SplitParams S, int n_cu,
+                                 int fb_grid, hipStream_t s);
+int64_t split_seg_slots(int64_t seg_tiles);
+
 }  // namespace lddl

@@ -1,0 +1,1197 @@
+// Tokenizer v5 (default): the per-tile scan and WordPiece are split into
+// separate kernels so that WordPiece runs at full lane occupancy.
+//
+// Same contract and results as tokenize_stream.hip (reference: HF
+// tokenizers' BertNormalizer / BertPreTokenizer / WordPiece behind
+// tokenizer.tokenize(s, max_length=512, truncation=True),
+// lddl/dask/bert/pretrain.py:79-80; restated in oracle/tokenizer_oracle.c).
+//
+// Why: in the one-kernel tile tokenizer (tok4) the WordPiece loop took ~60 %
+// of the wave time at ~17 % lane occupancy -- a 1 KiB tile has ~20 words
+// that are not whole-word vocab hits, each needing a serial chain of Bloom
+// scans and dependent bucket loads, so the wave idled behind the longest
+// chain with most lanes masked off.
+//
+//  scan_kernel     wave per 1 KiB tile (sentences starting in it), persistent:
+//                  bytes -> normalised bytes + break masks (tok4 phases 1-2),
+//                  units, dirty words normalised, specials, > 100-char words,
+//                  one whole-word bucket probe per unit.  Every unit that
+//                  yields tokens becomes an ENTRY of its sentence: a vocab id,
+//                  or (a word the probe did not resolve) a reference to a
+//                  64-B RECORD {len, count, key bytes} in a chunked queue.
+//                  Per sentence: #entries (capped at max_tok: each entry is
+//                  >= 1 token), #record slots, first slot, resolved count.
+//  wp_kernel       the records, one per lane with refill: greedy
+//                  longest-match-first (Bloom scan + 64-B bucket probe per
+//                  candidate, as tok4's loop), pieces and count written back
+//                  into the record.
+//  count_kernel    per sentence: ntok = min(resolved + sum of its records'
+//                  counts, max_tok).
+//  expand_kernel   per group of sentences: entries -> ids (a record's pieces
+//                  in place of its entry), sparse (the lddl_tokenize layout)
+//                  or dense at tokoff.
+// Tiles the scan does not model (window > 2 KiB, > 64 sentences, > 256
+// units... as tok4, a queued word longer than 56 bytes, record capacity) are
+// listed and re-run by tokenize_fallback_kernel (exact serial path).
+#include "common.h"
+#include "tokenize.h"
+#include "wave.h"
+#include "tokenize_serial.h"
+
+namespace lddl {
+namespace tok5 {
+
+constexpr int CAP = 2048;                // window bytes (32 per lane)
+constexpr int DCAP = 256;                // side buffer for dirty words
+constexpr int NBUF = CAP + DCAP + 64;    // + over-read pad of the key loads
+constexpr int UCAP = 256;                // units per round
+constexpr int NSCAP = 64;                // sentences per tile
+constexpr int XCAP = 32;                 // expansion markers per tile
+constexpr int KEYMAX = 56;               // key bytes a record holds
+constexpr int KEY1 = 28;                 // keys up to 28 bytes take one slot (<= 28 pieces)
+constexpr uint32_t BF = 0xFFu, BX = 0xFDu, BS = 0xF8u;  // filler, expansion, special k = BS+k
+enum : uint32_t { C_W = 1, C_I = 2, C_S = 4, C_D = 8, C_UP = 16, C_X = 32, C_CS = 64 };
+constexpr uint16_t U_EMPTY = 0xFFFEu, U_DEFER = 0xFFFFu;
+
+// work entry of a pending unit: unit | window position << 8 | byte length << 20
+__device__ __forceinline__ uint32_t wmake(int u, int src, int len) {
+  return (uint32_t)u | ((uint32_t)src << 8) | ((uint32_t)len << 20);
+}
+__device__ __forceinline__ int wsrc(uint32_t w) { return (int)((w >> 8) & 0xFFFu); }
+__device__ __forceinline__ int wlen(uint32_t w) { return (int)(w >> 20); }
+
+struct Lds {
+  union {
+    uint32_t rp[CAP / 4 + 4];  // phase 1: raw bytes
+    struct {
+      uint32_t urec[UCAP];     // window position | sentence << 16
+      uint32_t uwp[UCAP];      // pending unit (wmake), 0 once resolved
+    } u;
+  };
+  uint32_t nb[NBUF / 4];       // normalised bytes in window coordinates; side buffer at [CAP, CAP+DCAP)
+  uint32_t brk[64];            // break bits: unit starts, spaces, sentence starts
+  uint32_t dm[64];             // dirty bits: filler / expansion marker bytes
+  uint32_t sb[64];             // sentence-start bits
+  uint32_t sqb[NSCAP];         // record index of the sentence's first slot
+  uint32_t sdef[NSCAP];        // queued entries below max_tok
+  uint16_t uid[UCAP];          // vocab id, U_EMPTY (no token) or U_DEFER (queued)
+  uint16_t sst[NSCAP + 2];     // sentence starts (window coordinates)
+  uint16_t sent_n[NSCAP];      // entries so far (uncapped)
+  uint16_t sslot[NSCAP];       // record slots so far
+  uint32_t xent[XCAP];         // table entry of each expansion marker
+  uint8_t xlen[XCAP];          // its normalised byte length
+  int32_t misc[4];             // 0 side-buffer cursor, 1 #markers, 2 overflow
+};
+
+__device__ __forceinline__ void wsync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__device__ __forceinline__ uint32_t rawb(const Lds& L, int p) { return reinterpret_cast<const uint8_t*>(L.rp)[p]; }
+__device__ __forceinline__ uint32_t nbyte(const uint32_t* nb, int p) { return reinterpret_cast<const uint8_t*>(nb)[p]; }
+__device__ __forceinline__ void nput(uint32_t* nb, int p, uint32_t v) { reinterpret_cast<uint8_t*>(nb)[p] = (uint8_t)v; }
+
+// bit q of each byte of c -> 4 bits (byte 0 -> bit 0)
+__device__ __forceinline__ uint32_t gather4(uint32_t c, int q) { return (((c >> q) & 0x01010101u) * 0x01020408u) >> 24; }
+
+__device__ __forceinline__ int64_t uni64(int64_t x) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)(uint64_t)x);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)x >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ int lane_rank(uint64_t m) {
+  return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+__device__ __forceinline__ int utf8_put(uint32_t* nb, int p, uint32_t c) {
+  if (c < 0x80) { nput(nb, p, c); return 1; }
+  if (c < 0x800) { nput(nb, p, 0xC0 | (c >> 6)); nput(nb, p + 1, 0x80 | (c & 0x3F)); return 2; }
+  if (c < 0x10000) {
+    nput(nb, p, 0xE0 | (c >> 12)); nput(nb, p + 1, 0x80 | ((c >> 6) & 0x3F)); nput(nb, p + 2, 0x80 | (c & 0x3F));
+    return 3;
+  }
+  nput(nb, p, 0xF0 | (c >> 18)); nput(nb, p + 1, 0x80 | ((c >> 12) & 0x3F));
+  nput(nb, p + 2, 0x80 | ((c >> 6) & 0x3F)); nput(nb, p + 3, 0x80 | (c & 0x3F));
+  return 4;
+}
+
+// first break position > p (a unit's span end), at most nb
+__device__ __forceinline__ int span_end(const Lds& L, int p, int nb) {
+  int w = p >> 5;
+  uint32_t m = L.brk[w] & ~((2u << (p & 31)) - 1u);
+  while (m == 0) {
+    ++w;
+    if ((w << 5) >= nb) return nb;
+    m = L.brk[w];
+  }
+  return min((w << 5) + __ffs(m) - 1, nb);
+}
+
+__device__ __forceinline__ bool span_dirty(const Lds& L, int p, int q) {
+  for (int w = p >> 5; (w << 5) < q; ++w) {
+    const int lo = max(p - (w << 5), 0), hi = min(q - (w << 5), 32);
+    const uint32_t m = (hi >= 32 ? ~0u : ((1u << hi) - 1u)) & ~((1u << lo) - 1u);
+    if (L.dm[w] & m) return true;
+  }
+  return false;
+}
+
+// Compact / expand the dirty span [p, q) into the side buffer.  Returns its
+// normalised length (source in *src), -1 on overflow (flagged in misc[2]).
+__device__ int dirty_normalize(Lds& L, const TokParams& P, int p, int q, int* src) {
+  int len = 0;
+  for (int i = p; i < q;) {
+    const uint32_t b = nbyte(L.nb, i);
+    if (b == BF) {
+      ++i;
+    } else if (b == BX) {
+      len += L.xlen[nbyte(L.nb, i + 1)];
+      i += 2;
+    } else {
+      ++len;
+      ++i;
+    }
+  }
+  if (len == 0) return 0;
+  const int off = atomicAdd(&L.misc[0], len);
+  if (off + len > DCAP) {
+    L.misc[2] = 1;
+    return -1;
+  }
+  int o = CAP + off;
+  *src = o;
+  for (int i = p; i < q;) {
+    const uint32_t b = nbyte(L.nb, i);
+    if (b == BF) {
+      ++i;
+    } else if (b == BX) {
+      const uint32_t e = L.xent[nbyte(L.nb, i + 1)];
+      if (ent_kind(e) == KIND_MULTI) {
+        const uint4 m = P.multi[ent_payload(e)];
+        o += utf8_put(L.nb, o, ent_payload(m.y));
+        o += utf8_put(L.nb, o, ent_payload(m.z));
+        if (m.x > 2) o += utf8_put(L.nb, o, ent_payload(m.w));
+      } else {
+        o += utf8_put(L.nb, o, ent_payload(e));
+      }
+      i += 2;
+    } else {
+      nput(L.nb, o++, b);
+      ++i;
+    }
+  }
+  return len;
+}
+
+__device__ __forceinline__ int count_chars(const uint32_t* nb, int src, int len) {
+  int n = 0;
+  for (int i = 0; i < len; ++i) n += (nbyte(nb, src + i) & 0xC0u) != 0x80u;
+  return n;
+}
+
+// the first min(len, 24) bytes at s as six little-endian dwords, zero beyond
+struct Key6 {
+  uint32_t d0, d1, d2, d3, d4, d5;
+};
+__device__ __forceinline__ uint32_t keep_bytes(uint32_t c, int rem) {
+  return rem >= 4 ? c : rem <= 0 ? 0u : (c & ((1u << (8 * rem)) - 1u));
+}
+__device__ __forceinline__ Key6 load_key(const uint32_t* nb, int s, int len) {
+  const int a = s >> 2;
+  const uint32_t sh = (uint32_t)(s & 3);
+  const uint32_t x0 = nb[a], x1 = nb[a + 1], x2 = nb[a + 2], x3 = nb[a + 3], x4 = nb[a + 4], x5 = nb[a + 5],
+                 x6 = nb[a + 6];
+  const int lc = min(len, 24);
+  Key6 k;
+  k.d0 = keep_bytes(__builtin_amdgcn_alignbyte(x1, x0, sh), lc);
+  k.d1 = keep_bytes(__builtin_amdgcn_alignbyte(x2, x1, sh), lc - 4);
+  k.d2 = keep_bytes(__builtin_amdgcn_alignbyte(x3, x2, sh), lc - 8);
+  k.d3 = keep_bytes(__builtin_amdgcn_alignbyte(x4, x3, sh), lc - 12);
+  k.d4 = keep_bytes(__builtin_amdgcn_alignbyte(x5, x4, sh), lc - 16);
+  k.d5 = keep_bytes(__builtin_amdgcn_alignbyte(x6, x5, sh), lc - 20);
+  return k;
+}
+// == vhash (common.h) of a loaded key
+__device__ __forceinline__ uint32_t key_hash(const Key6& k, int len, uint32_t cont) {
+  const int lc = min(len, 24);
+  uint32_t h = VSEED;
+  if (lc > 0) h = vmix(h, k.d0);
+  if (lc > 4) h = vmix(h, k.d1);
+  if (lc > 8) h = vmix(h, k.d2);
+  if (lc > 12) h = vmix(h, k.d3);
+  if (lc > 16) h = vmix(h, k.d4);
+  if (lc > 20) h = vmix(h, k.d5);
+  return vfinal(h, (uint32_t)len, cont);
+}
+// branch-free (an && chain lets the compiler sink the slot's other loads
+// behind the first compare: a second dependent round trip on every hit)
+__device__ __forceinline__ bool slot_eq(const uint4& a, const uint4& b, const Key6& k, uint32_t want) {
+  return (((b.z & 0xFFFF0000u) ^ want) | (a.x ^ k.d0) | (a.y ^ k.d1) | (a.z ^ k.d2) | (a.w ^ k.d3) | (b.x ^ k.d4) |
+          (b.y ^ k.d5)) == 0u;
+}
+
+template <int WAVES>
+__global__ __launch_bounds__(64 * WAVES) void scan_kernel(TokParams P, SplitParams S) {
+  __shared__ Lds Ls[WAVES];
+  __shared__ uint32_t ctab32[64];
+  // ---- prologue: per-byte class table from the unicode table's ASCII page --
+  if (threadIdx.x < 64) {
+    uint32_t word = 0;
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t b = threadIdx.x * 4 + k;
+      uint32_t c;
+      if (b < 128) {
+        const uint32_t e = P.pages[(uint32_t)P.top[0] * 256u + b];
+        const uint32_t kind = ent_kind(e), cls = ent_cls(e);
+        c = C_CS;
+        if (kind == KIND_DROP_T || kind == KIND_DROP_D) c |= C_W | C_D;
+        else if (cls == CLS_SPACE) c |= C_S;
+        else if (cls == CLS_ISOLATE) c |= C_I;
+        else c |= C_W;
+        if (kind == KIND_MAP && cls == CLS_OTHER) c |= C_UP;  // A-Z -> a-z (checked at lddl_create)
+        if (b == '[') c |= C_X;
+      } else {
+        c = b >= 0xC0 ? (C_X | C_CS) : 0u;
+      }
+      word |= c << (8 * k);
+    }
+    ctab32[threadIdx.x] = word;
+  }
+  __syncthreads();
+  const uint8_t* ctab = reinterpret_cast<const uint8_t*>(ctab32);
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  Lds& L = Ls[wv];
+  const int64_t base = P.sent_off[0];
+  const int64_t ebase = S.t0 << 10;  // entry index = byte offset (from base) - ebase
+  const int64_t nwaves = (int64_t)gridDim.x * WAVES;
+  const int max_tok = P.max_tok;
+  // record chunk of this wave (wave-uniform): slots [cur, cend)
+  uint32_t cur = 0, cend = 0, cbase = 0;
+  int chunk = -1;
+  for (int64_t t = S.t0 + (int64_t)blockIdx.x * WAVES + wv; t < S.t1; t += nwaves) {
+    wsync();
+    const int64_t sa = uni64(S.tile_sent[t]), sb = uni64(S.tile_sent[t + 1]);
+    if (sa >= sb) continue;
+    const int ns = (int)(sb - sa);
+    // the tile goes to the exact serial kernel; its sentences are no-ops for
+    // the count / expand passes
+    auto fallback = [&]() {
+      if (lane == 0) {
+        const int at = atomicAdd(S.fb_count, 1);
+        S.fb_list[at] = (int32_t)t;
+      }
+      for (int j = lane; j < ns; j += 64) {
+        S.nent[sa + j] = SPLIT_NENT_FB;
+        S.nslot[sa + j] = 0;
+      }
+    };
+    const int64_t A = uni64(P.sent_off[sa]), B = uni64(P.sent_off[sb]);
+    const int aoff = (int)(reinterpret_cast<uintptr_t>(P.bytes + A) & 15u);
+    const uint8_t* wbase = P.bytes + (A - aoff);  // 16-B aligned
+    const int64_t nb64 = (B - A) + aoff;
+    if (nb64 > CAP || ns > NSCAP) {
+      fallback();
+      continue;
+    }
+    const int nb = (int)nb64;
+    // ---- sentence starts ----------------------------------------------------
+    L.sb[lane] = 0;
+    if (lane == 0) {
+      L.misc[0] = 0;
+      L.misc[1] = 0;
+      L.misc[2] = 0;
+    }
+    if (lane < ns) {
+      L.sent_n[lane] = 0;
+      L.sslot[lane] = 0;
+      L.sdef[lane] = 0;
+    }
+    wsync();
+    if (lane < ns) {
+      const int pos = (int)(P.sent_off[sa + lane] - A) + aoff;
+      L.sst[lane] = (uint16_t)pos;
+      if (pos < nb) atomicOr(&L.sb[pos >> 5], 1u << (pos & 31));
+    }
+    // ---- 1: raw bytes -> masks + normalised bytes in place ------------------
+    uint32_t W, I, S_, CS, D, X, inwin;
+    {
+      const int p0 = lane * 32;
+      uint4 v0 = make_uint4(0, 0, 0, 0), v1 = v0;
+      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+      const u32x4* gp = reinterpret_cast<const u32x4*>(wbase) + 2 * lane;
+      if (p0 < nb) {  // streamed once: non-temporal, keep L2 for the vocab table
+        const u32x4 a = __builtin_nontemporal_load(gp);
+        v0 = make_uint4(a.x, a.y, a.z, a.w);
+      }
+      if (p0 + 16 < nb) {
+        const u32x4 a = __builtin_nontemporal_load(gp + 1);
+        v1 = make_uint4(a.x, a.y, a.z, a.w);
+      }
+      *reinterpret_cast<uint4*>(&L.rp[lane * 8]) = v0;
+      *reinterpret_cast<uint4*>(&L.rp[lane * 8 + 4]) = v1;
+      const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+      uint32_t Wh = 0, Ih = 0, Sh = 0, CSh = 0, Dh = 0, Xh = 0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint32_t x = w[k];
+        const uint32_t c = (uint32_t)ctab[x & 0xFFu] | ((uint32_t)ctab[(x >> 8) & 0xFFu] << 8) |
+                           ((uint32_t)ctab[(x >> 16) & 0xFFu] << 16) | ((uint32_t)ctab[x >> 24] << 24);
+        L.nb[lane * 8 + k] = (x + ((c & 0x10101010u) << 1)) | (((c >> 3) & 0x01010101u) * 0xFFu);
+        const int sh = 4 * k;
+        Wh |= gather4(c, 0) << sh;
+        Ih |= gather4(c, 1) << sh;
+        Sh |= gather4(c, 2) << sh;
+        Dh |= gather4(c, 3) << sh;
+        Xh |= gather4(c, 5) << sh;
+        CSh |= gather4(c, 6) << sh;
+      }
+      const int wlo = min(max(aoff - p0, 0), 32), whi = min(max(nb - p0, 0), 32);
+      inwin = (whi >= 32 ? ~0u : ((1u << whi) - 1u)) & (wlo >= 32 ? 0u : ~((1u << wlo) - 1u));
+      W = Wh; I = Ih; S_ = Sh; CS = CSh; D = Dh; X = Xh & inwin;
+    }
+    wsync();
+    bool bad = false;
+    uint32_t sp_m = 0, sp_w = 0, sp_d = 0;  // this lane's last char / special running into the next lane
+    {
+      const int p0 = lane * 32;
+      for (uint32_t xm = X; xm;) {
+        const int i = __ffs(xm) - 1;
+        xm &= xm - 1;
+        const int p = p0 + i;
+        const uint32_t b = rawb(L, p);
+        if (b == '[') {
+          int se = nb;  // end of p's sentence
+          for (int j = 1; j < ns; ++j)
+            if (L.sst[j] > p) { se = L.sst[j]; break; }
+          int len = 0, sk = -1;
+          if (p + 5 <= se) {
+            const uint32_t c1 = rawb(L, p + 1), c2 = rawb(L, p + 2), c3 = rawb(L, p + 3), c4 = rawb(L, p + 4);
+            if (c1 == 'P' && c2 == 'A' && c3 == 'D' && c4 == ']') { sk = 0; len = 5; }
+            else if (c1 == 'U' && c2 == 'N' && c3 == 'K' && c4 == ']') { sk = 1; len = 5; }
+            else if (c1 == 'C' && c2 == 'L' && c3 == 'S' && c4 == ']') { sk = 2; len = 5; }
+            else if (c1 == 'S' && c2 == 'E' && c3 == 'P' && c4 == ']') { sk = 3; len = 5; }
+            else if (c1 == 'M' && c2 == 'A' && c3 == 'S' && c4 == 'K' && p + 6 <= se && rawb(L, p + 5) == ']') { sk = 4; len = 6; }
+          }
+          if (sk >= 0) {
+            nput(L.nb, p, BS + (uint32_t)sk);
+            const uint64_t cov = ((1ull << (len - 1)) - 1ull) << (i + 1);
+            const uint32_t cl = (uint32_t)cov;
+            W &= ~cl;
+            I &= ~cl;
+            S_ &= ~cl;
+            CS &= ~cl;
+            D &= ~cl;
+            sp_m |= (uint32_t)(cov >> 32);
+          }
+        } else {
+          const int n = utf8_len(b);
+          uint32_t cp = b & (0x3Fu >> (n - 1));
+          for (int q = 1; q < n; ++q) cp = (cp << 6) | (rawb(L, p + q) & 0x3Fu);
+          if (cp > 0x10FFFF) cp = 0xFFFD;
+          const uint32_t e = table_entry(P, cp);
+          const uint32_t kind = ent_kind(e), cls = ent_cls(e);
+          const uint64_t span = ((1ull << n) - 1ull) << i;
+          bool dirty = false, wordc = false;
+          if (ent_rank(e) != 0) bad = true;
+          if (kind == KIND_DROP_T || kind == KIND_DROP_D) {
+            for (int q = 0; q < n; ++q) nput(L.nb, p + q, BF);
+            dirty = true;
+            wordc = true;
+          } else if (cls == CLS_SPACE) {
+            S_ |= 1u << i;
+          } else {
+            if (cls == CLS_ISOLATE) I |= 1u << i;
+            else wordc = true;
+            if (kind != KIND_IDENT) {
+              uint32_t c0 = ent_payload(e), c1 = 0, c2 = 0;
+              int nc = 1;
+              if (kind == KIND_MULTI) {
+                const uint4 m = P.multi[ent_payload(e)];
+                nc = (int)m.x;
+                c0 = ent_payload(m.y);
+                c1 = ent_payload(m.z);
+                c2 = ent_payload(m.w);
+                if ((ent_rank(m.y) | ent_rank(m.z) | (nc > 2 ? ent_rank(m.w) : 0u)) != 0) bad = true;
+              }
+              const int T = utf8_enc_len(c0) + (nc > 1 ? utf8_enc_len(c1) : 0) + (nc > 2 ? utf8_enc_len(c2) : 0);
+              if (T <= n) {
+                int o = p + utf8_put(L.nb, p, c0);
+                if (nc > 1) o += utf8_put(L.nb, o, c1);
+                if (nc > 2) o += utf8_put(L.nb, o, c2);
+                for (; o < p + n; ++o) nput(L.nb, o, BF);
+                dirty = T < n;
+              } else {
+                const int xi = atomicAdd(&L.misc[1], 1);
+                if (xi >= XCAP) {
+                  bad = true;
+                } else {
+                  L.xent[xi] = e;
+                  L.xlen[xi] = (uint8_t)T;
+                  nput(L.nb, p, BX);
+                  nput(L.nb, p + 1, (uint32_t)xi);
+                  for (int q = 2; q < n; ++q) nput(L.nb, p + q, BF);
+                }
+                dirty = true;
+              }
+            }
+          }
+          const uint32_t slo = (uint32_t)span, shi = (uint32_t)(span >> 32);
+          if (wordc) {
+            W |= slo;
+            sp_w |= shi;
+          }
+          if (dirty) {
+            D |= slo;
+            sp_d |= shi;
+          }
+          sp_m |= shi;
+        }
+      }
+    }
+    {
+      const uint32_t im = wave_shr1(sp_m), iw = wave_shr1(sp_w), id = wave_shr1(sp_d);  // lane 0: 0
+      W = ((W & ~im) | iw) & inwin;
+      I &= ~im & inwin;
+      S_ &= ~im & inwin;
+      CS &= ~im & inwin;
+      D = ((D & ~im) | id) & inwin;
+    }
+    const bool wbad = __any(bad);
+    wsync();
+    // ---- 2: units -----------------------------------------------------------
+    uint32_t U, SBm;
+    int ub, sbb, n, nstarts;
+    {
+      SBm = L.sb[lane];
+      const uint32_t carry = wave_shr1(W) >> 31;
+      const uint32_t pw = (W << 1) | (lane ? carry : 0u);
+      U = CS & (I | (W & (~pw | SBm)));
+      L.brk[lane] = U | (S_ & CS) | SBm;
+      L.dm[lane] = D;
+      const uint32_t v = (uint32_t)__popc(U) | ((uint32_t)__popc(SBm) << 16);
+      const uint32_t x = wave_incl_add(v);
+      const uint32_t tot = lane_get(x, 63);
+      const uint32_t ex = x - v;
+      ub = (int)(ex & 0xFFFFu);
+      sbb = (int)(ex >> 16);
+      n = (int)(tot & 0xFFFFu);
+      nstarts = (int)(tot >> 16);
+    }
+    // every sentence start distinct (no empty sentence shares one): a unit's
+    // sentence is the number of starts at or before it, minus one
+    const bool starts_distinct = nstarts == ns;
+    if (wbad) {
+      fallback();
+      continue;
+    }
+    const int64_t ent0 = (A - base) - aoff - ebase;  // entry index of window position 0
+    int prev_sent = -1;
+    bool ovf = false;
+    for (int rb = 0; rb < n; rb += UCAP) {
+      const int nr = min(UCAP, n - rb);
+      if (lane == 0) L.misc[0] = 0;
+      {
+        const int p0 = lane * 32;
+        int u = ub;
+        for (uint32_t m = U; m; m &= m - 1, ++u) {
+          if (u < rb || u >= rb + nr) continue;
+          const int b = __ffs(m) - 1, p = p0 + b;
+          int lo;
+          if (starts_distinct) {
+            lo = sbb + __popc(SBm & ((2u << b) - 1u)) - 1;
+          } else {
+            lo = 0;  // last sentence starting at or before p
+            int hi = ns - 1;
+            while (lo < hi) {
+              const int mid = (lo + hi + 1) >> 1;
+              if ((int)L.sst[mid] <= p) lo = mid;
+              else hi = mid - 1;
+            }
+          }
+          L.u.urec[u - rb] = (uint32_t)p | ((uint32_t)lo << 16);
+        }
+      }
+      wsync();
+      // ---- 3: prep (spans, dirty words, specials, long words) ---------------
+      for (int r = 0; r < nr; r += 64) {
+        const int u = r + lane;
+        if (u < nr) {
+          const int p = (int)(L.u.urec[u] & 0xFFFFu);
+          const uint32_t b0 = nbyte(L.nb, p);
+          uint32_t w = 0;
+          uint16_t id;
+          if (b0 >= BS && b0 < BS + 5) {
+            id = (uint16_t)P.special[b0 - BS];
+          } else {
+            const int q = span_end(L, p, nb);
+            int src = p, len = q - p;
+            if (span_dirty(L, p, q)) len = max(dirty_normalize(L, P, p, q, &src), 0);
+            if (len == 0) {
+              id = U_EMPTY;
+            } else if (len > 100 && count_chars(L.nb, src, len) > 100) {
+              id = (uint16_t)P.unk;
+            } else {
+              id = U_DEFER;
+              w = wmake(u, src, len);
+              if (len > KEYMAX) L.misc[2] = 1;  // too long for a record: the tile falls back
+            }
+          }
+          L.uid[u] = id;
+          L.u.uwp[u] = w;
+        }
+      }
+      wsync();
+      // ---- 3b: whole-word probe of every pending unit, 4 bucket loads in
+      //      flight per lane; hits are resolved here
+      {
+        const int mb0 = (int)P.maxb[0];
+        const uint32_t vmask = P.vt_mask;
+#define TOK5_FP_ISSUE(k)                                                        \
+  uint4 fa##k = make_uint4(0, 0, 0, 0), fb##k = fa##k;                          \
+  bool fact##k = false;                                                         \
+  {                                                                             \
+    const int u = (k) * 64 + lane;                                              \
+    const uint32_t w = u < nr ? L.u.uwp[u] : 0u;                                \
+    const int len = wlen(w);                                                    \
+    if (w != 0 && len <= 24 && len <= mb0) {                                    \
+      const uint32_t h = key_hash(load_key(L.nb, wsrc(w), len), len, 0u);       \
+      const uint4* bk = P.vt + 4 * (h & vmask);                                 \
+      fa##k = bk[0];                                                            \
+      fb##k = bk[1];                                                            \
+      fact##k = true;                                                           \
+    }                                                                           \
+  }
+#define TOK5_FP_CHECK(k)                                                        \
+  if (fact##k) {                                                                \
+    const int u = (k) * 64 + lane;                                              \
+    const uint32_t w = L.u.uwp[u];                                              \
+    const int len = wlen(w);                                                    \
+    const Key6 key = load_key(L.nb, wsrc(w), len);                              \
+    if (slot_eq(fa##k, fb##k, key, ((uint32_t)len << 16) | 0x80000000u)) {       \
+      L.uid[u] = (uint16_t)(fb##k.z & 0xFFFFu);                                 \
+      L.u.uwp[u] = 0;                                                           \
+    }                                                                           \
+  }
+        TOK5_FP_ISSUE(0)
+        TOK5_FP_ISSUE(1)
+        TOK5_FP_ISSUE(2)
+        TOK5_FP_ISSUE(3)
+        TOK5_FP_CHECK(0)
+        TOK5_FP_CHECK(1)
+        TOK5_FP_CHECK(2)
+        TOK5_FP_CHECK(3)
+#undef TOK5_FP_ISSUE
+#undef TOK5_FP_CHECK
+        static_assert(UCAP == 256, "first-probe batches are unrolled for 4 units per lane");
+      }
+      wsync();
+      if (L.misc[2]) {
+        ovf = true;
+        break;
+      }
+      // ---- 4: entries and records -------------------------------------------
+      // Lane l holds units [l*per, l*per + per); segmented (by sentence)
+      // exclusive prefix sums give each unit its entry index and its record
+      // slot offset within the sentence; a sentence running on from the
+      // previous round continues its counts (carry).
+      {
+        constexpr int K = UCAP / 64;
+        const int per = (nr + 63) >> 6;
+        const int u0 = lane * per;
+        uint32_t sent[K], idv[K], ev[K], nsl[K], epre[K], spre[K];
+        bool valid[K], head[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          const int uu = u0 + k;
+          valid[k] = k < per && uu < nr;
+          sent[k] = valid[k] ? L.u.urec[uu] >> 16 : 0u;
+          idv[k] = valid[k] ? (uint32_t)L.uid[uu] : (uint32_t)U_EMPTY;
+          ev[k] = idv[k] != U_EMPTY ? 1u : 0u;
+          head[k] = valid[k] && (uu == 0 ? (int)sent[k] != prev_sent : (L.u.urec[uu - 1] >> 16) != sent[k]);
+        }
+        const int first_sent = (int)(L.u.urec[0] >> 16);
+        const bool cont = first_sent == prev_sent;
+        auto seg_scan = [&](const uint32_t(&v)[K], uint32_t carry, uint32_t(&pre)[K]) {
+          uint32_t run = 0, h = 0;
+#pragma unroll
+          for (int k = 0; k < K; ++k) {
+            pre[k] = 0;
+            if (valid[k]) {
+              if (head[k]) {
+                run = 0;
+                h = 1;
+              }
+              pre[k] = run;
+              run += v[k];
+            }
+          }
+          uint32_t hv = h, sv = run;
+          wave_seg_incl_add(hv, sv);
+          uint32_t ex = wave_shr1(sv);
+          if (!wave_shr1(hv)) ex += carry;  // no segment start before this lane
+          bool before = true;
+#pragma unroll
+          for (int k = 0; k < K; ++k) {
+            if (valid[k] && head[k]) before = false;
+            if (before) pre[k] += ex;
+          }
+        };
+        seg_scan(ev, cont ? (uint32_t)L.sent_n[first_sent] : 0u, epre);
+        // record slots of queued units whose entry is kept (< max_tok)
+        uint32_t mine = 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          nsl[k] = 0;
+          if (valid[k] && idv[k] == U_DEFER && (int)epre[k] < max_tok)
+            nsl[k] = wlen(L.u.uwp[u0 + k]) <= KEY1 ? 1u : 2u;
+          mine += nsl[k];
+        }
+        seg_scan(nsl, cont ? (uint32_t)L.sslot[first_sent] : 0u, spre);
+        const uint32_t xs = wave_incl_add(mine);
+        const uint32_t need = lane_get(xs, 63);
+        // this round's slots come from the wave's chunk; a sentence's slots
+        // stay contiguous: on a chunk switch, the slots the running sentence
+        // took in earlier rounds move to the new chunk
+        if (need > 0 && cur + need > cend) {
+          const uint32_t carried = cont ? (uint32_t)L.sslot[first_sent] : 0u;
+          if (carried + need > SPLIT_CHUNK) {  // (a sentence with > 1024 slots)
+            ovf = true;
+            break;
+          }
+          if (chunk >= 0 && lane == 0) S.chunk_fill[chunk] = cur - cbase;
+          int c = 0;
+          if (lane == 0) c = (int)atomicAdd(S.chunk_ctr, 1u);
+          c = __builtin_amdgcn_readfirstlane(c);
+          if ((uint32_t)c >= S.n_chunks) {  // record capacity exhausted
+            chunk = -1;
+            cur = cend = cbase = 0;
+            ovf = true;
+            break;
+          }
+          chunk = c;
+          cbase = cur = (uint32_t)c * SPLIT_CHUNK;
+          cend = cbase + SPLIT_CHUNK;
+          if (carried) {
+            // (records this wave stored in an earlier round: drain its stores first)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const uint32_t from = L.sqb[first_sent];
+            for (uint32_t i = lane; i < carried * 4; i += 64) S.rec[(size_t)cur * 4 + i] = S.rec[(size_t)from * 4 + i];
+            if (lane == 0) L.sqb[first_sent] = cur;
+            cur += carried;
+          }
+        }
+        uint32_t gp = cur + (xs - mine);  // global slot of this lane's first record
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          if (!valid[k]) continue;
+          const int uu = u0 + k;
+          const int sj = (int)sent[k];
+          const uint32_t e = epre[k], o = spre[k];
+          if (uu == nr - 1 || (int)(L.u.urec[uu + 1] >> 16) != sj) {  // the sentence's last unit of the round
+            L.sent_n[sj] = (uint16_t)min(e + ev[k], 65535u);
+            L.sslot[sj] = (uint16_t)(o + nsl[k]);
+          }
+          if (ev[k] && (int)e < max_tok) {
+            uint16_t* ep = S.ent + (ent0 + (int64_t)L.sst[sj] + e);
+            if (idv[k] != U_DEFER) {
+              *ep = (uint16_t)idv[k];
+            } else {
+              *ep = (uint16_t)(SPLIT_EDEF | o);
+              if (o == 0) L.sqb[sj] = gp;
+              atomicAdd(&L.sdef[sj], 1u);
+              // the record: {len | slots << 8 | valid, count, key bytes 0..55}
+              const uint32_t w = L.u.uwp[uu];
+              const int len = wlen(w), src = wsrc(w);
+              const int a = src >> 2;
+              const uint32_t sh = (uint32_t)(src & 3);
+              uint32_t x[15];
+#pragma unroll
+              for (int i = 0; i < 15; ++i) x[i] = L.nb[a + i];
+              uint32_t kd[14];
+#pragma unroll
+              for (int i = 0; i < 14; ++i) kd[i] = keep_bytes(__builtin_amdgcn_alignbyte(x[i + 1], x[i], sh), len - 4 * i);
+              uint4* rp = S.rec + (size_t)gp * 4;
+              rp[0] = make_uint4((uint32_t)len | (nsl[k] << 8) | 0x80000000u, 0u, kd[0], kd[1]);
+              rp[1] = make_uint4(kd[2], kd[3], kd[4], kd[5]);
+              rp[2] = make_uint4(kd[6], kd[7], kd[8], kd[9]);
+              rp[3] = make_uint4(kd[10], kd[11], kd[12], kd[13]);
+              if (nsl[k] == 2) {  // the extension slot: a zero header (skipped by wp_kernel), pieces 28..
+                const uint4 z = make_uint4(0, 0, 0, 0);
+                rp[4] = z;
+                rp[5] = z;
+                rp[6] = z;
+                rp[7] = z;
+              }
+            }
+          }
+          gp += nsl[k];
+        }
+        cur += need;
+      }
+      wsync();
+      prev_sent = (int)(L.u.urec[nr - 1] >> 16);
+      wsync();
+    }  // rounds
+    if (ovf) {
+      fallback();
+      continue;
+    }
+    if (lane < ns) {
+      const int64_t s = sa + lane;
+      const int ne = min((int)L.sent_n[lane], max_tok);
+      const int nsl = L.sslot[lane];
+      S.nent[s] = (uint16_t)ne;
+      S.nslot[s] = (uint16_t)nsl;
+      if (nsl) S.qb[s] = L.sqb[lane];
+      P.out_ntok[s] = ne - (int)L.sdef[lane];
+    }
+  }
+  if (chunk >= 0 && lane == 0) S.chunk_fill[chunk] = cur - cbase;
+}
+
+// ------------------------------------------------------------ WordPiece --
+constexpr int KB_DW = 21;  // per-lane key buffer in LDS (dwords; odd stride: no bank conflicts)
+
+// u16 index of piece q in a record (slot 0: pieces 0..27 from byte 8; the
+// extension slot keeps its zero header: pieces 28.. from its byte 4)
+__device__ __forceinline__ int piece_at(int q) { return q < 28 ? 4 + q : 34 + (q - 28); }
+
+template <int WAVES>
+__global__ __launch_bounds__(64 * WAVES) void wp_kernel(TokParams P, SplitParams S) {
+  __shared__ uint32_t bloom[BLOOM_WORDS];
+  __shared__ uint32_t kbuf[WAVES * 64 * KB_DW];
+  for (int i = threadIdx.x; i < BLOOM_WORDS; i += 64 * WAVES) bloom[i] = P.vbloom[i];
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint32_t* kb = kbuf + (wv * 64 + lane) * KB_DW;
+  const uint8_t* kb8 = reinterpret_cast<const uint8_t*>(kb);
+  const uint32_t nch = min(__builtin_amdgcn_readfirstlane(*S.chunk_ctr), S.n_chunks);
+  const uint32_t nwaves = gridDim.x * WAVES;
+  const int mb0 = (int)P.maxb[0], mb1 = (int)P.maxb[1];
+  const uint32_t vmask = P.vt_mask;
+  // the wave's slot stream: chunks gw, gw + nwaves, ...
+  uint32_t c = blockIdx.x * WAVES + wv, off = 0, fill = 0;
+  if (c < nch) fill = __builtin_amdgcn_readfirstlane(S.chunk_fill[c]);
+  auto advance = [&]() {
+    while (off >= fill && c < nch) {
+      c += nwaves;
+      off = 0;
+      fill = c < nch ? __builtin_amdgcn_readfirstlane(S.chunk_fill[c]) : 0u;
+    }
+  };
+  advance();
+  int r = -1;    // record slot being tokenised
+  int pr = -1;   // record slot loaded, not begun
+  uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0, q2 = q0, q3 = q0;
+  int s = 0, we = 0, e = 0, np = 0, bslot = -1;
+  uint32_t cont = 0;
+  bool asc = false;
+  uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0, c4 = 0, c5 = 0;
+  uint32_t H0 = VSEED, H1 = 0, H2 = 0, H3 = 0, H4 = 0, H5 = 0, H6 = 0;
+  auto load_cand = [&]() {
+    const int a = s >> 2;
+    const uint32_t sh = (uint32_t)(s & 3);
+    const uint32_t x0 = kb[a], x1 = kb[a + 1], x2 = kb[a + 2], x3 = kb[a + 3], x4 = kb[a + 4], x5 = kb[a + 5],
+                   x6 = kb[a + 6];
+    c0 = __builtin_amdgcn_alignbyte(x1, x0, sh);
+    c1 = __builtin_amdgcn_alignbyte(x2, x1, sh);
+    c2 = __builtin_amdgcn_alignbyte(x3, x2, sh);
+    c3 = __builtin_amdgcn_alignbyte(x4, x3, sh);
+    c4 = __builtin_amdgcn_alignbyte(x5, x4, sh);
+    c5 = __builtin_amdgcn_alignbyte(x6, x5, sh);
+    H1 = vmix(H0, c0);
+    H2 = vmix(H1, c1);
+    H3 = vmix(H2, c2);
+    H4 = vmix(H3, c3);
+    H5 = vmix(H4, c4);
+    H6 = vmix(H5, c5);
+    asc = ((c0 | c1 | c2 | c3 | c4 | c5) & 0x80808080u) == 0;
+  };
+  auto selH = [&](int q) { return q <= 0 ? H0 : q == 1 ? H1 : q == 2 ? H2 : q == 3 ? H3 : q == 4 ? H4 : q == 5 ? H5 : H6; };
+  auto selD = [&](int q) { return q <= 0 ? c0 : q == 1 ? c1 : q == 2 ? c2 : q == 3 ? c3 : q == 4 ? c4 : c5; };
+  auto hash_len = [&](int l) {  // == vhash of the candidate [s, s+l)
+    const int lc = min(l, 24), q = lc >> 2, rr = lc & 3;
+    uint32_t h = selH(q);
+    if (rr) h = vmix(h, selD(q) & ((1u << (8 * rr)) - 1u));
+    return vfinal(h, (uint32_t)l, cont);
+  };
+  auto bkey_len = [&](int l) {  // == vbkey of the candidate [s, s+l)
+    const int lc = min(l, 24), q = lc >> 2, rr = lc & 3;
+    return vbkey(selH(q), rr ? selD(q) & ((1u << (8 * rr)) - 1u) : 0u, (uint32_t)l, cont);
+  };
+  auto bloom_ok = [&](uint32_t h) {
+    const uint32_t bb = vbloom_bits(h);
+    return (bloom[vbloom_word(h)] & bb) == bb;
+  };
+  auto shrink = [&]() {  // previous char boundary
+    --e;
+    if (!(asc && e - s < 24))
+      while (e > s && (kb8[e] & 0xC0u) == 0x80u) --e;
+  };
+  auto start_piece = [&](int maxb) {
+    bslot = -1;
+    load_cand();
+    e = min(we, s + maxb);
+    if (e < we && !(asc && e - s < 24))
+      while (e > s && (kb8[e] & 0xC0u) == 0x80u) --e;
+  };
+  auto rec16 = [&]() { return reinterpret_cast<uint16_t*>(S.rec + (size_t)r * 4); };
+  auto finish = [&]() {
+    reinterpret_cast<uint32_t*>(S.rec + (size_t)r * 4)[1] = (uint32_t)np;
+    r = -1;
+  };
+  for (;;) {
+    // ---- A: candidate of each working lane: the longest length the Bloom
+    //      filter does not rule out, then its bucket load
+    bool fail = false;
+    uint4 a0 = make_uint4(0, 0, 0, 0), a1 = a0, b0 = a0, b1 = a0;
+    if (r >= 0) {
+      if (bslot < 0) {
+        int len = e - s;
+        bool found = false;
+        uint32_t hcur = 0;
+        if (asc && len <= 24) {
+          int fl = 0;
+          int ga = 0;
+#define TOK5_EXT(j, Hj1) \
+  ga = ((ga == (j)) & (4 * ((j) + 1) < len) & bloom_ok(vbkey_ext(Hj1, 4 * ((j) + 1), cont))) ? (j) + 1 : ga;
+          TOK5_EXT(0, H1)
+          TOK5_EXT(1, H2)
+          TOK5_EXT(2, H3)
+          TOK5_EXT(3, H4)
+          TOK5_EXT(4, H5)
+#undef TOK5_EXT
+#define TOK5_GROUP(k, Hk, Hk1, ck)                                                                              \
+  if (fl == 0 && 4 * (k) < len && (k) <= ga) {                                                                  \
+    const uint32_t g4 = vbkey(Hk1, 0u, 4 * (k) + 4, cont), g3 = vbkey(Hk, (ck) & 0xFFFFFFu, 4 * (k) + 3, cont), \
+                   g2 = vbkey(Hk, (ck) & 0xFFFFu, 4 * (k) + 2, cont),                                           \
+                   g1 = vbkey(Hk, (ck) & 0xFFu, 4 * (k) + 1, cont);                                             \
+    const bool o4 = (4 * (k) + 4 <= len) & bloom_ok(g4), o3 = (4 * (k) + 3 <= len) & bloom_ok(g3),              \
+               o2 = (4 * (k) + 2 <= len) & bloom_ok(g2), o1 = bloom_ok(g1);                                     \
+    if (o4 | o3 | o2 | o1) fl = o4 ? 4 * (k) + 4 : o3 ? 4 * (k) + 3 : o2 ? 4 * (k) + 2 : 4 * (k) + 1;           \
+  }
+          TOK5_GROUP(5, H5, H6, c5)
+          TOK5_GROUP(4, H4, H5, c4)
+          TOK5_GROUP(3, H3, H4, c3)
+          TOK5_GROUP(2, H2, H3, c2)
+          TOK5_GROUP(1, H1, H2, c1)
+          TOK5_GROUP(0, H0, H1, c0)
+#undef TOK5_GROUP
+          found = fl > 0;
+          e = s + fl;
+          if (found) hcur = hash_len(fl);
+        } else {
+          while (e > s) {
+            if (bloom_ok(bkey_len(e - s))) {
+              hcur = hash_len(e - s);
+              found = true;
+              break;
+            }
+            shrink();
+          }
+        }
+        if (found) bslot = (int)(hcur & vmask);
+        else fail = true;
+      }
+      if (!fail) {
+        const uint4* bk = P.vt + 4 * (uint32_t)bslot;
+        a0 = bk[0];
+        a1 = bk[1];
+        b0 = bk[2];
+        b1 = bk[3];
+      }
+    }
+    // ---- B: idle lanes take the next slots of the stream; their record
+    //      loads fly together with the bucket loads
+    {
+      const uint64_t idle = __ballot(r < 0 && pr < 0);
+      if (idle != 0 && c < nch) {
+        const uint32_t avail = fill - off;
+        const int k = lane_rank(idle);
+        if (r < 0 && pr < 0 && (uint32_t)k < avail) {
+          pr = (int)(c * SPLIT_CHUNK + off + (uint32_t)k);
+          const uint4* rp = S.rec + (size_t)pr * 4;
+          q0 = rp[0];
+          q1 = rp[1];
+          q2 = rp[2];
+          q3 = rp[3];
+        }
+        off += min((uint32_t)__popcll(idle), avail);
+        advance();
+      }
+    }
+    // ---- C: compare and advance
+    if (r >= 0) {
+      if (fail) {  // some position has no match: the whole word is [UNK]
+        np = 0;
+        rec16()[piece_at(0)] = (uint16_t)P.unk;
+        np = 1;
+        finish();
+      } else {
+        const int len = e - s;
+        const int lc = min(len, 24);
+        auto msk = [&](int k, uint32_t cc) {  // the key's bytes of dword k, branch-free
+          const int nbk = min(max(lc - 4 * k, 0), 4);
+          return cc & (nbk >= 4 ? 0xFFFFFFFFu : ((1u << (8 * nbk)) - 1u));
+        };
+        const uint32_t m0c = msk(0, c0), m1c = msk(1, c1), m2c = msk(2, c2), m3c = msk(3, c3), m4c = msk(4, c4),
+                       m5c = msk(5, c5);
+        const uint32_t want = ((uint32_t)len << 16) | (cont << 24) | 0x80000000u;
+        bool m0 = (((a1.z & 0xFFFF0000u) ^ want) | (a0.x ^ m0c) | (a0.y ^ m1c) | (a0.z ^ m2c) | (a0.w ^ m3c) |
+                   (a1.x ^ m4c) | (a1.y ^ m5c)) == 0u;
+        bool m1 = (((b1.z & 0xFFFF0000u) ^ want) | (b0.x ^ m0c) | (b0.y ^ m1c) | (b0.z ^ m2c) | (b0.w ^ m3c) |
+                   (b1.x ^ m4c) | (b1.y ^ m5c)) == 0u;
+        if (len > 24) {  // the rest of a long key against the pool
+          if (m0)
+            for (int k = 24; k < len; ++k) m0 = m0 && kb8[s + k] == P.pool[a1.w + k];
+          if (m1)
+            for (int k = 24; k < len; ++k) m1 = m1 && kb8[s + k] == P.pool[b1.w + k];
+        }
+        if (m0 || m1) {
+          rec16()[piece_at(np)] = (uint16_t)((m0 ? a1.z : b1.z) & 0xFFFFu);
+          ++np;
+          s = e;
+          if (s >= we) {
+            finish();
+          } else {
+            cont = 1;
+            start_piece(mb1);
+          }
+        } else if (!(a1.z & 0x80000000u) || !(b1.z & 0x80000000u)) {
+          bslot = -1;  // an empty slot ends the probe sequence: no such key
+          shrink();
+        } else {
+          bslot = (int)(((uint32_t)bslot + 1u) & vmask);
+        }
+      }
+    }
+    // ---- D: lanes with a loaded record begin it
+    if (r < 0 && pr >= 0) {
+      if (q0.x == 0u) {  // an extension slot
+        pr = -1;
+      } else {
+        const int len = (int)(q0.x & 0xFFu);
+        uint4* k4 = reinterpret_cast<uint4*>(kb);  // (KB_DW odd: dword stores)
+        (void)k4;
+        kb[0] = q0.z; kb[1] = q0.w;
+        kb[2] = q1.x; kb[3] = q1.y; kb[4] = q1.z; kb[5] = q1.w;
+        kb[6] = q2.x; kb[7] = q2.y; kb[8] = q2.z; kb[9] = q2.w;
+        kb[10] = q3.x; kb[11] = q3.y; kb[12] = q3.z; kb[13] = q3.w;
+#pragma unroll
+        for (int i = 14; i < KB_DW; ++i) kb[i] = 0u;
+        r = pr;
+        pr = -1;
+        s = 0;
+        we = len;
+        np = 0;
+        cont = 0;
+        start_piece(mb0);
+      }
+    }
+    if (__ballot(r >= 0 || pr >= 0) == 0 && c >= nch) break;
+  }
+}
+
+// ---------------------------------------------------------------- count --
+__global__ __launch_bounds__(256) void count_kernel(TokParams P, SplitParams S) {
+  const int64_t sA = S.tile_sent[S.t0], sB = S.tile_sent[S.t1];
+  for (int64_t s = sA + (int64_t)blockIdx.x * 256 + threadIdx.x; s < sB; s += (int64_t)gridDim.x * 256) {
+    const int nsl = S.nslot[s];
+    if (nsl == 0) continue;
+    const uint32_t g = S.qb[s];
+    int sum = 0;
+    for (int k = 0; k < nsl; ++k) sum += (int)reinterpret_cast<const uint32_t*>(S.rec + (size_t)(g + k) * 4)[1];
+    P.out_ntok[s] = min(P.out_ntok[s] + sum, P.max_tok);
+  }
+}
+
+// --------------------------------------------------------------- expand --
+// A wave per group of 64 sentences; their entries in steps of 256 (4 per
+// lane, contiguous); a record entry expands to its pieces.
+struct ExpLds {
+  uint32_t e0[65];      // group entry offsets
+  int64_t eoff[64];     // entry index of the sentence's first entry
+  int64_t dst[64];      // output index of its first token
+  uint32_t qb[64];
+  int32_t cap[64];      // its final token count
+};
+
+__global__ __launch_bounds__(256) void expand_kernel(TokParams P, SplitParams S) {
+  __shared__ ExpLds X[4];
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  ExpLds& E = X[wv];
+  const int64_t sA = uni64(S.tile_sent[S.t0]), sB = uni64(S.tile_sent[S.t1]);
+  const int64_t base = P.sent_off[0], ebase = S.t0 << 10;
+  const bool dense = S.dense != nullptr;
+  uint16_t* out = dense ? S.dense : P.out_ids;
+  const int64_t nwaves = (int64_t)gridDim.x * 4;
+  for (int64_t g0 = sA + ((int64_t)blockIdx.x * 4 + wv) * 64; g0 < sB; g0 += nwaves * 64) {
+    const int64_t s = g0 + lane;
+    uint32_t ne = 0;
+    bool fb = false;
+    if (s < sB) {
+      ne = S.nent[s];
+      fb = ne == SPLIT_NENT_FB;
+      const int64_t so = P.sent_off[s] - base;
+      const int32_t cap = P.out_ntok[s];
+      E.eoff[lane] = so - ebase;
+      E.dst[lane] = dense ? S.tokoff[s] : so;
+      E.qb[lane] = S.nslot[s] ? S.qb[s] : 0u;
+      E.cap[lane] = cap;
+      if (fb) ne = dense ? (uint32_t)cap : 0u;  // a fallback tile's sentence: its ids are final (sparse) already
+      if (fb) E.eoff[lane] = -1 - so;            // (dense: copy them from the sparse output)
+    }
+    const uint32_t x = wave_incl_add(ne);
+    E.e0[lane] = x - ne;
+    const uint32_t T = lane_get(x, 63);
+    if (lane == 63) E.e0[64] = T;
+    wsync();
+    uint32_t carry = 0;
+    for (uint32_t st = 0; st < T; st += 256) {
+      const uint32_t g = st + (uint32_t)lane * 4;
+      // sentence of this lane's first entry: last j with e0[j] <= g
+      int j = 0;
+      if (g < T) {
+        int lo = 0, hi = 63;
+        while (lo < hi) {
+          const int mid = (lo + hi + 1) >> 1;
+          if (E.e0[mid] <= g) lo = mid;
+          else hi = mid - 1;
+        }
+        j = lo;
+      }
+      uint32_t v[4], cnt[4], pre[4];
+      int js[4];
+      bool valid[4], head[4];
+      uint32_t run = 0, h = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t gg = g + k;
+        valid[k] = gg < T;
+        while (valid[k] && j < 63 && E.e0[j + 1] <= gg) ++j;
+        js[k] = j;
+        const uint32_t kk = valid[k] ? gg - E.e0[j] : 0u;
+        head[k] = valid[k] && kk == 0;
+        v[k] = 0;
+        cnt[k] = 0;
+        if (valid[k]) {
+          const int64_t eo = E.eoff[j];
+          if (eo >= 0) {
+            v[k] = S.ent[eo + kk];
+            cnt[k] = v[k] >= SPLIT_EDEF
+                         ? reinterpret_cast<const uint32_t*>(S.rec + (size_t)(E.qb[j] + (v[k] & 0xFFFu)) * 4)[1]
+                         : 1u;
+          } else {  // fallback sentence (dense): its final ids from the sparse output
+            v[k] = P.out_ids[(-1 - eo) + kk];
+            cnt[k] = 1;
+          }
+        }
+        if (head[k]) {
+          run = 0;
+          h = 1;
+        }
+        pre[k] = run;
+        run += cnt[k];
+      }
+      uint32_t hv = h, sv = run;
+      wave_seg_incl_add(hv, sv);
+      uint32_t ex = wave_shr1(sv);
+      if (!wave_shr1(hv)) ex += carry;
+      bool before = true;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (valid[k] && head[k]) before = false;
+        if (before) pre[k] += ex;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (!valid[k]) continue;
+        const int jj = js[k];
+        uint16_t* o = out + E.dst[jj];
+        const int cap = E.cap[jj];
+        if (v[k] < SPLIT_EDEF || E.eoff[jj] < 0) {
+          if ((int)pre[k] < cap) o[pre[k]] = (uint16_t)v[k];
+        } else {
+          const uint16_t* pc = reinterpret_cast<const uint16_t*>(S.rec + (size_t)(E.qb[jj] + (v[k] & 0xFFFu)) * 4);
+          for (uint32_t q = 0; q < cnt[k] && (int)(pre[k] + q) < cap; ++q) o[pre[k] + q] = pc[piece_at((int)q)];
+        }
+      }
+      // running total of the step's last entry (its sentence may continue)
+      const uint32_t lastg = min(T, st + 256) - 1 - st;  // index within the step
+      const int ll = (int)(lastg >> 2), lk = (int)(lastg & 3);
+      uint32_t mytot = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (k == lk) mytot = pre[k] + cnt[k];
+      carry = lane_get(mytot, ll);
+    }
+    wsync();
+  }
+}
+
+template <int WAVES>
+static hipError_t launch_scan(const TokParams& P, const SplitParams& S, int n_cu, hipStream_t s) {
+  static int per_cu = 0;
+  if (per_cu == 0 &&
+      (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, scan_kernel<WAVES>, 64 * WAVES, 0) != hipSuccess ||
+       per_cu < 1))
+    per_cu = 1;
+  int64_t grid = (int64_t)n_cu * per_cu;
+  const int64_t need = (S.t1 - S.t0 + WAVES - 1) / WAVES;
+  if (grid > need) grid = need;
+  if (grid < 1) grid = 1;
+  hipLaunchKernelGGL(scan_kernel<WAVES>, dim3((unsigned)grid), dim3(64 * WAVES), 0, s, P, S);
+  return hipGetLastError();
+}
+
+template <int WAVES>
+static hipError_t launch_wp(const TokParams& P, const SplitParams& S, int n_cu, hipStream_t s) {
+  static int per_cu = 0;
+  if (per_cu == 0 &&
+      (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, wp_kernel<WAVES>, 64 * WAVES, 0) != hipSuccess ||
+       per_cu < 1))
+    per_cu = 1;
+  const int64_t grid = (int64_t)n_cu * per_cu;
+  hipLaunchKernelGGL(wp_kernel<WAVES>, dim3((unsigned)grid), dim3(64 * WAVES), 0, s, P, S);
+  return hipGetLastError();
+}
+
+}  // namespace tok5
+
+constexpr int SCAN_WAVES = 8, WP_WAVES = 8;
+
+int64_t split_seg_slots(int64_t seg_tiles) {
+  // 1 slot per 16 input bytes (the synthetic Wikipedia corpus queues ~0.02
+  // words per byte) + one partly used chunk per scanning wave
+  const int64_t waves = 256 * 32;
+  const int64_t chunks = (seg_tiles * 1024 / 16 + SPLIT_CHUNK - 1) / SPLIT_CHUNK + std::min(waves, seg_tiles) + 16;
+  return chunks * SPLIT_CHUNK;
+}
+
+hipError_t launch_tokenize_split(const TokParams& P, int64_t nbytes, int64_t* tile_sent, SplitParams S, int n_cu,
+                                 int fb_grid, hipStream_t s) {
+  const int64_t n_tiles = tile_count(nbytes);
+  hipError_t e = launch_tile_bounds(P.sent_off, P.n_sent, n_tiles, tile_sent, s);
+  if (e != hipSuccess) return e;
+  if ((e = hipMemsetAsync(S.fb_count, 0, 4, s)) != hipSuccess) return e;
+  S.tile_sent = tile_sent;
+  const int64_t seg = S.seg_tiles > 0 ? S.seg_tiles : SPLIT_SEG_TILES;
+  for (int64_t t0 = 0; t0 < n_tiles; t0 += seg) {
+    S.t0 = t0;
+    S.t1 = std::min(n_tiles, t0 + seg);
+    if ((e = hipMemsetAsync(S.chunk_ctr, 0, 4, s)) != hipSuccess) return e;
+    if ((e = tok5::launch_scan<SCAN_WAVES>(P, S, n_cu, s)) != hipSuccess) return e;
+    if ((e = tok5::launch_wp<WP_WAVES>(P, S, n_cu, s)) != hipSuccess) return e;
+    hipLaunchKernelGGL(tok5::count_kernel, dim3((unsigned)std::max(1, n_cu * 8)), dim3(256), 0, s, P, S);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(tok5::expand_kernel, dim3((unsigned)std::max(1, n_cu * 8)), dim3(256), 0, s, P, S);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
+  return launch_tokenize_fallback(P, tile_sent, S.fb_list, S.fb_count, fb_grid, s);
+}
+
+}  // namespace lddl

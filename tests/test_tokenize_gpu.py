@@ -107,7 +107,7 @@ def adversarial_sentences(rng, n):
   return out
 
 
-@pytest.mark.parametrize('algo', ['1', '2', '3', '4'])
+@pytest.mark.parametrize('algo', ['1', '2', '3', '4', '5'])
 @pytest.mark.parametrize('name', ['bert', 'codebert'])
 def test_hip_tokenize_adversarial_vs_oracle(gpu, monkeypatch, algo, name):
   from lddl_amd.synth import corpus_from_sentences
@@ -126,7 +126,7 @@ def test_hip_tokenize_adversarial_vs_oracle(gpu, monkeypatch, algo, name):
       assert np.array_equal(a.astype(np.int64), b.astype(np.int64)), (i, repr(sents[i][:80]))
 
 
-@pytest.mark.parametrize('algo', ['1', '2', '3', '4'])
+@pytest.mark.parametrize('algo', ['1', '2', '3', '4', '5'])
 def test_hip_tokenize_algos_agree_on_wiki(gpu, monkeypatch, algo):
   from lddl_amd import synth
   from lddl_amd.tokenizer import Tokenizer
@@ -153,3 +153,24 @@ def test_hip_tokenize_tiles_in_several_launches(gpu, monkeypatch):
   assert np.array_equal(ntok, ontok)
   for a, b in zip(compact(ids, ntok, c.sent_off), compact(oids, ontok, c.sent_off)):
     assert np.array_equal(a.astype(np.int64), b.astype(np.int64))
+
+
+@pytest.mark.parametrize('env', [{'LDDL_SPLIT_SEG': '97'}, {'LDDL_SPLIT_CHUNKS': '3'},
+                                 {'LDDL_SPLIT_SEG': '61', 'LDDL_SPLIT_CHUNKS': '40'}])
+@pytest.mark.parametrize('name', ['bert', 'codebert'])
+def test_hip_tokenize_split_segments_and_capacity(gpu, monkeypatch, env, name):
+  """The split tokenizer (v5) over many small segments (seams between
+  segments) and with too few WordPiece record chunks (tiles that run out of
+  record capacity go to the exact fallback kernel): still exact."""
+  from lddl_amd import synth
+  from lddl_amd.tokenizer import Tokenizer
+  monkeypatch.setenv('LDDL_TOKENIZE_ALGO', '5')
+  for k, v in env.items():
+    monkeypatch.setenv(k, v)
+  c = synth.make_wiki(2_000_000, seed=29) if name == 'bert' else synth.make_code(1500, seed=31)
+  for max_tok in (512, 5):
+    ids, ntok = run_hip(Tokenizer(VOCABS[name]), c.data, c.sent_off, max_tok)
+    oids, ontok = OracleTokenizer(VOCABS[name]).run(c.data, c.sent_off, max_tok, nthreads=8)
+    assert np.array_equal(ntok, ontok)
+    for a, b in zip(compact(ids, ntok, c.sent_off), compact(oids, ontok, c.sent_off)):
+      assert np.array_equal(a.astype(np.int64), b.astype(np.int64))
