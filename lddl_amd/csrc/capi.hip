@@ -63,12 +63,13 @@ struct lddl_ctx {
   uint32_t* d_vbloom = nullptr;  // its Bloom filter
   bool tok4_ok = false;          // the ASCII page fits tokenize_stream's class table
   int tok4_cfg = 0;
+  int tok5_cfg = 0;
   // pack workspace (grown on demand)
   struct Buf {
     void* p = nullptr;
     size_t cap = 0;
   };
-  Buf ws[40];
+  Buf ws[48];
   PackParams pp{};
   int64_t last_npairs = -1, last_ntok = -1;
   int64_t* h_tot = nullptr;  // pinned [8]
@@ -350,6 +351,8 @@ extern "C" int lddl_create(const char* vocab_path, const char* table_path, int d
   if (c->tok_algo == 4 && !c->tok4_ok) c->tok_algo = 3;
   const char* cfg = getenv("LDDL_TOK4_CFG");  // waves per workgroup / Bloom (tokenize.h)
   c->tok4_cfg = cfg ? atoi(cfg) : 4;
+  const char* cfg5 = getenv("LDDL_TOK5_CFG");  // split tokenizer variants (tokenize_split.hip)
+  c->tok5_cfg = cfg5 ? atoi(cfg5) : 0;
   const char* tchunk = getenv("LDDL_TILE_CHUNK");  // tiles per launch (tests force several launches)
   c->tile_chunk = tchunk ? atoll(tchunk) : 0;
   const char* mcap = getenv("LDDL_MLM_CAP");  // initial masking arena (tests force the regrow path)
@@ -458,12 +461,24 @@ extern "C" int lddl_tokenize(lddl_ctx* c, const uint8_t* d_bytes, int64_t nbytes
         (rc = ws_get(c, 21, 16, &S.fb_count)) || (rc = ws_get(c, 34, (size_t)seg * 1024 + 4096, &S.ent)) ||
         (rc = ws_get(c, 35, (size_t)slots * 4, &S.rec)) || (rc = ws_get(c, 36, (size_t)n_chunks + 16, &S.chunk_fill)) ||
         (rc = ws_get(c, 37, n_sent, &S.nent)) || (rc = ws_get(c, 38, n_sent, &S.nslot)) ||
-        (rc = ws_get(c, 39, n_sent, &S.qb)))
+        (rc = ws_get(c, 39, n_sent, &S.qb)) || (rc = ws_get(c, 40, n_sent, &S.fdef)))
       return rc;
     S.chunk_ctr = S.chunk_fill + n_chunks;
     S.n_chunks = (uint32_t)n_chunks;
     S.seg_tiles = seg;
-    HIP_TRY(launch_tokenize_split(P, nbytes, tile_sent, S, c->n_cu, c->tok_grid, st));
+    HIP_TRY(launch_tokenize_split(P, nbytes, tile_sent, S, c->n_cu, c->tok_grid, c->tok5_cfg, st));
+    if (P.dbg) {
+      uint64_t h[12];
+      int32_t nfb = 0;
+      HIP_TRY(hipMemcpyAsync(h, P.dbg, sizeof h, hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipMemcpyAsync(&nfb, S.fb_count, 4, hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipStreamSynchronize(st));
+      const char* nm[12] = {"loop", "setup", "classify", "except", "units", "urec", "prep", "probe", "entries",
+                            "tile_end", "stages", "tiles"};
+      fprintf(stderr, "[lddl tok5 dbg] ntiles=%lld fallback=%d", (long long)nt, nfb);
+      for (int k = 0; k < 12; ++k) fprintf(stderr, " %s=%llu", nm[k], (unsigned long long)h[k]);
+      fprintf(stderr, "\n");
+    }
   } else if (c->tok_algo == 4) {
     const int64_t nt = tile_count(nbytes);
     int64_t* tile_sent;

@@ -63,12 +63,13 @@ hipError_t launch_tokenize_stream(const TokParams& P, int64_t nbytes, int64_t* t
 // hands every other word to a WordPiece record queue; a full-occupancy
 // WordPiece kernel runs the records, a count pass and an expand pass write
 // the ids.  Scratch per segment of tiles (SPLIT_SEG_TILES):
-//   ent    u16 per byte of the segment: sentence s's entries at
-//          sent_off[s] - sent_off[0] - t0 * 1 KiB + k: a vocab id, or
-//          SPLIT_EDEF | (record slot - qb[s]) for a word of the queue
+//   ent    u16 per byte of the segment: sentence s's entries from its first
+//          queued word on (k >= fdef[s]) at sent_off[s] - sent_off[0] -
+//          t0 * 1 KiB + k: a vocab id, or SPLIT_EDEF | (record slot - qb[s])
+//          for a word of the queue; the ids before it are final and go
+//          straight to the output
 //   rec    64-B record slots in chunks of SPLIT_CHUNK, chunk_fill[c] used
-//   nent / nslot / qb per sentence; out_ntok holds the resolved count until
-//   the count pass adds the records' piece counts
+//   nent / nslot / qb / fdef per sentence
 constexpr int64_t SPLIT_SEG_TILES = int64_t(1) << 20;  // 1 GiB of input per segment
 constexpr uint32_t SPLIT_CHUNK = 1024;                 // record slots per allocation chunk (64 KiB)
 constexpr uint32_t SPLIT_EDEF = 0xF000u;               // entry >= EDEF: a queued word
@@ -88,11 +89,10 @@ struct SplitParams {
   uint32_t* qb;
   int32_t* fb_list;
   int32_t* fb_count;
-  uint16_t* dense;         // expand: dense output (null: sparse, the lddl_tokenize layout)
-  const int64_t* tokoff;   // expand: dense offsets
+  uint16_t* fdef;          // entry index of the sentence's first queued word (nslot > 0)
 };
 hipError_t launch_tokenize_split(const TokParams& P, int64_t nbytes, int64_t* tile_sent, SplitParams S, int n_cu,
-                                 int fb_grid, hipStream_t s);
+                                 int fb_grid, int cfg, hipStream_t s);
 int64_t split_seg_slots(int64_t seg_tiles);
 
 }  // namespace lddl

@@ -25,11 +25,10 @@
 //                  longest-match-first (Bloom scan + 64-B bucket probe per
 //                  candidate, as tok4's loop), pieces and count written back
 //                  into the record.
-//  count_kernel    per sentence: ntok = min(resolved + sum of its records'
-//                  counts, max_tok).
-//  expand_kernel   per group of sentences: entries -> ids (a record's pieces
-//                  in place of its entry), sparse (the lddl_tokenize layout)
-//                  or dense at tokoff.
+//  expand_kernel   per group of sentences: the entries from each sentence's
+//                  first queued word on -> ids (a record's pieces in place of
+//                  its entry) and the token count; the ids before it were
+//                  final and written by the scan.
 // Tiles the scan does not model (window > 2 KiB, > 64 sentences, > 256
 // units... as tok4, a queued word longer than 56 bytes, record capacity) are
 // listed and re-run by tokenize_fallback_kernel (exact serial path).
@@ -62,19 +61,22 @@ __device__ __forceinline__ int wlen(uint32_t w) { return (int)(w >> 20); }
 
 struct Lds {
   union {
-    uint32_t rp[CAP / 4 + 4];  // phase 1: raw bytes
+    uint32_t rp[CAP / 4 + 4];  // phase 1: raw bytes of the tile (LDS-DMA)
     struct {
       uint32_t urec[UCAP];     // window position | sentence << 16
       uint32_t uwp[UCAP];      // pending unit (wmake), 0 once resolved
     } u;
   };
+  uint32_t pb[8];              // the tile's bounds: tile_sent[t], tile_sent[t+1], sent_off of both (LDS-DMA)
   uint32_t nb[NBUF / 4];       // normalised bytes in window coordinates; side buffer at [CAP, CAP+DCAP)
   uint32_t brk[64];            // break bits: unit starts, spaces, sentence starts
   uint32_t dm[64];             // dirty bits: filler / expansion marker bytes
   uint32_t sb[64];             // sentence-start bits
+  uint16_t uid[UCAP];          // vocab id, U_EMPTY (no token) or U_DEFER (queued); in phase 4
+                               // (once read) the queued units of the round in unit order
   uint32_t sqb[NSCAP];         // record index of the sentence's first slot
   uint32_t sdef[NSCAP];        // queued entries below max_tok
-  uint16_t uid[UCAP];          // vocab id, U_EMPTY (no token) or U_DEFER (queued)
+  uint32_t sfdef[NSCAP];       // entry index of the first queued word
   uint16_t sst[NSCAP + 2];     // sentence starts (window coordinates)
   uint16_t sent_n[NSCAP];      // entries so far (uncapped)
   uint16_t sslot[NSCAP];       // record slots so far
@@ -231,8 +233,19 @@ __device__ __forceinline__ bool slot_eq(const uint4& a, const uint4& b, const Ke
           (b.y ^ k.d5)) == 0u;
 }
 
-template <int WAVES>
-__global__ __launch_bounds__(64 * WAVES) void scan_kernel(TokParams P, SplitParams S) {
+// DBG: phase stamps (s_memtime, diagnostics build only: LDDL_TOK_DEBUG=1)
+// OCC: the waves per SIMD the register allocation is held to (LDS admits 5)
+template <int WAVES, bool DBG, int OCC>
+__global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, SplitParams S) {
+  uint64_t acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t tprev = 0;
+#define STAMP(k)                                                                   \
+  if (DBG) {                                                                       \
+    uint64_t t_;                                                                   \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");   \
+    acc[k] += t_ - tprev;                                                          \
+    tprev = t_;                                                                    \
+  }
   __shared__ Lds Ls[WAVES];
   __shared__ uint32_t ctab32[64];
   // ---- prologue: per-byte class table from the unicode table's ASCII page --
@@ -270,10 +283,67 @@ __global__ __launch_bounds__(64 * WAVES) void scan_kernel(TokParams P, SplitPara
   // record chunk of this wave (wave-uniform): slots [cur, cend)
   uint32_t cur = 0, cend = 0, cbase = 0;
   int chunk = -1;
-  for (int64_t t = S.t0 + (int64_t)blockIdx.x * WAVES + wv; t < S.t1; t += nwaves) {
+  // The tile's bounds (pb) and raw bytes (rp) arrive by LDS-DMA (no VGPRs,
+  // no register-to-LDS copy of the bytes).  (A software-pipelined variant
+  // that loaded the next tile while this one ran measured no faster: the
+  // kernel is bound by its LDS round trips and instruction issue.)
+  int64_t n_sa = 0, n_sb = 0, n_A = 0, n_B = 0, n_spos = 0;
+  int nst = 0;
+  bool dma_pending = false;  // raw-byte DMA issued and not yet waited for
+  int64_t tn = S.t0 + (int64_t)blockIdx.x * WAVES + wv;
+  // (LDS-DMA: lane i of the instruction writes dword i at the LDS base)
+  auto dma4 = [&](const void* g, uint32_t* l) {
+    __builtin_amdgcn_global_load_lds((const uint32_t*)g, (__attribute__((address_space(3))) uint32_t*)l, 4, 0, 0);
+  };
+  auto drain = [&]() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); };
+  auto stage1 = [&]() {
+    if (tn < S.t1 && lane < 4) dma4(reinterpret_cast<const uint32_t*>(S.tile_sent + tn) + lane, L.pb);
+    nst = 1;
+  };
+  auto stage2 = [&]() {
+    if (nst != 1) return;
+    nst = 2;
+    n_sa = n_sb = 0;
+    if (tn >= S.t1) return;
+    drain();
+    n_sa = uni64(*reinterpret_cast<const int64_t*>(&L.pb[0]));
+    n_sb = uni64(*reinterpret_cast<const int64_t*>(&L.pb[2]));
+    if (n_sa >= n_sb) return;
+    if (lane < 2) dma4(reinterpret_cast<const uint32_t*>(P.sent_off + n_sa) + lane, L.pb + 4);
+    if (lane < 2) dma4(reinterpret_cast<const uint32_t*>(P.sent_off + n_sb) + lane, L.pb + 6);
+    if (lane < n_sb - n_sa) n_spos = P.sent_off[n_sa + lane];
+  };
+  auto stage3 = [&]() {
+    if (nst != 2) return;
+    nst = 3;
+    if (n_sa >= n_sb) return;
+    drain();
+    n_A = uni64(*reinterpret_cast<const int64_t*>(&L.pb[4]));
+    n_B = uni64(*reinterpret_cast<const int64_t*>(&L.pb[6]));
+    const int aoff = (int)(reinterpret_cast<uintptr_t>(P.bytes + n_A) & 15u);
+    const int64_t nb64 = (n_B - n_A) + aoff;
+    if (nb64 > CAP || n_sb - n_sa > NSCAP) return;  // the tile falls back: no bytes needed
+    dma_pending = true;
+    // streamed once: non-temporal (aux bit 1), keep L2 for the vocab table
+    const uint8_t* g = P.bytes + (n_A - aoff) + 16 * lane;
+    if (16 * lane < nb64)
+      __builtin_amdgcn_global_load_lds((const uint32_t*)g, (__attribute__((address_space(3))) uint32_t*)L.rp, 16, 0, 2);
+    if (1024 + 16 * lane < nb64)
+      __builtin_amdgcn_global_load_lds((const uint32_t*)(g + 1024), (__attribute__((address_space(3))) uint32_t*)(L.rp + 256), 16, 0, 2);
+  };
+  if (DBG) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(tprev)::"memory");
+  for (int64_t t = tn; t < S.t1; t = tn) {
     wsync();
-    const int64_t sa = uni64(S.tile_sent[t]), sb = uni64(S.tile_sent[t + 1]);
-    if (sa >= sb) continue;
+    stage1();
+    stage2();
+    stage3();
+    const int64_t sa = n_sa, sb = n_sb, A = n_A, B = n_B, spos = n_spos;
+    STAMP(0);
+    if (dma_pending) drain();  // this tile's raw bytes
+    dma_pending = false;
+    tn = t + nwaves;
+    [&]() {
+    if (sa >= sb) return;
     const int ns = (int)(sb - sa);
     // the tile goes to the exact serial kernel; its sentences are no-ops for
     // the count / expand passes
@@ -287,13 +357,12 @@ __global__ __launch_bounds__(64 * WAVES) void scan_kernel(TokParams P, SplitPara
         S.nslot[sa + j] = 0;
       }
     };
-    const int64_t A = uni64(P.sent_off[sa]), B = uni64(P.sent_off[sb]);
     const int aoff = (int)(reinterpret_cast<uintptr_t>(P.bytes + A) & 15u);
     const uint8_t* wbase = P.bytes + (A - aoff);  // 16-B aligned
     const int64_t nb64 = (B - A) + aoff;
     if (nb64 > CAP || ns > NSCAP) {
       fallback();
-      continue;
+      return;
     }
     const int nb = (int)nb64;
     // ---- sentence starts ----------------------------------------------------
@@ -310,27 +379,20 @@ __global__ __launch_bounds__(64 * WAVES) void scan_kernel(TokParams P, SplitPara
     }
     wsync();
     if (lane < ns) {
-      const int pos = (int)(P.sent_off[sa + lane] - A) + aoff;
+      const int pos = (int)(spos - A) + aoff;
       L.sst[lane] = (uint16_t)pos;
       if (pos < nb) atomicOr(&L.sb[pos >> 5], 1u << (pos & 31));
     }
+    STAMP(1);
     // ---- 1: raw bytes -> masks + normalised bytes in place ------------------
     uint32_t W, I, S_, CS, D, X, inwin;
     {
       const int p0 = lane * 32;
-      uint4 v0 = make_uint4(0, 0, 0, 0), v1 = v0;
-      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-      const u32x4* gp = reinterpret_cast<const u32x4*>(wbase) + 2 * lane;
-      if (p0 < nb) {  // streamed once: non-temporal, keep L2 for the vocab table
-        const u32x4 a = __builtin_nontemporal_load(gp);
-        v0 = make_uint4(a.x, a.y, a.z, a.w);
-      }
-      if (p0 + 16 < nb) {
-        const u32x4 a = __builtin_nontemporal_load(gp + 1);
-        v1 = make_uint4(a.x, a.y, a.z, a.w);
-      }
-      *reinterpret_cast<uint4*>(&L.rp[lane * 8]) = v0;
-      *reinterpret_cast<uint4*>(&L.rp[lane * 8 + 4]) = v1;
+      (void)wbase;  // the raw bytes came with the prefetch (stage3), bytes >= nb zero
+      uint4 v0 = *reinterpret_cast<const uint4*>(&L.rp[lane * 8]);
+      uint4 v1 = *reinterpret_cast<const uint4*>(&L.rp[lane * 8 + 4]);
+      if (p0 >= nb) v0 = make_uint4(0, 0, 0, 0);
+      if (p0 + 16 >= nb) v1 = make_uint4(0, 0, 0, 0);
       const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
       uint32_t Wh = 0, Ih = 0, Sh = 0, CSh = 0, Dh = 0, Xh = 0;
 #pragma unroll
@@ -352,45 +414,78 @@ __global__ __launch_bounds__(64 * WAVES) void scan_kernel(TokParams P, SplitPara
       W = Wh; I = Ih; S_ = Sh; CS = CSh; D = Dh; X = Xh & inwin;
     }
     wsync();
+    STAMP(2);
     bool bad = false;
     uint32_t sp_m = 0, sp_w = 0, sp_d = 0;  // this lane's last char / special running into the next lane
     {
       const int p0 = lane * 32;
-      for (uint32_t xm = X; xm;) {
-        const int i = __ffs(xm) - 1;
-        xm &= xm - 1;
-        const int p = p0 + i;
-        const uint32_t b = rawb(L, p);
-        if (b == '[') {
-          int se = nb;  // end of p's sentence
-          for (int j = 1; j < ns; ++j)
-            if (L.sst[j] > p) { se = L.sst[j]; break; }
-          int len = 0, sk = -1;
-          if (p + 5 <= se) {
-            const uint32_t c1 = rawb(L, p + 1), c2 = rawb(L, p + 2), c3 = rawb(L, p + 3), c4 = rawb(L, p + 4);
-            if (c1 == 'P' && c2 == 'A' && c3 == 'D' && c4 == ']') { sk = 0; len = 5; }
-            else if (c1 == 'U' && c2 == 'N' && c3 == 'K' && c4 == ']') { sk = 1; len = 5; }
-            else if (c1 == 'C' && c2 == 'L' && c3 == 'S' && c4 == ']') { sk = 2; len = 5; }
-            else if (c1 == 'S' && c2 == 'E' && c3 == 'P' && c4 == ']') { sk = 3; len = 5; }
-            else if (c1 == 'M' && c2 == 'A' && c3 == 'S' && c4 == 'K' && p + 6 <= se && rawb(L, p + 5) == ']') { sk = 4; len = 6; }
+      // exceptions in batches of 4 per lane: the table lookups of a batch
+      // (code point -> page -> entry -> multi expansion) go out together
+      for (uint32_t xm = X; __any(xm != 0);) {
+        constexpr int XB = 4;
+        int xi_[XB];
+        uint32_t xcp[XB], xt[XB], xe[XB];
+        uint4 xmul[XB];
+#pragma unroll
+        for (int j = 0; j < XB; ++j) {
+          xi_[j] = -1;
+          xcp[j] = 0;
+          if (xm) {
+            const int i = __ffs(xm) - 1;
+            xm &= xm - 1;
+            xi_[j] = i;
+            const int p = p0 + i;
+            const uint32_t b = rawb(L, p);
+            if (b != '[') {
+              const int n = utf8_len(b);
+              uint32_t cp = b & (0x3Fu >> (n - 1));
+              for (int q = 1; q < n; ++q) cp = (cp << 6) | (rawb(L, p + q) & 0x3Fu);
+              if (cp > 0x10FFFF) cp = 0xFFFD;
+              xcp[j] = cp | 0x80000000u;  // (flag: a char, not '[')
+            }
           }
-          if (sk >= 0) {
-            nput(L.nb, p, BS + (uint32_t)sk);
-            const uint64_t cov = ((1ull << (len - 1)) - 1ull) << (i + 1);
-            const uint32_t cl = (uint32_t)cov;
-            W &= ~cl;
-            I &= ~cl;
-            S_ &= ~cl;
-            CS &= ~cl;
-            D &= ~cl;
-            sp_m |= (uint32_t)(cov >> 32);
+        }
+#pragma unroll
+        for (int j = 0; j < XB; ++j) xt[j] = (xcp[j] >> 31) ? (uint32_t)P.top[(xcp[j] & 0x1FFFFFu) >> 8] : 0u;
+#pragma unroll
+        for (int j = 0; j < XB; ++j) xe[j] = (xcp[j] >> 31) ? P.pages[xt[j] * 256u + (xcp[j] & 255u)] : 0u;
+#pragma unroll
+        for (int j = 0; j < XB; ++j)
+          xmul[j] = (xcp[j] >> 31) && ent_kind(xe[j]) == KIND_MULTI ? P.multi[ent_payload(xe[j])] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int j = 0; j < XB; ++j) {
+          if (xi_[j] < 0) continue;
+          const int i = xi_[j];
+          const int p = p0 + i;
+          const uint32_t b = rawb(L, p);
+          if (!(xcp[j] >> 31)) {  // '['
+            int se = nb;  // end of p's sentence
+            for (int jj = 1; jj < ns; ++jj)
+              if (L.sst[jj] > p) { se = L.sst[jj]; break; }
+            int len = 0, sk = -1;
+            if (p + 5 <= se) {
+              const uint32_t c1 = rawb(L, p + 1), c2 = rawb(L, p + 2), c3 = rawb(L, p + 3), c4 = rawb(L, p + 4);
+              if (c1 == 'P' && c2 == 'A' && c3 == 'D' && c4 == ']') { sk = 0; len = 5; }
+              else if (c1 == 'U' && c2 == 'N' && c3 == 'K' && c4 == ']') { sk = 1; len = 5; }
+              else if (c1 == 'C' && c2 == 'L' && c3 == 'S' && c4 == ']') { sk = 2; len = 5; }
+              else if (c1 == 'S' && c2 == 'E' && c3 == 'P' && c4 == ']') { sk = 3; len = 5; }
+              else if (c1 == 'M' && c2 == 'A' && c3 == 'S' && c4 == 'K' && p + 6 <= se && rawb(L, p + 5) == ']') { sk = 4; len = 6; }
+            }
+            if (sk >= 0) {
+              nput(L.nb, p, BS + (uint32_t)sk);
+              const uint64_t cov = ((1ull << (len - 1)) - 1ull) << (i + 1);
+              const uint32_t cl = (uint32_t)cov;
+              W &= ~cl;
+              I &= ~cl;
+              S_ &= ~cl;
+              CS &= ~cl;
+              D &= ~cl;
+              sp_m |= (uint32_t)(cov >> 32);
+            }
+            continue;
           }
-        } else {
           const int n = utf8_len(b);
-          uint32_t cp = b & (0x3Fu >> (n - 1));
-          for (int q = 1; q < n; ++q) cp = (cp << 6) | (rawb(L, p + q) & 0x3Fu);
-          if (cp > 0x10FFFF) cp = 0xFFFD;
-          const uint32_t e = table_entry(P, cp);
+          const uint32_t e = xe[j];
           const uint32_t kind = ent_kind(e), cls = ent_cls(e);
           const uint64_t span = ((1ull << n) - 1ull) << i;
           bool dirty = false, wordc = false;
@@ -408,7 +503,7 @@ __global__ __launch_bounds__(64 * WAVES) void scan_kernel(TokParams P, SplitPara
               uint32_t c0 = ent_payload(e), c1 = 0, c2 = 0;
               int nc = 1;
               if (kind == KIND_MULTI) {
-                const uint4 m = P.multi[ent_payload(e)];
+                const uint4 m = xmul[j];
                 nc = (int)m.x;
                 c0 = ent_payload(m.y);
                 c1 = ent_payload(m.z);
@@ -459,6 +554,7 @@ __global__ __launch_bounds__(64 * WAVES) void scan_kernel(TokParams P, SplitPara
       D = ((D & ~im) | id) & inwin;
     }
     const bool wbad = __any(bad);
+    STAMP(3);
     wsync();
     // ---- 2: units -----------------------------------------------------------
     uint32_t U, SBm;
@@ -482,11 +578,13 @@ __global__ __launch_bounds__(64 * WAVES) void scan_kernel(TokParams P, SplitPara
     // every sentence start distinct (no empty sentence shares one): a unit's
     // sentence is the number of starts at or before it, minus one
     const bool starts_distinct = nstarts == ns;
+    STAMP(4);
     if (wbad) {
       fallback();
-      continue;
+      return;
     }
-    const int64_t ent0 = (A - base) - aoff - ebase;  // entry index of window position 0
+    const int64_t obase = (A - base) - aoff;  // output index of window position 0
+    const int64_t ent0 = obase - ebase;       // entry index of window position 0
     int prev_sent = -1;
     bool ovf = false;
     for (int rb = 0; rb < n; rb += UCAP) {
@@ -514,6 +612,7 @@ __global__ __launch_bounds__(64 * WAVES) void scan_kernel(TokParams P, SplitPara
         }
       }
       wsync();
+      STAMP(5);
       // ---- 3: prep (spans, dirty words, specials, long words) ---------------
       for (int r = 0; r < nr; r += 64) {
         const int u = r + lane;
@@ -543,6 +642,7 @@ __global__ __launch_bounds__(64 * WAVES) void scan_kernel(TokParams P, SplitPara
         }
       }
       wsync();
+      STAMP(6);
       // ---- 3b: whole-word probe of every pending unit, 4 bucket loads in
       //      flight per lane; hits are resolved here
       {
@@ -574,6 +674,7 @@ __global__ __launch_bounds__(64 * WAVES) void scan_kernel(TokParams P, SplitPara
       L.u.uwp[u] = 0;                                                           \
     }                                                                           \
   }
+        // (slot 0 of the home bucket only: checking slot 1 too measured slower)
         TOK5_FP_ISSUE(0)
         TOK5_FP_ISSUE(1)
         TOK5_FP_ISSUE(2)
@@ -591,6 +692,7 @@ __global__ __launch_bounds__(64 * WAVES) void scan_kernel(TokParams P, SplitPara
         ovf = true;
         break;
       }
+      STAMP(7);
       // ---- 4: entries and records -------------------------------------------
       // Lane l holds units [l*per, l*per + per); segmented (by sentence)
       // exclusive prefix sums give each unit its entry index and its record
@@ -648,9 +750,16 @@ __global__ __launch_bounds__(64 * WAVES) void scan_kernel(TokParams P, SplitPara
             nsl[k] = wlen(L.u.uwp[u0 + k]) <= KEY1 ? 1u : 2u;
           mine += nsl[k];
         }
-        seg_scan(nsl, cont ? (uint32_t)L.sslot[first_sent] : 0u, spre);
-        const uint32_t xs = wave_incl_add(mine);
-        const uint32_t need = lane_get(xs, 63);
+        // slots and queued entries per sentence in one scan (slots | count << 16)
+        uint32_t nsd[K], ndef = 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          nsd[k] = nsl[k] | (nsl[k] ? 0x10000u : 0u);
+          ndef += nsl[k] ? 1u : 0u;
+        }
+        seg_scan(nsd, cont ? ((uint32_t)L.sslot[first_sent] | (L.sdef[first_sent] << 16)) : 0u, spre);
+        const uint32_t xs = wave_incl_add(mine | (ndef << 16));
+        const uint32_t need = lane_get(xs, 63) & 0xFFFFu;
         // this round's slots come from the wave's chunk; a sentence's slots
         // stay contiguous: on a chunk switch, the slots the running sentence
         // took in earlier rounds move to the new chunk
@@ -682,61 +791,85 @@ __global__ __launch_bounds__(64 * WAVES) void scan_kernel(TokParams P, SplitPara
             cur += carried;
           }
         }
-        uint32_t gp = cur + (xs - mine);  // global slot of this lane's first record
+        const uint32_t xpre = xs - (mine | (ndef << 16));
+        uint32_t gp = cur + (xpre & 0xFFFFu);  // global slot of this lane's first record
+        uint32_t qi = xpre >> 16;              // its rank among the round's queued units
+        uint16_t* qlist = L.uid;
+        wsync();  // (every lane has read its units' uid)
 #pragma unroll
         for (int k = 0; k < K; ++k) {
           if (!valid[k]) continue;
           const int uu = u0 + k;
           const int sj = (int)sent[k];
-          const uint32_t e = epre[k], o = spre[k];
+          const uint32_t e = epre[k], o = spre[k] & 0xFFFFu;
           if (uu == nr - 1 || (int)(L.u.urec[uu + 1] >> 16) != sj) {  // the sentence's last unit of the round
             L.sent_n[sj] = (uint16_t)min(e + ev[k], 65535u);
             L.sslot[sj] = (uint16_t)(o + nsl[k]);
+            L.sdef[sj] = (spre[k] >> 16) + (nsl[k] ? 1u : 0u);
           }
           if (ev[k] && (int)e < max_tok) {
-            uint16_t* ep = S.ent + (ent0 + (int64_t)L.sst[sj] + e);
+            const int64_t at = (int64_t)L.sst[sj] + e;
             if (idv[k] != U_DEFER) {
-              *ep = (uint16_t)idv[k];
+              if (o == 0) P.out_ids[obase + at] = (uint16_t)idv[k];  // no queued word before it: final
+              else S.ent[ent0 + at] = (uint16_t)idv[k];
             } else {
-              *ep = (uint16_t)(SPLIT_EDEF | o);
-              if (o == 0) L.sqb[sj] = gp;
-              atomicAdd(&L.sdef[sj], 1u);
-              // the record: {len | slots << 8 | valid, count, key bytes 0..55}
-              const uint32_t w = L.u.uwp[uu];
-              const int len = wlen(w), src = wsrc(w);
-              const int a = src >> 2;
-              const uint32_t sh = (uint32_t)(src & 3);
-              uint32_t x[15];
-#pragma unroll
-              for (int i = 0; i < 15; ++i) x[i] = L.nb[a + i];
-              uint32_t kd[14];
-#pragma unroll
-              for (int i = 0; i < 14; ++i) kd[i] = keep_bytes(__builtin_amdgcn_alignbyte(x[i + 1], x[i], sh), len - 4 * i);
-              uint4* rp = S.rec + (size_t)gp * 4;
-              rp[0] = make_uint4((uint32_t)len | (nsl[k] << 8) | 0x80000000u, 0u, kd[0], kd[1]);
-              rp[1] = make_uint4(kd[2], kd[3], kd[4], kd[5]);
-              rp[2] = make_uint4(kd[6], kd[7], kd[8], kd[9]);
-              rp[3] = make_uint4(kd[10], kd[11], kd[12], kd[13]);
-              if (nsl[k] == 2) {  // the extension slot: a zero header (skipped by wp_kernel), pieces 28..
-                const uint4 z = make_uint4(0, 0, 0, 0);
-                rp[4] = z;
-                rp[5] = z;
-                rp[6] = z;
-                rp[7] = z;
+              S.ent[ent0 + at] = (uint16_t)(SPLIT_EDEF | o);
+              if (o == 0) {
+                L.sqb[sj] = gp;
+                L.sfdef[sj] = e;
               }
+              qlist[qi++] = (uint16_t)uu;
             }
           }
           gp += nsl[k];
+        }
+        wsync();
+        // the records, one queued unit per lane:
+        // {len | slots << 8 | valid, count, key bytes 0..55}
+        const uint32_t nq = lane_get(xs, 63) >> 16;
+        // (the list is in unit order, as the slots: a scan of the slot counts places them)
+        uint32_t qslot = cur;
+        for (uint32_t q0 = 0; q0 < nq; q0 += 64) {
+          const uint32_t q = q0 + lane;
+          const uint32_t w = q < nq ? L.u.uwp[qlist[q]] : 0u;
+          const uint32_t nslq = q < nq ? (wlen(w) <= KEY1 ? 1u : 2u) : 0u;
+          const uint32_t xq = wave_incl_add(nslq);
+          const uint32_t slot = qslot + xq - nslq;
+          qslot += lane_get(xq, 63);
+          if (q >= nq) continue;
+          const int len = wlen(w), src = wsrc(w);
+          const int a = src >> 2;
+          const uint32_t sh = (uint32_t)(src & 3);
+          uint32_t x[15];
+#pragma unroll
+          for (int i = 0; i < 15; ++i) x[i] = L.nb[a + i];
+          uint32_t kd[14];
+#pragma unroll
+          for (int i = 0; i < 14; ++i) kd[i] = keep_bytes(__builtin_amdgcn_alignbyte(x[i + 1], x[i], sh), len - 4 * i);
+          const uint32_t slots = len <= KEY1 ? 1u : 2u;
+          uint4* rp = S.rec + (size_t)slot * 4;
+          rp[0] = make_uint4((uint32_t)len | (slots << 8) | 0x80000000u, 0u, kd[0], kd[1]);
+          rp[1] = make_uint4(kd[2], kd[3], kd[4], kd[5]);
+          rp[2] = make_uint4(kd[6], kd[7], kd[8], kd[9]);
+          rp[3] = make_uint4(kd[10], kd[11], kd[12], kd[13]);
+          if (slots == 2) {  // the extension slot: a zero header (skipped by wp_kernel), pieces 28..
+            const uint4 z = make_uint4(0, 0, 0, 0);
+            rp[4] = z;
+            rp[5] = z;
+            rp[6] = z;
+            rp[7] = z;
+          }
         }
         cur += need;
       }
       wsync();
       prev_sent = (int)(L.u.urec[nr - 1] >> 16);
       wsync();
+      STAMP(8);
     }  // rounds
     if (ovf) {
       fallback();
-      continue;
+      return;
     }
     if (lane < ns) {
       const int64_t s = sa + lane;
@@ -744,15 +877,27 @@ __global__ __launch_bounds__(64 * WAVES) void scan_kernel(TokParams P, SplitPara
       const int nsl = L.sslot[lane];
       S.nent[s] = (uint16_t)ne;
       S.nslot[s] = (uint16_t)nsl;
-      if (nsl) S.qb[s] = L.sqb[lane];
+      if (nsl) {
+        S.qb[s] = L.sqb[lane];
+        S.fdef[s] = (uint16_t)L.sfdef[lane];
+      }
       P.out_ntok[s] = ne - (int)L.sdef[lane];
     }
+  
+    }();
+    STAMP(9);
+    STAMP(10);
+    if (DBG) acc[11] += 1;
   }
+  if (DBG && lane == 0)
+    for (int k = 0; k < 12; ++k) atomicAdd((unsigned long long*)&P.dbg[k], (unsigned long long)acc[k]);
+#undef STAMP
   if (chunk >= 0 && lane == 0) S.chunk_fill[chunk] = cur - cbase;
 }
 
 // ------------------------------------------------------------ WordPiece --
-constexpr int KB_DW = 21;  // per-lane key buffer in LDS (dwords; odd stride: no bank conflicts)
+constexpr int KB_DW = 16;  // per-lane key buffer in LDS: dword i of lane l at [i][l] (conflict-free
+                           // reads at any per-lane offset); reads past dword 15 are clamped (zeros)
 
 // u16 index of piece q in a record (slot 0: pieces 0..27 from byte 8; the
 // extension slot keeps its zero header: pieces 28.. from its byte 4)
@@ -766,8 +911,9 @@ __global__ __launch_bounds__(64 * WAVES) void wp_kernel(TokParams P, SplitParams
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  uint32_t* kb = kbuf + (wv * 64 + lane) * KB_DW;
-  const uint8_t* kb8 = reinterpret_cast<const uint8_t*>(kb);
+  uint32_t* kb = kbuf + wv * 64 * KB_DW + lane;  // dword i at kb[64 * i]
+  auto kdw = [&](int i) { return kb[64 * min(i, KB_DW - 1)]; };
+  auto kbyte = [&](int i) { return (kdw(i >> 2) >> (8 * (i & 3))) & 0xFFu; };
   const uint32_t nch = min(__builtin_amdgcn_readfirstlane(*S.chunk_ctr), S.n_chunks);
   const uint32_t nwaves = gridDim.x * WAVES;
   const int mb0 = (int)P.maxb[0], mb1 = (int)P.maxb[1];
@@ -794,8 +940,8 @@ __global__ __launch_bounds__(64 * WAVES) void wp_kernel(TokParams P, SplitParams
   auto load_cand = [&]() {
     const int a = s >> 2;
     const uint32_t sh = (uint32_t)(s & 3);
-    const uint32_t x0 = kb[a], x1 = kb[a + 1], x2 = kb[a + 2], x3 = kb[a + 3], x4 = kb[a + 4], x5 = kb[a + 5],
-                   x6 = kb[a + 6];
+    const uint32_t x0 = kdw(a), x1 = kdw(a + 1), x2 = kdw(a + 2), x3 = kdw(a + 3), x4 = kdw(a + 4), x5 = kdw(a + 5),
+                   x6 = kdw(a + 6);
     c0 = __builtin_amdgcn_alignbyte(x1, x0, sh);
     c1 = __builtin_amdgcn_alignbyte(x2, x1, sh);
     c2 = __builtin_amdgcn_alignbyte(x3, x2, sh);
@@ -829,14 +975,14 @@ __global__ __launch_bounds__(64 * WAVES) void wp_kernel(TokParams P, SplitParams
   auto shrink = [&]() {  // previous char boundary
     --e;
     if (!(asc && e - s < 24))
-      while (e > s && (kb8[e] & 0xC0u) == 0x80u) --e;
+      while (e > s && (kbyte(e) & 0xC0u) == 0x80u) --e;
   };
   auto start_piece = [&](int maxb) {
     bslot = -1;
     load_cand();
     e = min(we, s + maxb);
     if (e < we && !(asc && e - s < 24))
-      while (e > s && (kb8[e] & 0xC0u) == 0x80u) --e;
+      while (e > s && (kbyte(e) & 0xC0u) == 0x80u) --e;
   };
   auto rec16 = [&]() { return reinterpret_cast<uint16_t*>(S.rec + (size_t)r * 4); };
   auto finish = [&]() {
@@ -946,9 +1092,9 @@ __global__ __launch_bounds__(64 * WAVES) void wp_kernel(TokParams P, SplitParams
                    (b1.x ^ m4c) | (b1.y ^ m5c)) == 0u;
         if (len > 24) {  // the rest of a long key against the pool
           if (m0)
-            for (int k = 24; k < len; ++k) m0 = m0 && kb8[s + k] == P.pool[a1.w + k];
+            for (int k = 24; k < len; ++k) m0 = m0 && kbyte(s + k) == P.pool[a1.w + k];
           if (m1)
-            for (int k = 24; k < len; ++k) m1 = m1 && kb8[s + k] == P.pool[b1.w + k];
+            for (int k = 24; k < len; ++k) m1 = m1 && kbyte(s + k) == P.pool[b1.w + k];
         }
         if (m0 || m1) {
           rec16()[piece_at(np)] = (uint16_t)((m0 ? a1.z : b1.z) & 0xFFFFu);
@@ -974,14 +1120,12 @@ __global__ __launch_bounds__(64 * WAVES) void wp_kernel(TokParams P, SplitParams
         pr = -1;
       } else {
         const int len = (int)(q0.x & 0xFFu);
-        uint4* k4 = reinterpret_cast<uint4*>(kb);  // (KB_DW odd: dword stores)
-        (void)k4;
-        kb[0] = q0.z; kb[1] = q0.w;
-        kb[2] = q1.x; kb[3] = q1.y; kb[4] = q1.z; kb[5] = q1.w;
-        kb[6] = q2.x; kb[7] = q2.y; kb[8] = q2.z; kb[9] = q2.w;
-        kb[10] = q3.x; kb[11] = q3.y; kb[12] = q3.z; kb[13] = q3.w;
-#pragma unroll
-        for (int i = 14; i < KB_DW; ++i) kb[i] = 0u;
+        kb[0] = q0.z; kb[64] = q0.w;
+        kb[128] = q1.x; kb[192] = q1.y; kb[256] = q1.z; kb[320] = q1.w;
+        kb[384] = q2.x; kb[448] = q2.y; kb[512] = q2.z; kb[576] = q2.w;
+        kb[640] = q3.x; kb[704] = q3.y; kb[768] = q3.z; kb[832] = q3.w;
+        kb[896] = 0u;
+        kb[960] = 0u;
         r = pr;
         pr = -1;
         s = 0;
@@ -995,28 +1139,19 @@ __global__ __launch_bounds__(64 * WAVES) void wp_kernel(TokParams P, SplitParams
   }
 }
 
-// ---------------------------------------------------------------- count --
-__global__ __launch_bounds__(256) void count_kernel(TokParams P, SplitParams S) {
-  const int64_t sA = S.tile_sent[S.t0], sB = S.tile_sent[S.t1];
-  for (int64_t s = sA + (int64_t)blockIdx.x * 256 + threadIdx.x; s < sB; s += (int64_t)gridDim.x * 256) {
-    const int nsl = S.nslot[s];
-    if (nsl == 0) continue;
-    const uint32_t g = S.qb[s];
-    int sum = 0;
-    for (int k = 0; k < nsl; ++k) sum += (int)reinterpret_cast<const uint32_t*>(S.rec + (size_t)(g + k) * 4)[1];
-    P.out_ntok[s] = min(P.out_ntok[s] + sum, P.max_tok);
-  }
-}
-
 // --------------------------------------------------------------- expand --
-// A wave per group of 64 sentences; their entries in steps of 256 (4 per
-// lane, contiguous); a record entry expands to its pieces.
+// A wave per group of 64 sentences; their entries in steps of 512 (8 per
+// lane, contiguous).  Per step, two rounds of loads: the entries, then the
+// records' count and first 4 pieces (one 12-B load); a segmented scan of the
+// token counts gives the positions; the sentence's last entry writes its
+// token count (a sentence with no queued word keeps the scan's count).
+constexpr int EXP_PER = 4;
 struct ExpLds {
   uint32_t e0[65];      // group entry offsets
   int64_t eoff[64];     // entry index of the sentence's first entry
   int64_t dst[64];      // output index of its first token
-  uint32_t qb[64];
-  int32_t cap[64];      // its final token count
+  uint32_t qb[64];      // its first record slot
+  uint32_t f[64];       // entry index of its first queued word (the entries before it are done)
 };
 
 __global__ __launch_bounds__(256) void expand_kernel(TokParams P, SplitParams S) {
@@ -1026,24 +1161,28 @@ __global__ __launch_bounds__(256) void expand_kernel(TokParams P, SplitParams S)
   ExpLds& E = X[wv];
   const int64_t sA = uni64(S.tile_sent[S.t0]), sB = uni64(S.tile_sent[S.t1]);
   const int64_t base = P.sent_off[0], ebase = S.t0 << 10;
-  const bool dense = S.dense != nullptr;
-  uint16_t* out = dense ? S.dense : P.out_ids;
+  const uint32_t max_tok0 = (uint32_t)P.max_tok;
   const int64_t nwaves = (int64_t)gridDim.x * 4;
+  typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
   for (int64_t g0 = sA + ((int64_t)blockIdx.x * 4 + wv) * 64; g0 < sB; g0 += nwaves * 64) {
     const int64_t s = g0 + lane;
     uint32_t ne = 0;
-    bool fb = false;
     if (s < sB) {
+      // entries from the first queued word on (the ids before it are final;
+      // a sentence without queued words or of a fallback tile is done)
       ne = S.nent[s];
-      fb = ne == SPLIT_NENT_FB;
-      const int64_t so = P.sent_off[s] - base;
-      const int32_t cap = P.out_ntok[s];
+      uint32_t f = 0;
+      if (ne == SPLIT_NENT_FB || S.nslot[s] == 0) {
+        ne = 0;
+      } else {
+        f = S.fdef[s];
+        ne -= f;
+      }
+      const int64_t so = P.sent_off[s] - base + f;
       E.eoff[lane] = so - ebase;
-      E.dst[lane] = dense ? S.tokoff[s] : so;
-      E.qb[lane] = S.nslot[s] ? S.qb[s] : 0u;
-      E.cap[lane] = cap;
-      if (fb) ne = dense ? (uint32_t)cap : 0u;  // a fallback tile's sentence: its ids are final (sparse) already
-      if (fb) E.eoff[lane] = -1 - so;            // (dense: copy them from the sparse output)
+      E.dst[lane] = so;
+      E.qb[lane] = ne ? S.qb[s] : 0u;
+      E.f[lane] = f;
     }
     const uint32_t x = wave_incl_add(ne);
     E.e0[lane] = x - ne;
@@ -1051,11 +1190,10 @@ __global__ __launch_bounds__(256) void expand_kernel(TokParams P, SplitParams S)
     if (lane == 63) E.e0[64] = T;
     wsync();
     uint32_t carry = 0;
-    for (uint32_t st = 0; st < T; st += 256) {
-      const uint32_t g = st + (uint32_t)lane * 4;
-      // sentence of this lane's first entry: last j with e0[j] <= g
+    for (uint32_t st = 0; st < T; st += 64 * EXP_PER) {
+      const uint32_t g = st + (uint32_t)lane * EXP_PER;
       int j = 0;
-      if (g < T) {
+      if (g < T) {  // sentence of this lane's first entry: last j with e0[j] <= g
         int lo = 0, hi = 63;
         while (lo < hi) {
           const int mid = (lo + hi + 1) >> 1;
@@ -1064,33 +1202,30 @@ __global__ __launch_bounds__(256) void expand_kernel(TokParams P, SplitParams S)
         }
         j = lo;
       }
-      uint32_t v[4], cnt[4], pre[4];
-      int js[4];
-      bool valid[4], head[4];
+      int js[EXP_PER];
+      uint32_t kk[EXP_PER], v[EXP_PER], cnt[EXP_PER], pre[EXP_PER];
+      u32x3 rq[EXP_PER];
+#pragma unroll
+      for (int k = 0; k < EXP_PER; ++k) {
+        const uint32_t gg = g + k;
+        while (gg < T && j < 63 && E.e0[j + 1] <= gg) ++j;
+        js[k] = j;
+        kk[k] = gg < T ? gg - E.e0[j] : 0xFFFFFFFFu;
+      }
+#pragma unroll
+      for (int k = 0; k < EXP_PER; ++k) v[k] = kk[k] != 0xFFFFFFFFu ? S.ent[E.eoff[js[k]] + kk[k]] : 0u;
+#pragma unroll
+      for (int k = 0; k < EXP_PER; ++k) {
+        rq[k] = u32x3{1u, 0u, 0u};
+        if (kk[k] != 0xFFFFFFFFu && v[k] >= SPLIT_EDEF)
+          rq[k] = *reinterpret_cast<const u32x3*>(reinterpret_cast<const uint32_t*>(
+                      S.rec + (size_t)(E.qb[js[k]] + (v[k] & 0xFFFu)) * 4) + 1);
+      }
       uint32_t run = 0, h = 0;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const uint32_t gg = g + k;
-        valid[k] = gg < T;
-        while (valid[k] && j < 63 && E.e0[j + 1] <= gg) ++j;
-        js[k] = j;
-        const uint32_t kk = valid[k] ? gg - E.e0[j] : 0u;
-        head[k] = valid[k] && kk == 0;
-        v[k] = 0;
-        cnt[k] = 0;
-        if (valid[k]) {
-          const int64_t eo = E.eoff[j];
-          if (eo >= 0) {
-            v[k] = S.ent[eo + kk];
-            cnt[k] = v[k] >= SPLIT_EDEF
-                         ? reinterpret_cast<const uint32_t*>(S.rec + (size_t)(E.qb[j] + (v[k] & 0xFFFu)) * 4)[1]
-                         : 1u;
-          } else {  // fallback sentence (dense): its final ids from the sparse output
-            v[k] = P.out_ids[(-1 - eo) + kk];
-            cnt[k] = 1;
-          }
-        }
-        if (head[k]) {
+      for (int k = 0; k < EXP_PER; ++k) {
+        cnt[k] = kk[k] != 0xFFFFFFFFu ? rq[k].x : 0u;
+        if (kk[k] == 0) {
           run = 0;
           h = 1;
         }
@@ -1103,29 +1238,39 @@ __global__ __launch_bounds__(256) void expand_kernel(TokParams P, SplitParams S)
       if (!wave_shr1(hv)) ex += carry;
       bool before = true;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        if (valid[k] && head[k]) before = false;
+      for (int k = 0; k < EXP_PER; ++k) {
+        if (kk[k] == 0) before = false;
         if (before) pre[k] += ex;
       }
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        if (!valid[k]) continue;
+      for (int k = 0; k < EXP_PER; ++k) {
+        if (kk[k] == 0xFFFFFFFFu) continue;
         const int jj = js[k];
-        uint16_t* o = out + E.dst[jj];
-        const int cap = E.cap[jj];
-        if (v[k] < SPLIT_EDEF || E.eoff[jj] < 0) {
-          if ((int)pre[k] < cap) o[pre[k]] = (uint16_t)v[k];
+        uint16_t* o = P.out_ids + E.dst[jj];
+        const uint32_t p = pre[k];
+        const uint32_t max_tok = max_tok0 - E.f[jj];  // (entries are kept below max_tok: f < max_tok)
+        if (v[k] < SPLIT_EDEF) {
+          if (p < max_tok) o[p] = (uint16_t)v[k];
         } else {
-          const uint16_t* pc = reinterpret_cast<const uint16_t*>(S.rec + (size_t)(E.qb[jj] + (v[k] & 0xFFFu)) * 4);
-          for (uint32_t q = 0; q < cnt[k] && (int)(pre[k] + q) < cap; ++q) o[pre[k] + q] = pc[piece_at((int)q)];
+          const uint32_t c = cnt[k];
+          if (p < max_tok) o[p] = (uint16_t)(rq[k].y & 0xFFFFu);
+          if (c > 1 && p + 1 < max_tok) o[p + 1] = (uint16_t)(rq[k].y >> 16);
+          if (c > 2 && p + 2 < max_tok) o[p + 2] = (uint16_t)(rq[k].z & 0xFFFFu);
+          if (c > 3 && p + 3 < max_tok) o[p + 3] = (uint16_t)(rq[k].z >> 16);
+          if (c > 4) {
+            const uint16_t* pc =
+                reinterpret_cast<const uint16_t*>(S.rec + (size_t)(E.qb[jj] + (v[k] & 0xFFFu)) * 4);
+            for (uint32_t q = 4; q < c && p + q < max_tok; ++q) o[p + q] = pc[piece_at((int)q)];
+          }
         }
+        if (kk[k] + 1 == E.e0[jj + 1] - E.e0[jj]) P.out_ntok[g0 + jj] = (int32_t)min(E.f[jj] + p + cnt[k], max_tok0);
       }
       // running total of the step's last entry (its sentence may continue)
-      const uint32_t lastg = min(T, st + 256) - 1 - st;  // index within the step
-      const int ll = (int)(lastg >> 2), lk = (int)(lastg & 3);
+      const uint32_t lastg = min(T, st + 64 * EXP_PER) - 1 - st;
+      const int ll = (int)(lastg / EXP_PER), lk = (int)(lastg % EXP_PER);
       uint32_t mytot = 0;
 #pragma unroll
-      for (int k = 0; k < 4; ++k)
+      for (int k = 0; k < EXP_PER; ++k)
         if (k == lk) mytot = pre[k] + cnt[k];
       carry = lane_get(mytot, ll);
     }
@@ -1133,18 +1278,19 @@ __global__ __launch_bounds__(256) void expand_kernel(TokParams P, SplitParams S)
   }
 }
 
-template <int WAVES>
+template <int WAVES, bool DBG, int OCC>
 static hipError_t launch_scan(const TokParams& P, const SplitParams& S, int n_cu, hipStream_t s) {
   static int per_cu = 0;
   if (per_cu == 0 &&
-      (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, scan_kernel<WAVES>, 64 * WAVES, 0) != hipSuccess ||
+      (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, scan_kernel<WAVES, DBG, OCC>, 64 * WAVES, 0) !=
+           hipSuccess ||
        per_cu < 1))
     per_cu = 1;
   int64_t grid = (int64_t)n_cu * per_cu;
   const int64_t need = (S.t1 - S.t0 + WAVES - 1) / WAVES;
   if (grid > need) grid = need;
   if (grid < 1) grid = 1;
-  hipLaunchKernelGGL(scan_kernel<WAVES>, dim3((unsigned)grid), dim3(64 * WAVES), 0, s, P, S);
+  hipLaunchKernelGGL((scan_kernel<WAVES, DBG, OCC>), dim3((unsigned)grid), dim3(64 * WAVES), 0, s, P, S);
   return hipGetLastError();
 }
 
@@ -1162,7 +1308,7 @@ static hipError_t launch_wp(const TokParams& P, const SplitParams& S, int n_cu, 
 
 }  // namespace tok5
 
-constexpr int SCAN_WAVES = 8, WP_WAVES = 8;
+constexpr int SCAN_WAVES = 4, WP_WAVES = 12;
 
 int64_t split_seg_slots(int64_t seg_tiles) {
   // 1 slot per 16 input bytes (the synthetic Wikipedia corpus queues ~0.02
@@ -1173,7 +1319,7 @@ int64_t split_seg_slots(int64_t seg_tiles) {
 }
 
 hipError_t launch_tokenize_split(const TokParams& P, int64_t nbytes, int64_t* tile_sent, SplitParams S, int n_cu,
-                                 int fb_grid, hipStream_t s) {
+                                 int fb_grid, int cfg, hipStream_t s) {
   const int64_t n_tiles = tile_count(nbytes);
   hipError_t e = launch_tile_bounds(P.sent_off, P.n_sent, n_tiles, tile_sent, s);
   if (e != hipSuccess) return e;
@@ -1184,10 +1330,12 @@ hipError_t launch_tokenize_split(const TokParams& P, int64_t nbytes, int64_t* ti
     S.t0 = t0;
     S.t1 = std::min(n_tiles, t0 + seg);
     if ((e = hipMemsetAsync(S.chunk_ctr, 0, 4, s)) != hipSuccess) return e;
-    if ((e = tok5::launch_scan<SCAN_WAVES>(P, S, n_cu, s)) != hipSuccess) return e;
+    // cfg (LDDL_TOK5_CFG, tuning): 1 = registers unconstrained (4 waves/SIMD)
+    if (P.dbg) e = tok5::launch_scan<SCAN_WAVES, true, 5>(P, S, n_cu, s);
+    else if (cfg == 1) e = tok5::launch_scan<SCAN_WAVES, false, 1>(P, S, n_cu, s);
+    else e = tok5::launch_scan<SCAN_WAVES, false, 5>(P, S, n_cu, s);
+    if (e != hipSuccess) return e;
     if ((e = tok5::launch_wp<WP_WAVES>(P, S, n_cu, s)) != hipSuccess) return e;
-    hipLaunchKernelGGL(tok5::count_kernel, dim3((unsigned)std::max(1, n_cu * 8)), dim3(256), 0, s, P, S);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
     hipLaunchKernelGGL(tok5::expand_kernel, dim3((unsigned)std::max(1, n_cu * 8)), dim3(256), 0, s, P, S);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }

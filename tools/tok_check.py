@@ -34,6 +34,7 @@ def main():
     algo, _, cfg = v.partition(':')
     os.environ['LDDL_TOKENIZE_ALGO'] = algo
     os.environ['LDDL_TOK4_CFG'] = cfg or '0'
+    os.environ['LDDL_TOK5_CFG'] = cfg or '0'
     tok = Tokenizer()
     ids, ntok = tok.tokenize_device(d, o)
     torch.cuda.synchronize()
