@@ -311,10 +311,37 @@ def attach_args(parser=None):
   return parser
 
 
-def main(args, rank=0, world=1):
+def rank_world():
+  """(rank, world) of this process: torch.distributed.run (RANK / WORLD_SIZE)
+  or mpirun / srun (OMPI_COMM_WORLD_*, PMI_*, SLURM_*), as the reference
+  balancer runs under MPI (load_balance.py:381-445)."""
+  for r, w in (('RANK', 'WORLD_SIZE'), ('OMPI_COMM_WORLD_RANK', 'OMPI_COMM_WORLD_SIZE'), ('PMI_RANK', 'PMI_SIZE'),
+               ('SLURM_PROCID', 'SLURM_NTASKS')):
+    if r in os.environ and w in os.environ:
+      return int(os.environ[r]), int(os.environ[w])
+  return 0, 1
+
+
+def _barrier(world):
+  """host barrier between the ranks (gloo; initialised from the launcher's
+  env, MASTER_ADDR / MASTER_PORT)"""
+  if world <= 1:
+    return
+  import torch.distributed as dist
+  if not dist.is_initialized():
+    rank, world = rank_world()
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+  dist.barrier()
+
+
+def main(args, rank=None, world=None):
   """Counts from the parquet footers (no table reads), plan, write, and
-  .num_samples.json (rank 0)."""
+  .num_samples.json (rank 0).  Every rank plans the same shards and writes
+  shard k when k % world == rank (load_balance.py:129-140 ownership); once
+  every rank is done, rank 0 removes the input files (unless --keep-orig)."""
   import pyarrow.parquet as pq
+  if rank is None or world is None:
+    rank, world = rank_world()
   outdir = args.indir if args.outdir is None else os.path.abspath(os.path.expanduser(args.outdir))
   os.makedirs(outdir, exist_ok=True)
   paths = sorted(os.path.join(r, f) for r, _, fs in os.walk(args.indir) for f in fs
@@ -322,10 +349,13 @@ def main(args, rank=0, world=1):
   counts = [pq.ParquetFile(p).metadata.num_rows for p in paths]
   shards, ns = plan_files(paths, counts, args.num_shards, args.bin_ids)
   written = write_shards(shards, outdir, rank, world)
-  if not args.keep_orig and world == 1:
-    for p in paths:
-      os.remove(p)
+  _barrier(world)
   if rank == 0:
+    if not args.keep_orig:
+      keep = set(os.path.abspath(p) for p in written) | {os.path.abspath(os.path.join(outdir, n)) for n, _, _ in shards}
+      for p in paths:
+        if os.path.abspath(p) not in keep:
+          os.remove(p)
     store_num_samples(ns, outdir)
   return written, ns
 

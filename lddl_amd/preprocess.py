@@ -8,19 +8,30 @@ Same flags, same input layout, same output files:
   ``--books``, ``--common-crawl`` (``**.txt``), or ``--code`` (CodeBERT,
   ``**.txt`` of ``id<CODESPLIT>docstring<CODESPLIT>code`` records separated
   by ``\\r\\n``, readers.py:119-128); one document per non-empty stripped line
-  (readers.py:30-31), id = text up to the first whitespace, body = the rest
-  after skipping one character (readers.py:142-147);
+  as dask's read_text cuts lines (lddl_amd/readers.py), id = text up to the
+  first whitespace, body = the rest after skipping one character
+  (readers.py:142-147);
+* partitions: one per input file, or per dask read_bytes block of each file
+  with ``--block-size`` / ``--num-blocks`` (readers.py:43-57); CodeBERT: one
+  per file (pretrain_codebert.py:479-485);
 * output: ``--sink``/``part.{i}.parquet`` or ``part.{i}.parquet_{b}`` with
   the reference schema (lddl_amd/writer.py), ready for the load balancer
-  (``python -m lddl_amd.balance``, load_balance.py).
+  (``python -m lddl_amd.balance``, load_balance.py); or, with
+  ``--num-shards``, balanced straight away: the per-(partition, bin) row
+  counts of every rank come from the packer through ONE all-gather (RCCL on
+  the GPUs, ``balance.gather_bin_counts``) in place of the balancer's count
+  pass over the files (load_balance.py:222-233), and each rank writes its
+  ``shard-{k}.parquet[_b]`` files from the plan.
 
 What runs where:
-  host   read + --sample-ratio sampling + document shuffle + partitioning of
-         the shuffled raw documents into --num-blocks / --block-size byte
-         blocks (readers.py:48-57; like the reference's partitions they are
-         fixed before the split) + sentence split (NLTK Punkt when
-         importable, pretrain.py:86; else a rule-based stand-in, see
-         ``_rule_split``);
+  host   an index of the input records (file, offset, length: integers
+         only; with several ranks each indexes a share of the files and the
+         shares are all-gathered) + --sample-ratio sampling + document
+         shuffle over the index + partitioning of the shuffled records
+         (equal bytes, fixed before the split like the reference's
+         partitions) + reading and sentence-splitting ONLY this rank's
+         records (NLTK Punkt when importable, pretrain.py:86; else a
+         rule-based stand-in, see ``_rule_split``);
   GPU    tokenize -> pair packing -> binning -> materialisation -> string
          rendering (liblddl_amd.so), then the host parquet encoder.
   The rank's partitions stream through in chunks of --chunk-mb raw MB:
@@ -55,25 +66,15 @@ from . import synth
 
 
 # ----------------------------------------------------------------- input --
-def find_files_under(path, extensions=('.txt',)):
-  """readers.py:34-40"""
-  out = []
-  for d, _, names in os.walk(path):
-    out.extend(os.path.join(d, n) for n in names if os.path.splitext(n)[1] in extensions)
-  return sorted(out)
+from .readers import find_files_under, parse_str_of_num_bytes, estimate_block_size, count_partitions, \
+    iter_lines, RecordIndex  # noqa: E402
 
 
 def read_records(files, linedelimiter=None):
-  """db.read_text + _filter_empty_strs (readers.py:30-31, 60-70): stripped,
-  non-empty lines (records split on linedelimiter for code)."""
+  """db.read_text + _filter_empty_strs (readers.py:30-31, 60-70): the
+  stripped, non-empty lines of the files in order (lddl_amd/readers.py)."""
   for path in files:
-    with open(path, encoding='utf-8', newline='' if linedelimiter else None) as f:
-      text = f.read()
-    parts = text.split(linedelimiter) if linedelimiter else text.splitlines()
-    for s in parts:
-      s = s.strip()
-      if s:
-        yield s
+    yield from iter_lines(path, linedelimiter)
 
 
 def split_id_text(raw):
@@ -127,16 +128,21 @@ def sentence_splitter(kind='auto'):
   return _rule_split, 'rules'
 
 
-def sample_shuffle(records, seed, sample_ratio):
+def sample_order(n, seed, sample_ratio):
   """--sample-ratio sampling (readers.py:67-68) and the document shuffle
-  (pretrain.py:101-112), both from PCG64(seed)."""
+  (pretrain.py:101-112) over n records, both from PCG64(seed): the kept
+  record indices in shuffled order."""
   rng = np.random.Generator(np.random.PCG64(seed))
-  records = list(records)
+  keep = np.arange(n, dtype=np.int64)
   if sample_ratio < 1.0:
-    keep = rng.random(len(records)) < sample_ratio
-    records = [r for r, k in zip(records, keep) if k]
-  order = rng.permutation(len(records))
-  return [records[i] for i in order]
+    keep = keep[rng.random(n) < sample_ratio]
+  return keep[rng.permutation(len(keep))]
+
+
+def sample_shuffle(records, seed, sample_ratio):
+  """sample_order over a list of records (tests, tools)."""
+  records = list(records)
+  return [records[i] for i in sample_order(len(records), seed, sample_ratio)]
 
 
 def split_records(records, codebert=False, splitter=None):
@@ -170,21 +176,26 @@ def build_corpus(records, seed, sample_ratio, codebert=False, splitter=None):
   return split_records(sample_shuffle(records, seed, sample_ratio), codebert, splitter)
 
 
+def partition_by_size(sizes, n_part):
+  """Record offsets of n_part partitions of ~equal bytes over records of the
+  given sizes (in order), documents kept whole."""
+  sizes = np.asarray(sizes, dtype=np.int64)
+  n = max(1, int(n_part))
+  cum = np.concatenate([[0], np.cumsum(sizes)])
+  cuts = np.searchsorted(cum, np.linspace(0, cum[-1], n + 1)[1:-1])
+  off = np.concatenate([[0], cuts, [len(sizes)]]).astype(np.int64)
+  return np.maximum.accumulate(off)
+
+
 def partition_records(records, block_size=None, num_blocks=None):
-  """--block-size / --num-blocks (readers.py:43-57) over the shuffled raw
-  documents: record offsets of partitions of ~equal raw size, documents
-  kept whole (= document offsets of split_records' corpus)."""
+  """--block-size / --num-blocks over a record list (tests, tools): ~equal
+  byte partitions, num_blocks of them, or total / block_size."""
   if num_blocks is not None and block_size is not None:
     raise ValueError('Only one of num_blocks or blocksize needs to be set!')
   sizes = np.fromiter((len(r) for r in records), dtype=np.int64, count=len(records))
-  total = int(sizes.sum())
   if num_blocks is None:
-    num_blocks = max(1, int(round(total / block_size))) if block_size else 1
-  n = max(1, min(num_blocks, max(1, len(records))))
-  cum = np.concatenate([[0], np.cumsum(sizes)])
-  cuts = np.searchsorted(cum, np.linspace(0, cum[-1], n + 1)[1:-1])
-  off = np.concatenate([[0], cuts, [len(records)]]).astype(np.int64)
-  return np.maximum.accumulate(off)
+    num_blocks = max(1, int(round(int(sizes.sum()) / block_size))) if block_size else 1
+  return partition_by_size(sizes, min(num_blocks, max(1, len(records))))
 
 
 def partition_docs(corpus, block_size=None, num_blocks=None):
@@ -219,7 +230,8 @@ def attach_args(parser=None, codebert=False):
   p.add_argument('--output-format', type=str, default='parquet', choices=['parquet'])
   p.add_argument('--target-seq-length', type=int, default=128)
   p.add_argument('--short-seq-prob', type=float, default=0.1)
-  p.add_argument('--block-size', type=int, default=None)
+  p.add_argument('--block-size', type=lambda x: parse_str_of_num_bytes(x, return_str=False), default=None,
+                 help='n[KMG] bytes per dask block (lddl/download/utils.py:42-51)')
   p.add_argument('--num-blocks', type=int, default=None)
   p.add_argument('--bin-size', type=int, default=None)
   p.add_argument('--sample-ratio', type=float, default=0.9)
@@ -236,6 +248,10 @@ def attach_args(parser=None, codebert=False):
                       'the writer on chunk k)')
   p.add_argument('--split-workers', type=int, default=4,
                  help='host processes splitting sentences ahead of the GPU (0: split inline)')
+  p.add_argument('--num-shards', type=int, default=None,
+                 help='balance the output into this many shard-{k}.parquet[_b] files (balance_dask_output, '
+                      'load_balance.py) with counts all-gathered from the packer')
+  p.add_argument('--keep-orig', action='store_true', help='with --num-shards: keep the part files')
   return p
 
 
@@ -247,20 +263,75 @@ def _check(args):
       raise ValueError('Please provide a bin size that can divide the target sequence length.')
 
 
-_FE = {}  # the split workers' fork-inherited state (records, mode, splitter)
+_FE = {}  # the split workers' fork-inherited state (record index, order, mode, splitter)
 
 
 def _split_worker(a, b):
   ts = time.perf_counter()
-  corpus, ids = split_records(_FE['recs'][a:b], _FE['codebert'], _FE['split'])
+  recs = _FE['index'].texts(_FE['order'][a:b])
+  corpus, ids = split_records(recs, _FE['codebert'], _FE['split'])
   return corpus, ids, time.perf_counter() - ts
+
+
+def input_files(args, codebert=False):
+  """(files in the reference's bag order, line delimiter, source roots)"""
+  if codebert:
+    if not args.code:
+      raise ValueError('--code is required')
+    return find_files_under(args.code), '\r\n', [args.code]
+  if not (args.wikipedia or args.books or args.common_crawl):
+    raise ValueError('at least one of --wikipedia, --books and --common-crawl needs to be set')
+  srcs = [os.path.join(args.wikipedia, args.wikipedia_lang) if args.wikipedia else None, args.books,
+          args.common_crawl]
+  # db.concat(bags) of read_wikipedia / read_books / read_common_crawl (pretrain.py:412-438)
+  return [f for s in srcs if s for f in find_files_under(s)], None, [args.wikipedia, args.books, args.common_crawl]
+
+
+def plan_input(args, codebert=False, rank=0, world=1, gloo=None):
+  """The record index of the whole input, the sampled + shuffled record order
+  and the partition offsets into it.  With several ranks each indexes every
+  world-th file and the shares are all-gathered (host, gloo)."""
+  files, delim, roots = input_files(args, codebert)
+  if args.num_blocks is not None and args.block_size is not None:
+    raise ValueError('Only one of num_blocks or blocksize needs to be set!')
+  if codebert:  # read_code ignores the block flags: one partition per file (pretrain_codebert.py:479-485)
+    n_part = len(files)
+  else:
+    bs = args.block_size
+    if args.num_blocks is not None:
+      bs = estimate_block_size(roots, args.num_blocks)  # readers.py:48-57 (the wikipedia ROOT, as the reference)
+    n_part = count_partitions(files, bs)
+  mine = set(range(rank, len(files), world))
+  idx = RecordIndex.build(files, delim, file_ids=mine)
+  if world > 1:
+    import torch.distributed as dist
+    parts = [None] * world
+    dist.all_gather_object(parts, (idx.fid, idx.off, idx.len), group=gloo)
+    idx = RecordIndex.merge(files, [RecordIndex(files, *p) for p in parts])
+  order = sample_order(len(idx), args.seed, args.sample_ratio)
+  pro = partition_by_size(idx.len[order], max(1, n_part))
+  return idx, order, pro
+
+
+def _dist_init(world):
+  """One process per GPU (torch.distributed.run env): the default group on
+  RCCL (nccl backend) for the count all-gather, a gloo group for host
+  objects.  Returns the gloo group (None when single-process)."""
+  if world <= 1:
+    return None
+  import torch
+  import torch.distributed as dist
+  if not dist.is_initialized():
+    # LDDL_DIST_BACKEND=gloo: several ranks on one GPU (tests; RCCL needs a GPU per rank)
+    backend = os.environ.get('LDDL_DIST_BACKEND') or ('nccl' if torch.cuda.is_available() else 'gloo')
+    dist.init_process_group(backend)
+  return dist.new_group(backend='gloo')
 
 
 def main(args, codebert=False):
   """Returns (files written by this rank, timings dict)."""
   import torch
-  from concurrent.futures import ThreadPoolExecutor
-  from . import pipeline, writer
+  from . import pipeline, writer, balance
   _check(args)
   rank = int(os.environ.get('RANK', 0))
   world = int(os.environ.get('WORLD_SIZE', 1))
@@ -270,27 +341,14 @@ def main(args, codebert=False):
     raise ValueError('--vocab-file must be a local vocab.txt (no hub access): %s' % vocab)
   t = {}
   wall0 = t0 = time.perf_counter()
-  if codebert:
-    if not args.code:
-      raise ValueError('--code is required')
-    files = find_files_under(args.code)
-    recs = read_records(files, linedelimiter='\r\n')
-    split, how = None, 'code-lines'
-  else:
-    srcs = [os.path.join(args.wikipedia, args.wikipedia_lang) if args.wikipedia else None, args.books,
-            args.common_crawl]
-    if not any(srcs):
-      raise ValueError('at least one of --wikipedia, --books and --common-crawl needs to be set')
-    files = [f for s in srcs if s for f in find_files_under(s)]
-    recs = read_records(files)
-    split, how = sentence_splitter(args.sentence_splitter)
-  recs = sample_shuffle(recs, args.seed, args.sample_ratio)
-  pro = partition_records(recs, args.block_size, args.num_blocks)
+  gloo = _dist_init(world)
+  split, how = (None, 'code-lines') if codebert else sentence_splitter(args.sentence_splitter)
+  index, order, pro = plan_input(args, codebert, rank, world, gloo)
   n_part = len(pro) - 1
   lo, hi = rank * n_part // world, (rank + 1) * n_part // world
   t['host_read_s'] = time.perf_counter() - t0
   # chunks of this rank's partitions, ~--chunk-mb raw MB each
-  sizes = np.fromiter((len(r) for r in recs[pro[lo]:pro[hi]]), dtype=np.int64, count=int(pro[hi] - pro[lo]))
+  sizes = index.len[order[pro[lo]:pro[hi]]]
   cum = np.concatenate([[0], np.cumsum(sizes)])
   part_end = cum[pro[lo + 1:hi + 1] - pro[lo]]
   chunk_b = max(1, int(args.chunk_mb * (1 << 20)))
@@ -303,12 +361,13 @@ def main(args, codebert=False):
   bounds.append(hi)
   chunks = [(a, b) for a, b in zip(bounds[:-1], bounds[1:]) if b > a]
 
-  # split workers: forked here, before anything touches the GPU
+  # split workers: forked here, before anything touches the GPU; they read
+  # their records from the index (integers only are inherited)
   nw = min(max(0, args.split_workers), len(chunks)) if len(chunks) > 1 else 0
   pool = None
   if nw > 0:
     import multiprocessing
-    _FE.update(recs=recs, codebert=codebert, split=split)
+    _FE.update(index=index, order=order, codebert=codebert, split=split)
     pool = multiprocessing.get_context('fork').Pool(nw)
     _FE.clear()
 
@@ -317,7 +376,7 @@ def main(args, codebert=False):
     if pool is not None:
       return pool.apply_async(_split_worker, (a, b))
     ts = time.perf_counter()
-    corpus, ids = split_records(recs[a:b], codebert, split)
+    corpus, ids = split_records(index.texts(order[a:b]), codebert, split)
 
     class Done:
       def get(self):
@@ -329,6 +388,8 @@ def main(args, codebert=False):
   pk = pipeline.Packer(vocab, local)
   sink = os.path.abspath(os.path.expanduser(args.sink))
   out = []
+  nbins = args.target_seq_length // args.bin_size if args.bin_size else 1
+  counts = torch.zeros(hi - lo, nbins, dtype=torch.int64, device=device)  # rows per (partition, bin)
   t.update(host_split_s=0.0, split_wait_s=0.0, gpu_s=0.0, write_s=0.0, pairs=0, split_workers=nw)
   try:
     ahead = max(1, nw)
@@ -347,6 +408,7 @@ def main(args, codebert=False):
       res = pk.pack(sh, ids_d, ntok, target_seq_length=args.target_seq_length, short_seq_prob=args.short_seq_prob,
                     duplicate_factor=args.duplicate_factor, seed=args.seed + a, bin_size=args.bin_size,
                     codebert=codebert, masking=args.masking and not codebert, masked_lm_ratio=args.masked_lm_ratio)
+      counts[a - lo:b - lo] = res.bin_count.view(b - a, -1).to(torch.int64)
       torch.cuda.synchronize()
       t['gpu_s'] += time.perf_counter() - t0
       t0 = time.perf_counter()
@@ -358,12 +420,45 @@ def main(args, codebert=False):
     if pool is not None:
       pool.terminate()
       pool.join()
+    index.close()
+  if args.num_shards:
+    # balance_dask_output's job (load_balance.py:321-369) from the packer's
+    # counts: one all-gather (RCCL) instead of its per-file count pass + MPI
+    # Allreduce (:222-233); the plan is the same on every rank; shard k is
+    # written by rank k % world from slices of the part files
+    t0 = time.perf_counter()
+    if world > 1:
+      import torch.distributed as dist
+      allc = balance.gather_bin_counts(counts if dist.get_backend() == 'nccl' else counts.cpu(), lo)
+    else:
+      allc = counts.cpu().numpy()
+    shards, ns = balance.balance_counts(allc, args.num_shards, args.bin_size is not None, outdir=sink)
+    written = balance.write_shards(shards, sink, rank, world)
+    if world > 1:
+      import torch.distributed as dist
+      dist.barrier(group=gloo)
+    if rank == 0:
+      balance.store_num_samples(ns, sink)
+      if not args.keep_orig:
+        for p in out_all_parts(sink, allc.shape[0], nbins, args.bin_size is not None):
+          if os.path.exists(p):
+            os.remove(p)
+    t['balance_s'] = time.perf_counter() - t0
+    t['shards'] = len(written)
+    out = written
   t['wall_s'] = time.perf_counter() - wall0
   # the part of the host split hidden behind the GPU and the writer
   t['host_split_hidden_s'] = max(0.0, t['host_split_s'] - t['split_wait_s'])
   t.update(rank=rank, world=world, partitions=[lo, hi], documents=int(pro[hi] - pro[lo]), chunks=len(chunks),
-           sentence_splitter=how)
+           sentence_splitter=how, n_partitions=n_part)
   return out, t
+
+
+def out_all_parts(sink, n_part, nbins, binned):
+  """paths of every part file of the run"""
+  if binned:
+    return [os.path.join(sink, 'part.%d.parquet_%d' % (p, b)) for p in range(n_part) for b in range(nbins)]
+  return [os.path.join(sink, 'part.%d.parquet' % p) for p in range(n_part)]
 
 
 def console_script(argv=None, codebert=False):

@@ -96,3 +96,125 @@ def test_build_corpus_is_shuffle_then_split():
   c, ids = preprocess.build_corpus(recs, 4, 0.8, splitter=preprocess._rule_split)
   c2, ids2 = preprocess.split_records(preprocess.sample_shuffle(recs, 4, 0.8), splitter=preprocess._rule_split)
   assert ids == ids2 and np.array_equal(c.data, c2.data) and np.array_equal(c.doc_sent_off, c2.doc_sent_off)
+
+
+# ---- reader semantics of db.read_text (readers.py:60-70) ----------------------
+def _write(path, data):
+  path.parent.mkdir(parents=True, exist_ok=True)
+  path.write_bytes(data)
+  return str(path)
+
+
+def test_reader_breaks_lines_only_where_read_text_does(tmp_path):
+  """read_text iterates a text-mode file: lines end at \\n, \\r\\n or \\r only.
+  U+2028/2029, U+0085, \\v, \\f and \\x1c-\\x1e stay inside a record (str.splitlines
+  would break there); str.strip() still removes them at the edges."""
+  from lddl_amd import readers
+  body = ('wiki-1 one still one and one\x85too\x0bv\x0cf\x1cx\x1dy\x1ez\n'
+          'wiki-2 two\r\n'
+          'wiki-3 three\rwiki-4 four\n'
+          '   \n　 \n'
+          '  wiki-5 padded \x85\x0c\n'
+          'wiki-6 été no newline at end')
+  f = _write(tmp_path / 'src' / 'a.txt', body.encode('utf-8'))
+  want = ['wiki-1 one still one and one\x85too\x0bv\x0cf\x1cx\x1dy\x1ez', 'wiki-2 two', 'wiki-3 three',
+          'wiki-4 four', 'wiki-5 padded', 'wiki-6 été no newline at end']
+  assert list(readers.iter_lines(f)) == want
+  idx = readers.RecordIndex.build([f])
+  assert idx.texts(range(len(idx))) == want
+  assert list(preprocess.read_records([f])) == want
+
+
+def test_reader_code_records_split_on_crlf_only(tmp_path):
+  from lddl_amd import readers
+  f = _write(tmp_path / 'c.txt', b'py_0<CODESPLIT>doc\n more<CODESPLIT>x = 1\r\n  \r\npy_1<CODESPLIT>a\rb<CODESPLIT>y\r\n')
+  want = ['py_0<CODESPLIT>doc\n more<CODESPLIT>x = 1', 'py_1<CODESPLIT>a\rb<CODESPLIT>y']
+  assert list(readers.iter_lines(f, '\r\n')) == want
+  idx = readers.RecordIndex.build([f], '\r\n')
+  assert idx.texts(range(len(idx))) == want
+
+
+def test_reader_index_matches_text_mode_on_random_bytes(tmp_path):
+  """RecordIndex (vectorised, bytes) == Python text mode + strip + filter on
+  random mixtures of terminators, ASCII / Unicode spaces and text."""
+  from lddl_amd import readers
+  rng = np.random.default_rng(3)
+  atoms = ['a', 'bc', ' ', '\t', '\n', '\r', '\r\n', '\x0b', '\x0c', '\x1c', '\x1f', '\x85', '\xa0', ' ',
+           '　', 'é', '中', '😀', '​']
+  for k in range(6):
+    s = ''.join(atoms[i] for i in rng.integers(0, len(atoms), 3000))
+    f = _write(tmp_path / ('r%d.txt' % k), s.encode('utf-8'))
+    for d in (None, '\r\n'):
+      idx = readers.RecordIndex.build([f], d)
+      assert idx.texts(range(len(idx))) == list(readers.iter_lines(f, d)), (k, d)
+
+
+def test_block_size_flag_and_partition_counts(tmp_path):
+  from lddl_amd import readers
+  assert readers.parse_str_of_num_bytes('128M') == 128 << 20
+  assert readers.parse_str_of_num_bytes('2k') == 2048
+  assert readers.parse_str_of_num_bytes('1000') == 100  # the reference drops a plain number's last digit
+  with pytest.raises(ValueError):
+    readers.parse_str_of_num_bytes('x')
+  a = preprocess.attach_args().parse_args(['--sink', 'x', '--block-size', '64M'])
+  assert a.block_size == 64 << 20
+  # dask.bytes.read_bytes: max(1, size // blocksize) even blocks, none for an empty file
+  assert [readers.dask_blocks(s, 100) for s in (0, 1, 99, 100, 199, 200, 250, 1000, 1050)] == [0, 1, 1, 1, 1, 2, 2, 10, 10]
+  fs = [_write(tmp_path / 'w' / ('f%d.txt' % i), b'x y\n' * (10 + 40 * i)) for i in range(3)]
+  assert readers.count_partitions(fs) == 3            # no block size: one partition per file
+  assert readers.count_partitions(fs, 160) == sum(max(1, os.path.getsize(f) // 160) for f in fs)
+  assert readers.estimate_block_size([str(tmp_path / 'w'), None], 4) == round(sum(map(os.path.getsize, fs)) / 4)
+
+
+def test_default_partitions_are_one_per_input_file(tmp_path):
+  """Without --num-blocks / --block-size the reference's read_text gives one
+  partition per file (the previous front end made a single partition)."""
+  for i in range(5):
+    _write(tmp_path / 'src' / 'en' / ('wiki_%d.txt' % i),
+           ''.join('wiki-%d-%d Some text here. More.\n' % (i, j) for j in range(20)).encode())
+  args = preprocess.attach_args().parse_args(['--wikipedia', str(tmp_path / 'src'), '--sink', 'x'])
+  idx, order, pro = preprocess.plan_input(args)
+  assert len(pro) - 1 == 5
+  assert len(idx) == 100 and 80 < len(order) < 100  # --sample-ratio 0.9
+  args = preprocess.attach_args(codebert=True).parse_args(['--code', str(tmp_path / 'src'), '--sink', 'x',
+                                                           '--num-blocks', '3'])
+  _, _, pro = preprocess.plan_input(args, codebert=True)
+  assert len(pro) - 1 == 5  # CodeBERT ignores the block flags (pretrain_codebert.py:479-485)
+
+
+def _plan_worker(rank, world, root, port, q):
+  import torch.distributed as dist
+  os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+  dist.init_process_group('gloo', rank=rank, world_size=world)
+  args = preprocess.attach_args().parse_args(['--wikipedia', root, '--sink', 'x', '--num-blocks', '7'])
+  idx, order, pro = preprocess.plan_input(args, rank=rank, world=world, gloo=dist.group.WORLD)
+  q.put((rank, idx.fid.tolist(), idx.off.tolist(), idx.len.tolist(), order.tolist(), pro.tolist()))
+  dist.destroy_process_group()
+
+
+def test_plan_input_sharded_over_ranks_matches_one_rank(tmp_path):
+  """Each of 2 gloo ranks indexes half of the files; the all-gathered index,
+  sample, shuffle and partitions equal the single-rank plan."""
+  import socket
+  import torch.multiprocessing as mp
+  rng = np.random.default_rng(9)
+  for i in range(7):
+    _write(tmp_path / 'src' / 'en' / ('w%d.txt' % i),
+           ''.join('wiki-%d-%d %s\n' % (i, j, 'word ' * int(rng.integers(1, 40))) for j in range(int(rng.integers(5, 60)))).encode())
+  root = str(tmp_path / 'src')
+  args = preprocess.attach_args().parse_args(['--wikipedia', root, '--sink', 'x', '--num-blocks', '7'])
+  idx, order, pro = preprocess.plan_input(args)
+  with socket.socket() as s:
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+  ctx = mp.get_context('spawn')
+  q = ctx.Queue()
+  ps = [ctx.Process(target=_plan_worker, args=(r, 2, root, port, q)) for r in range(2)]
+  for p in ps:
+    p.start()
+  got = [q.get(timeout=120) for _ in ps]
+  for p in ps:
+    p.join(timeout=60)
+  for _, fid, off, ln, od, pr in got:
+    assert fid == idx.fid.tolist() and off == idx.off.tolist() and ln == idx.len.tolist()
+    assert od == order.tolist() and pr == pro.tolist()

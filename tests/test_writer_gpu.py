@@ -146,8 +146,18 @@ def test_cli_bert_end_to_end(gpu, tmp_path):
       ['--wikipedia', str(tmp_path / 'wiki'), '--sink', str(sink), '--target-seq-length', '128', '--bin-size', '32',
        '--num-blocks', '4', '--sentence-splitter', 'rules', '--seed', '5', '--split-workers', '0'])
   files, t = preprocess.main(args)
+  from lddl_amd import readers
+  idx, order, pdo = preprocess.plan_input(args)
+  n_part = len(pdo) - 1
+  in_files = preprocess.find_files_under(str(src))
+  assert n_part == readers.count_partitions(in_files, readers.estimate_block_size([str(tmp_path / 'wiki')], 4))
   assert sorted(os.path.basename(f) for f in files) == sorted(
-      'part.%d.parquet_%d' % (p, b) for p in range(4) for b in range(4))
+      'part.%d.parquet_%d' % (p, b) for p in range(n_part) for b in range(4))
+  # the records in the plan's sampled / shuffled order are Python text-mode
+  # lines (read_text's), independently of the byte-level record index
+  all_recs = list(readers.iter_lines(in_files[0])) + list(readers.iter_lines(in_files[1]))
+  recs = [all_recs[i] for i in preprocess.sample_order(len(all_recs), 5, 0.9)]
+  assert recs == idx.texts(order)
   # several pipeline chunks split ahead by forked worker processes give the
   # same files: the CLI in a fresh process (its workers fork before the GPU
   # is touched, as in production), and inline chunks in this one
@@ -160,14 +170,12 @@ def test_cli_bert_end_to_end(gpu, tmp_path):
                      common, cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))), capture_output=True,
                      text=True, timeout=300)
   assert r.returncode == 0, r.stderr[-2000:]
-  assert "'split_workers': 2" in r.stdout and "'chunks': 4" in r.stdout, r.stdout
+  assert "'split_workers': 2" in r.stdout and ("'chunks': %d" % n_part) in r.stdout, r.stdout
   files3, t3 = preprocess.main(preprocess.attach_args().parse_args(['--sink', str(sink3), '--split-workers', '0'] +
                                                                      common))
   assert t3['chunks'] > 1 and t['chunks'] == 1
   for f in files:
     assert _read(f) == _read(str(sink2 / os.path.basename(f))) == _read(str(sink3 / os.path.basename(f)))
-  recs = preprocess.sample_shuffle(preprocess.read_records(preprocess.find_files_under(str(src))), 5, 0.9)
-  pdo = preprocess.partition_records(recs, num_blocks=4)
   corpus, ids = preprocess.split_records(recs, splitter=preprocess._rule_split)
   oids, ontok = OracleTokenizer(pipeline.VOCAB_BERT).run(corpus.data, corpus.sent_off, 512, nthreads=8)
   exp = po.run_bert_shards(corpus, oids, ontok, pdo, 128, 0.1, 5, 5, 32)
@@ -197,16 +205,19 @@ def test_cli_codebert_end_to_end(gpu, tmp_path):
   from oracle.oracle import OracleTokenizer
   lines = synth.make_code_lines(300, seed=9)
   (tmp_path / 'code').mkdir()
-  (tmp_path / 'code' / 'a.txt').write_bytes('\r\n'.join(lines).encode('utf-8'))
+  # two files: read_code gives one partition per file whatever --num-blocks says
+  (tmp_path / 'code' / 'a.txt').write_bytes('\r\n'.join(lines[:170]).encode('utf-8'))
+  (tmp_path / 'code' / 'b.txt').write_bytes('\r\n'.join(lines[170:]).encode('utf-8'))
   sink = tmp_path / 'out'
   args = preprocess.attach_args(codebert=True).parse_args(
       ['--code', str(tmp_path / 'code'), '--sink', str(sink), '--target-seq-length', '128', '--num-blocks', '2',
        '--seed', '8', '--sample-ratio', '1.0', '--split-workers', '0', '--chunk-mb', '0.1'])
   files, t = preprocess.main(args, codebert=True)
   assert sorted(os.path.basename(f) for f in files) == ['part.0.parquet', 'part.1.parquet']
-  recs = preprocess.sample_shuffle(
-      preprocess.read_records([str(tmp_path / 'code' / 'a.txt')], linedelimiter='\r\n'), 8, 1.0)
-  pdo = preprocess.partition_records(recs, num_blocks=2)
+  idx, order, pdo = preprocess.plan_input(args, codebert=True)
+  all_recs = list(preprocess.read_records([str(tmp_path / 'code' / n) for n in ('a.txt', 'b.txt')], '\r\n'))
+  recs = [all_recs[i] for i in preprocess.sample_order(len(all_recs), 8, 1.0)]
+  assert recs == idx.texts(order) and len(pdo) == 3
   c, ids = preprocess.split_records(recs, codebert=True)
   oids, ontok = OracleTokenizer(pipeline.VOCAB_CODEBERT).run(c.data, c.sent_off, 512, nthreads=8)
   vocab = _vocab(pipeline.VOCAB_CODEBERT)
@@ -229,3 +240,70 @@ def test_cli_codebert_end_to_end(gpu, tmp_path):
       want_code.append(_join(vocab, [t for (d, s) in code_s for t in docs[d][s]][cw[0]:cw[1]]))
       want_id.append(ids[dmap[code_s[0][0]]])
     assert got['doc'] == want_doc and got['code'] == want_code and got['id'] == want_id
+
+
+def _read_dir(d):
+  out = {}
+  for n in sorted(os.listdir(d)):
+    if n.startswith('shard-'):
+      out[n] = _read(os.path.join(d, n))
+  return out
+
+
+def test_cli_num_shards_all_gather_over_ranks(gpu, tmp_path):
+  """--num-shards: the balanced shards come straight from the packer's counts
+  (one all-gather over the ranks, load_balance.py:222-233 replaced).  Two
+  ranks (gloo on one GPU) write the same shard files and .num_samples.json
+  as one rank, and as the standalone balancer over the same part files."""
+  import json
+  import socket
+  import subprocess
+  import sys
+  from lddl_amd import synth, balance
+  c = synth.make_wiki(250_000, seed=77)
+  docs = c.documents()
+  src = tmp_path / 'wiki' / 'en'
+  src.mkdir(parents=True)
+  for k in range(3):
+    with open(str(src / ('wiki_%d.txt' % k)), 'w', encoding='utf-8') as f:
+      for d in range(k, len(docs), 3):
+        f.write('wiki-%d %s\n' % (d, ' '.join(docs[d])))
+  common = ['--wikipedia', str(tmp_path / 'wiki'), '--target-seq-length', '128', '--bin-size', '64',
+            '--num-blocks', '6', '--sentence-splitter', 'rules', '--seed', '3', '--split-workers', '0',
+            '--num-shards', '4', '--keep-orig']
+  root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+  one, two = tmp_path / 'one', tmp_path / 'two'
+  r = subprocess.run([sys.executable, '-m', 'lddl_amd.preprocess', '--sink', str(one)] + common, cwd=root,
+                     capture_output=True, text=True, timeout=300)
+  assert r.returncode == 0, r.stderr[-3000:]
+  with socket.socket() as s:
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+  procs = []
+  for rank in range(2):
+    env = dict(os.environ, RANK=str(rank), WORLD_SIZE='2', LOCAL_RANK='0', MASTER_ADDR='127.0.0.1',
+               MASTER_PORT=str(port), LDDL_DIST_BACKEND='gloo')
+    procs.append(subprocess.Popen([sys.executable, '-m', 'lddl_amd.preprocess', '--sink', str(two)] + common,
+                                  cwd=root, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+  for p in procs:
+    out, err = p.communicate(timeout=300)
+    assert p.returncode == 0, err[-3000:]
+  a, b = _read_dir(str(one)), _read_dir(str(two))
+  assert a and sorted(a) == sorted(b)
+  for n in a:
+    assert a[n] == b[n], n
+  ns1 = json.load(open(str(one / '.num_samples.json')))
+  assert ns1 == json.load(open(str(two / '.num_samples.json')))
+  # the standalone balancer (counts from the parquet footers) plans the same shards
+  import shutil
+  parts, bal = tmp_path / 'parts', tmp_path / 'bal'
+  parts.mkdir()
+  for n in os.listdir(str(one)):
+    if n.startswith('part.'):
+      shutil.copy(str(one / n), str(parts / n))
+  written, ns = balance.main(balance.attach_args().parse_args(
+      ['--indir', str(parts), '--outdir', str(bal), '--num-shards', '4', '--keep-orig']), rank=0, world=1)
+  assert ns == ns1
+  c3 = _read_dir(str(bal))
+  for n in a:
+    assert c3[n] == a[n], n
