@@ -246,6 +246,7 @@ def main():
   from lddl_amd.pipeline import VOCAB_BERT, VOCAB_CODEBERT
   code = args.corpus == 'code'
   pk = Packer(VOCAB_CODEBERT if code else VOCAB_BERT, device=local)
+  pk.tok.set_timing(True)  # per-kernel HIP events inside the tokenize call (the roofline's kernel time)
   kw = dict(target_seq_length=args.target_seq_length, short_seq_prob=0.1, duplicate_factor=args.duplicate_factor,
             seed=args.seed + rank * 10_000_000, bin_size=args.bin_size, masking=args.masking, codebert=code)
   tok_ms = []
@@ -286,6 +287,7 @@ def main():
   if not bool((per_rep == per_rep[0]).all()):
     raise RuntimeError('tokenize: replicas disagree: %s' % per_rep.tolist()[:16])
   tk = float(np.mean([a.elapsed_time(b) for a, b in tok_ms]))
+  ks = pk.tok.stats()  # the last timed step's tokenize kernels
   if dist is not None:
     t = torch.tensor([el, float(n_tok)], dtype=torch.float64, device=device)
     mx = t.clone()
@@ -299,9 +301,16 @@ def main():
     dist.destroy_process_group()
     return
   value = tot_tok * args.steps / el
-  # roofline of the dominant kernel (tokenize): algorithmic bytes / launch
-  alg = sh.nbytes + 2 * n_tok + 8 * (sh.n_sent + 1) + 4 * sh.n_sent
-  achieved = alg / (tk * 1e-3) / 1e9
+  # roofline of the dominant kernel, the tokenizer's tile scan
+  # (lddl::tok5::scan_kernel): its algorithmic bytes are
+  # the corpus read once, the sentence offsets (8 B) and its per-sentence
+  # outputs (nent, nslot, fdef u16; qb u32; ntok i32: 14 B), 2 B per token
+  # (each token's id or entry written once) and a 64-B record per word handed
+  # to WordPiece; divided by its HIP-event time inside the call
+  # (per launch: the call runs one scan launch per 1 GiB segment)
+  nl = max(1, ks['launches'])
+  alg = (sh.nbytes + 22 * sh.n_sent + 2 * n_tok + 64 * ks['records']) / nl
+  achieved = alg / (ks['scan_ms'] / nl * 1e-3) / 1e9
   line = {
       'metric': METRIC, 'value': value, 'unit': 'tokens/s', 'n_gpus': world, 'steps': args.steps,
       'warmup': args.warmup, 'ms_per_step': el * 1e3 / args.steps, 'higher_is_better': True,
@@ -320,10 +329,13 @@ def main():
                  'pairs_per_gpu': res.n_pairs, 'packed_tokens_per_gpu': res.n_tokens,
                  'masked_positions_per_gpu': res.n_masked,
                  'parallelism': 'shard%d' % world},
-      'roofline': {'bound': 'hbm', 'kernel': os.environ.get('LDDL_BENCH_KERNEL', 'lddl::tok4::tok4_kernel'), 'achieved': achieved, 'peak': HBM_PEAK_GBS,
+      'roofline': {'bound': 'hbm', 'kernel': 'lddl::tok5::scan_kernel', 'achieved': achieved, 'peak': HBM_PEAK_GBS,
                    'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS, 'traffic': None,
-                   'algorithmic_bytes_per_launch': alg, 'avg_launch_ms': tk},
-      'tokenize_ms': tk, 'gen_s': gen_s,
+                   'algorithmic_bytes_per_launch': alg, 'avg_launch_ms': ks['scan_ms'] / nl,
+                   'launches_per_step': nl},
+      'tokenize_ms': tk, 'tokenize_kernels_ms': {'scan': ks['scan_ms'], 'wordpiece': ks['wordpiece_ms'],
+                                                 'expand': ks['expand_ms']},
+      'wordpiece_records_per_gpu': ks['records'], 'gen_s': gen_s,
   }
   # HBM traffic of the tokenize call from the committed PMC passes of this
   # same workload (rocprofv3 cannot run inside the timed process)

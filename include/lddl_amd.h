@@ -68,6 +68,15 @@ int lddl_vocab_token(const lddl_ctx *ctx, int32_t id, char *buf, int64_t cap);
 int lddl_tokenize(lddl_ctx *ctx, const uint8_t *d_bytes, int64_t nbytes, const int64_t *d_sent_off,
                   int64_t n_sent, int32_t max_tok, uint16_t *d_out_ids, int32_t *d_out_ntok, void *stream);
 
+/* Per-kernel timing of lddl_tokenize (diagnostics / bench): with timing on,
+ * every call records HIP events around its kernels on the call's stream;
+ * lddl_tokenize_stats (synchronises on them) returns out[0..4] = scan,
+ * WordPiece and expand milliseconds of the last call (summed over its
+ * segments), the number of WordPiece records it ran and the number of
+ * segments (launches of each kernel). */
+int lddl_set_timing(lddl_ctx *ctx, int on);
+int lddl_tokenize_stats(lddl_ctx *ctx, double *out, int n);
+
 /* Pack every partition of a tokenised shard set.
  * Partition p = docs [d_part_doc_off[p], d_part_doc_off[p+1]); doc d =
  * sentences [d_doc_sent_off[d], d_doc_sent_off[d+1]); d_ids / d_ntok /

@@ -64,6 +64,11 @@ struct lddl_ctx {
   bool tok4_ok = false;          // the ASCII page fits tokenize_stream's class table
   int tok4_cfg = 0;
   int tok5_cfg = 0;
+  // per-kernel timing of the split tokenizer (lddl_set_timing)
+  bool timing = false;
+  SplitTiming* tm = nullptr;
+  unsigned long long* d_nrec = nullptr;
+  int64_t last_tok_bytes = 0, last_tok_sent = 0;
   // pack workspace (grown on demand)
   struct Buf {
     void* p = nullptr;
@@ -125,6 +130,13 @@ static void free_ctx(lddl_ctx* c) {
   (void)hipFree(c->d_ovf);
   (void)hipFree(c->d_counter);
   (void)hipFree(c->d_ctab);
+  (void)hipFree(c->d_nrec);
+  if (c->tm) {
+    for (int k = 0; k < 3; ++k)
+      for (int j = 0; j < 2; ++j)
+        for (int i = 0; i < 64; ++i) (void)hipEventDestroy(c->tm->ev[k][j][i]);
+    delete c->tm;
+  }
   for (auto& b : c->ws) (void)hipFree(b.p);
   if (c->h_tot) (void)hipHostFree(c->h_tot);
   delete c;
@@ -466,7 +478,14 @@ extern "C" int lddl_tokenize(lddl_ctx* c, const uint8_t* d_bytes, int64_t nbytes
     S.chunk_ctr = S.chunk_fill + n_chunks;
     S.n_chunks = (uint32_t)n_chunks;
     S.seg_tiles = seg;
-    HIP_TRY(launch_tokenize_split(P, nbytes, tile_sent, S, c->n_cu, c->tok_grid, c->tok5_cfg, st));
+    if (c->timing) {
+      S.n_rec = c->d_nrec;
+      HIP_TRY(hipMemsetAsync(c->d_nrec, 0, 8, st));
+    }
+    c->last_tok_bytes = nbytes;
+    c->last_tok_sent = n_sent;
+    HIP_TRY(launch_tokenize_split(P, nbytes, tile_sent, S, c->n_cu, c->tok_grid, c->tok5_cfg, st,
+                                  c->timing ? c->tm : nullptr));
     if (P.dbg) {
       uint64_t h[12];
       int32_t nfb = 0;
@@ -541,6 +560,41 @@ extern "C" int lddl_tokenize(lddl_ctx* c, const uint8_t* d_bytes, int64_t nbytes
       fprintf(stderr, " probes=%llu fallbacks=%llu\n", (unsigned long long)h[12], (unsigned long long)h[13]);
     }
   }
+  return 0;
+}
+
+extern "C" int lddl_set_timing(lddl_ctx* c, int on) {
+  if (!c) return set_err(LDDL_EINVAL, "null ctx");
+  HIP_TRY(hipSetDevice(c->device));
+  if (on && !c->tm) {
+    c->tm = new SplitTiming();
+    for (int k = 0; k < 3; ++k)
+      for (int j = 0; j < 2; ++j)
+        for (int i = 0; i < 64; ++i) HIP_TRY(hipEventCreate(&c->tm->ev[k][j][i]));
+    HIP_TRY(hipMalloc((void**)&c->d_nrec, 16));
+  }
+  c->timing = on != 0;
+  return 0;
+}
+
+extern "C" int lddl_tokenize_stats(lddl_ctx* c, double* out, int n) {
+  if (!c || !out || n < 5) return set_err(LDDL_EINVAL, "need out[5]");
+  if (!c->timing || !c->tm) return set_err(LDDL_EINVAL, "timing is off (lddl_set_timing)");
+  HIP_TRY(hipSetDevice(c->device));
+  for (int k = 0; k < 3; ++k) {
+    double ms = 0.0;
+    for (int i = 0; i < c->tm->n[k]; ++i) {
+      HIP_TRY(hipEventSynchronize(c->tm->ev[k][1][i]));
+      float f = 0.0f;
+      HIP_TRY(hipEventElapsedTime(&f, c->tm->ev[k][0][i], c->tm->ev[k][1][i]));
+      ms += f;
+    }
+    out[k] = ms;
+  }
+  unsigned long long nrec = 0;
+  HIP_TRY(hipMemcpy(&nrec, c->d_nrec, 8, hipMemcpyDeviceToHost));
+  out[3] = (double)nrec;
+  out[4] = (double)c->tm->n[0];
   return 0;
 }
 

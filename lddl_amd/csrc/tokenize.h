@@ -90,9 +90,16 @@ struct SplitParams {
   int32_t* fb_list;
   int32_t* fb_count;
   uint16_t* fdef;          // entry index of the sentence's first queued word (nslot > 0)
+  unsigned long long* n_rec;  // optional: records run by wp_kernel (summed over the call)
+};
+// optional per-kernel timing of a call: event pairs recorded around every
+// launch (scan / wp / expand per segment)
+struct SplitTiming {
+  hipEvent_t ev[3][2][64];
+  int n[3];
 };
 hipError_t launch_tokenize_split(const TokParams& P, int64_t nbytes, int64_t* tile_sent, SplitParams S, int n_cu,
-                                 int fb_grid, int cfg, hipStream_t s);
+                                 int fb_grid, int cfg, hipStream_t s, SplitTiming* tm = nullptr);
 int64_t split_seg_slots(int64_t seg_tiles);
 
 }  // namespace lddl

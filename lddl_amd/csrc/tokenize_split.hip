@@ -929,6 +929,7 @@ __global__ __launch_bounds__(64 * WAVES) void wp_kernel(TokParams P, SplitParams
     }
   };
   advance();
+  uint32_t nrec = 0;  // records this lane ran
   int r = -1;    // record slot being tokenised
   int pr = -1;   // record slot loaded, not begun
   uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0, q2 = q0, q3 = q0;
@@ -1128,6 +1129,7 @@ __global__ __launch_bounds__(64 * WAVES) void wp_kernel(TokParams P, SplitParams
         kb[960] = 0u;
         r = pr;
         pr = -1;
+        ++nrec;
         s = 0;
         we = len;
         np = 0;
@@ -1136,6 +1138,10 @@ __global__ __launch_bounds__(64 * WAVES) void wp_kernel(TokParams P, SplitParams
       }
     }
     if (__ballot(r >= 0 || pr >= 0) == 0 && c >= nch) break;
+  }
+  if (S.n_rec) {
+    const uint32_t tot = lane_get(wave_incl_add(nrec), 63);
+    if (lane == 0 && tot) atomicAdd(S.n_rec, (unsigned long long)tot);
   }
 }
 
@@ -1319,7 +1325,14 @@ int64_t split_seg_slots(int64_t seg_tiles) {
 }
 
 hipError_t launch_tokenize_split(const TokParams& P, int64_t nbytes, int64_t* tile_sent, SplitParams S, int n_cu,
-                                 int fb_grid, int cfg, hipStream_t s) {
+                                 int fb_grid, int cfg, hipStream_t s, SplitTiming* tm) {
+  if (tm) tm->n[0] = tm->n[1] = tm->n[2] = 0;
+  auto mark = [&](int k, int side) -> hipError_t {  // (at most 64 segments timed per kernel)
+    if (!tm || tm->n[k] >= 64) return hipSuccess;
+    const hipError_t e = hipEventRecord(tm->ev[k][side][tm->n[k]], s);
+    if (side == 1) ++tm->n[k];
+    return e;
+  };
   const int64_t n_tiles = tile_count(nbytes);
   hipError_t e = launch_tile_bounds(P.sent_off, P.n_sent, n_tiles, tile_sent, s);
   if (e != hipSuccess) return e;
@@ -1331,13 +1344,15 @@ hipError_t launch_tokenize_split(const TokParams& P, int64_t nbytes, int64_t* ti
     S.t1 = std::min(n_tiles, t0 + seg);
     if ((e = hipMemsetAsync(S.chunk_ctr, 0, 4, s)) != hipSuccess) return e;
     // cfg (LDDL_TOK5_CFG, tuning): 1 = registers unconstrained (4 waves/SIMD)
+    if ((e = mark(0, 0)) != hipSuccess) return e;
     if (P.dbg) e = tok5::launch_scan<SCAN_WAVES, true, 5>(P, S, n_cu, s);
     else if (cfg == 1) e = tok5::launch_scan<SCAN_WAVES, false, 1>(P, S, n_cu, s);
     else e = tok5::launch_scan<SCAN_WAVES, false, 5>(P, S, n_cu, s);
-    if (e != hipSuccess) return e;
+    if (e != hipSuccess || (e = mark(0, 1)) != hipSuccess || (e = mark(1, 0)) != hipSuccess) return e;
     if ((e = tok5::launch_wp<WP_WAVES>(P, S, n_cu, s)) != hipSuccess) return e;
+    if ((e = mark(1, 1)) != hipSuccess || (e = mark(2, 0)) != hipSuccess) return e;
     hipLaunchKernelGGL(tok5::expand_kernel, dim3((unsigned)std::max(1, n_cu * 8)), dim3(256), 0, s, P, S);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = hipGetLastError()) != hipSuccess || (e = mark(2, 1)) != hipSuccess) return e;
   }
   return launch_tokenize_fallback(P, tile_sent, S.fb_list, S.fb_count, fb_grid, s);
 }

@@ -81,6 +81,19 @@ class Tokenizer:
                                         _ptr(out_ids), _ptr(out_ntok), _stream(stream)))
     return out_ids, out_ntok
 
+  def set_timing(self, on=True):
+    """per-kernel timing of the following tokenize calls (lddl_set_timing)"""
+    _lib.check(_lib.lib().lddl_set_timing(self.handle, 1 if on else 0))
+
+  def stats(self):
+    """{'scan_ms', 'wordpiece_ms', 'expand_ms' (summed over the call's
+    segments), 'records', 'launches' (segments)} of the last call
+    (synchronises on its events)"""
+    out = (ctypes.c_double * 5)()
+    _lib.check(_lib.lib().lddl_tokenize_stats(self.handle, out, 5))
+    return {'scan_ms': out[0], 'wordpiece_ms': out[1], 'expand_ms': out[2], 'records': int(out[3]),
+            'launches': int(out[4])}
+
   def encode_batch(self, sentences, max_tok=512):
     """list[str] -> list[list[int]] (compact host result)."""
     enc = [s.encode('utf-8') for s in sentences]
