@@ -38,9 +38,10 @@ def parse():
   ap.add_argument('--steps', type=int, default=3)
   ap.add_argument('--warmup', type=int, default=1)
   ap.add_argument('--corpus-gb', type=float, default=20.0)
-  ap.add_argument('--corpus', choices=('wiki', 'code'), default='wiki',
+  ap.add_argument('--corpus', choices=('wiki', 'code', 'wikibooks'), default='wiki',
                   help='wiki: BERT on Wikipedia-style text (configs[1]); code: CodeBERT codebert_52000 vocab on '
-                       'code-style CodeSearchNet lines (configs[2], one GPU of it)')
+                       'code-style CodeSearchNet lines (configs[2], one GPU of it); wikibooks: Wikipedia + '
+                       'Books-style text (configs[4]: 200 GB over 8 GPUs = --corpus-gb 25 per GPU)')
   ap.add_argument('--unique-mb', type=int, default=None, help='unique synthetic MB (default 256 wiki / 16 code)')
   ap.add_argument('--target-seq-length', type=int, default=512)
   ap.add_argument('--bin-size', type=int, default=64)
@@ -70,6 +71,8 @@ def build_shards(args, rank, device):
   if args.corpus == 'code':
     # ~1.7 KB per CodeSearchNet-style line (docstring + code segments)
     base = synth.make_code(max(1, (args.unique_mb << 20) // 1700), seed=20261015 + rank)
+  elif args.corpus == 'wikibooks':
+    base = synth.make_wikibooks(args.unique_mb << 20, seed=20261015 + rank)
   else:
     base = synth.make_wiki(args.unique_mb << 20, seed=20261015 + rank)
   gen_s = time.time() - t0
@@ -316,8 +319,10 @@ def main():
       'warmup': args.warmup, 'ms_per_step': el * 1e3 / args.steps, 'higher_is_better': True,
       'scaling': 'weak', 'vs_baseline': None, 'dtype': 'u8',
       'data': 'synthetic (%s, %d MB unique tiled x%d per GPU)' % (
-          'CodeSearchNet-style code' if code else 'Wikipedia-style', args.unique_mb, reps),
-      'config': {'workload': '%s_seq%d_bin%d_%dGB_per_gpu%s' % ('codebert' if code else 'bert',
+          {'code': 'CodeSearchNet-style code', 'wiki': 'Wikipedia-style',
+           'wikibooks': 'Wikipedia + Books-style'}[args.corpus], args.unique_mb, reps),
+      'config': {'workload': '%s_seq%d_bin%d_%dGB_per_gpu%s' % ({'code': 'codebert', 'wiki': 'bert',
+                                                                   'wikibooks': 'bert_wikibooks'}[args.corpus],
                                                                  args.target_seq_length, args.bin_size,
                                                                    round(sh.nbytes / (1 << 30)),
                                                                    '_masking' if args.masking else ''),

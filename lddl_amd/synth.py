@@ -10,6 +10,15 @@ There is no network here, so every corpus is synthetic.  Two styles:
   rare >100-char words and literal ``[SEP]`` / ``[MASK]``.  Capitalised
   sentence starts.  Line format of the reference downloader
   (``lddl/download/wikipedia.py:58-63``): ``wiki-<id> <text>``.
+* Books-style (``make_books``, BookCorpus as read by ``--books``,
+  readers.py:88-99): long documents (300-3000 sentences) of short sentences
+  (lognormal, median 11 words, clipped to [1, 80]); words as Wikipedia's but
+  fewer OOV composites and ~14 % narrative tokens -- dialogue quotes and
+  tags, contractions (``don't``, ``I'm``: apostrophes split as punctuation),
+  em dashes, ellipses, chapter headings, character names.
+  ``make_wikibooks`` mixes both at the documents' level (~72 % / 28 % of the
+  bytes, English Wikipedia vs BookCorpus), as the reference's Wikipedia+Books
+  runs shuffle them together (pretrain.py:100-111).
 * Code-style (``make_code``): CodeSearchNet-like lines
   ``<lang>_<i><CODESPLIT><docstring><CODESPLIT><code>`` with 30 % empty
   docstrings and indented multi-line code
@@ -91,14 +100,23 @@ def _build_pool(vocab, rng, n_oov=20000):
   return alpha, oov
 
 
+_NARRATIVE = ['"', '"', "'", "I'm", "don't", "can't", "it's", "you're", "he'd", "she'll", "won't", "'s",
+              "didn't", "I'll", "we're", "they'd", "ain't", "y'all", '—', '…', '...', 'Mr.', 'Mrs.', 'Dr.',
+              '" he said', '" she whispered', '," I asked', '?"', '!"', 'Chapter', 'CHAPTER', 'Prologue',
+              'Harry', 'Elizabeth', 'Darcy', 'Jonah', 'Kaelen', 'okay', 'yeah', 'Oh', 'gonna', 'wanna', '?!',
+              'Hmm', 'Shh', 'Mom', 'Dad']
+
+
 class _WordTable:
   """Byte pool of words + per-category index ranges and sampling weights."""
 
-  def __init__(self, vocab, rng):
+  def __init__(self, vocab, rng, books=False):
     alpha, oov = _build_pool(vocab, rng)
     longw = [''.join(chr(97 + int(c)) for c in rng.integers(0, 26, int(n)))
              for n in rng.integers(101, 160, 16)]
     cats = [alpha, oov, _PUNCT, _EXOTIC, longw, ['[SEP]', '[MASK]']]
+    if books:
+      cats.append(_NARRATIVE)
     self.words = [w for c in cats for w in c]
     enc = [w.encode('utf-8') for w in self.words]
     self.wlen = np.array([len(b) for b in enc], dtype=np.int64)
@@ -108,7 +126,10 @@ class _WordTable:
     bases = np.cumsum([0] + [len(c) for c in cats])
     self.cat_base = bases[:-1]
     self.cat_size = np.array([len(c) for c in cats])
-    self.cat_p = np.array([0.85, 0.10, 0.03, 0.0099889, 1e-5, 1e-6])
+    if books:
+      self.cat_p = np.array([0.80, 0.04, 0.018, 0.002, 1e-6, 1e-7, 0.14])
+    else:
+      self.cat_p = np.array([0.85, 0.10, 0.03, 0.0099889, 1e-5, 1e-6])
     self.cat_p /= self.cat_p.sum()
     r = np.arange(1, len(alpha) + 1, dtype=np.float64)
     z = r ** -1.1
@@ -137,14 +158,54 @@ def _assemble(pool, src_off, lens):
 
 def make_wiki(target_bytes, seed=20261015, vocab_path=None):
   """Wikipedia-style sentence-split corpus of about ``target_bytes`` bytes."""
+  return _make_prose(target_bytes, seed, vocab_path, books=False)
+
+
+def make_books(target_bytes, seed=20261015, vocab_path=None):
+  """Books-style (BookCorpus) sentence-split corpus of about ``target_bytes``."""
+  return _make_prose(target_bytes, seed, vocab_path, books=True)
+
+
+def make_wikibooks(target_bytes, seed=20261015, vocab_path=None, books_frac=0.28):
+  """Wikipedia + Books: both styles, documents interleaved in a random order."""
+  w = make_wiki(int(target_bytes * (1 - books_frac)), seed, vocab_path)
+  b = make_books(int(target_bytes * books_frac), seed + 1, vocab_path)
+  return interleave_documents([w, b], np.random.default_rng(seed + 2))
+
+
+def interleave_documents(corpora, rng):
+  """One corpus of every document of the given corpora in a random order."""
+  spans, nsent = [], []  # (corpus, doc) byte spans and sentence counts
+  datas = [c.data[c.sent_off[0]:c.sent_off[-1]] for c in corpora]
+  base = np.cumsum([0] + [len(d) for d in datas])
+  pool = np.concatenate(datas) if datas else np.zeros(0, np.uint8)
+  d_beg, d_len, s_lens = [], [], []
+  for k, c in enumerate(corpora):
+    so = c.sent_off - c.sent_off[0]
+    d_beg.append(base[k] + so[c.doc_sent_off[:-1]])
+    d_len.append(so[c.doc_sent_off[1:]] - so[c.doc_sent_off[:-1]])
+    s_lens.append([np.diff(so[c.doc_sent_off[d]:c.doc_sent_off[d + 1] + 1]) for d in range(c.n_doc)])
+  d_beg, d_len = np.concatenate(d_beg), np.concatenate(d_len)
+  s_all = [x for sl in s_lens for x in sl]
+  order = rng.permutation(len(d_beg))
+  data, _ = _assemble(pool, d_beg[order], d_len[order])
+  sl = np.concatenate([s_all[i] for i in order]) if len(order) else np.zeros(0, np.int64)
+  sent_off = np.concatenate([[0], np.cumsum(sl)]).astype(np.int64)
+  doc_sent_off = np.concatenate([[0], np.cumsum([len(s_all[i]) for i in order])]).astype(np.int64)
+  del spans, nsent
+  return Corpus(data, sent_off, doc_sent_off)
+
+
+def _make_prose(target_bytes, seed, vocab_path, books):
   rng = np.random.default_rng(seed)
   vocab = _load_vocab(vocab_path or os.path.join(DATA_DIR, 'bert_vocab.txt'))
-  table = _WordTable(vocab, rng)
-  avg_word = 6.2
+  table = _WordTable(vocab, rng, books=books)
+  avg_word = 5.0 if books else 6.2
   n_words = max(64, int(target_bytes / avg_word))
   # sentence lengths (words) and document sizes (sentences)
-  n_sent_est = n_words // 22 + 8
-  slen = np.clip(np.rint(rng.lognormal(np.log(22.0), 0.55, n_sent_est)), 3, 120).astype(np.int64)
+  med, sig, lo, hi = (11.0, 0.65, 1, 80) if books else (22.0, 0.55, 3, 120)
+  n_sent_est = int(n_words // med) + 8
+  slen = np.clip(np.rint(rng.lognormal(np.log(med), sig, n_sent_est)), lo, hi).astype(np.int64)
   csum = np.cumsum(slen)
   n_sent = int(np.searchsorted(csum, n_words)) + 1
   n_sent = min(n_sent, len(slen))
@@ -190,8 +251,8 @@ def make_wiki(target_bytes, seed=20261015, vocab_path=None):
   sent_off[:-1] = sent_beg
   sent_off[-1] = sent_end[-1]
   assert np.all(sent_off[1:] == sent_end)
-  # documents: 3-60 sentences
-  dl = rng.integers(3, 61, n_sent // 3 + 2)
+  # documents: 3-60 sentences (an article), 300-3000 (a book)
+  dl = rng.integers(300, 3001, n_sent // 300 + 2) if books else rng.integers(3, 61, n_sent // 3 + 2)
   dcs = np.cumsum(dl)
   n_doc = int(np.searchsorted(dcs, n_sent)) + 1
   doc_sent_off = np.concatenate([[0], np.minimum(dcs[:n_doc], n_sent)]).astype(np.int64)

@@ -117,6 +117,24 @@ def test_bert_end_to_end_vs_oracle(gpu, monkeypatch, seq, bin_size, nparts, caps
     assert np.array_equal(bc[p], cnt)
 
 
+@pytest.mark.parametrize('nparts', [2, 5])
+def test_wikibooks_seq512_bin64_vs_oracle(gpu, nparts):
+  """BASELINE config C5 at a size the oracle finishes quickly: a Wikipedia +
+  Books-style corpus (--wikipedia + --books, readers.py:73-99; books are long
+  documents of short sentences with dialogue and contractions), seq 512,
+  --bin-size 64, duplicate factor 5."""
+  from lddl_amd import synth, pipeline
+  c = synth.make_wikibooks(1_500_000, seed=40 + nparts)
+  res = pipeline.run_bert(c, target_seq_length=512, bin_size=64, n_partitions=nparts, seed=2024, check_host=True)
+  oids, ontok = OracleTokenizer(pipeline.VOCAB_BERT).run(c.data, c.sent_off, 512, nthreads=8)
+  assert np.array_equal(res.ntok_host, ontok)
+  exp = po.run_bert_shards(c, oids, ontok, res.part_doc_off, 512, 0.1, 5, 2024, 64)
+  pipeline.assert_same_pairs(res, exp)
+  bc = res.bin_count.cpu().numpy()
+  for p, part in enumerate(exp):
+    assert np.array_equal(bc[p], np.bincount([po.bin_of(r[3], 64, 8) for r in part], minlength=8))
+
+
 @pytest.mark.parametrize('mat,algo', [(None, None), ('1', None), (None, '1')])
 def test_codebert_end_to_end_vs_oracle(gpu, monkeypatch, mat, algo):
   from lddl_amd import synth, pipeline
