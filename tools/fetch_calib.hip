@@ -3,7 +3,11 @@
 //   mode 0: one 16-B load per lane, contiguous across the wave
 //   mode 1: two 16-B non-temporal loads per lane at a 32-B lane stride
 //           (tok4's window load, tokenize_stream.hip)
-// and writes 2-B ids in ~460-B runs at 1 KiB stride (mode 2, tok4's output).
+// and writes 2-B ids in ~460-B runs at 1 KiB stride (mode 2, tok4's output);
+// random vocab-bucket probes over a 4 GiB table (past the 256 MiB MALL, so
+// every probe is a miss at the memory side): 32 B per lane (two 16-B loads of
+// one 64-B bucket: the scan's first probe) and 64 B per lane (the whole
+// bucket: WordPiece's probe), 2^24 probes each.
 // Build: hipcc --offload-arch=gfx950 -O3 -o tools/fetch_calib tools/fetch_calib.hip
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -38,6 +42,25 @@ __global__ void wr_runs(unsigned short* out, size_t n_tiles) {
   for (int k = lane; k < 230; k += 64) out[base + k] = (unsigned short)(k + t);
 }
 
+__device__ __forceinline__ unsigned hmix(unsigned x) {
+  x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
+  return x;
+}
+// NB 16-B loads per lane from a random 64-B bucket of nbk buckets
+template <int NB>
+__global__ void rnd_probe(const u32x4* t, unsigned nbk_mask, size_t n, unsigned* sink) {
+  unsigned acc = 0;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const u32x4* b = t + 4 * (size_t)(hmix((unsigned)i * 2654435761u + 12345u) & nbk_mask);
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+      const u32x4 a = b[k];
+      acc ^= a.x ^ a.y ^ a.z ^ a.w;
+    }
+  }
+  if (acc == 0x12345678u) sink[0] = acc;
+}
+
 int main() {
   const size_t bytes = (size_t)1 << 30;
   void* p;
@@ -51,5 +74,16 @@ int main() {
   wr_runs<<<(unsigned)((n_tiles * 64 + 255) / 256), 256>>>((unsigned short*)p, n_tiles);
   if (hipDeviceSynchronize() != hipSuccess) return 2;
   printf("read bytes per kernel %zu; wr_runs algorithmic bytes %zu\n", bytes, n_tiles * 230 * 2);
+  const size_t tbytes = (size_t)4 << 30, nprobe = (size_t)1 << 24;
+  void* tb;
+  if (hipMalloc(&tb, tbytes) != hipSuccess) return 3;
+  hipMemset(tb, 3, tbytes);
+  hipDeviceSynchronize();
+  const unsigned mask = (unsigned)(tbytes / 64 - 1);
+  rnd_probe<2><<<4096, 256>>>((const u32x4*)tb, mask, nprobe, sink);
+  rnd_probe<4><<<4096, 256>>>((const u32x4*)tb, mask, nprobe, sink);
+  if (hipDeviceSynchronize() != hipSuccess) return 4;
+  printf("rnd_probe: %zu probes of 32 B (%zu B) and of 64 B (%zu B) over a %zu-B table\n", nprobe, nprobe * 32,
+         nprobe * 64, tbytes);
   return 0;
 }
