@@ -23,12 +23,30 @@ def _newer(target, deps):
 
 
 def build_hip(force=False, verbose=False):
+  """Each .hip compiled to its own object in parallel (device code is per
+  translation unit: the kernels share headers only), then linked."""
   srcs = sorted(glob.glob(os.path.join(CSRC, '*.hip')))
-  deps = srcs + glob.glob(os.path.join(CSRC, '*.h')) + [os.path.join(ROOT, 'include', 'lddl_amd.h')]
-  if not force and not _newer(LIB, deps):
+  hdrs = glob.glob(os.path.join(CSRC, '*.h')) + [os.path.join(ROOT, 'include', 'lddl_amd.h')]
+  if not force and not _newer(LIB, srcs + hdrs):
     return LIB
-  cmd = ['hipcc', '--offload-arch=%s' % ARCH, '-O3', '-std=c++17', '-fPIC', '-shared',
-         '-Wno-unused-result', '-o', LIB + '.tmp'] + srcs
+  from concurrent.futures import ThreadPoolExecutor
+  odir = os.path.join(CSRC, 'build')
+  os.makedirs(odir, exist_ok=True)
+  flags = ['--offload-arch=%s' % ARCH, '-O3', '-std=c++17', '-fPIC', '-Wno-unused-result']
+
+  def obj(src):
+    o = os.path.join(odir, os.path.basename(src)[:-4] + '.o')
+    if force or _newer(o, [src] + hdrs):
+      cmd = ['hipcc'] + flags + ['-c', '-o', o + '.tmp', src]
+      if verbose:
+        print(' '.join(cmd))
+      subprocess.run(cmd, check=True, cwd=CSRC)
+      os.replace(o + '.tmp', o)
+    return o
+
+  with ThreadPoolExecutor(max_workers=min(len(srcs), max(1, min(8, os.cpu_count() or 1)))) as ex:
+    objs = list(ex.map(obj, srcs))
+  cmd = ['hipcc', '--offload-arch=%s' % ARCH, '-shared', '-fPIC', '-o', LIB + '.tmp'] + objs
   if verbose:
     print(' '.join(cmd))
   subprocess.run(cmd, check=True, cwd=CSRC)

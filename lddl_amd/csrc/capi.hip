@@ -49,6 +49,7 @@ struct lddl_ctx {
   // device tables
   uint16_t* d_top = nullptr;
   uint32_t* d_pages = nullptr;
+  uint32_t* d_bmp = nullptr;  // flat entries of the Basic Multilingual Plane (top/pages resolved)
   uint4* d_multi = nullptr;
   uint4* d_slots = nullptr;
   uint32_t* d_bloom = nullptr;
@@ -62,7 +63,6 @@ struct lddl_ctx {
   uint32_t vt_mask = 0;
   uint32_t* d_vbloom = nullptr;  // its Bloom filter
   bool tok4_ok = false;          // the ASCII page fits tokenize_stream's class table
-  int tok4_cfg = 0;
   int tok5_cfg = 0;
   // per-kernel timing of the split tokenizer (lddl_set_timing)
   bool timing = false;
@@ -86,8 +86,7 @@ struct lddl_ctx {
   int pack_codebert = 0;
   // scratch
   int tok_grid = 0;
-  int tok_algo = 3;  // 3 = workgroup tiles, 2 = wave windows, 1 = lane per sentence
-  int64_t tile_chunk = 0;  // tiles per tile-kernel launch (0 = default)
+  int tok_algo = 5;  // 5 = split tokenizer, 0 = every tile through the exact serial path
   uint8_t* d_ovf = nullptr;
   uint32_t* d_counter = nullptr;
   // collate: whole-token vocab table (built on first use)
@@ -118,6 +117,7 @@ static void free_ctx(lddl_ctx* c) {
   if (!c) return;
   (void)hipFree(c->d_top);
   (void)hipFree(c->d_pages);
+  (void)hipFree(c->d_bmp);
   (void)hipFree(c->d_multi);
   (void)hipFree(c->d_slots);
   (void)hipFree(c->d_bloom);
@@ -197,6 +197,10 @@ static int load_table(lddl_ctx* c, const char* path) {
   if ((rc = upload(&c->d_top, top.data(), top.size() * 2))) return rc;
   if ((rc = upload(&c->d_pages, pages.data(), pages.size() * 4))) return rc;
   if ((rc = upload(&c->d_multi, multi.data(), multi.size() * 4))) return rc;
+  // the BMP flattened (256 KiB, L2-resident): one load per code point < U+10000
+  std::vector<uint32_t> bmp(0x10000);
+  for (uint32_t cp = 0; cp < 0x10000; ++cp) bmp[cp] = pages[(size_t)top[cp >> 8] * 256 + (cp & 255)];
+  if ((rc = upload(&c->d_bmp, bmp.data(), bmp.size() * 4))) return rc;
   return 0;
 }
 
@@ -356,33 +360,23 @@ extern "C" int lddl_create(const char* vocab_path, const char* table_path, int d
   if (hipGetDeviceProperties(&prop, device) != hipSuccess) { free_ctx(c); return set_err(LDDL_EHIP, "hipGetDeviceProperties"); }
   c->n_cu = prop.multiProcessorCount;
   if ((rc = load_table(c, table_path)) || (rc = load_vocab(c, vocab_path))) { free_ctx(c); return rc; }
+  // 5: the split tokenizer (default); 0: every tile through the exact serial
+  // path -- forced by LDDL_TOKENIZE_ALGO=0 (tests), or taken when the split
+  // tokenizer does not model the tables (its entries keep ids below
+  // SPLIT_EDEF; it derives a byte-class table from the ASCII page)
   const char* algo = getenv("LDDL_TOKENIZE_ALGO");
-  c->tok_algo = (algo && algo[0] >= '1' && algo[0] <= '5') ? algo[0] - '0' : 5;
-  // v5 entries keep ids below SPLIT_EDEF; both need tok4's ASCII class table
-  if (c->tok_algo == 5 && (!c->tok4_ok || c->vocab_size > (int)SPLIT_EDEF)) c->tok_algo = 4;
-  if (c->tok_algo == 4 && !c->tok4_ok) c->tok_algo = 3;
-  const char* cfg = getenv("LDDL_TOK4_CFG");  // waves per workgroup / Bloom (tokenize.h)
-  c->tok4_cfg = cfg ? atoi(cfg) : 4;
+  c->tok_algo = (algo && algo[0] == '0') ? 0 : 5;
+  if (c->tok_algo == 5 && (!c->tok4_ok || c->vocab_size > (int)SPLIT_EDEF)) c->tok_algo = 0;
   const char* cfg5 = getenv("LDDL_TOK5_CFG");  // split tokenizer variants (tokenize_split.hip)
   c->tok5_cfg = cfg5 ? atoi(cfg5) : 0;
-  const char* tchunk = getenv("LDDL_TILE_CHUNK");  // tiles per launch (tests force several launches)
-  c->tile_chunk = tchunk ? atoll(tchunk) : 0;
   const char* mcap = getenv("LDDL_MLM_CAP");  // initial masking arena (tests force the regrow path)
   c->mlm_cap = mcap ? (uint64_t)atoll(mcap) : 0;
   int per_cu = 0;
-  if (c->tok_algo != 2) {
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, tokenize_kernel_ptr(), 256, 0) != hipSuccess || per_cu < 1)
-      per_cu = 4;
-    c->tok_grid = c->n_cu * per_cu;
-  } else {
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, tokenize_wave_kernel_ptr(), 64 * TOK_WAVES, 0) !=
-            hipSuccess ||
-        per_cu < 1)
-      per_cu = 2;
-    c->tok_grid = c->n_cu * per_cu;
-  }
-  const size_t ovf_bytes = c->tok_algo != 2 ? (size_t)c->tok_grid * 256 * WB_OVF
-                                            : (size_t)c->tok_grid * TOK_WAVES * (WB_OVF + 64);
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, tokenize_fallback_kernel_ptr(), 256, 0) != hipSuccess ||
+      per_cu < 1)
+    per_cu = 4;
+  c->tok_grid = c->n_cu * per_cu;
+  const size_t ovf_bytes = (size_t)c->tok_grid * 256 * WB_OVF;
   if (hipMalloc((void**)&c->d_ovf, ovf_bytes) != hipSuccess ||
       hipMalloc((void**)&c->d_counter, 64) != hipSuccess) {
     free_ctx(c);
@@ -424,11 +418,11 @@ extern "C" int lddl_tokenize(lddl_ctx* c, const uint8_t* d_bytes, int64_t nbytes
   P.sent_off = d_sent_off;
   P.n_sent = n_sent;
   P.max_tok = max_tok;
-  P.chunk = c->tok_algo == 1 ? 64 : 128;
   P.out_ids = d_out_ids;
   P.out_ntok = d_out_ntok;
   P.top = c->d_top;
   P.pages = c->d_pages;
+  P.bmp = c->d_bmp;
   P.multi = c->d_multi;
   P.slots = c->d_slots;
   P.slot_mask = c->slot_mask;
@@ -445,8 +439,6 @@ extern "C" int lddl_tokenize(lddl_ctx* c, const uint8_t* d_bytes, int64_t nbytes
   P.ovf = c->d_ovf;
   P.work_counter = c->d_counter;
   HIP_TRY(hipMemsetAsync(c->d_counter, 0, 64, st));
-  const char* abl = getenv("LDDL_TOK_ABLATE");
-  P.dbg_mode = abl ? atoi(abl) : 0;
   const char* dbgenv = getenv("LDDL_TOK_DEBUG");
   static uint64_t* d_dbg = nullptr;
   if (dbgenv && dbgenv[0] == '1') {
@@ -454,7 +446,6 @@ extern "C" int lddl_tokenize(lddl_ctx* c, const uint8_t* d_bytes, int64_t nbytes
     HIP_TRY(hipMemsetAsync(d_dbg, 0, 16 * 8, st));
     P.dbg = d_dbg;
   }
-  const int64_t chunks = (n_sent + P.chunk - 1) / P.chunk;
   if (c->tok_algo == 5) {
     const int64_t nt = tile_count(nbytes);
     // LDDL_SPLIT_SEG (tiles per segment) / LDDL_SPLIT_CHUNKS (record chunks):
@@ -498,67 +489,15 @@ extern "C" int lddl_tokenize(lddl_ctx* c, const uint8_t* d_bytes, int64_t nbytes
       for (int k = 0; k < 12; ++k) fprintf(stderr, " %s=%llu", nm[k], (unsigned long long)h[k]);
       fprintf(stderr, "\n");
     }
-  } else if (c->tok_algo == 4) {
-    const int64_t nt = tile_count(nbytes);
-    int64_t* tile_sent;
-    int32_t *fb_list, *fb_count;
-    int rc;
-    if ((rc = ws_get(c, 19, nt + 1, &tile_sent)) || (rc = ws_get(c, 20, nt, &fb_list)) ||
-        (rc = ws_get(c, 21, 16, &fb_count)))
-      return rc;
-    HIP_TRY(launch_tokenize_stream(P, nbytes, tile_sent, fb_list, fb_count, c->tok_grid, c->n_cu, c->tok4_cfg, st));
-    if (P.dbg) {
-      uint64_t h[16];
-      int32_t nfb = 0;
-      HIP_TRY(hipMemcpyAsync(h, P.dbg, sizeof h, hipMemcpyDeviceToHost, st));
-      HIP_TRY(hipMemcpyAsync(&nfb, fb_count, 4, hipMemcpyDeviceToHost, st));
-      HIP_TRY(hipStreamSynchronize(st));
-      const char* nm[16] = {"bytes", "exceptions", "units", "prep", "wordpiece", "output",
-                            "probes_l0", "bloom_rejects_l0", "nunits", "wp_iters", "tiles", "fallback",
-                            "wp_scan", "wp_probe", "wp_refill", "fb_dirty"};
-      fprintf(stderr, "[lddl tok4 dbg] cfg=%d ntiles=%lld fallback_list=%d", c->tok4_cfg, (long long)nt, nfb);
-      for (int k = 0; k < 16; ++k) fprintf(stderr, " %s=%llu", nm[k], (unsigned long long)h[k]);
-      fprintf(stderr, "\n");
-    }
-  } else if (c->tok_algo == 3) {
-    const int64_t nt = tile_count(nbytes);
-    int64_t* tile_sent;
-    int32_t *fb_list, *fb_count;
-    int rc;
-    if ((rc = ws_get(c, 19, nt + 1, &tile_sent)) || (rc = ws_get(c, 20, nt, &fb_list)) ||
-        (rc = ws_get(c, 21, 16, &fb_count)))
-      return rc;
-    HIP_TRY(launch_tokenize_tiles(P, nbytes, tile_sent, fb_list, fb_count, c->tok_grid, c->tile_chunk, st));
-    if (P.dbg) {
-      uint64_t h[16];
-      int32_t nfb = 0;
-      HIP_TRY(hipMemcpyAsync(h, P.dbg, sizeof h, hipMemcpyDeviceToHost, st));
-      HIP_TRY(hipMemcpyAsync(&nfb, fb_count, 4, hipMemcpyDeviceToHost, st));
-      HIP_TRY(hipStreamSynchronize(st));
-      const char* nm[12] = {"setup", "A1", "A2", "B", "Cinit", "Cround_A", "Cround_B", "Cfinish", "D", "write",
-                            "rounds", "tiles"};
-      fprintf(stderr, "[lddl tile dbg] ntiles=%lld fallback=%d", (long long)nt, nfb);
-      for (int k = 0; k < 12; ++k) fprintf(stderr, " %s=%llu", nm[k], (unsigned long long)h[k]);
-      fprintf(stderr, "\n");
-    }
-  } else if (c->tok_algo == 1) {
-    int grid = (int)((chunks + 3) / 4);
-    if (grid > c->tok_grid) grid = c->tok_grid;
-    HIP_TRY(launch_tokenize(P, grid, st));
   } else {
-    const int64_t wg_needed = (chunks + TOK_WAVES - 1) / TOK_WAVES;
-    int grid = (int)(wg_needed < c->tok_grid ? wg_needed : c->tok_grid);
-    HIP_TRY(launch_tokenize_wave(P, grid, st));
-    if (P.dbg) {
-      uint64_t h[16];
-      HIP_TRY(hipMemcpyAsync(h, P.dbg, sizeof h, hipMemcpyDeviceToHost, st));
-      HIP_TRY(hipStreamSynchronize(st));
-      const char* nm[10] = {"chunk/loop", "rawload", "passA", "passB+write", "units+defer", "wordpiece", "scan+scatter",
-                            "finish", "windows", "units"};
-      fprintf(stderr, "[lddl tok dbg] grid=%d chunks=%lld", grid, (long long)chunks);
-      for (int k = 0; k < 10; ++k) fprintf(stderr, " %s=%llu", nm[k], (unsigned long long)h[k]);
-      fprintf(stderr, " probes=%llu fallbacks=%llu\n", (unsigned long long)h[12], (unsigned long long)h[13]);
-    }
+    const int64_t nt = tile_count(nbytes);
+    int64_t* tile_sent;
+    int32_t *fb_list, *fb_count;
+    int rc;
+    if ((rc = ws_get(c, 19, nt + 1, &tile_sent)) || (rc = ws_get(c, 20, nt, &fb_list)) ||
+        (rc = ws_get(c, 21, 16, &fb_count)))
+      return rc;
+    HIP_TRY(launch_tokenize_serial(P, nbytes, tile_sent, fb_list, fb_count, c->tok_grid, st));
   }
   return 0;
 }
@@ -651,7 +590,6 @@ static int pack_common(lddl_ctx* c, int codebert, const int32_t* d_ntok, const i
   if ((rc = ws_get(c, 0, n_sent, &P.fs_ntok)) || (rc = ws_get(c, 1, n_sent, &P.fs_base)) ||
       (rc = ws_get(c, 2, n_doc, &P.fd_first)) || (rc = ws_get(c, 3, n_doc, &P.fd_n)) ||
       (rc = ws_get(c, 4, n_doc, &P.fd_nd)) ||
-      (rc = ws_get(c, 5, (size_t)((n_part + 63) / 64) * 156 * 64, &P.mt)) ||
       (rc = ws_get(c, 6, npair_cap, &P.pairs)) || (rc = ws_get(c, 7, npair_cap, &P.order)) ||
       (rc = ws_get(c, 8, npair_cap, &P.binned)) || (rc = ws_get(c, 9, npair_cap, &P.tok_local)) ||
       (rc = ws_get(c, 10, n_part, &P.part_npairs)) || (rc = ws_get(c, 11, n_part, &P.part_ntok)) ||
@@ -692,9 +630,7 @@ static int pack_common(lddl_ctx* c, int codebert, const int32_t* d_ntok, const i
     HIP_TRY(launch_sent_special(d_ids, d_sent_off, d_ntok, n_sent, P.cls_id, P.sep_id, sent_spec, st));
     if (!c->mlm_cap) c->mlm_cap = (uint64_t)n_part * 4 * MLM_CHUNK + (uint64_t)duplicate_factor * n_sent * 4;
   }
-  const char* palgo = getenv("LDDL_PACK_ALGO");
-  const bool lane_packer = !masking && palgo && palgo[0] == '1';
-  if (!codebert && !lane_packer) {
+  if (!codebert) {
     // Wave packer: one 64-lane workgroup per partition runs a serial chain, so
     // throughput is partitions in flight; measured on the bench workload the
     // per-partition arrays are best left in global memory (L2), keeping the
@@ -727,10 +663,8 @@ static int pack_common(lddl_ctx* c, int codebert, const int32_t* d_ntok, const i
       HIP_TRY(hipMemsetAsync(d_pdbg, 0, 16 * 8, st));
       P.dbg = d_pdbg;
     }
-    const bool lane_cb = palgo && palgo[0] == '1';  // LDDL_PACK_ALGO=1: the lane-serial packers
-    HIP_TRY(codebert ? (lane_cb ? launch_pack_codebert(P, st) : launch_pack_codebert_wave(P, st))
-                     : lane_packer ? launch_pack_bert(P, st) : launch_pack_bert_wave(P, st));
-    if (P.dbg && !codebert && !lane_packer) {
+    HIP_TRY(codebert ? launch_pack_codebert_wave(P, st) : launch_pack_bert_wave(P, st));
+    if (P.dbg && !codebert) {
       uint64_t h[13];
       HIP_TRY(hipMemcpyAsync(h, P.dbg, sizeof h, hipMemcpyDeviceToHost, st));
       HIP_TRY(hipStreamSynchronize(st));

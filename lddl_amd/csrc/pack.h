@@ -43,7 +43,6 @@ struct PackParams {
   int64_t* fd_first;            // [n_doc]
   int32_t* fd_n;                // [n_doc]
   int32_t* fd_nd;               // [n_doc] CodeBERT docstring segment count
-  uint4* mt;                    // [ceil(n_part/64) * 156 * 64]
   PairRec* pairs;               // [dup * n_sent]
   int32_t* order;               // [dup * n_sent]
   int32_t* binned;              // [dup * n_sent]
@@ -125,10 +124,8 @@ struct MatParams {
   int64_t* out_part;            // [n_pairs] partition id (for ids / file names)
 };
 
-hipError_t launch_pack_bert(const PackParams& P, hipStream_t s);
 hipError_t launch_pack_bert_wave(const PackParams& P, hipStream_t s);
 size_t pack_dyn_bytes(int cap_lens, int cap_docs, int cap_pairs, bool mask);
-hipError_t launch_pack_codebert(const PackParams& P, hipStream_t s);
 hipError_t launch_pack_codebert_wave(const PackParams& P, hipStream_t s);
 hipError_t launch_scan_parts(const int64_t* a, const int64_t* b, int64_t n, int64_t* sa, int64_t* sb,
                              const int32_t* err, int32_t* err_any, hipStream_t s);

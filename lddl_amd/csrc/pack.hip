@@ -12,292 +12,14 @@
 // Partition p (docs [part_doc_off[p], part_doc_off[p+1])) is the unit of
 // independence: the random-next document is drawn from the same partition
 // and the RNG stream (CPython MT19937 seeded with seed + p) is serial within
-// it.  v1 mapping: one lane per partition runs the serial decision logic
-// (filter -> pack -> shuffle -> bin) writing compact pair records (32 B) into
-// the partition's slot range; materialisation (the bulk byte work: gathering
-// token ids into [CLS] A [SEP] B [SEP] rows) is wave-parallel per pair.
+// it.  The packers (one wave per partition) are in pack_wave.hip; this file
+// holds the partition scans, materialisation (the bulk byte work: gathering
+// token ids into [CLS] A [SEP] B [SEP] rows, wave-parallel per 64 rows), the
+// dense id compaction and the static-masking kernels.
 #include "common.h"
-#include "mt19937.h"
 #include "pack.h"
 
 namespace lddl {
-
-struct PartView {
-  int64_t d0, d1;   // doc range
-  int64_t s0;       // first sentence slot
-  int64_t pb;       // first pair slot = dup * s0
-  int64_t nd;       // filtered docs
-};
-
-// Drop empty sentences and empty documents (pretrain.py:89-97,
-// pretrain_codebert.py:143-161 + filter len(d) > 0).
-__device__ PartView filter_partition(const PackParams& P, int64_t p, bool codebert) {
-  PartView v;
-  v.d0 = P.part_doc_off[p];
-  v.d1 = P.part_doc_off[p + 1];
-  v.s0 = P.doc_sent_off[v.d0];
-  v.pb = (int64_t)P.dup * v.s0;
-  const int64_t base = P.sent_off[0];
-  int64_t slot = v.s0, nd = 0;
-  for (int64_t d = v.d0; d < v.d1; ++d) {
-    const int64_t first = slot;
-    const int64_t sa = P.doc_sent_off[d], sb = P.doc_sent_off[d + 1];
-    const int64_t sdoc_end = codebert ? sa + P.doc_nseg_doc[d] : sa;
-    int32_t ndoc_seg = 0;
-    for (int64_t s = sa; s < sb; ++s) {
-      const int32_t n = P.ntok[s];
-      if (n > 0) {
-        P.fs_ntok[slot] = n;
-        P.fs_base[slot] = P.sent_off[s] - base;
-        P.fs_dense[slot] = P.tokoff[s];
-        ++slot;
-        if (s < sdoc_end) ++ndoc_seg;
-      }
-    }
-    const int32_t cnt = (int32_t)(slot - first);
-    // CodeBERT keeps a pair only if it has code segments (len(CodePair) > 0)
-    const bool keep = codebert ? (cnt - ndoc_seg) > 0 : cnt > 0;
-    if (keep) {
-      P.fd_first[v.d0 + nd] = first;
-      P.fd_n[v.d0 + nd] = cnt;
-      if (codebert) P.fd_nd[v.d0 + nd] = ndoc_seg;
-      ++nd;
-    } else {
-      slot = first;
-    }
-  }
-  v.nd = nd;
-  return v;
-}
-
-__device__ __forceinline__ MTLane lane_rng(const PackParams& P, int64_t p) {
-  MTLane r;
-  r.S = P.mt + ((size_t)(p >> 6) * 156) * 64 + (p & 63);
-  r.idx = MT_N;
-  return r;
-}
-
-// random.shuffle(partition_pairs) (pretrain.py:401) on the record order,
-// then the stable bin partition + per-pair token offsets.
-__device__ void shuffle_and_bin(const PackParams& P, int64_t p, const PartView& v, int64_t np, MTLane& rng) {
-  int32_t* order = P.order + v.pb;
-  for (int64_t k = 0; k < np; ++k) order[k] = (int32_t)k;
-  for (int64_t k = np - 1; k >= 1; --k) {
-    const int64_t j = rng.randbelow((uint32_t)(k + 1));
-    const int32_t t = order[k];
-    order[k] = order[j];
-    order[j] = t;
-  }
-  const int32_t nb = P.nbins;
-  int64_t* cnt = P.bin_count + p * nb;
-  for (int32_t b = 0; b < nb; ++b) cnt[b] = 0;
-  const PairRec* pr = P.pairs + v.pb;
-  for (int64_t k = 0; k < np; ++k) {
-    int32_t b = ((int32_t)pr[order[k]].num_tokens - 1) / P.bin_size;
-    cnt[b > nb - 1 ? nb - 1 : b]++;
-  }
-  // exclusive per-bin starts: registers when nb <= 16, else bin_cursor
-  int64_t* cur = P.bin_cursor + p * nb;
-  int64_t acc = 0;
-  int64_t cur_r[16];
-  const bool small = nb <= 16;
-  for (int32_t b = 0; b < nb; ++b) {
-    if (small) cur_r[b] = acc; else cur[b] = acc;
-    acc += cnt[b];
-  }
-  int32_t* binned = P.binned + v.pb;
-  for (int64_t k = 0; k < np; ++k) {
-    const int32_t rec = order[k];
-    int32_t b = ((int32_t)pr[rec].num_tokens - 1) / P.bin_size;
-    b = b > nb - 1 ? nb - 1 : b;
-    int64_t pos;
-    if (small) {
-      pos = 0;
-#pragma unroll
-      for (int q = 0; q < 16; ++q)
-        if (q == b) pos = cur_r[q]++;
-    } else {
-      pos = cur[b]++;
-    }
-    binned[pos] = rec;
-  }
-  int64_t* tl = P.tok_local + v.pb;
-  acc = 0;
-  for (int64_t k = 0; k < np; ++k) {
-    tl[k] = acc;
-    acc += pr[binned[k]].num_tokens;
-  }
-  P.part_npairs[p] = np;
-  P.part_ntok[p] = acc;
-}
-
-// ---------------------------------------------------------------- BERT ----
-__global__ __launch_bounds__(64) void pack_bert_kernel(PackParams P) {
-  const int64_t p = (int64_t)blockIdx.x * 64 + threadIdx.x;
-  if (p >= P.n_part) return;
-  const PartView v = filter_partition(P, p, false);
-  MTLane rng = lane_rng(P, p);
-  rng.seed(P.seed + (uint64_t)p);
-  const int32_t max_num = P.max_seq - 3;
-  PairRec* out = P.pairs + v.pb;
-  int64_t np = 0;
-  int32_t err = PACK_OK;
-  for (int32_t dup = 0; dup < P.dup && !err; ++dup) {
-    for (int64_t di = 0; di < v.nd && !err; ++di) {
-      const int64_t first = P.fd_first[v.d0 + di];
-      const int32_t len = P.fd_n[v.d0 + di];
-      int32_t target = max_num;
-      if (rng.random() < P.short_seq_prob) target = (int32_t)rng.randint(2, max_num);
-      int32_t cs = 0, nchunk = 0, cur = 0;
-      for (int32_t i = 0; i < len; ++i) {
-        if (nchunk == 0) cs = i;
-        ++nchunk;
-        cur += P.fs_ntok[first + i];
-        if (i == len - 1 || cur >= target) {
-          int32_t a_end = 1;
-          if (nchunk >= 2) a_end = (int32_t)rng.randint(1, nchunk - 1);
-          int32_t la = 0;
-          for (int32_t j = 0; j < a_end; ++j) la += P.fs_ntok[first + cs + j];
-          PairRec r;
-          r.fs0 = first + cs;
-          r.n0 = (uint16_t)a_end;
-          int32_t lb = 0;
-          bool rn;
-          if (nchunk == 1 || rng.random() < 0.5) {
-            rn = true;
-            const int32_t tb = target - la;
-            int64_t rdi = 0;
-            for (int t = 0; t < 10; ++t) {
-              rdi = rng.randint(0, v.nd - 1);
-              if (rdi != di) break;
-            }
-            if (rdi == di) rn = false;
-            const int64_t rfirst = P.fd_first[v.d0 + rdi];
-            const int32_t rlen = P.fd_n[v.d0 + rdi];
-            const int32_t rstart = (int32_t)rng.randint(0, rlen - 1);
-            int32_t bn = 0;
-            for (int32_t j = rstart; j < rlen; ++j) {
-              lb += P.fs_ntok[rfirst + j];
-              ++bn;
-              if (lb >= tb) break;
-            }
-            r.fs1 = rfirst + rstart;
-            r.n1 = (uint16_t)bn;
-            i -= nchunk - a_end;
-          } else {
-            rn = false;
-            r.fs1 = first + cs + a_end;
-            r.n1 = (uint16_t)(nchunk - a_end);
-            for (int32_t j = a_end; j < nchunk; ++j) lb += P.fs_ntok[first + cs + j];
-          }
-          // _truncate_seq_pair: longer side (ties -> B), front/back by coin
-          int32_t alo = 0, ahi = la, blo = 0, bhi = lb;
-          while ((ahi - alo) + (bhi - blo) > max_num) {
-            const bool ta = (ahi - alo) > (bhi - blo);
-            if (rng.random() < 0.5) { if (ta) ++alo; else ++blo; }
-            else { if (ta) --ahi; else --bhi; }
-          }
-          if (ahi - alo < 1 || bhi - blo < 1) { err = PACK_EASSERT; break; }
-          r.lo0 = (uint16_t)alo; r.hi0 = (uint16_t)ahi;
-          r.lo1 = (uint16_t)blo; r.hi1 = (uint16_t)bhi;
-          r.flags = (uint16_t)((rn ? 1 : 0) | 2);
-          r.num_tokens = (uint16_t)((ahi - alo) + (bhi - blo) + 3);
-          out[np++] = r;
-          nchunk = 0;
-          cur = 0;
-        }
-      }
-    }
-  }
-  P.part_err[p] = err;
-  if (err) { P.part_npairs[p] = 0; P.part_ntok[p] = 0; return; }
-  shuffle_and_bin(P, p, v, np, rng);
-}
-
-// ------------------------------------------------------------- CodeBERT ----
-// _truncate_seq: 1 coin per excess token; deleting from an empty list is the
-// reference's IndexError (reported as PACK_EINDEX).
-__device__ __forceinline__ bool truncate_seq(MTLane& rng, int32_t& lo, int32_t& hi, int32_t max_n) {
-  while (hi - lo > max_n) {
-    if (hi - lo == 0) return false;
-    if (rng.random() < 0.5) ++lo; else --hi;
-  }
-  return true;
-}
-
-__global__ __launch_bounds__(64) void pack_codebert_kernel(PackParams P) {
-  const int64_t p = (int64_t)blockIdx.x * 64 + threadIdx.x;
-  if (p >= P.n_part) return;
-  const PartView v = filter_partition(P, p, true);
-  MTLane rng = lane_rng(P, p);
-  rng.seed(P.seed + (uint64_t)p);
-  const int32_t max_doc = P.max_seq >= 512 ? 64 : 32;
-  PairRec* out = P.pairs + v.pb;
-  int64_t np = 0;
-  int32_t err = PACK_OK;
-  for (int32_t dup = 0; dup < P.dup && !err; ++dup) {
-    for (int64_t di = 0; di < v.nd && !err; ++di) {
-      const int64_t first = P.fd_first[v.d0 + di];
-      const int32_t nd = P.fd_nd[v.d0 + di];
-      const int32_t nc = P.fd_n[v.d0 + di] - nd;
-      const int64_t cfirst = first + nd;
-      const int32_t special = nd ? 3 : 2;
-      const int32_t max_num = P.max_seq - special;
-      const double sp = rng.random();
-      // docstring part (pretrain_codebert.py:375-396)
-      int64_t dfs = first;
-      int32_t dn = 0, dlo = 0, dhi = 0;
-      if (nd && sp < P.short_seq_prob) {
-        dn = 1;
-        dhi = P.fs_ntok[first];
-      } else {
-        int32_t cur = 0, cn = 0;
-        for (int32_t i = 0; i < nd; ++i) {
-          ++cn;
-          cur += P.fs_ntok[first + i];
-          if (i == nc - 1 || cur > max_doc) {  // quirk: code-segment count
-            const int32_t end = (cur > max_doc && cn > 1) ? cn - 1 : cn;
-            dn = end;
-            for (int32_t j = 0; j < end; ++j) dhi += P.fs_ntok[first + j];
-            if (!truncate_seq(rng, dlo, dhi, max_doc)) err = PACK_EINDEX;
-            break;
-          }
-        }
-      }
-      if (err) break;
-      const int32_t doc_len = dhi - dlo;
-      // code part (:400-440); the chunk is contiguous: [cs, cs + cn)
-      int32_t cs = 0, cn = 0, cur = doc_len;
-      int64_t nout = 0;
-      for (int32_t i = 0; i < nc; ++i) {
-        if (cn == 0) cs = i;
-        ++cn;
-        cur += P.fs_ntok[cfirst + i];
-        if (i == nc - 1 || cur > max_num) {
-          const bool stay = cur > max_num && cn > 1;
-          int32_t clo = 0, chi = 0;
-          for (int32_t j = 0; j < cn; ++j) chi += P.fs_ntok[cfirst + cs + j];
-          if (!truncate_seq(rng, clo, chi, max_num - doc_len)) { err = PACK_EINDEX; break; }
-          if (chi - clo < 1) { err = PACK_EASSERT; break; }
-          if (nout == 0 || chi - clo >= 16) {
-            PairRec r;
-            r.fs0 = dfs; r.n0 = (uint16_t)dn; r.lo0 = (uint16_t)dlo; r.hi0 = (uint16_t)dhi;
-            r.fs1 = cfirst + cs; r.n1 = (uint16_t)cn; r.lo1 = (uint16_t)clo; r.hi1 = (uint16_t)chi;
-            r.flags = (uint16_t)(special == 3 ? 2 : 0);
-            r.num_tokens = (uint16_t)(doc_len + (chi - clo) + special);
-            out[np++] = r;
-            ++nout;
-          }
-          if (stay) { cs = i; cn = 1; cur = P.fs_ntok[cfirst + i] + doc_len; }
-          else { cn = 0; cur = doc_len; }
-        }
-      }
-    }
-  }
-  P.part_err[p] = err;
-  if (err) { P.part_npairs[p] = 0; P.part_ntok[p] = 0; return; }
-  shuffle_and_bin(P, p, v, np, rng);
-}
 
 // ------------------------------------------------- partition scans ----
 // exclusive scans of two int64 arrays (n entries) into n+1 entries, one block
@@ -813,18 +535,6 @@ hipError_t launch_compact_ids(const uint16_t* ids, const int64_t* sent_off, cons
   if (grid > 8192) grid = 8192;
   hipLaunchKernelGGL(compact_ids_kernel, dim3((unsigned)grid), dim3(256), 0, s, ids, sent_off, ntok, tokoff, n_sent,
                      dense);
-  return hipGetLastError();
-}
-
-hipError_t launch_pack_bert(const PackParams& P, hipStream_t s) {
-  const int grid = (int)((P.n_part + 63) / 64);
-  hipLaunchKernelGGL(pack_bert_kernel, dim3(grid), dim3(64), 0, s, P);
-  return hipGetLastError();
-}
-
-hipError_t launch_pack_codebert(const PackParams& P, hipStream_t s) {
-  const int grid = (int)((P.n_part + 63) / 64);
-  hipLaunchKernelGGL(pack_codebert_kernel, dim3(grid), dim3(64), 0, s, P);
   return hipGetLastError();
 }
 

@@ -67,6 +67,13 @@ __device__ __forceinline__ void wsync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// global writes of this wave visible to its later reads (other lanes)
+__device__ __forceinline__ void gsync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
 __device__ __forceinline__ int wscan_incl(int v, int lane) {
   (void)lane;
   return wave_incl_add(v);
@@ -183,7 +190,8 @@ struct WaveRng {
   // is already decided for every draw the batch could give it (r < n_lo:
   // accepted, r >= n_hi: rejected); only the words with r in [n_lo, n_hi) are
   // walked in order, one ballot step each.
-  __device__ __noinline__ void shuffle_draws(int m, uint16_t* jb) {
+  template <class T>
+  __device__ __noinline__ void shuffle_draws(int m, T* jb) {
     int q = m - 1;
     while (q >= 1) {
       if (idx >= MT_N) refill();
@@ -222,7 +230,7 @@ struct WaveRng {
         end = lim - 1;
         s = __popcll(accm);
       }
-      if (lane <= end && (accm >> lane & 1ull)) jb[q - pre] = (uint16_t)r;
+      if (lane <= end && (accm >> lane & 1ull)) jb[q - pre] = (T)r;
       idx += end + 1;
       q -= s;
     }
@@ -284,6 +292,68 @@ struct WaveRng {
     wsync();
   }
 };
+
+// random.shuffle(x) over x = order[0..np) (random.py: for i = n-1 .. 1,
+// j = _randbelow(i+1), swap x[i], x[j]), order in global memory.  The draws
+// first (shuffle_draws: the same MT words as the sequential calls) into
+// scratch jq[q]; then the swaps in batches of 64 positions [qmin, qb]: the
+// batch's slots -- its 64 positions (lane t = position qb - t) and the <= 64
+// distinct positions below it that its draws hit -- are gathered into two
+// registers per lane, the 64 swaps run in order on them (readlane +
+// lane select), and the slots are scattered back.  Per 64 swaps: one coalesced
+// read + write and <= 64 parallel gathers, where the swap loop paid a
+// dependent global round trip per swap.
+__device__ __forceinline__ void shuffle_global(WaveRng& rng, int np, int32_t* order, int32_t* jq, int lane) {
+  rng.shuffle_draws(np, jq);
+  gsync();
+  for (int qb = np - 1; qb >= 1; qb -= 64) {
+    const int qmin = max(qb - 63, 1);
+    const int q = qb - lane;
+    const bool vq = q >= qmin;
+    const int j = vq ? jq[q] : 0;
+    int va = vq ? order[q] : 0;
+    const bool low = vq && j < qmin;
+    // the first lane whose draw hits the same position below the batch
+    int first = 64;
+    for (uint64_t m = __ballot(low); m;) {
+      const int a = __ffsll((unsigned long long)m) - 1;
+      const int ja = __builtin_amdgcn_readlane(j, a);
+      const bool same = low && j == ja;
+      if (same) first = a;
+      m &= ~__ballot(same);
+    }
+    const bool own = low && first == lane;
+    int vb = own ? order[j] : 0;
+    const int sj = !vq ? lane : j >= qmin ? qb - j : 64 + first;  // slot of position j
+    const int nq = qb - qmin + 1;
+    for (int t = 0; t < nq; ++t) {
+      const int s2 = __builtin_amdgcn_readlane(sj, t);
+      const int x = __builtin_amdgcn_readlane(va, t);
+      const int y = s2 < 64 ? __builtin_amdgcn_readlane(va, s2) : __builtin_amdgcn_readlane(vb, s2 - 64);
+      va = lane == t ? y : va;
+      if (s2 < 64) va = lane == s2 ? x : va;
+      else vb = lane == s2 - 64 ? x : vb;
+    }
+    if (vq) order[q] = va;
+    if (own) order[j] = vb;
+    gsync();
+  }
+}
+
+// binning reads the shuffled order once with each record's num_tokens packed
+// in (rec | nt << 21; the record reads are random), then every bin pass
+// reads it linearly
+constexpr int PACKED_REC_BITS = 21;
+__device__ __forceinline__ bool order_packable(int np, int max_seq) {
+  return np < (1 << PACKED_REC_BITS) && max_seq < (1 << (32 - PACKED_REC_BITS));
+}
+__device__ __forceinline__ void pack_order_nt(int32_t* order, const PairRec* out, int np, int lane) {
+  for (int k = lane; k < np; k += 64) {
+    const int rec = order[k];
+    order[k] = rec | ((int)out[rec].num_tokens << PACKED_REC_BITS);
+  }
+  gsync();
+}
 
 // smallest k in [k0, n) with (k == n-1) or (sum lens[k0..k] >= target);
 // returns k and the sum.  lens via GET (LDS or global).
@@ -469,12 +539,20 @@ __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
     }
     return f;
   };
+  // a document of <= 64 sentences keeps its lengths in a register, loaded
+  // one document visit ahead (the load flies while this visit's pairs run)
+  auto doc_lens = [&](int d) -> int {
+    const int f = doc_first(d), n = doc_n(d);
+    return n <= 64 && lane < n ? len_at(f + lane) : 0;
+  };
+  int dl_next = nd > 0 ? doc_lens(0) : 0;
   for (int dup = 0; dup < P.dup && !err; ++dup) {
     for (int di = 0; di < nd && !err; ++di) {
       const int first = doc_first(di), len = doc_n(di);
-      // a document of <= 64 sentences keeps its lengths in a register
       const bool dreg = len <= 64;
-      const int dl = dreg && lane < len ? len_at(first + lane) : 0;
+      const int dl = dl_next;
+      if (di + 1 < nd) dl_next = doc_lens(di + 1);
+      else if (dup + 1 < P.dup) dl_next = doc_lens(0);
       int target = max_num;
       if (rng.random() < P.short_seq_prob) target = (int)rng.randint(2, max_num);
       int i = 0;
@@ -684,20 +762,25 @@ __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __builtin_amdgcn_s_waitcnt(0);
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-  // lane 0 alone touches the order array here (program order suffices)
-  for (int k = np - 1; k >= 1; --k) {
-    const int j = (int)rng.randbelow((uint32_t)(k + 1));
-    if (lane == 0) {
-      if (ores) { const uint16_t t = D.order[k]; D.order[k] = D.order[j]; D.order[j] = t; }
-      else { const int32_t t = gorder[k]; gorder[k] = gorder[j]; gorder[j] = t; }
+  if (ores) {
+    // lane 0 alone touches the order array here (program order suffices)
+    for (int k = np - 1; k >= 1; --k) {
+      const int j = (int)rng.randbelow((uint32_t)(k + 1));
+      if (lane == 0) { const uint16_t t = D.order[k]; D.order[k] = D.order[j]; D.order[j] = t; }
     }
+  } else {
+    shuffle_global(rng, np, gorder, P.binned + pb, lane);  // (binned: draw scratch until binning)
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __builtin_amdgcn_s_waitcnt(0);
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   PW_STAMP(4)
-  auto ord_at = [&](int k) -> int { return ores ? (int)D.order[k] : gorder[k]; };
-  auto ntk_at = [&](int rec) -> int { return ores ? (int)D.ntk[rec] : (int)out[rec].num_tokens; };
+  const bool packed = !ores && order_packable(np, P.max_seq);
+  if (packed) pack_order_nt(gorder, out, np, lane);
+  auto ord_at = [&](int k) -> int { return ores ? (int)D.order[k] : packed ? gorder[k] & ((1 << PACKED_REC_BITS) - 1) : gorder[k]; };
+  auto ntk_at = [&](int k, int rec) -> int {
+    return ores ? (int)D.ntk[rec] : packed ? (int)((uint32_t)gorder[k] >> PACKED_REC_BITS) : (int)out[rec].num_tokens;
+  };
   // ---- stable bin partition + token offsets -------------------------------
   const int nb = P.nbins;
   int32_t* binned = P.binned + pb;
@@ -712,7 +795,7 @@ __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
       bool in = false;
       if (kk < np) {
         rec = ord_at(kk);
-        nt = ntk_at(rec);
+        nt = ntk_at(kk, rec);
         int bb = (nt - 1) / P.bin_size;
         bb = bb > nb - 1 ? nb - 1 : bb;
         in = bb == b;
@@ -959,13 +1042,9 @@ __global__ __launch_bounds__(64) void pack_codebert_wave_kernel(PackParams P) {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __builtin_amdgcn_s_waitcnt(0);
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-  for (int k = np - 1; k >= 1; --k) {
-    const int j = (int)rng.randbelow((uint32_t)(k + 1));
-    if (lane == 0) { const int32_t t = gorder[k]; gorder[k] = gorder[j]; gorder[j] = t; }
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  __builtin_amdgcn_s_waitcnt(0);
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  shuffle_global(rng, np, gorder, P.binned + pb, lane);  // (binned: draw scratch until binning)
+  const bool packed = order_packable(np, P.max_seq);
+  if (packed) pack_order_nt(gorder, out, np, lane);
   // ---- stable bin partition + token offsets ---------------------------------
   const int nb = P.nbins;
   int32_t* binned = P.binned + pb;
@@ -979,8 +1058,9 @@ __global__ __launch_bounds__(64) void pack_codebert_wave_kernel(PackParams P) {
       int rec = 0, nt = 0;
       bool in = false;
       if (kk < np) {
-        rec = gorder[kk];
-        nt = out[rec].num_tokens;
+        const int v = gorder[kk];
+        rec = packed ? v & ((1 << PACKED_REC_BITS) - 1) : v;
+        nt = packed ? (int)((uint32_t)v >> PACKED_REC_BITS) : (int)out[rec].num_tokens;
         int bb = (nt - 1) / P.bin_size;
         bb = bb > nb - 1 ? nb - 1 : bb;
         in = bb == b;

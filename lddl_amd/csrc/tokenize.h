@@ -14,13 +14,13 @@ struct TokParams {
   const int64_t* sent_off;
   int64_t n_sent;
   int32_t max_tok;
-  int32_t chunk;
   uint16_t* out_ids;
   int32_t* out_ntok;
   // unicode table
   const uint16_t* top;
   const uint32_t* pages;
   const uint4* multi;
+  const uint32_t* bmp;    // [0x10000] pages[top[cp >> 8] * 256 + (cp & 255)] for cp < U+10000
   // vocab
   const uint4* slots;
   const uint32_t* bloom;  // [BLOOM_WORDS]
@@ -38,26 +38,17 @@ struct TokParams {
   uint8_t* ovf;
   uint32_t* work_counter;
   uint64_t* dbg;  // optional phase stamps (LDDL_TOK_DEBUG=1), else null
-  int32_t dbg_mode;  // ablation (LDDL_TOK_ABLATE): 1 = skip WordPiece, 2 = filter-only lookups,
-                     // 3 = WordPiece without bucket loads (tok4)
 };
 
-hipError_t launch_tokenize(const TokParams& P, int grid, hipStream_t stream);
-const void* tokenize_kernel_ptr();
-hipError_t launch_tokenize_wave(const TokParams& P, int grid, hipStream_t stream);
-const void* tokenize_wave_kernel_ptr();
 int64_t tile_count(int64_t nbytes);
-hipError_t launch_tokenize_tiles(const TokParams& P, int64_t nbytes, int64_t* tile_sent, int32_t* fb_list,
-                                 int32_t* fb_count, int fb_grid, int64_t chunk, hipStream_t s);
 hipError_t launch_tile_bounds(const int64_t* sent_off, int64_t n_sent, int64_t n_tiles, int64_t* tile_sent,
                               hipStream_t s);
 hipError_t launch_tokenize_fallback(const TokParams& P, const int64_t* tile_sent, const int32_t* fb_list,
                                     const int32_t* fb_count, int grid, hipStream_t s);
-// v4 (tokenize_stream.hip): wave per 1 KiB tile, persistent; cfg selects
-// waves per workgroup / Bloom filter (0: 4+Bloom, 1: 4, 2: 12+Bloom, 3: 8+Bloom,
-// 4: 16+Bloom = default), 5 / 6: two 1 KiB tiles per wave (8 / 4 waves + Bloom)
-hipError_t launch_tokenize_stream(const TokParams& P, int64_t nbytes, int64_t* tile_sent, int32_t* fb_list,
-                                  int32_t* fb_count, int fb_grid, int n_cu, int cfg, hipStream_t s);
+const void* tokenize_fallback_kernel_ptr();
+// every tile through the exact serial path (tokenize_fallback.hip)
+hipError_t launch_tokenize_serial(const TokParams& P, int64_t nbytes, int64_t* tile_sent, int32_t* fb_list,
+                                  int32_t* fb_count, int fb_grid, hipStream_t s);
 
 // v5 (tokenize_split.hip): the tile scan resolves whole-word vocab hits and
 // hands every other word to a WordPiece record queue; a full-occupancy

@@ -1,0 +1,93 @@
+// Tile bounds and the exact serial tokenizer path.
+//
+// Tiles: tile t owns the sentences whose first byte lies in
+// [t * 1 KiB, (t+1) * 1 KiB) (relative to sent_off[0]); no sentence crosses a
+// tile, so every tile is independent.  tile_sent[t] = first sentence of tile
+// t (tile_bounds_kernel, one pass over the sentences).
+//
+// tokenize_fallback_kernel re-runs listed tiles one lane per sentence
+// (tokenize_serial.h: the serial restatement of HF tokenizers'
+// BertNormalizer / BertPreTokenizer / WordPiece behind
+// tokenizer.tokenize(s, max_length=512, truncation=True),
+// lddl/dask/bert/pretrain.py:79-80, as oracle/tokenizer_oracle.c).  The
+// split tokenizer (tokenize_split.hip) lists the tiles it does not model;
+// launch_tokenize_serial lists every tile (vocabularies / unicode tables the
+// split tokenizer does not take: > 61440 ids, or an ASCII page with more
+// than the A-Z -> a-z mapping).
+#include "common.h"
+#include "tokenize.h"
+#include "tokenize_serial.h"
+
+namespace lddl {
+
+constexpr int TILE_SHIFT = 10;  // nominal tile: sentences starting in 1 KiB
+
+// tile_sent[t] = first sentence whose start (relative) >= t * TILE
+__global__ void tile_bounds_kernel(const int64_t* sent_off, int64_t n_sent, int64_t n_tiles, int64_t* tile_sent) {
+  const int64_t base = sent_off[0];
+  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s <= n_sent; s += (int64_t)gridDim.x * blockDim.x) {
+    // tiles t with off[s-1] < t*TILE <= off[s] map to s (s = n_sent: the rest)
+    const int64_t hi = s < n_sent ? sent_off[s] - base : (n_tiles << TILE_SHIFT);
+    const int64_t lo = s > 0 ? sent_off[s - 1] - base : -1;
+    int64_t t0 = (lo >> TILE_SHIFT) + 1;  // first t with t*TILE > lo
+    if (lo < 0) t0 = 0;
+    const int64_t t1 = hi >> TILE_SHIFT;  // last t with t*TILE <= hi
+    for (int64_t t = t0; t <= t1 && t <= n_tiles; ++t) tile_sent[t] = s;
+  }
+}
+
+// Exact serial path for the listed tiles: lane per sentence (tokenize_serial.h).
+__global__ __launch_bounds__(256) void tokenize_fallback_kernel(TokParams P, const int64_t* tile_sent,
+                                                                const int32_t* fb_list, const int32_t* fb_count) {
+  __shared__ uint32_t ascii_tab[128];
+  if (threadIdx.x < 128) ascii_tab[threadIdx.x] = P.pages[(uint32_t)P.top[0] * 256u + threadIdx.x];
+  __syncthreads();
+  const int n = *fb_count;
+  const LdsWordBuf wb{P.ovf + ((size_t)blockIdx.x * 256 + threadIdx.x) * WB_OVF};
+  const int64_t base = P.sent_off[0];
+  const int wave = (blockIdx.x * 256 + threadIdx.x) >> 6, lane = threadIdx.x & 63;
+  const int nw = (gridDim.x * 256) >> 6;
+  for (int k = wave; k < n; k += nw) {
+    const int64_t t = fb_list[k];
+    const int64_t sa = tile_sent[t], sb = tile_sent[t + 1];
+    for (int64_t s = sa + lane; s < sb; s += 64) {
+      SentState st{P.sent_off[s], P.sent_off[s + 1], P.sent_off[s] - base, 0};
+      while (st.p < st.e && st.ntok < P.max_tok) step(P, st, wb, ascii_tab);
+      P.out_ntok[s] = min(st.ntok, P.max_tok);
+    }
+  }
+}
+
+int64_t tile_count(int64_t nbytes) { return (nbytes >> TILE_SHIFT) + 1; }
+const void* tokenize_fallback_kernel_ptr() { return reinterpret_cast<const void*>(&tokenize_fallback_kernel); }
+
+
+__global__ void list_all_tiles_kernel(int64_t n_tiles, int32_t* fb_list, int32_t* fb_count) {
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n_tiles; t += (int64_t)gridDim.x * blockDim.x)
+    fb_list[t] = (int32_t)t;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *fb_count = (int32_t)n_tiles;
+}
+
+hipError_t launch_tokenize_serial(const TokParams& P, int64_t nbytes, int64_t* tile_sent, int32_t* fb_list,
+                                  int32_t* fb_count, int fb_grid, hipStream_t s) {
+  const int64_t n_tiles = tile_count(nbytes);
+  hipError_t e = launch_tile_bounds(P.sent_off, P.n_sent, n_tiles, tile_sent, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(list_all_tiles_kernel, dim3(1024), dim3(256), 0, s, n_tiles, fb_list, fb_count);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  return launch_tokenize_fallback(P, tile_sent, fb_list, fb_count, fb_grid, s);
+}
+
+hipError_t launch_tile_bounds(const int64_t* sent_off, int64_t n_sent, int64_t n_tiles, int64_t* tile_sent,
+                              hipStream_t s) {
+  hipLaunchKernelGGL(tile_bounds_kernel, dim3(4096), dim3(256), 0, s, sent_off, n_sent, n_tiles, tile_sent);
+  return hipGetLastError();
+}
+
+hipError_t launch_tokenize_fallback(const TokParams& P, const int64_t* tile_sent, const int32_t* fb_list,
+                                    const int32_t* fb_count, int grid, hipStream_t s) {
+  hipLaunchKernelGGL(tokenize_fallback_kernel, dim3(grid), dim3(256), 0, s, P, tile_sent, fb_list, fb_count);
+  return hipGetLastError();
+}
+
+}  // namespace lddl

@@ -1,6 +1,5 @@
-// Serial (one lane per sentence) tokenizer path shared by the kernels:
-// v1 tokenize_kernel, the window kernel's and the tile kernel's exact
-// fallbacks.  Restates oracle/tokenizer_oracle.c (HF tokenizers
+// Serial (one lane per sentence) tokenizer path of tokenize_fallback_kernel
+// (the split tokenizer's exact fallback).  Restates oracle/tokenizer_oracle.c (HF tokenizers
 // BertNormalizer + BertPreTokenizer + WordPiece, reference call site
 // lddl/dask/bert/pretrain.py:79-80).
 #pragma once
@@ -98,7 +97,6 @@ __device__ __forceinline__ int probe(const TokParams& P, const GET& get, int s, 
                                      const FILT& filt) {
   const uint64_t key = hash_key(h, (uint32_t)len, cont);
   if (!filt(key)) return -1;  // exact negative
-  if (P.dbg_mode == 2) return (int)(key & 0x3FFF);  // ablation: no global probe
   uint32_t idx = (uint32_t)key & P.slot_mask;
   const uint32_t fp = (uint32_t)(key >> 32);
   const uint32_t want = ((uint32_t)len << 16) | (cont << 24) | 0x80000000u;

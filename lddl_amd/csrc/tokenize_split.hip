@@ -445,10 +445,14 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
             }
           }
         }
+        // (code points of the BMP: one load from the flat table; above it, top -> page)
 #pragma unroll
-        for (int j = 0; j < XB; ++j) xt[j] = (xcp[j] >> 31) ? (uint32_t)P.top[(xcp[j] & 0x1FFFFFu) >> 8] : 0u;
+        for (int j = 0; j < XB; ++j) xt[j] = (xcp[j] >> 31) && (xcp[j] & 0x1FFFFFu) >= 0x10000u ? (uint32_t)P.top[(xcp[j] & 0x1FFFFFu) >> 8] : 0u;
 #pragma unroll
-        for (int j = 0; j < XB; ++j) xe[j] = (xcp[j] >> 31) ? P.pages[xt[j] * 256u + (xcp[j] & 255u)] : 0u;
+        for (int j = 0; j < XB; ++j) {
+          const uint32_t cp = xcp[j] & 0x1FFFFFu;
+          xe[j] = !(xcp[j] >> 31) ? 0u : cp < 0x10000u ? P.bmp[cp] : P.pages[xt[j] * 256u + (cp & 255u)];
+        }
 #pragma unroll
         for (int j = 0; j < XB; ++j)
           xmul[j] = (xcp[j] >> 31) && ent_kind(xe[j]) == KIND_MULTI ? P.multi[ent_payload(xe[j])] : make_uint4(0, 0, 0, 0);

@@ -68,12 +68,8 @@ def test_bert_golden(packer, k, binned):
       assert bn == po.bin_of(e['num_tokens'], case['bin_size'], case['nbins'])
 
 
-@pytest.mark.parametrize('algo', [None, '1'])
 @pytest.mark.parametrize('k', range(len(CODE['cases'])))
-def test_codebert_golden(cpacker, monkeypatch, k, algo):
-  """algo: the wave-per-partition packer (default) or the lane-serial one (1)"""
-  if algo:
-    monkeypatch.setenv('LDDL_PACK_ALGO', algo)
+def test_codebert_golden(cpacker, k):
   case = CODE['cases'][k]
   c = case['cfg']
   sh, ids, ntok = shards_from_docs(case['docs'], case['ndoc'])
@@ -135,13 +131,11 @@ def test_wikibooks_seq512_bin64_vs_oracle(gpu, nparts):
     assert np.array_equal(bc[p], np.bincount([po.bin_of(r[3], 64, 8) for r in part], minlength=8))
 
 
-@pytest.mark.parametrize('mat,algo', [(None, None), ('1', None), (None, '1')])
-def test_codebert_end_to_end_vs_oracle(gpu, monkeypatch, mat, algo):
+@pytest.mark.parametrize('mat', [None, '1'])
+def test_codebert_end_to_end_vs_oracle(gpu, monkeypatch, mat):
   from lddl_amd import synth, pipeline
   if mat:
     monkeypatch.setenv('LDDL_MAT_ALGO', mat)
-  if algo:
-    monkeypatch.setenv('LDDL_PACK_ALGO', algo)
   c = synth.make_code(400, seed=31)
   pdo = pipeline.partition_by_bytes(c, 3)
   res = pipeline.run_bert(c, vocab_file=pipeline.VOCAB_CODEBERT, target_seq_length=512, bin_size=64,
@@ -277,11 +271,38 @@ def test_bert_masked_special_tokens_and_arena_regrow(gpu, monkeypatch):
   assert_same_pairs(res, exp)
 
 
+def codebert_oracle_rows(docs, ndoc, pdo, seq, ssp, dup, seed, bin_size, nbins):
+  """oracle/pack_oracle.py over pre-tokenised CodeBERT documents: the rows
+  (partition, doc tokens, code tokens, num_tokens) in output order and the
+  per-(partition, bin) counts; raises IndexError like the reference's
+  _truncate_seq quirk (pretrain_codebert.py:236-247)"""
+  rows, counts = [], []
+  for p in range(len(pdo) - 1):
+    D, nd = [], []
+    for d in range(pdo[p], pdo[p + 1]):  # empty segments / docs without code dropped (:143-161)
+      ds = [x for x in docs[d][:ndoc[d]] if x]
+      cs = [x for x in docs[d][ndoc[d]:] if x]
+      if cs:
+        D.append(ds + cs)
+        nd.append(len(ds))
+    pairs = po.partition_pairs(D, seed + p, lambda X, di, r: po.codebert_pairs(X, nd, di, seq, ssp, r), dup)
+    exp = []
+    for (doc_s, code_s, dw, cw) in pairs:
+      dt = [t for (d, s) in doc_s for t in D[d][s]][dw[0]:dw[1]]
+      ct = [t for (d, s) in code_s for t in D[d][s]][cw[0]:cw[1]]
+      exp.append((dt, ct, len(dt) + len(ct) + (3 if nd[code_s[0][0]] else 2)))
+    order, cnt = po.binned_order([e[2] for e in exp], bin_size, nbins)
+    rows += [(p,) + exp[i] for i in order]
+    counts.append(cnt)
+  return rows, counts
+
+
 @pytest.mark.parametrize('seq,ssp,dup', [(512, 0.1, 1), (128, 0.0, 2), (512, 1.0, 1), (128, 0.3, 3)])
-def test_codebert_wave_vs_lane_long_documents(cpacker, monkeypatch, seq, ssp, dup):
+def test_codebert_long_documents_vs_oracle(cpacker, seq, ssp, dup):
   """Documents with > 64 code and docstring segments (multi-window scans),
   long segments (truncation rounds across MT twists), empty segments: the
-  wave packer against the lane-serial one (itself pinned by the goldens)."""
+  wave packer against the oracle (oracle/pack_oracle.py codebert_pairs,
+  itself pinned by the reference goldens)."""
   rng = np.random.default_rng(seq + dup)
   docs, ndoc = [], []
   for d in range(60):
@@ -296,14 +317,18 @@ def test_codebert_wave_vs_lane_long_documents(cpacker, monkeypatch, seq, ssp, du
     docs.append(segs)
     ndoc.append(nds)
   pdo = [0, 13, 13, 40, 60]
-  out = {}
-  for algo in ('', '1'):
-    monkeypatch.setenv('LDDL_PACK_ALGO', algo)
-    sh, ids, ntok = shards_from_docs(docs, ndoc, part_doc_off=pdo)
-    try:
-      res = cpacker.pack(sh, ids, ntok, target_seq_length=seq, short_seq_prob=ssp, duplicate_factor=dup,
-                         seed=77, codebert=True, bin_size=seq // 4)
-      out[algo] = (res.rows(), res.bin_count.cpu().numpy().tolist())
-    except IndexError:
-      out[algo] = 'IndexError'
-  assert out[''] == out['1']
+  sh, ids, ntok = shards_from_docs(docs, ndoc, part_doc_off=pdo)
+  try:
+    exp, counts = codebert_oracle_rows(docs, ndoc, pdo, seq, ssp, dup, 77, seq // 4, 4)
+  except IndexError:
+    with pytest.raises(IndexError):
+      cpacker.pack(sh, ids, ntok, target_seq_length=seq, short_seq_prob=ssp, duplicate_factor=dup, seed=77,
+                   codebert=True, bin_size=seq // 4)
+    return
+  res = cpacker.pack(sh, ids, ntok, target_seq_length=seq, short_seq_prob=ssp, duplicate_factor=dup, seed=77,
+                     codebert=True, bin_size=seq // 4)
+  rows = res.rows()
+  assert len(rows) == len(exp)
+  for (p, a, b, fl, bn, tok), e in zip(rows, exp):
+    assert (p, a, b, len(tok)) == e
+  assert res.bin_count.cpu().numpy().tolist() == counts

@@ -107,7 +107,7 @@ def adversarial_sentences(rng, n):
   return out
 
 
-@pytest.mark.parametrize('algo', ['1', '2', '3', '4', '5'])
+@pytest.mark.parametrize('algo', ['0', '5'])
 @pytest.mark.parametrize('name', ['bert', 'codebert'])
 def test_hip_tokenize_adversarial_vs_oracle(gpu, monkeypatch, algo, name):
   from lddl_amd.synth import corpus_from_sentences
@@ -126,28 +126,12 @@ def test_hip_tokenize_adversarial_vs_oracle(gpu, monkeypatch, algo, name):
       assert np.array_equal(a.astype(np.int64), b.astype(np.int64)), (i, repr(sents[i][:80]))
 
 
-@pytest.mark.parametrize('algo', ['1', '2', '3', '4', '5'])
+@pytest.mark.parametrize('algo', ['0', '5'])
 def test_hip_tokenize_algos_agree_on_wiki(gpu, monkeypatch, algo):
   from lddl_amd import synth
   from lddl_amd.tokenizer import Tokenizer
   monkeypatch.setenv('LDDL_TOKENIZE_ALGO', algo)
   c = synth.make_wiki(3_000_000, seed=17)
-  ids, ntok = run_hip(Tokenizer(VOCABS['bert']), c.data, c.sent_off)
-  oids, ontok = OracleTokenizer(VOCABS['bert']).run(c.data, c.sent_off, 512, nthreads=8)
-  assert np.array_equal(ntok, ontok)
-  for a, b in zip(compact(ids, ntok, c.sent_off), compact(oids, ontok, c.sent_off)):
-    assert np.array_equal(a.astype(np.int64), b.astype(np.int64))
-
-
-def test_hip_tokenize_tiles_in_several_launches(gpu, monkeypatch):
-  """The tile kernel goes out in chunks of <= 2^22 workgroups (a dispatch's
-  grid is 32-bit in work-items); force small chunks so the seams between
-  launches are exercised at a size the oracle finishes quickly."""
-  from lddl_amd import synth
-  from lddl_amd.tokenizer import Tokenizer
-  monkeypatch.setenv('LDDL_TOKENIZE_ALGO', '3')
-  monkeypatch.setenv('LDDL_TILE_CHUNK', '997')
-  c = synth.make_wiki(3_000_000, seed=23)
   ids, ntok = run_hip(Tokenizer(VOCABS['bert']), c.data, c.sent_off)
   oids, ontok = OracleTokenizer(VOCABS['bert']).run(c.data, c.sent_off, 512, nthreads=8)
   assert np.array_equal(ntok, ontok)

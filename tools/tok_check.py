@@ -1,6 +1,6 @@
 """GPU tokenizer check + timing for the kernel variants (GPU box tool).
 
-    python tools/tok_check.py [MB] [algo[:cfg] ...]
+    python tools/tok_check.py [MB] [algo[:cfg] ...]   (algo 5: split tokenizer, 0: serial path)
 
 Tokenizes a synthetic Wikipedia-style corpus of MB megabytes with each
 variant, compares ids / counts with the oracle (first MB only, for speed)
@@ -17,7 +17,7 @@ import torch  # noqa: E402
 
 def main():
   mb = int(sys.argv[1]) if len(sys.argv) > 1 else 64
-  variants = sys.argv[2:] or ['3', '4']
+  variants = sys.argv[2:] or ['5']
   from lddl_amd import synth
   from lddl_amd.tokenizer import Tokenizer
   from lddl_amd.pipeline import VOCAB_BERT
@@ -33,7 +33,6 @@ def main():
   for v in variants:
     algo, _, cfg = v.partition(':')
     os.environ['LDDL_TOKENIZE_ALGO'] = algo
-    os.environ['LDDL_TOK4_CFG'] = cfg or '0'
     os.environ['LDDL_TOK5_CFG'] = cfg or '0'
     tok = Tokenizer()
     ids, ntok = tok.tokenize_device(d, o)
@@ -55,7 +54,9 @@ def main():
         print('  ntok differs in sentence %d (%d vs %d): %r' % (i, h_ntok[i], ontok[i], c.sentence(i)[:200]))
     ok = len(bad) == 0 and nbad_ids == 0
     ntoks = int(h_ntok.sum())
-    times = []
+    times, ks = [], []
+    if algo == '5':
+      tok.set_timing(True)
     for _ in range(3):
       s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
       s.record()
@@ -63,7 +64,13 @@ def main():
       e.record()
       torch.cuda.synchronize()
       times.append(s.elapsed_time(e))
+      if algo == '5':
+        ks.append(tok.stats())
     ms = min(times)
+    if ks:
+      print('  per kernel (min of 3): scan %.3f  wordpiece %.3f  expand %.3f ms; %d records' % (
+          min(k['scan_ms'] for k in ks), min(k['wordpiece_ms'] for k in ks), min(k['expand_ms'] for k in ks),
+          ks[0]['records']))
     print('variant %s: parity(%d sents) %s (ntok bad %d, ids bad %d)  %.3f ms  %.1f GB/s  %.2f Gtok/s' % (
         v, ns_chk, 'OK' if ok else 'FAIL', len(bad), nbad_ids, ms, c.nbytes / ms / 1e6, ntoks / ms / 1e6),
           flush=True)
