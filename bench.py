@@ -51,6 +51,8 @@ def parse():
   ap.add_argument('--seed', type=int, default=12345)
   ap.add_argument('--masking', action='store_true', help='static masking (--masking of the reference)')
   ap.add_argument('--no-cpu-baseline', action='store_true')
+  ap.add_argument('--no-sample-check', action='store_true',
+                  help='skip the oracle comparison of one full-size partition after the timed steps')
   ap.add_argument('--cpu-seconds', type=float, default=12.0)
   ap.add_argument('--parquet-parts', type=int, default=64,
                   help='after timing: write this many partitions as parquet shards and report the writer rate '
@@ -121,28 +123,47 @@ def _code_docs(base, ids, ntok, d0, d1):
   return docs, nd
 
 
-def reference_tokenizer_rate(args, base, seconds):
+def _ref_tok_worker(a):
+  """one host process: the reference's per-sentence tokenize call over its
+  sentences for ~seconds -> (tokens, sentences, elapsed)"""
+  vocab, sents, seconds = a
+  import transformers
+  tok = transformers.BertTokenizerFast(vocab)
+  n = k = 0
+  t = time.perf_counter()
+  while k < len(sents) and (k & 255 or time.perf_counter() - t < seconds):
+    n += min(512, len(tok.tokenize(sents[k], max_length=512, truncation=True)))
+    k += 1
+  return n, k, time.perf_counter() - t
+
+
+def reference_tokenizer_rate(args, base, seconds, procs):
   """The reference's own tokenizer call (pretrain.py:79-80: HF
   BertTokenizerFast(vocab).tokenize(s, max_length=512, truncation=True), one
-  Python call per sentence in each single-threaded Dask worker) on one host
-  core, over the first sentences of the same corpus for ~seconds.  The
-  reference runs one such worker per core, so its node rate is about this x
-  the cores.  None when transformers is not importable."""
+  Python call per sentence in each single-threaded Dask worker), run by
+  `procs` host processes at once (the reference runs one such worker per
+  core), each over its own sentences of the same corpus for ~seconds; the
+  node rate is the sum of the per-process rates.  None when transformers is
+  not importable."""
   try:
     import transformers
   except Exception:
     return None
+  import multiprocessing
   from lddl_amd.pipeline import VOCAB_BERT, VOCAB_CODEBERT
-  tok = transformers.BertTokenizerFast(VOCAB_CODEBERT if args.corpus == 'code' else VOCAB_BERT)
-  n = k = 0
-  t = time.perf_counter()
-  while k < base.n_sent and (k & 255 or time.perf_counter() - t < seconds):
-    n += min(512, len(tok.tokenize(base.sentence(k), max_length=512, truncation=True)))
-    k += 1
-  el = time.perf_counter() - t
-  return {'tokens_per_s_per_core': n / el, 'unit': 'tokens/s', 'cores': 1, 'kind': 'reference-library',
-          'sample': 'transformers %s BertTokenizerFast.tokenize per sentence (the call at pretrain.py:79-80) on %d '
-                    'sentences, %.1f s, 1 core' % (transformers.__version__, k, el)}
+  vocab = VOCAB_CODEBERT if args.corpus == 'code' else VOCAB_BERT
+  per = min(base.n_sent // max(1, procs), 30_000)
+  work = [(vocab, [base.sentence(k) for k in range(i * per, (i + 1) * per)], seconds) for i in range(procs)]
+  # spawned (not forked) workers: this process holds a GPU context
+  with multiprocessing.get_context('spawn').Pool(procs) as pool:
+    out = pool.map(_ref_tok_worker, work)
+  rates = [n / el for n, k, el in out]
+  return {'value': sum(rates), 'tokens_per_s_per_core': float(np.mean(rates)), 'unit': 'tokens/s', 'cores': procs,
+          'kind': 'reference-library',
+          'sample': 'transformers %s BertTokenizerFast.tokenize per sentence (the call at pretrain.py:79-80) in %d '
+                    'host processes at once, %d sentences in %.1f s each on average' % (
+                        transformers.__version__, procs, int(np.mean([k for n, k, el in out])),
+                        float(np.mean([el for n, k, el in out])))}
 
 
 def cpu_baseline(args, base, pdo, seconds):
@@ -193,7 +214,7 @@ def cpu_baseline(args, base, pdo, seconds):
   e2e = None
   if pack_rate:
     e2e = 1.0 / (1.0 / tok_rate + 1.0 / (pack_rate * threads))
-  ref = reference_tokenizer_rate(args, base, min(3.0, seconds * 0.25))
+  ref = reference_tokenizer_rate(args, base, min(3.0, seconds * 0.25), threads)
   return {'value': e2e if e2e else tok_rate, 'unit': 'tokens/s', 'cores': threads, 'kind': 'port',
           'reference_library': ref,
           'sample': ('oracle/tokenizer_oracle.c on %d sentences (%.1f MB, %.1f s, %.3g tok/s at %d threads) + '
@@ -202,6 +223,75 @@ def cpu_baseline(args, base, pdo, seconds):
                          ns, (base.sent_off[ns] - base.sent_off[0]) / 1e6, tok_s, tok_rate, threads, p, pack_s,
                          pack_rate or 0, threads)),
           'tokenize_tokens_per_s': tok_rate, 'pack_tokens_per_s_per_thread': pack_rate}
+
+
+def sample_partition_check(args, pk, res, base, pdo, reps, seed0):
+  """One full-size partition of the timed run (the middle partition of the
+  middle replica) against the oracle, outside the timed region: its rows
+  (partition, A, B, is_random_next, num_tokens[, masked positions / labels])
+  in output order must be identical."""
+  from oracle.oracle import OracleTokenizer
+  from oracle import pack_oracle as po
+  from lddl_amd.synth import Corpus
+  t0 = time.time()
+  code = args.corpus == 'code'
+  npb = len(pdo) - 1
+  r, q = reps // 2, npb // 2
+  p = r * npb + q
+  bc = res.bin_count.cpu().numpy()
+  g0, n = int(bc[:p].sum()), int(bc[p].sum())
+  off = res.tok_off[g0:g0 + n + 1].cpu().numpy()
+  tok = res.tokens[int(off[0]):int(off[-1])].cpu().numpy().view(np.uint16).astype(np.int64)
+  l0 = res.len0[g0:g0 + n].cpu().numpy().view(np.uint16).astype(np.int64)
+  l1 = res.len1[g0:g0 + n].cpu().numpy().view(np.uint16).astype(np.int64)
+  fl = res.flags[g0:g0 + n].cpu().numpy()
+  pt = res.part[g0:g0 + n].cpu().numpy()
+  if res.mlm_off is not None:
+    moff = res.mlm_off[g0:g0 + n + 1].cpu().numpy()
+    mpos = res.mlm_pos[int(moff[0]):int(moff[-1])].cpu().numpy().view(np.uint16).astype(np.int64)
+    mlab = res.mlm_label[int(moff[0]):int(moff[-1])].cpu().numpy().view(np.uint16).astype(np.int64)
+  got = []
+  for g in range(n):
+    row = tok[off[g] - off[0]:off[g + 1] - off[0]]
+    k0 = 1 + int(l0[g]) + (1 if fl[g] & 2 else 0)
+    e = (int(pt[g]), row[1:1 + l0[g]].tolist(), row[k0:k0 + l1[g]].tolist(), int(fl[g]) & 1, len(row))
+    if res.mlm_off is not None:
+      e += (mpos[moff[g] - moff[0]:moff[g + 1] - moff[0]].tolist(), mlab[moff[g] - moff[0]:moff[g + 1] - moff[0]].tolist())
+    got.append(e)
+  # the oracle over the partition's documents of the unique corpus
+  d0, d1 = int(pdo[q]), int(pdo[q + 1])
+  s0, s1 = int(base.doc_sent_off[d0]), int(base.doc_sent_off[d1])
+  b0 = int(base.sent_off[s0])
+  sub = Corpus(np.ascontiguousarray(base.data[b0:int(base.sent_off[s1])]), base.sent_off[s0:s1 + 1] - b0,
+               base.doc_sent_off[d0:d1 + 1] - s0,
+               None if base.doc_nseg_doc is None else base.doc_nseg_doc[d0:d1])
+  oids, ontok = OracleTokenizer(pk.tok.vocab_file).run(sub.data, sub.sent_off, 512,
+                                                        nthreads=min(os.cpu_count() or 1, 16))
+  nbins = args.target_seq_length // args.bin_size
+  if code:
+    docs, nd = _code_docs(sub, oids, ontok, 0, d1 - d0)
+    pairs = po.partition_pairs(docs, seed0 + p, lambda D, di, rr: po.codebert_pairs(
+        D, nd, di, args.target_seq_length, 0.1, rr), args.duplicate_factor)
+    rows = []
+    for (doc_s, code_s, dw, cw) in pairs:
+      dt = [t for (d, x) in doc_s for t in docs[d][x]][dw[0]:dw[1]]
+      ct = [t for (d, x) in code_s for t in docs[d][x]][cw[0]:cw[1]]
+      rows.append((dt, ct, 0, len(dt) + len(ct) + (3 if nd[code_s[0][0]] else 2)))
+    order, _ = po.binned_order([x[3] for x in rows], args.bin_size, nbins)
+    exp = [rows[i] for i in order]
+  else:
+    mask = (0.15, pk.tok.vocab_size, pk.tok.cls_id, pk.tok.sep_id, pk.tok.mask_id) if args.masking else None
+    exp = po.run_bert_shards(sub, oids, ontok, [0, d1 - d0], args.target_seq_length, 0.1, args.duplicate_factor,
+                             seed0 + p, args.bin_size, mask)[0]
+  exp = [(p, list(x[0]), list(x[1]), int(bool(x[2])), x[3]) + ((list(x[4]), list(x[5])) if len(x) > 4 else ())
+         for x in exp]
+  if code:  # (CodeBERT rows carry no is_random_next)
+    got = [(x[0], x[1], x[2], 0) + x[4:] for x in got]
+  if got != exp:
+    bad = next(i for i, (a, b) in enumerate(zip(got + [None] * len(exp), exp + [None] * len(got))) if a != b)
+    raise RuntimeError('sampled partition %d differs from the oracle at row %d of %d / %d' % (p, bad, len(got),
+                                                                                            len(exp)))
+  return {'partition': p, 'rows': n, 'sentences': s1 - s0, 'identical': True, 'seconds': time.time() - t0}
 
 
 def parquet_sample(args, pk, res, sh):
@@ -363,8 +453,10 @@ def main():
     pass
   if args.parquet_parts > 0:
     line['parquet_writer'] = parquet_sample(args, pk, res, sh)
-  if not args.no_cpu_baseline and world == 1:  # the host baseline: rank 0 at N=1 only
+  if not args.no_cpu_baseline and world == 1:  # the host leg (the oracle): rank 0 at N=1 only
     line['cpu_baseline'] = cpu_baseline(args, base, pdo, args.cpu_seconds)
+    if not args.no_sample_check:  # the oracle as the checker of one full-size partition of the timed run
+      line['cpu_baseline']['sample_check'] = sample_partition_check(args, pk, res, base, pdo, reps, kw['seed'])
   print(json.dumps(line), flush=True)
   if dist is not None:
     dist.destroy_process_group()
