@@ -22,17 +22,18 @@ def _newer(target, deps):
   return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build_hip(force=False, verbose=False):
+def build_hip(force=False, verbose=False, lib=LIB, defines=()):
   """Each .hip compiled to its own object in parallel (device code is per
-  translation unit: the kernels share headers only), then linked."""
+  translation unit: the kernels share headers only), then linked.
+  lib / defines: A/B builds of variants (tools/ab_build.py)."""
   srcs = sorted(glob.glob(os.path.join(CSRC, '*.hip')))
   hdrs = glob.glob(os.path.join(CSRC, '*.h')) + [os.path.join(ROOT, 'include', 'lddl_amd.h')]
-  if not force and not _newer(LIB, srcs + hdrs):
-    return LIB
+  if not force and not _newer(lib, srcs + hdrs):
+    return lib
   from concurrent.futures import ThreadPoolExecutor
-  odir = os.path.join(CSRC, 'build')
+  odir = os.path.join(CSRC, 'build') if lib == LIB else os.path.splitext(lib)[0] + '_obj'
   os.makedirs(odir, exist_ok=True)
-  flags = ['--offload-arch=%s' % ARCH, '-O3', '-std=c++17', '-fPIC', '-Wno-unused-result']
+  flags = ['--offload-arch=%s' % ARCH, '-O3', '-std=c++17', '-fPIC', '-Wno-unused-result'] + ['-D' + d for d in defines]
 
   def obj(src):
     o = os.path.join(odir, os.path.basename(src)[:-4] + '.o')
@@ -46,12 +47,12 @@ def build_hip(force=False, verbose=False):
 
   with ThreadPoolExecutor(max_workers=min(len(srcs), max(1, min(8, os.cpu_count() or 1)))) as ex:
     objs = list(ex.map(obj, srcs))
-  cmd = ['hipcc', '--offload-arch=%s' % ARCH, '-shared', '-fPIC', '-o', LIB + '.tmp'] + objs
+  cmd = ['hipcc', '--offload-arch=%s' % ARCH, '-shared', '-fPIC', '-o', lib + '.tmp'] + objs
   if verbose:
     print(' '.join(cmd))
   subprocess.run(cmd, check=True, cwd=CSRC)
-  os.replace(LIB + '.tmp', LIB)
-  return LIB
+  os.replace(lib + '.tmp', lib)
+  return lib
 
 
 def build_oracle(force=False):

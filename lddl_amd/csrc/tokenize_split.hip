@@ -47,6 +47,18 @@ constexpr int UCAP = 256;                // units per round
 constexpr int NSCAP = 64;                // sentences per tile
 constexpr int XCAP = 32;                 // expansion markers per tile
 constexpr int KEYMAX = 56;               // key bytes a record holds
+#ifndef TOK5_XB
+#define TOK5_XB 4
+#endif
+#ifndef TOK5_PLANES
+#define TOK5_PLANES 1
+#endif
+#ifndef TOK5_MERGED_PROBE
+#define TOK5_MERGED_PROBE 1
+#endif
+#ifndef TOK5_INPLACE
+#define TOK5_INPLACE 1
+#endif
 constexpr int KEY1 = 28;                 // keys up to 28 bytes take one slot (<= 28 pieces)
 constexpr uint32_t BF = 0xFFu, BX = 0xFDu, BS = 0xF8u;  // filler, expansion, special k = BS+k
 enum : uint32_t { C_W = 1, C_I = 2, C_S = 4, C_D = 8, C_UP = 16, C_X = 32, C_CS = 64 };
@@ -97,6 +109,29 @@ __device__ __forceinline__ void nput(uint32_t* nb, int p, uint32_t v) { reinterp
 // bit q of each byte of c -> 4 bits (byte 0 -> bit 0)
 __device__ __forceinline__ uint32_t gather4(uint32_t c, int q) { return (((c >> q) & 0x01010101u) * 0x01020408u) >> 24; }
 
+// byte j of a_k -> byte k of t_j (a 4x4 byte transpose, v_perm_b32)
+__device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel) {
+  return __builtin_amdgcn_perm(hi, lo, sel);
+}
+__device__ __forceinline__ void byte_transpose4(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3, uint32_t& t0,
+                                                uint32_t& t1, uint32_t& t2, uint32_t& t3) {
+  const uint32_t l01 = perm(a1, a0, 0x05010400u), h01 = perm(a1, a0, 0x07030602u);  // a0.b0 a1.b0 a0.b1 a1.b1 | .b2 .b3
+  const uint32_t l23 = perm(a3, a2, 0x05010400u), h23 = perm(a3, a2, 0x07030602u);
+  t0 = perm(l23, l01, 0x05040100u);
+  t1 = perm(l23, l01, 0x07060302u);
+  t2 = perm(h23, h01, 0x05040100u);
+  t3 = perm(h23, h01, 0x07060302u);
+}
+// bit q of byte k of t_j -> bit 4k + j (16 positions)
+__device__ __forceinline__ uint32_t class_plane16(uint32_t t0, uint32_t t1, uint32_t t2, uint32_t t3, int q) {
+  uint32_t m = (t0 >> q) & 0x01010101u;
+  m |= ((t1 >> q) & 0x01010101u) << 1;
+  m |= ((t2 >> q) & 0x01010101u) << 2;
+  m |= ((t3 >> q) & 0x01010101u) << 3;  // bit 8k + j
+  m = (m | (m >> 4)) & 0x00FF00FFu;
+  return (m | (m >> 8)) & 0xFFFFu;
+}
+
 __device__ __forceinline__ int64_t uni64(int64_t x) {
   const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)(uint64_t)x);
   const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)x >> 32));
@@ -139,9 +174,21 @@ __device__ __forceinline__ bool span_dirty(const Lds& L, int p, int q) {
   return false;
 }
 
-// Compact / expand the dirty span [p, q) into the side buffer.  Returns its
-// normalised length (source in *src), -1 on overflow (flagged in misc[2]).
+// Compact / expand the dirty span [p, q).  Returns its normalised length
+// (source in *src), -1 on overflow (flagged in misc[2]).  Without expansion
+// markers in the tile (misc[1] == 0) a dirty span holds only fillers
+// (dropped / shortened chars): it compacts in place, one pass; otherwise it
+// goes to the side buffer (count pass, then the expansions written).
 __device__ int dirty_normalize(Lds& L, const TokParams& P, int p, int q, int* src) {
+  if (TOK5_INPLACE && L.misc[1] == 0) {
+    int o = p;
+    for (int i = p; i < q; ++i) {
+      const uint32_t b = nbyte(L.nb, i);
+      if (b != BF) nput(L.nb, o++, b);
+    }
+    *src = p;
+    return o - p;
+  }
   int len = 0;
   for (int i = p; i < q;) {
     const uint32_t b = nbyte(L.nb, i);
@@ -394,6 +441,31 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
       if (p0 >= nb) v0 = make_uint4(0, 0, 0, 0);
       if (p0 + 16 >= nb) v1 = make_uint4(0, 0, 0, 0);
       const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#if TOK5_PLANES
+      // class bytes c[k] (byte j = position 4k + j), then the per-position
+      // class bits as 32-bit planes without multiplies: 4x4 byte transposes
+      // put position 4k + j at byte k of t[j]; a plane gathers bit q of the
+      // four t[j] (bit 8k + j) and compresses the nibbles (bit 4k + j)
+      uint32_t c[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint32_t x = w[k];
+        c[k] = (uint32_t)ctab[x & 0xFFu] | ((uint32_t)ctab[(x >> 8) & 0xFFu] << 8) |
+               ((uint32_t)ctab[(x >> 16) & 0xFFu] << 16) | ((uint32_t)ctab[x >> 24] << 24);
+        // drop bytes -> filler 0xFF: 0x80 - 0x01 | 0x80 per byte (a shift-subtract of the 0x01 form
+        // becomes a quarter-rate multiply in LLVM)
+        const uint32_t dmk = (c[k] >> 3) & 0x01010101u;  // drop bytes -> filler 0xFF
+        L.nb[lane * 8 + k] = (x + ((c[k] & 0x10101010u) << 1)) | ((dmk << 8) - dmk);
+      }
+      uint32_t t[8];
+      byte_transpose4(c[0], c[1], c[2], c[3], t[0], t[1], t[2], t[3]);
+      byte_transpose4(c[4], c[5], c[6], c[7], t[4], t[5], t[6], t[7]);
+      auto plane = [&](int q) {
+        return class_plane16(t[0], t[1], t[2], t[3], q) | (class_plane16(t[4], t[5], t[6], t[7], q) << 16);
+      };
+      const uint32_t Wh = plane(0), Ih = plane(1), Sh = plane(2), Dh = plane(3), Xh = plane(5);
+      const uint32_t CSh = Wh | Ih | Sh | Xh;  // every byte but UTF-8 continuations (ctab)
+#else
       uint32_t Wh = 0, Ih = 0, Sh = 0, CSh = 0, Dh = 0, Xh = 0;
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
@@ -409,6 +481,7 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
         Xh |= gather4(c, 5) << sh;
         CSh |= gather4(c, 6) << sh;
       }
+#endif
       const int wlo = min(max(aoff - p0, 0), 32), whi = min(max(nb - p0, 0), 32);
       inwin = (whi >= 32 ? ~0u : ((1u << whi) - 1u)) & (wlo >= 32 ? 0u : ~((1u << wlo) - 1u));
       W = Wh; I = Ih; S_ = Sh; CS = CSh; D = Dh; X = Xh & inwin;
@@ -422,7 +495,7 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
       // exceptions in batches of 4 per lane: the table lookups of a batch
       // (code point -> page -> entry -> multi expansion) go out together
       for (uint32_t xm = X; __any(xm != 0);) {
-        constexpr int XB = 4;
+        constexpr int XB = TOK5_XB;
         int xi_[XB];
         uint32_t xcp[XB], xt[XB], xe[XB];
         uint4 xmul[XB];
@@ -617,6 +690,61 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
       }
       wsync();
       STAMP(5);
+#if TOK5_MERGED_PROBE
+      // ---- 3: prep (spans, dirty words, specials, long words) + the
+      //      whole-word probe of each pending unit (slot 0 of its home
+      //      bucket), one unit per lane: the key is loaded and hashed once
+      {
+        const int mb0 = (int)P.maxb[0];
+        const uint32_t vmask = P.vt_mask;
+        for (int r = 0; r < nr; r += 64) {
+          const int u = r + lane;
+          uint32_t w = 0;
+          uint16_t id = U_EMPTY;
+          if (u < nr) {
+            const int p = (int)(L.u.urec[u] & 0xFFFFu);
+            const uint32_t b0 = nbyte(L.nb, p);
+            if (b0 >= BS && b0 < BS + 5) {
+              id = (uint16_t)P.special[b0 - BS];
+            } else {
+              const int q = span_end(L, p, nb);
+              int src = p, len = q - p;
+              if (span_dirty(L, p, q)) len = max(dirty_normalize(L, P, p, q, &src), 0);
+              if (len == 0) {
+                id = U_EMPTY;
+              } else if (len > 100 && count_chars(L.nb, src, len) > 100) {
+                id = (uint16_t)P.unk;
+              } else {
+                id = U_DEFER;
+                w = wmake(u, src, len);
+                if (len > KEYMAX) L.misc[2] = 1;  // too long for a record: the tile falls back
+              }
+            }
+          }
+          const int len = wlen(w);
+          if (w != 0 && len <= 24 && len <= mb0) {
+            const Key6 key = load_key(L.nb, wsrc(w), len);
+            const uint4* bk = P.vt + 4 * (key_hash(key, len, 0u) & vmask);
+            const uint4 fa = bk[0], fb = bk[1];
+            if (slot_eq(fa, fb, key, ((uint32_t)len << 16) | 0x80000000u)) {
+              id = (uint16_t)(fb.z & 0xFFFFu);
+              w = 0;
+            }
+          }
+          if (u < nr) {
+            L.uid[u] = id;
+            L.u.uwp[u] = w;
+          }
+        }
+      }
+      wsync();
+      STAMP(6);
+      STAMP(7);
+      if (L.misc[2]) {
+        ovf = true;
+        break;
+      }
+#else
       // ---- 3: prep (spans, dirty words, specials, long words) ---------------
       for (int r = 0; r < nr; r += 64) {
         const int u = r + lane;
@@ -697,6 +825,7 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
         break;
       }
       STAMP(7);
+#endif
       // ---- 4: entries and records -------------------------------------------
       // Lane l holds units [l*per, l*per + per); segmented (by sentence)
       // exclusive prefix sums give each unit its entry index and its record

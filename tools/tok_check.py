@@ -24,6 +24,9 @@ def main():
   from oracle.oracle import OracleTokenizer, compact
   t0 = time.time()
   c = synth.make_wiki(mb << 20, seed=1)
+  if os.environ.get('ASCII') == '1':  # diagnostics: no exception bytes (non-ASCII -> 'x', '[' -> '(')
+    c.data[c.data >= 0x80] = ord('x')
+    c.data[c.data == ord('[')] = ord('(')
   print('gen %.1fs: %d bytes %d sentences' % (time.time() - t0, c.nbytes, c.n_sent), flush=True)
   d = torch.from_numpy(np.concatenate([c.data, np.zeros(16, np.uint8)])).cuda()
   o = torch.from_numpy(c.sent_off).cuda()
