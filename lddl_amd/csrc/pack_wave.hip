@@ -109,6 +109,7 @@ struct WaveRng {
   int lane;
   int idx;            // wave-uniform
   int wbase = -1024;  // tw[wbase + lane] is held in `win` (one LDS read per 64 draws)
+  int wend = 0;       // min(wbase + 64, MT_N): draws below it come from `win`
   uint32_t win = 0;
 
   __device__ __forceinline__ void seed(uint64_t n) {
@@ -149,16 +150,19 @@ struct WaveRng {
     pack_mt_refill((lds_u32*)L.mt, lane);
     idx = 0;
     wbase = -1024;
+    wend = 0;
   }
 
+  // a draw: one compare on the fast path (the window ends at the state's end,
+  // so idx < wend also means no twist is due)
   __device__ __forceinline__ uint32_t next() {
-    if (idx >= MT_N) refill();
-    int o = idx - wbase;
-    if (o < 0 || o >= 64) {
+    if (idx >= wend) {
+      if (idx >= MT_N) refill();
       wbase = idx;
+      wend = min(idx + 64, MT_N);
       win = temper(L.mt[idx + lane < MT_N ? idx + lane : MT_N - 1]);
-      o = 0;
     }
+    const int o = idx - wbase;
     ++idx;
     return (uint32_t)__builtin_amdgcn_readlane((int)win, o);
   }

@@ -1284,7 +1284,13 @@ __global__ __launch_bounds__(64 * WAVES) void wp_kernel(TokParams P, SplitParams
 // records' count and first 4 pieces (one 12-B load); a segmented scan of the
 // token counts gives the positions; the sentence's last entry writes its
 // token count (a sentence with no queued word keeps the scan's count).
-constexpr int EXP_PER = 4;
+#ifndef TOK5_EXP_BLOCKS
+#define TOK5_EXP_BLOCKS 8
+#endif
+#ifndef TOK5_EXP_PER
+#define TOK5_EXP_PER 1
+#endif
+constexpr int EXP_PER = TOK5_EXP_PER;
 struct ExpLds {
   uint32_t e0[65];      // group entry offsets
   int64_t eoff[64];     // entry index of the sentence's first entry
@@ -1484,7 +1490,7 @@ hipError_t launch_tokenize_split(const TokParams& P, int64_t nbytes, int64_t* ti
     if (e != hipSuccess || (e = mark(0, 1)) != hipSuccess || (e = mark(1, 0)) != hipSuccess) return e;
     if ((e = tok5::launch_wp<WP_WAVES>(P, S, n_cu, s)) != hipSuccess) return e;
     if ((e = mark(1, 1)) != hipSuccess || (e = mark(2, 0)) != hipSuccess) return e;
-    hipLaunchKernelGGL(tok5::expand_kernel, dim3((unsigned)std::max(1, n_cu * 8)), dim3(256), 0, s, P, S);
+    hipLaunchKernelGGL(tok5::expand_kernel, dim3((unsigned)std::max(1, n_cu * TOK5_EXP_BLOCKS)), dim3(256), 0, s, P, S);
     if ((e = hipGetLastError()) != hipSuccess || (e = mark(2, 1)) != hipSuccess) return e;
   }
   return launch_tokenize_fallback(P, tile_sent, S.fb_list, S.fb_count, fb_grid, s);
