@@ -670,8 +670,10 @@ static int pack_common(lddl_ctx* c, int codebert, const int32_t* d_ntok, const i
       HIP_TRY(hipStreamSynchronize(st));
       const char* nm[13] = {"filter", "ldsfill", "seed", "generate", "shuffle", "bin", "pairs", "parts",
                             "m_cand", "m_draws", "m_trace", "m_choices", "m_write"};
+      const char* gn[5] = {"g_doc", "g_fill", "g_pairB", "g_trunc", "g_store"};  // unmasked: generate sub-phases
       fprintf(stderr, "[lddl pack dbg]");
-      for (int k = 0; k < (P.masking ? 13 : 8); ++k) fprintf(stderr, " %s=%llu", nm[k], (unsigned long long)h[k]);
+      for (int k = 0; k < 13; ++k)
+        fprintf(stderr, " %s=%llu", k < 8 || P.masking ? nm[k] : gn[k - 8], (unsigned long long)h[k]);
       fprintf(stderr, "\n");
     }
     HIP_TRY(launch_scan_parts(P.part_npairs, P.part_ntok, n_part, pair_base, tok_base, P.part_err, err_any, st));

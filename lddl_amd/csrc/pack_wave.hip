@@ -427,6 +427,13 @@ __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
   // pair generation, shuffle, binning; masking: candidates, shuffle draws,
   // pick trace, 80/10/10 choices, sorted writes
   uint64_t ph[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, tprev = P.dbg ? __builtin_amdgcn_s_memtime() : 0;
+// generate sub-phases of the unmasked packer reuse the masking slots 6-10
+#define PW_GSTAMP(k)                                    \
+  if (!MASK && P.dbg) {                                 \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime();   \
+    ph[k] += t_ - tprev;                                \
+    tprev = t_;                                         \
+  }
 #define PW_STAMP(k)                                     \
   if (P.dbg) {                                          \
     const uint64_t t_ = __builtin_amdgcn_s_memtime();   \
@@ -559,6 +566,7 @@ __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
       else if (dup + 1 < P.dup) dl_next = doc_lens(0);
       int target = max_num;
       if (rng.random() < P.short_seq_prob) target = (int)rng.randint(2, max_num);
+      PW_GSTAMP(6)
       int i = 0;
       while (i < len) {
         const int cs = i;
@@ -571,6 +579,7 @@ __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
         const int la = a_end == nchunk ? cur
                        : dreg ? range_sum_reg(dl, cs, cs + a_end, lane)
                               : range_sum([&](int k) { return len_at(first + k); }, cs, cs + a_end, lane);
+        PW_GSTAMP(7)
         PairRec r;
         r.fs0 = s0 + first + cs;
         r.n0 = (uint16_t)a_end;
@@ -599,6 +608,7 @@ __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
           r.n1 = (uint16_t)(nchunk - a_end);
           i_next = j + 1;
         }
+        PW_GSTAMP(8)
         // _truncate_seq_pair, 64 steps per round
         int alo = 0, ahi = la, blo = 0, bhi = lb;
         int E = la + lb - max_num;
@@ -629,6 +639,7 @@ __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
           t0 += n;
           E -= n;
         }
+        PW_GSTAMP(9)
         if (ahi - alo < 1 || bhi - blo < 1) { err = PACK_EASSERT; break; }
         r.lo0 = (uint16_t)alo; r.hi0 = (uint16_t)ahi;
         r.lo1 = (uint16_t)blo; r.hi1 = (uint16_t)bhi;
@@ -748,6 +759,7 @@ __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
         }
         ++np;
         i = i_next;
+        PW_GSTAMP(10)
       }
     }
   }
@@ -836,6 +848,7 @@ __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
     for (int k = 6; k < 11; ++k) atomicAdd((unsigned long long*)&P.dbg[k + 2], (unsigned long long)ph[k]);
   }
 #undef PW_STAMP
+#undef PW_GSTAMP
 }
 
 hipError_t launch_pack_bert_wave(const PackParams& P, hipStream_t s) {
