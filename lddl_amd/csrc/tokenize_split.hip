@@ -50,6 +50,9 @@ constexpr int KEYMAX = 56;               // key bytes a record holds
 #ifndef TOK5_XB
 #define TOK5_XB 4
 #endif
+#ifndef TOK5_NB128
+#define TOK5_NB128 1
+#endif
 #ifndef TOK5_PLANES
 #define TOK5_PLANES 1
 #endif
@@ -71,7 +74,7 @@ __device__ __forceinline__ uint32_t wmake(int u, int src, int len) {
 __device__ __forceinline__ int wsrc(uint32_t w) { return (int)((w >> 8) & 0xFFFu); }
 __device__ __forceinline__ int wlen(uint32_t w) { return (int)(w >> 20); }
 
-struct Lds {
+struct alignas(16) Lds {
   union {
     uint32_t rp[CAP / 4 + 4];  // phase 1: raw bytes of the tile (LDS-DMA)
     struct {
@@ -446,17 +449,24 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
       // class bits as 32-bit planes without multiplies: 4x4 byte transposes
       // put position 4k + j at byte k of t[j]; a plane gathers bit q of the
       // four t[j] (bit 8k + j) and compresses the nibbles (bit 4k + j)
-      uint32_t c[8];
+      uint32_t c[8], nv[8];
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const uint32_t x = w[k];
         c[k] = (uint32_t)ctab[x & 0xFFu] | ((uint32_t)ctab[(x >> 8) & 0xFFu] << 8) |
                ((uint32_t)ctab[(x >> 16) & 0xFFu] << 16) | ((uint32_t)ctab[x >> 24] << 24);
-        // drop bytes -> filler 0xFF: 0x80 - 0x01 | 0x80 per byte (a shift-subtract of the 0x01 form
-        // becomes a quarter-rate multiply in LLVM)
         const uint32_t dmk = (c[k] >> 3) & 0x01010101u;  // drop bytes -> filler 0xFF
-        L.nb[lane * 8 + k] = (x + ((c[k] & 0x10101010u) << 1)) | ((dmk << 8) - dmk);
+        nv[k] = (x + ((c[k] & 0x10101010u) << 1)) | ((dmk << 8) - dmk);
       }
+#if TOK5_NB128
+      // two 16-B stores per lane (8 dword stores at a 32-B lane stride hit
+      // 1/8 of the banks)
+      *reinterpret_cast<uint4*>(&L.nb[lane * 8]) = make_uint4(nv[0], nv[1], nv[2], nv[3]);
+      *reinterpret_cast<uint4*>(&L.nb[lane * 8 + 4]) = make_uint4(nv[4], nv[5], nv[6], nv[7]);
+#else
+#pragma unroll
+      for (int k = 0; k < 8; ++k) L.nb[lane * 8 + k] = nv[k];
+#endif
       uint32_t t[8];
       byte_transpose4(c[0], c[1], c[2], c[3], t[0], t[1], t[2], t[3]);
       byte_transpose4(c[4], c[5], c[6], c[7], t[4], t[5], t[6], t[7]);
