@@ -195,7 +195,9 @@ struct WaveRng {
   // accepted, r >= n_hi: rejected); only the words with r in [n_lo, n_hi) are
   // walked in order, one ballot step each.
   template <class T>
-  __device__ __noinline__ void shuffle_draws(int m, T* jb) {
+  __device__ __noinline__ void shuffle_draws(int m, T* jb) { shuffle_draws_inl(m, jb); }
+  template <class T>
+  __device__ __forceinline__ void shuffle_draws_inl(int m, T* jb) {
     int q = m - 1;
     while (q >= 1) {
       if (idx >= MT_N) refill();
@@ -308,7 +310,7 @@ struct WaveRng {
 // read + write and <= 64 parallel gathers, where the swap loop paid a
 // dependent global round trip per swap.
 __device__ __forceinline__ void shuffle_global(WaveRng& rng, int np, int32_t* order, int32_t* jq, int lane) {
-  rng.shuffle_draws(np, jq);
+  rng.shuffle_draws_inl(np, jq);  // (inline: a call's clobbers cost the caller's SGPRs as spills)
   gsync();
   for (int qb = np - 1; qb >= 1; qb -= 64) {
     const int qmin = max(qb - 63, 1);
