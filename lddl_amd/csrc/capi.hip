@@ -442,8 +442,8 @@ extern "C" int lddl_tokenize(lddl_ctx* c, const uint8_t* d_bytes, int64_t nbytes
   const char* dbgenv = getenv("LDDL_TOK_DEBUG");
   static uint64_t* d_dbg = nullptr;
   if (dbgenv && dbgenv[0] == '1') {
-    if (!d_dbg) HIP_TRY(hipMalloc((void**)&d_dbg, 16 * 8));
-    HIP_TRY(hipMemsetAsync(d_dbg, 0, 16 * 8, st));
+    if (!d_dbg) HIP_TRY(hipMalloc((void**)&d_dbg, 32 * 8));
+    HIP_TRY(hipMemsetAsync(d_dbg, 0, 32 * 8, st));
     P.dbg = d_dbg;
   }
   if (c->tok_algo == 5) {
@@ -478,7 +478,7 @@ extern "C" int lddl_tokenize(lddl_ctx* c, const uint8_t* d_bytes, int64_t nbytes
     HIP_TRY(launch_tokenize_split(P, nbytes, tile_sent, S, c->n_cu, c->tok_grid, c->tok5_cfg, st,
                                   c->timing ? c->tm : nullptr));
     if (P.dbg) {
-      uint64_t h[12];
+      uint64_t h[18];
       int32_t nfb = 0;
       HIP_TRY(hipMemcpyAsync(h, P.dbg, sizeof h, hipMemcpyDeviceToHost, st));
       HIP_TRY(hipMemcpyAsync(&nfb, S.fb_count, 4, hipMemcpyDeviceToHost, st));
@@ -487,6 +487,8 @@ extern "C" int lddl_tokenize(lddl_ctx* c, const uint8_t* d_bytes, int64_t nbytes
                             "tile_end", "stages", "tiles"};
       fprintf(stderr, "[lddl tok5 dbg] ntiles=%lld fallback=%d", (long long)nt, nfb);
       for (int k = 0; k < 12; ++k) fprintf(stderr, " %s=%llu", nm[k], (unsigned long long)h[k]);
+      const char* wn[6] = {"wp_A", "wp_B", "wp_C", "wp_D", "wp_steps", "wp_lane_steps"};
+      for (int k = 0; k < 6; ++k) fprintf(stderr, " %s=%llu", wn[k], (unsigned long long)h[12 + k]);
       fprintf(stderr, "\n");
     }
   } else {

@@ -50,6 +50,9 @@ constexpr int KEYMAX = 56;               // key bytes a record holds
 #ifndef TOK5_XB
 #define TOK5_XB 4
 #endif
+#ifndef TOK5_WP_GROUPS_ANY
+#define TOK5_WP_GROUPS_ANY 1
+#endif
 #ifndef TOK5_NB128
 #define TOK5_NB128 1
 #endif
@@ -1133,6 +1136,19 @@ __global__ __launch_bounds__(64 * WAVES) void wp_kernel(TokParams P, SplitParams
     reinterpret_cast<uint32_t*>(S.rec + (size_t)r * 4)[1] = (uint32_t)np;
     r = -1;
   };
+  // optional stamps (P.dbg, LDDL_TOK_DEBUG=1): A (Bloom scan + bucket
+  // issue), B (refill issue), C (compare; waits for the loads), D (record
+  // start), steps, lane-steps with a record
+  uint64_t wacc[6] = {0, 0, 0, 0, 0, 0}, wprev = 0;
+  const bool wdbg = P.dbg != nullptr;
+#define WP_STAMP(k)                                                              \
+  if (wdbg) {                                                                    \
+    uint64_t t_;                                                                 \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
+    wacc[k] += t_ - wprev;                                                       \
+    wprev = t_;                                                                  \
+  }
+  if (wdbg) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(wprev)::"memory");
   for (;;) {
     // ---- A: candidate of each working lane: the longest length the Bloom
     //      filter does not rule out, then its bucket load
@@ -1143,7 +1159,12 @@ __global__ __launch_bounds__(64 * WAVES) void wp_kernel(TokParams P, SplitParams
         int len = e - s;
         bool found = false;
         uint32_t hcur = 0;
-        if (asc && len <= 24) {
+        // candidates of <= 24 bytes: the dword-group Bloom scan over every
+        // byte length (a non-ASCII prefix ending inside a character never
+        // equals a vocab key, which is valid UTF-8: its Bloom false
+        // positives only cost a failed probe, then shrink() steps back to a
+        // character boundary)
+        if ((TOK5_WP_GROUPS_ANY || asc) && len <= 24) {
           int fl = 0;
           int ga = 0;
 #define TOK5_EXT(j, Hj1) \
@@ -1194,6 +1215,7 @@ __global__ __launch_bounds__(64 * WAVES) void wp_kernel(TokParams P, SplitParams
         b1 = bk[3];
       }
     }
+    WP_STAMP(0)
     // ---- B: idle lanes take the next slots of the stream; their record
     //      loads fly together with the bucket loads
     {
@@ -1213,6 +1235,7 @@ __global__ __launch_bounds__(64 * WAVES) void wp_kernel(TokParams P, SplitParams
         advance();
       }
     }
+    WP_STAMP(1)
     // ---- C: compare and advance
     if (r >= 0) {
       if (fail) {  // some position has no match: the whole word is [UNK]
@@ -1258,6 +1281,7 @@ __global__ __launch_bounds__(64 * WAVES) void wp_kernel(TokParams P, SplitParams
         }
       }
     }
+    WP_STAMP(2)
     // ---- D: lanes with a loaded record begin it
     if (r < 0 && pr >= 0) {
       if (q0.x == 0u) {  // an extension slot
@@ -1280,8 +1304,16 @@ __global__ __launch_bounds__(64 * WAVES) void wp_kernel(TokParams P, SplitParams
         start_piece(mb0);
       }
     }
+    WP_STAMP(3)
+    if (wdbg) {
+      wacc[4] += 1;
+      wacc[5] += __popcll(__ballot(r >= 0));
+    }
     if (__ballot(r >= 0 || pr >= 0) == 0 && c >= nch) break;
   }
+  if (wdbg && lane == 0)
+    for (int k = 0; k < 6; ++k) atomicAdd((unsigned long long*)&P.dbg[12 + k], (unsigned long long)wacc[k]);
+#undef WP_STAMP
   if (S.n_rec) {
     const uint32_t tot = lane_get(wave_incl_add(nrec), 63);
     if (lane == 0 && tot) atomicAdd(S.n_rec, (unsigned long long)tot);
