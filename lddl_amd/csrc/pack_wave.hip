@@ -692,19 +692,54 @@ __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
           // Picks pk, pk + 64 per lane; 8 swaps per 16-B LDS read (measured
           // against u16 reads / readlane swaps: 2.87 vs 3.82 / 3.23 s per step)
           auto pick_pos = [&](int q) { return (uint16_t)(expl ? (int)ML.cand[q] : (q < la2 ? 1 + q : 2 + q)); };
+          // Final position pk < nm of the shuffled list = the element the
+          // swaps move there.  Split the swaps at nm: the late ones
+          // (q = nm-1 .. 1, all j_q <= q < nm) only permute positions < nm
+          // and are traced back per pick (lane per pick, O(nm)); the early
+          // ones (q >= nm) only move elements INTO positions < nm: the element
+          // at v < nm after them is found by successor chains -- F[v] = the
+          // smallest q >= nm with j_q = v (the last early swap writing v), then
+          // F[q] = the smallest q' > q with j_q' = q, ... until no swap wrote
+          // the position (its original element).  One atomicMin pass builds F
+          // (u32 over the mpos + mid lists, unused until the picks are known).
+          constexpr int MCAP = MASK == 1 ? 512 : MLM_MAX_SEQ;
+          const int nm8 = (nm + 7) & ~7;
+          const bool split = nm < m && nm8 + nm <= MCAP;
+          const int tr8 = split ? nm8 : (m + 7) & ~7;  // the traced swaps: [1, tr8)
+          if (split) {
+            uint32_t* F = reinterpret_cast<uint32_t*>(ML.mpos);
+            static_assert(sizeof(ML.mpos) + sizeof(ML.mid) >= 4 * MCAP, "F spans mpos + mid");
+            for (int k = lane; k < m; k += 64) F[k] = 0xFFFFFFFFu;
+            wsync();
+            for (int q = nm + lane; q < m; q += 64) {
+              const uint32_t j = ML.jb[q];
+              if ((uint32_t)q > j) atomicMin(&F[j], (uint32_t)q);
+            }
+            wsync();
+            // element at v after the early swaps -> jb[nm8 + v]
+            for (int v = lane; v < nm; v += 64) {
+              uint32_t val = (uint32_t)v, t = F[v];
+              while (t != 0xFFFFFFFFu) {
+                val = t;
+                t = F[t];
+              }
+              ML.jb[nm8 + v] = (uint16_t)val;
+            }
+          }
           {
-            // identity swaps pad the list: jb[0] = 0, jb[q] = q for q in [m, m8)
-            const int m8 = (m + 7) & ~7;
+            // identity swaps pad the traced list: jb[0] = 0, jb[q] = q for q in [end, tr8)
+            const int end = split ? nm : m;
             if (lane == 0) ML.jb[0] = 0;
-            if (m + lane < m8) ML.jb[m + lane] = (uint16_t)(m + lane);
+            if (end + lane < tr8) ML.jb[end + lane] = (uint16_t)(end + lane);
             wsync();
             const uint4* jb4 = reinterpret_cast<const uint4*>(ML.jb);
+            auto elem = [&](int q) { return split ? (int)ML.jb[nm8 + q] : q; };
             for (int pb0 = 0; pb0 < nm; pb0 += 128) {
               const int pk = pb0 + lane, pk2 = pk + 64;
               int qa = pk, qb = pk2;
               // swaps q < pb0 leave picks >= pb0 in place (j_q <= q)
               if (nm - pb0 <= 64) {  // one pick per lane (seq 128: always)
-                for (int c = pb0; c < m8; c += 8) {
+                for (int c = pb0; c < tr8; c += 8) {
                   const uint4 w = jb4[c >> 3];
                   const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
@@ -714,7 +749,7 @@ __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
                   }
                 }
               } else {
-                for (int c = pb0; c < m8; c += 8) {
+                for (int c = pb0; c < tr8; c += 8) {
                   const uint4 w = jb4[c >> 3];
                   const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
@@ -725,8 +760,10 @@ __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
                   }
                 }
               }
-              if (pk < nm) ML.mpos[pk] = pick_pos(qa);
-              if (pk2 < nm) ML.mpos[pk2] = pick_pos(qb);
+              const int ea = pk < nm ? elem(qa) : 0, eb = pk2 < nm ? elem(qb) : 0;
+              wsync();  // (mpos overlaps F: every lane has read its chains)
+              if (pk < nm) ML.mpos[pk] = pick_pos(ea);
+              if (pk2 < nm) ML.mpos[pk2] = pick_pos(eb);
             }
           }
           // 80% [MASK], 10% keep, 10% random word, in pick order
