@@ -123,7 +123,9 @@ int lddl_materialize(lddl_ctx *ctx, const uint16_t *d_ids, uint16_t *d_out_token
  * [2+len(A):...], pretrain.py:232-233) and write, per row g,
  * d_out_mlm_pos[d_out_mlm_off[g] .. d_out_mlm_off[g+1]) = masked_lm_positions
  * (ascending, row coordinates incl. [CLS]) and d_out_mlm_label[...] =
- * masked_lm_labels as token ids (pretrain.py:225-238, :340-361). */
+ * masked_lm_labels as token ids (pretrain.py:225-238, :340-361).  Reads
+ * the rows and their partitions (d_out_tokens, d_out_tok_off, d_out_part)
+ * of that lddl_materialize call, which must still be live. */
 int lddl_masked_lm(lddl_ctx *ctx, int64_t *d_out_mlm_off, uint16_t *d_out_mlm_pos, uint16_t *d_out_mlm_label,
                    void *stream);
 

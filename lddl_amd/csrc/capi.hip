@@ -81,7 +81,8 @@ struct lddl_ctx {
   int64_t last_nmask = -1;
   int64_t last_nsent = 0, last_ndense = 0;  // sentences / tokens of the last pack (dense id array)
   uint16_t* last_tokens = nullptr;  // rows of the last lddl_materialize
-  const int64_t* last_tok_off = nullptr;   // masked entries of the last pack (-1: no masking)
+  const int64_t* last_tok_off = nullptr;
+  const int64_t* last_part = nullptr;     // partition of every materialised row (lddl_materialize's out_part)   // masked entries of the last pack (-1: no masking)
   uint64_t mlm_cap = 0;      // masking arena capacity that last sufficed
   int pack_codebert = 0;
   // scratch
@@ -791,6 +792,7 @@ extern "C" int lddl_materialize(lddl_ctx* c, const uint16_t* d_ids, uint16_t* d_
     HIP_TRY(hipMemcpyAsync(d_bin_count, P.bin_count, (size_t)P.n_part * P.nbins * 8, hipMemcpyDeviceToDevice, st));
   c->last_tokens = d_out_tokens;
   c->last_tok_off = d_out_tok_off;
+  c->last_part = d_out_part;
   return 0;
 }
 
@@ -820,6 +822,7 @@ extern "C" int lddl_masked_lm(lddl_ctx* c, int64_t* d_out_mlm_off, uint16_t* d_o
     M.dup = P.dup;
     M.tokens = c->last_tokens;
     M.tok_off = c->last_tok_off;
+    M.row_part = c->last_part;
     M.out_off = d_out_mlm_off;
     M.out_pos = d_out_mlm_pos;
     M.out_label = d_out_mlm_label;

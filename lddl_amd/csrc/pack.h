@@ -88,6 +88,7 @@ struct MlmParams {
   int32_t dup;
   uint16_t* tokens;             // rows written by lddl_materialize (masked in place)
   const int64_t* tok_off;
+  const int64_t* row_part;      // [n_pairs] partition of each row (materialize's out_part)
   int64_t* out_off;             // [n_pairs+1]
   uint16_t* out_pos;            // [n_masked]
   uint16_t* out_label;          // [n_masked]

@@ -568,17 +568,15 @@ __global__ __launch_bounds__(256) void sent_special_kernel(const uint16_t* ids, 
 // Row g of the materialised output: copy its masked entries (sorted by
 // position, pretrain.py:225) to the global position/label lists and apply the
 // replacement in place.  label = the row's token before replacement.
+// Four rows per wave (16 lanes each): a row's metadata is a chain of
+// dependent loads (partition -> its bases -> binned record -> masking ref),
+// so the wave keeps four chains in flight.
 __global__ __launch_bounds__(256) void masked_lm_kernel(MlmParams M) {
-  const int lane = threadIdx.x & 63;
+  const int sl = threadIdx.x & 15;
   const int64_t total = M.pair_base[M.n_part];
-  const int64_t nw = (int64_t)gridDim.x * 4;
-  for (int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); g < total; g += nw) {
-    int64_t lo = 0, hi = M.n_part;
-    while (hi - lo > 1) {
-      const int64_t mid = (lo + hi) >> 1;
-      if (M.pair_base[mid] <= g) lo = mid; else hi = mid;
-    }
-    const int64_t p = lo;
+  const int64_t ng = (int64_t)gridDim.x * 16;  // row groups of 16 lanes
+  for (int64_t g = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4); g < total; g += ng) {
+    const int64_t p = M.row_part[g];  // (materialize wrote every row's partition)
     const int64_t i = g - M.pair_base[p];
     const int64_t pb = (int64_t)M.dup * M.doc_sent_off[M.part_doc_off[p]];
     const int64_t ref = M.mref[pb + M.binned[pb + i]];
@@ -586,11 +584,11 @@ __global__ __launch_bounds__(256) void masked_lm_kernel(MlmParams M) {
     const int64_t aoff = ref & ((int64_t(1) << 48) - 1);
     const int64_t ooff = M.mask_base[p] + M.mloc[pb + i];
     uint16_t* row = M.tokens + M.tok_off[g];
-    if (lane == 0) {
+    if (sl == 0) {
       M.out_off[g] = ooff;
       if (g == total - 1) M.out_off[total] = ooff + nm;
     }
-    for (int k = lane; k < nm; k += 64) {
+    for (int k = sl; k < nm; k += 16) {
       const uint32_t e = M.marena[aoff + k];
       const uint32_t pos = e & 0xFFFFu, nid = e >> 16;
       const uint16_t label = row[pos];

@@ -195,7 +195,7 @@ struct WaveRng {
   // accepted, r >= n_hi: rejected); only the words with r in [n_lo, n_hi) are
   // walked in order, one ballot step each.
   template <class T>
-  __device__ __noinline__ void shuffle_draws(int m, T* jb) { shuffle_draws_inl(m, jb); }
+  __device__ __forceinline__ void shuffle_draws(int m, T* jb) { shuffle_draws_inl(m, jb); }
   template <class T>
   __device__ __forceinline__ void shuffle_draws_inl(int m, T* jb) {
     int q = m - 1;
@@ -221,10 +221,9 @@ struct WaveRng {
       while (ambm) {
         const int a = __ffsll((unsigned long long)ambm) - 1;
         ambm &= ambm - 1;
-        if (A < __builtin_amdgcn_readlane(u, a)) {
-          ++A;
-          accm |= 1ull << a;
-        }
+        const int ok = A < __builtin_amdgcn_readlane(u, a) ? 1 : 0;  // (scalar select, no branch)
+        A += ok;
+        accm |= (uint64_t)ok << a;
       }
       const int pre = __popcll(accm & lt);
       const uint64_t hit = __ballot((accm >> lane & 1ull) && pre == dmax - 1);
@@ -251,7 +250,7 @@ struct WaveRng {
   // <= 64 words; the scalar walk then hops from pick to pick.  A pick that
   // runs past the window starts the next window; one that cannot fit before
   // the state's end is drawn sequentially.
-  __device__ __noinline__ void mlm_choices(int nm, uint32_t V, uint32_t mask_id, uint32_t keep_id, uint16_t* mid) {
+  __device__ __forceinline__ void mlm_choices(int nm, uint32_t V, uint32_t mask_id, uint32_t keep_id, uint16_t* mid) {
     const int kV = 32 - __clz(V);
     int pk = 0;
     while (pk < nm) {
