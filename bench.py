@@ -338,7 +338,7 @@ def main():
   sh, base, pdo, reps, gen_s = build_shards(args, rank, device)
   from lddl_amd.pipeline import VOCAB_BERT, VOCAB_CODEBERT
   code = args.corpus == 'code'
-  pk = Packer(VOCAB_CODEBERT if code else VOCAB_BERT, device=local)
+  pk = Packer(VOCAB_CODEBERT if code else VOCAB_BERT, device=local, masking=args.masking)
   pk.tok.set_timing(True)  # per-kernel HIP events inside the tokenize call (the roofline's kernel time)
   kw = dict(target_seq_length=args.target_seq_length, short_seq_prob=0.1, duplicate_factor=args.duplicate_factor,
             seed=args.seed + rank * 10_000_000, bin_size=args.bin_size, masking=args.masking, codebert=code)

@@ -77,6 +77,13 @@ int lddl_tokenize(lddl_ctx *ctx, const uint8_t *d_bytes, int64_t nbytes, const i
 int lddl_set_timing(lddl_ctx *ctx, int on);
 int lddl_tokenize_stats(lddl_ctx *ctx, double *out, int n);
 
+/* With on != 0, every following lddl_tokenize also records which sentences
+ * hold a [CLS] / [SEP] token (pretrain.py:187-190 excludes those tokens
+ * from the masking candidates); a masked lddl_pack_bert over the same
+ * d_out_ids / d_out_ntok buffers then reuses the flags instead of a pass
+ * over the ids.  Off by default (the unmasked path does not need them). */
+int lddl_set_special_flags(lddl_ctx *ctx, int on);
+
 /* Pack every partition of a tokenised shard set.
  * Partition p = docs [d_part_doc_off[p], d_part_doc_off[p+1]); doc d =
  * sentences [d_doc_sent_off[d], d_doc_sent_off[d+1]); d_ids / d_ntok /

@@ -69,6 +69,12 @@ struct lddl_ctx {
   SplitTiming* tm = nullptr;
   unsigned long long* d_nrec = nullptr;
   int64_t last_tok_bytes = 0, last_tok_sent = 0;
+  // per-sentence [CLS]/[SEP] flags written by the last lddl_tokenize (ws 41),
+  // reused by a masked lddl_pack_bert over the same id / count buffers
+  const void* spec_ids = nullptr;
+  const void* spec_ntok = nullptr;
+  int64_t spec_nsent = -1;
+  bool spec_flags = false;  // lddl_set_special_flags
   // pack workspace (grown on demand)
   struct Buf {
     void* p = nullptr;
@@ -421,6 +427,14 @@ extern "C" int lddl_tokenize(lddl_ctx* c, const uint8_t* d_bytes, int64_t nbytes
   P.max_tok = max_tok;
   P.out_ids = d_out_ids;
   P.out_ntok = d_out_ntok;
+  c->spec_ids = nullptr;
+  if (c->spec_flags) {
+    int rc;
+    if ((rc = ws_get(c, 41, n_sent, &P.sent_spec))) return rc;
+    c->spec_ids = d_out_ids;
+    c->spec_ntok = d_out_ntok;
+    c->spec_nsent = n_sent;
+  }
   P.top = c->d_top;
   P.pages = c->d_pages;
   P.bmp = c->d_bmp;
@@ -502,6 +516,12 @@ extern "C" int lddl_tokenize(lddl_ctx* c, const uint8_t* d_bytes, int64_t nbytes
       return rc;
     HIP_TRY(launch_tokenize_serial(P, nbytes, tile_sent, fb_list, fb_count, c->tok_grid, st));
   }
+  return 0;
+}
+
+extern "C" int lddl_set_special_flags(lddl_ctx* c, int on) {
+  if (!c) return set_err(LDDL_EINVAL, "null ctx");
+  c->spec_flags = on != 0;
   return 0;
 }
 
@@ -623,14 +643,16 @@ static int pack_common(lddl_ctx* c, int codebert, const int32_t* d_ntok, const i
     P.mask_id = c->special[4];
     P.ids = d_ids;
     uint8_t *sent_spec, *fs_spec;
-    if ((rc = ws_get(c, 22, n_sent, &sent_spec)) || (rc = ws_get(c, 23, n_sent, &fs_spec)) ||
+    // the flags of the last lddl_tokenize into these buffers, else a pass over the ids
+    const bool spec_ok = c->spec_ids == d_ids && c->spec_ntok == d_ntok && c->spec_nsent == n_sent;
+    if ((rc = ws_get(c, spec_ok ? 41 : 22, n_sent, &sent_spec)) || (rc = ws_get(c, 23, n_sent, &fs_spec)) ||
         (rc = ws_get(c, 24, npair_cap, &P.mref)) || (rc = ws_get(c, 25, npair_cap, &P.mloc)) ||
         (rc = ws_get(c, 26, n_part, &P.part_nmask)) || (rc = ws_get(c, 27, n_part + 1, &mask_base)) ||
         (rc = ws_get(c, 28, n_part + 1, &mask_base2)) || (rc = ws_get(c, 29, 1, &P.mcounter)))
       return rc;
     P.sent_spec = sent_spec;
     P.fs_spec = fs_spec;
-    HIP_TRY(launch_sent_special(d_ids, d_sent_off, d_ntok, n_sent, P.cls_id, P.sep_id, sent_spec, st));
+    if (!spec_ok) HIP_TRY(launch_sent_special(d_ids, d_sent_off, d_ntok, n_sent, P.cls_id, P.sep_id, sent_spec, st));
     if (!c->mlm_cap) c->mlm_cap = (uint64_t)n_part * 4 * MLM_CHUNK + (uint64_t)duplicate_factor * n_sent * 4;
   }
   if (!codebert) {

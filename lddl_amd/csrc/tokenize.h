@@ -16,6 +16,7 @@ struct TokParams {
   int32_t max_tok;
   uint16_t* out_ids;
   int32_t* out_ntok;
+  uint8_t* sent_spec;     // optional [n_sent]: the sentence's tokens include [CLS] / [SEP]
   // unicode table
   const uint16_t* top;
   const uint32_t* pages;

@@ -53,7 +53,14 @@ __global__ __launch_bounds__(256) void tokenize_fallback_kernel(TokParams P, con
     for (int64_t s = sa + lane; s < sb; s += 64) {
       SentState st{P.sent_off[s], P.sent_off[s + 1], P.sent_off[s] - base, 0};
       while (st.p < st.e && st.ntok < P.max_tok) step(P, st, wb, ascii_tab);
-      P.out_ntok[s] = min(st.ntok, P.max_tok);
+      const int nt = min(st.ntok, P.max_tok);
+      P.out_ntok[s] = nt;
+      if (P.sent_spec) {  // the sentence holds a [CLS] / [SEP] token
+        const uint16_t* ids = P.out_ids + (P.sent_off[s] - base);
+        uint32_t f = 0;
+        for (int k = 0; k < nt; ++k) f |= (ids[k] == P.special[2]) | (ids[k] == P.special[3]);
+        P.sent_spec[s] = (uint8_t)f;
+      }
     }
   }
 }

@@ -101,6 +101,7 @@ struct alignas(16) Lds {
   uint32_t xent[XCAP];         // table entry of each expansion marker
   uint8_t xlen[XCAP];          // its normalised byte length
   int32_t misc[4];             // 0 side-buffer cursor, 1 #markers, 2 overflow
+  uint32_t sspec[2];           // sentences holding a [CLS] / [SEP] token (P.sent_spec)
 };
 
 __device__ __forceinline__ void wsync() {
@@ -424,6 +425,8 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
       L.misc[0] = 0;
       L.misc[1] = 0;
       L.misc[2] = 0;
+      L.sspec[0] = 0;
+      L.sspec[1] = 0;
     }
     if (lane < ns) {
       L.sent_n[lane] = 0;
@@ -958,6 +961,8 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
             if (idv[k] != U_DEFER) {
               if (o == 0) P.out_ids[obase + at] = (uint16_t)idv[k];  // no queued word before it: final
               else S.ent[ent0 + at] = (uint16_t)idv[k];
+              // ([CLS] / [SEP] come only from literal specials, never from WordPiece)
+              if (idv[k] == P.special[2] || idv[k] == P.special[3]) atomicOr(&L.sspec[sj >> 5], 1u << (sj & 31));
             } else {
               S.ent[ent0 + at] = (uint16_t)(SPLIT_EDEF | o);
               if (o == 0) {
@@ -1028,6 +1033,7 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
         S.fdef[s] = (uint16_t)L.sfdef[lane];
       }
       P.out_ntok[s] = ne - (int)L.sdef[lane];
+      if (P.sent_spec) P.sent_spec[s] = (uint8_t)((L.sspec[lane >> 5] >> (lane & 31)) & 1u);
     }
   
     }();

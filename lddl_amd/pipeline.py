@@ -138,8 +138,10 @@ class PackResult:
 class Packer:
   """One GPU's tokenize -> pack -> bin -> materialise pipeline (one lddl_ctx)."""
 
-  def __init__(self, vocab_file=VOCAB_BERT, device=None):
+  def __init__(self, vocab_file=VOCAB_BERT, device=None, masking=False):
     self.tok = Tokenizer(vocab_file, device)
+    if masking:  # the tokenizer records the [CLS]/[SEP] sentences the masked packer needs
+      self.tok.set_special_flags(True)
     self.device = self.tok.device
     self._out = {}
 
@@ -209,7 +211,7 @@ def run_bert(corpus, vocab_file=VOCAB_BERT, target_seq_length=128, bin_size=None
   device = device or torch.device('cuda', 0)
   if part_doc_off is None:
     part_doc_off = partition_by_bytes(corpus, n_partitions)
-  pk = Packer(vocab_file, device.index)
+  pk = Packer(vocab_file, device.index, masking=masking)
   sh = upload(corpus, part_doc_off, device)
   res = pk.run(sh, target_seq_length=target_seq_length, short_seq_prob=short_seq_prob,
                duplicate_factor=duplicate_factor, seed=seed, bin_size=bin_size, codebert=codebert,

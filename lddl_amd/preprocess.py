@@ -385,7 +385,7 @@ def main(args, codebert=False):
 
   device = torch.device('cuda', local)
   torch.cuda.set_device(device)
-  pk = pipeline.Packer(vocab, local)
+  pk = pipeline.Packer(vocab, local, masking=args.masking and not codebert)
   sink = os.path.abspath(os.path.expanduser(args.sink))
   out = []
   nbins = args.target_seq_length // args.bin_size if args.bin_size else 1

@@ -81,6 +81,11 @@ class Tokenizer:
                                         _ptr(out_ids), _ptr(out_ntok), _stream(stream)))
     return out_ids, out_ntok
 
+  def set_special_flags(self, on=True):
+    """following tokenize calls record per-sentence [CLS]/[SEP] flags for a
+    masked pack over the same buffers (lddl_set_special_flags)"""
+    _lib.check(_lib.lib().lddl_set_special_flags(self.handle, 1 if on else 0))
+
   def set_timing(self, on=True):
     """per-kernel timing of the following tokenize calls (lddl_set_timing)"""
     _lib.check(_lib.lib().lddl_set_timing(self.handle, 1 if on else 0))

@@ -332,3 +332,29 @@ def test_codebert_long_documents_vs_oracle(cpacker, seq, ssp, dup):
   for (p, a, b, fl, bn, tok), e in zip(rows, exp):
     assert (p, a, b, len(tok)) == e
   assert res.bin_count.cpu().numpy().tolist() == counts
+
+
+def test_masked_special_flags_from_tokenizer(gpu):
+  """With masking, sentences holding a literal [CLS] / [SEP] token build an
+  explicit candidate list (pretrain.py:187-190).  The tokenizer writes those
+  per-sentence flags (scan kernel + serial fallback) and a masked pack over
+  the same id buffers reuses them; a pack over a copy of the ids recomputes
+  them with a pass over the ids: both must give identical rows."""
+  from lddl_amd import pipeline
+  from lddl_amd.synth import corpus_from_sentences
+  rng = np.random.default_rng(5)
+  words = ['the', 'cat', 'sat', 'on', 'mat', 'running', 'unbelievable', '[CLS]', '[SEP]', '[MASK]', 'x[SEP]y',
+           'é', 'naïve', '中文']
+  sents, dso = [], [0]
+  for d in range(300):
+    for s in range(int(rng.integers(1, 12))):
+      sents.append(' '.join(rng.choice(words, int(rng.integers(1, 40)))))
+    dso.append(len(sents))
+  c = corpus_from_sentences(sents, dso)
+  pk = pipeline.Packer(pipeline.VOCAB_BERT, 0, masking=True)
+  sh = pipeline.upload(c, pipeline.partition_by_bytes(c, 3), torch.device('cuda', 0))
+  ids, ntok = pk.tokenize(sh)
+  kw = dict(target_seq_length=128, duplicate_factor=2, seed=3, bin_size=32, masking=True)
+  a = pk.pack(sh, ids, ntok, **kw).rows()
+  b = pk.pack(sh, ids.clone(), ntok, **kw).rows()
+  assert len(a) == len(b) and a == b
