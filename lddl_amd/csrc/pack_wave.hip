@@ -30,6 +30,9 @@ namespace lddl {
 // partition (PackParams cap_*); a partition that does not fit runs the same
 // code on global memory (wave-uniform branch).
 constexpr int PW_DOCS = 512;    // documents held in static LDS by the global-only variant
+#ifndef PACK_DRAW_ROUNDS
+#define PACK_DRAW_ROUNDS 3      // shuffle_draws: bound-propagation rounds before the ordered walk
+#endif
 struct PackWaveLds {
   uint32_t mt[MT_N];            // MT19937 state; draws temper on the fly
   uint16_t dfirst[PW_DOCS];     // global-only variant: the partition's documents
@@ -211,12 +214,29 @@ struct WaveRng {
       const uint64_t defm = __ballot(valid && r < (uint32_t)n_lo);
       uint64_t ambm = __ballot(valid && r >= (uint32_t)n_lo && r < (uint32_t)n_hi);
       const uint64_t lt = (1ull << lane) - 1ull;
-      // ambiguous word a (in order) is accepted iff the draws before it,
-      // D_a definite + A earlier accepted ambiguous, leave its bound above r:
-      // A < n_hi - r - D_a =: u_a.  Lanes past the batch's last draw are
-      // resolved too and cut below (their outcome never feeds back).
-      const int u = n_hi - (int)r - __popcll(defm & lt);
+      // bound propagation first: the words accepted before ambiguous word a
+      // number at least L_a (decided accepts before a) and at most U_a (L_a +
+      // undecided before a), so r < n_hi - U_a accepts it and r >= n_hi - L_a
+      // rejects it.  Each round decides the first undecided word and, in
+      // practice, most of the others: two rounds leave ~4 of a seq-512
+      // shuffle's ~150 ambiguous words to the ordered walk below.
       uint64_t accm = defm;
+#pragma unroll
+      for (int it = 0; it < PACK_DRAW_ROUNDS; ++it) {
+        if (!ambm) break;
+        const bool und = (ambm >> lane) & 1ull;
+        const int Lc = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(accm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)accm, 0u));
+        const int Uc = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(ambm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ambm, (uint32_t)Lc));
+        const uint64_t acc_new = __ballot(und && (int)r < n_hi - Uc);
+        const uint64_t rej_new = __ballot(und && (int)r >= n_hi - Lc);
+        accm |= acc_new;
+        ambm &= ~(acc_new | rej_new);
+      }
+      // a still-ambiguous word a (in order) is accepted iff the draws before
+      // it, D_a decided + A earlier accepted ambiguous, leave its bound above
+      // r: A < n_hi - r - D_a =: u_a.  Lanes past the batch's last draw are
+      // resolved too and cut below (their outcome never feeds back).
+      const int u = n_hi - (int)r - __popcll(accm & lt);
       int A = 0;
       while (ambm) {
         const int a = __ffsll((unsigned long long)ambm) - 1;
@@ -776,12 +796,34 @@ __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
             mend = mcur + MLM_CHUNK;
           }
           const bool fits = (uint64_t)mend <= P.mcap;
-          for (int pb0 = 0; pb0 < nm; pb0 += 64) {
-            const int pk = pb0 + lane;
-            if (pk < nm && fits) {
+          // sorted(masked_lms) by position: the picks are distinct positions
+          // < MCAP, so a pick's rank = the set bits below it in a position
+          // bitmap (jb is free after the trace): per-dword prefix counts
+          // by one wave scan, then two LDS reads per pick
+          {
+            constexpr int NW = MCAP / 32;
+            static_assert(2 * NW <= MCAP / 2, "bitmap + prefix counts fit in jb");
+            uint32_t* bm = reinterpret_cast<uint32_t*>(ML.jb);
+            uint32_t* pre = bm + NW;
+            for (int w = lane; w < NW; w += 64) bm[w] = 0;
+            wsync();
+            for (int pk = lane; pk < nm; pk += 64) {
               const uint32_t pos = ML.mpos[pk];
-              int rank = 0;
-              for (int k2 = 0; k2 < nm; ++k2) rank += ML.mpos[k2] < pos;
+              atomicOr(&bm[pos >> 5], 1u << (pos & 31));
+            }
+            wsync();
+            uint32_t carry = 0;
+            for (int w0 = 0; w0 < NW; w0 += 64) {
+              const uint32_t c = w0 + lane < NW ? (uint32_t)__popc(bm[w0 + lane]) : 0u;
+              const uint32_t x = wave_incl_add(c);
+              if (w0 + lane < NW) pre[w0 + lane] = carry + x - c;
+              carry += lane_get(x, 63);
+            }
+            wsync();
+            for (int pk = lane; pk < nm; pk += 64) {
+              if (!fits) break;
+              const uint32_t pos = ML.mpos[pk];
+              const int rank = (int)(pre[pos >> 5] + __popc(bm[pos >> 5] & ((1u << (pos & 31)) - 1u)));
               P.marena[mcur + rank] = pos | ((uint32_t)ML.mid[pk] << 16);
             }
           }
