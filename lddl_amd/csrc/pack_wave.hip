@@ -218,8 +218,9 @@ struct WaveRng {
       // number at least L_a (decided accepts before a) and at most U_a (L_a +
       // undecided before a), so r < n_hi - U_a accepts it and r >= n_hi - L_a
       // rejects it.  Each round decides the first undecided word and, in
-      // practice, most of the others: two rounds leave ~4 of a seq-512
-      // shuffle's ~150 ambiguous words to the ordered walk below.
+      // practice, most of the others: three rounds leave ~0.5 of a seq-512
+      // shuffle's ~150 ambiguous words to the ordered walk below (simulated;
+      // 1 / 2 / 3 rounds measured 2.11 / 1.91 / 1.87 e12 draw ticks per step).
       uint64_t accm = defm;
 #pragma unroll
       for (int it = 0; it < PACK_DRAW_ROUNDS; ++it) {

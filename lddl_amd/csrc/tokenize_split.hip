@@ -41,11 +41,17 @@ namespace lddl {
 namespace tok5 {
 
 constexpr int CAP = 2048;                // window bytes (32 per lane)
-constexpr int DCAP = 256;                // side buffer for dirty words
+#ifndef TOK5_DCAP
+#define TOK5_DCAP 256
+#endif
+#ifndef TOK5_XCAP
+#define TOK5_XCAP 32
+#endif
+constexpr int DCAP = TOK5_DCAP;          // side buffer for dirty words
 constexpr int NBUF = CAP + DCAP + 64;    // + over-read pad of the key loads
 constexpr int UCAP = 256;                // units per round
 constexpr int NSCAP = 64;                // sentences per tile
-constexpr int XCAP = 32;                 // expansion markers per tile
+constexpr int XCAP = TOK5_XCAP;          // expansion markers per tile
 constexpr int KEYMAX = 56;               // key bytes a record holds
 #ifndef TOK5_XB
 #define TOK5_XB 4
@@ -93,8 +99,8 @@ struct alignas(16) Lds {
   uint16_t uid[UCAP];          // vocab id, U_EMPTY (no token) or U_DEFER (queued); in phase 4
                                // (once read) the queued units of the round in unit order
   uint32_t sqb[NSCAP];         // record index of the sentence's first slot
-  uint32_t sdef[NSCAP];        // queued entries below max_tok
-  uint32_t sfdef[NSCAP];       // entry index of the first queued word
+  uint16_t sdef[NSCAP];        // queued entries below max_tok
+  uint16_t sfdef[NSCAP];       // entry index of the first queued word (< max_tok)
   uint16_t sst[NSCAP + 2];     // sentence starts (window coordinates)
   uint16_t sent_n[NSCAP];      // entries so far (uncapped)
   uint16_t sslot[NSCAP];       // record slots so far
@@ -906,7 +912,7 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
           nsd[k] = nsl[k] | (nsl[k] ? 0x10000u : 0u);
           ndef += nsl[k] ? 1u : 0u;
         }
-        seg_scan(nsd, cont ? ((uint32_t)L.sslot[first_sent] | (L.sdef[first_sent] << 16)) : 0u, spre);
+        seg_scan(nsd, cont ? ((uint32_t)L.sslot[first_sent] | ((uint32_t)L.sdef[first_sent] << 16)) : 0u, spre);
         const uint32_t xs = wave_incl_add(mine | (ndef << 16));
         const uint32_t need = lane_get(xs, 63) & 0xFFFFu;
         // this round's slots come from the wave's chunk; a sentence's slots
@@ -954,7 +960,7 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
           if (uu == nr - 1 || (int)(L.u.urec[uu + 1] >> 16) != sj) {  // the sentence's last unit of the round
             L.sent_n[sj] = (uint16_t)min(e + ev[k], 65535u);
             L.sslot[sj] = (uint16_t)(o + nsl[k]);
-            L.sdef[sj] = (spre[k] >> 16) + (nsl[k] ? 1u : 0u);
+            L.sdef[sj] = (uint16_t)((spre[k] >> 16) + (nsl[k] ? 1u : 0u));
           }
           if (ev[k] && (int)e < max_tok) {
             const int64_t at = (int64_t)L.sst[sj] + e;
@@ -967,7 +973,7 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
               S.ent[ent0 + at] = (uint16_t)(SPLIT_EDEF | o);
               if (o == 0) {
                 L.sqb[sj] = gp;
-                L.sfdef[sj] = e;
+                L.sfdef[sj] = (uint16_t)e;
               }
               qlist[qi++] = (uint16_t)uu;
             }
