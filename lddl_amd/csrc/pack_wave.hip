@@ -30,6 +30,12 @@ namespace lddl {
 // partition (PackParams cap_*); a partition that does not fit runs the same
 // code on global memory (wave-uniform branch).
 constexpr int PW_DOCS = 512;    // documents held in static LDS by the global-only variant
+#ifndef PACK_CHOICE_JUMP
+#define PACK_CHOICE_JUMP 1      // mlm_choices: the picks of a window by pointer doubling, not a scalar walk
+#endif
+#ifndef PACK_TRACE_ONE
+#define PACK_TRACE_ONE 1        // pick trace: one pick per lane, passes of 64 (not two picks per lane)
+#endif
 #ifndef PACK_DRAW_ROUNDS
 #define PACK_DRAW_ROUNDS 3      // shuffle_draws: bound-propagation rounds before the ordered walk
 #endif
@@ -57,6 +63,7 @@ struct MaskLds {
   alignas(16) uint16_t jb[CAP + 8];  // shuffle draws: swap x[i] <-> x[jb[i]]
   uint16_t mpos[CAP];           // picked positions in pick order
   uint16_t mid[CAP];            // their replacement ids (MLM_KEEP = unchanged)
+  uint32_t mark[16];            // mlm_choices: chain marks (one byte per word of a window)
 };
 struct NoMaskLds {};
 
@@ -271,7 +278,8 @@ struct WaveRng {
   // <= 64 words; the scalar walk then hops from pick to pick.  A pick that
   // runs past the window starts the next window; one that cannot fit before
   // the state's end is drawn sequentially.
-  __device__ __forceinline__ void mlm_choices(int nm, uint32_t V, uint32_t mask_id, uint32_t keep_id, uint16_t* mid) {
+  __device__ __forceinline__ void mlm_choices(int nm, uint32_t V, uint32_t mask_id, uint32_t keep_id, uint16_t* mid,
+                                              uint32_t* mark) {
     const int kV = 32 - __clz(V);
     int pk = 0;
     while (pk < nm) {
@@ -298,11 +306,43 @@ struct WaveRng {
       uint64_t chosen = 0;
       int pos = 0;
       const int pk0 = pk;
+#if PACK_CHOICE_JUMP
+      // the walk 0 -> nx[0] -> ... over resolved words (nx = l + len; it
+      // stops at an unresolved word), found by pointer doubling: round i
+      // marks the 2^i-step successors J of the chain words found so far
+      // (LDS byte marks), then J = J[J].  len >= 2, so five rounds reach
+      // every chain word of a 64-word window; the first nm - pk are picks.
+      // (A scalar walk cost ~10 scalar instructions per pick on the CU's
+      // one scalar unit, the packer's bottleneck.)
+      if (resm & 1ull) {
+        const int nx = res ? lane + len : 64;
+        int J = nx;
+        uint64_t on = 1ull;
+        uint8_t* mk = reinterpret_cast<uint8_t*>(mark);
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+          mk[lane] = 0;
+          wsync();
+          if ((on >> lane & 1ull) && J < 64) mk[J] = 1;
+          wsync();
+          on |= __ballot(mk[lane] != 0) & resm;
+          const int JJ = __shfl(J, J < 64 ? J : 0);
+          J = J < 64 ? JJ : 64;
+        }
+        const int K = nm - pk;
+        const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(on >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)on, 0u));
+        chosen = __ballot((on >> lane & 1ull) && rank < K);
+        const int last = 63 - __clzll((long long)chosen);
+        pos = __builtin_amdgcn_readlane(nx, last);
+        pk += __popcll(chosen);
+      }
+#else
       while (pk < nm && pos < lim && (resm >> pos & 1ull)) {
         chosen |= 1ull << pos;
         ++pk;
         pos += __builtin_amdgcn_readlane(len, pos);
       }
+#endif
       if (chosen >> lane & 1ull) mid[pk0 + __popcll(chosen & ((1ull << lane) - 1ull))] = (uint16_t)nid;
       if (pos == 0) {  // the pick does not fit before the state's end: sequential
         uint32_t v;
@@ -754,6 +794,26 @@ __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
             wsync();
             const uint4* jb4 = reinterpret_cast<const uint4*>(ML.jb);
             auto elem = [&](int q) { return split ? (int)ML.jb[nm8 + q] : q; };
+#if PACK_TRACE_ONE
+            // one pick per lane, 64 picks per pass: swaps below a pass's first
+            // pick leave its picks in place, so pass k traces [64k, tr8)
+            for (int pb0 = 0; pb0 < nm; pb0 += 64) {
+              const int pk = pb0 + lane;
+              int qa = pk;
+              for (int c = pb0; c < tr8; c += 8) {
+                const uint4 w = jb4[c >> 3];
+                const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+                for (int t = 0; t < 8; ++t) {
+                  const int i2 = c + t, j = (int)((ww[t >> 1] >> (16 * (t & 1))) & 0xFFFFu);
+                  qa = qa == i2 ? j : (qa == j ? i2 : qa);
+                }
+              }
+              const int ea = pk < nm ? elem(qa) : 0;
+              wsync();  // (mpos overlaps F: every lane has read its chains)
+              if (pk < nm) ML.mpos[pk] = pick_pos(ea);
+            }
+#else
             for (int pb0 = 0; pb0 < nm; pb0 += 128) {
               const int pk = pb0 + lane, pk2 = pk + 64;
               int qa = pk, qb = pk2;
@@ -785,10 +845,11 @@ __global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
               if (pk < nm) ML.mpos[pk] = pick_pos(ea);
               if (pk2 < nm) ML.mpos[pk2] = pick_pos(eb);
             }
+#endif
           }
           // 80% [MASK], 10% keep, 10% random word, in pick order
           PW_STAMP(8)
-          rng.mlm_choices(nm, P.n_vocab, P.mask_id, MLM_KEEP, ML.mid);
+          rng.mlm_choices(nm, P.n_vocab, P.mask_id, MLM_KEEP, ML.mid, ML.mark);
           PW_STAMP(9)
           if (mcur + nm > mend) {
             unsigned long long b0 = 0;
