@@ -219,7 +219,8 @@ def test_bert_masked_golden(packer, k, binned):
     assert np.asarray(pos, dtype=np.uint16).tobytes().hex() in e['masked_lm_positions_npy']
 
 
-@pytest.mark.parametrize('seq,bin_size,nparts', [(128, 32, 5), (512, 64, 2)])
+# (seq 1024: the MASK = 2 packer instantiation, MaskLds<1024>, 10-bit shuffle draws)
+@pytest.mark.parametrize('seq,bin_size,nparts', [(128, 32, 5), (512, 64, 2), (1024, 128, 2)])
 def test_bert_masked_end_to_end_vs_oracle(gpu, seq, bin_size, nparts):
   from lddl_amd import synth, pipeline
   c = synth.make_wiki(500_000, seed=seq + 3 * nparts)
