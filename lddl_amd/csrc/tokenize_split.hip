@@ -1510,10 +1510,11 @@ static hipError_t launch_wp(const TokParams& P, const SplitParams& S, int n_cu, 
 constexpr int SCAN_WAVES = 4, WP_WAVES = 12;
 
 int64_t split_seg_slots(int64_t seg_tiles) {
-  // 1 slot per 16 input bytes (the synthetic Wikipedia corpus queues ~0.02
-  // words per byte) + one partly used chunk per scanning wave
+  // 1 slot per 14 input bytes (the synthetic Wikipedia corpus queues ~0.02
+  // words per byte, the CodeSearchNet-style code corpus ~0.065) + one partly
+  // used chunk per scanning wave; past it tiles fall back to the serial path
   const int64_t waves = 256 * 32;
-  const int64_t chunks = (seg_tiles * 1024 / 16 + SPLIT_CHUNK - 1) / SPLIT_CHUNK + std::min(waves, seg_tiles) + 16;
+  const int64_t chunks = (seg_tiles * 1024 / 14 + SPLIT_CHUNK - 1) / SPLIT_CHUNK + std::min(waves, seg_tiles) + 16;
   return chunks * SPLIT_CHUNK;
 }
 

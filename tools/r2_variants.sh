@@ -6,7 +6,7 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 OUT=gpurun_out/${TAG:-r2_variants}; mkdir -p $OUT
 export TMPDIR=/tmp
-for v in "mask512:--masking" "code:--corpus code" "wikibooks:--corpus wikibooks"; do
+for v in "default:" "mask512:--masking" "code:--corpus code" "wikibooks:--corpus wikibooks"; do
   n=${v%%:*}; a=${v#*:}
   timeout -k 10 900 python -u bench.py $a > $OUT/bench_$n.log 2>&1 || { echo "$n failed"; tail -20 $OUT/bench_$n.log; exit 1; }
   grep -h '"metric"' $OUT/bench_$n.log | tail -1 > $OUT/bench_$n.json
