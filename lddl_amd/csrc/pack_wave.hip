@@ -30,6 +30,9 @@ namespace lddl {
 // partition (PackParams cap_*); a partition that does not fit runs the same
 // code on global memory (wave-uniform branch).
 constexpr int PW_DOCS = 512;    // documents held in static LDS by the global-only variant
+#ifndef PACK_OCC
+#define PACK_OCC 8              // BERT packer held to 8 waves/SIMD (78 SGPRs; 7 at 106): pack 36.7 -> 35.6 ms
+#endif
 #ifndef PACK_CHOICE_JUMP
 #define PACK_CHOICE_JUMP 1      // mlm_choices: the picks of a window by pointer doubling, not a scalar walk
 #endif
@@ -467,7 +470,7 @@ __device__ __forceinline__ int range_sum_reg(int dl, int k0, int k1, int lane) {
 // LDSOK = false: every LDS capacity is 0 (the default), the arrays are in
 // global memory and the LDS/global branches compile away
 template <int MASK, bool LDSOK>
-__global__ __launch_bounds__(64) void pack_bert_wave_kernel(PackParams P) {
+__global__ __launch_bounds__(64, PACK_OCC) void pack_bert_wave_kernel(PackParams P) {
   __shared__ PackWaveLds L;
   __shared__ typename std::conditional<MASK != 0, MaskLds<MASK == 1 ? 512 : MLM_MAX_SEQ>, NoMaskLds>::type ML;
   PackDyn D;
