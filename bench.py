@@ -402,7 +402,7 @@ def main():
   # and entries the scan hands to wp_kernel / expand_kernel are this design's
   # intermediates, not algorithmic (they show in roofline.traffic).  Divided
   # by the scan's HIP-event time inside the call (events on the launch
-  # stream; one scan launch per segment of SPLIT_SEG_TILES KiB, 2 GiB).
+  # stream; one scan launch per segment of SPLIT_SEG_TILES KiB, 4 GiB).
   nl = max(1, ks['launches'])
   alg_call = sh.nbytes + 12 * sh.n_sent + 2 * n_tok
   alg = alg_call / nl

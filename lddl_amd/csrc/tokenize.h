@@ -62,11 +62,11 @@ hipError_t launch_tokenize_serial(const TokParams& P, int64_t nbytes, int64_t* t
 //          straight to the output
 //   rec    64-B record slots in chunks of SPLIT_CHUNK, chunk_fill[c] used
 //   nent / nslot / qb / fdef per sentence
-// 2 GiB of input per segment: 14 GB of scratch (entries 2 B/byte, record
-// slots 64 B per 14 B); fewer kernel boundaries than 1 GiB segments (bench
-// step 250.8 -> 249.1 ms; 4 GiB: 246.7 but 28 GB of scratch, too close to
-// the 288 GB of HBM with static masking's arenas at 20 GB of corpus)
-constexpr int64_t SPLIT_SEG_TILES = int64_t(1) << 21;
+// 4 GiB of input per segment: 48 GB of scratch (entries 2 B/byte, record
+// slots and WordPiece outputs 64 B per 14 B each); fewer kernel boundaries
+// than 1 GiB segments (bench step 250.8 -> 246.7 ms; 2 GiB: 249.1).  The
+// masked bench at 20 GB of corpus leaves ~147 GB of the 309 GB free.
+constexpr int64_t SPLIT_SEG_TILES = int64_t(1) << 22;
 constexpr uint32_t SPLIT_CHUNK = 1024;                 // record slots per allocation chunk (64 KiB)
 constexpr uint32_t SPLIT_EDEF = 0xF000u;               // entry >= EDEF: a queued word
 constexpr uint16_t SPLIT_NENT_FB = 0xFFFFu;            // nent of a sentence of a fallback tile
@@ -77,6 +77,7 @@ struct SplitParams {
   const int64_t* tile_sent;
   uint16_t* ent;
   uint4* rec;              // 4 uint4 per slot
+  uint4* pcs;              // TOK5_PCS: WordPiece output (count + pieces) per slot, apart from the keys
   uint32_t* chunk_fill;
   uint32_t* chunk_ctr;     // [0] chunks handed out
   uint32_t n_chunks;

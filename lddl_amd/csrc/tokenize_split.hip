@@ -65,6 +65,9 @@ constexpr int KEYMAX = 56;               // key bytes a record holds
 #ifndef TOK5_PLANES
 #define TOK5_PLANES 1
 #endif
+#ifndef TOK5_PCS
+#define TOK5_PCS 1
+#endif
 #ifndef TOK5_MERGED_PROBE
 #define TOK5_MERGED_PROBE 1
 #endif
@@ -1143,9 +1146,12 @@ __global__ __launch_bounds__(64 * WAVES) void wp_kernel(TokParams P, SplitParams
     if (e < we && !(asc && e - s < 24))
       while (e > s && (kbyte(e) & 0xC0u) == 0x80u) --e;
   };
-  auto rec16 = [&]() { return reinterpret_cast<uint16_t*>(S.rec + (size_t)r * 4); };
+  // (TOK5_PCS: the pieces and count go to a buffer of their own, so the
+  // record lines other lanes are still loading stay read-only)
+  uint4* const outs = TOK5_PCS ? S.pcs : S.rec;
+  auto rec16 = [&]() { return reinterpret_cast<uint16_t*>(outs + (size_t)r * 4); };
   auto finish = [&]() {
-    reinterpret_cast<uint32_t*>(S.rec + (size_t)r * 4)[1] = (uint32_t)np;
+    reinterpret_cast<uint32_t*>(outs + (size_t)r * 4)[1] = (uint32_t)np;
     r = -1;
   };
   // optional stamps (P.dbg, LDDL_TOK_DEBUG=1): A (Bloom scan + bucket
@@ -1418,7 +1424,7 @@ __global__ __launch_bounds__(256) void expand_kernel(TokParams P, SplitParams S)
         rq[k] = u32x3{1u, 0u, 0u};
         if (kk[k] != 0xFFFFFFFFu && v[k] >= SPLIT_EDEF)
           rq[k] = *reinterpret_cast<const u32x3*>(reinterpret_cast<const uint32_t*>(
-                      S.rec + (size_t)(E.qb[js[k]] + (v[k] & 0xFFFu)) * 4) + 1);
+                      (TOK5_PCS ? S.pcs : S.rec) + (size_t)(E.qb[js[k]] + (v[k] & 0xFFFu)) * 4) + 1);
       }
       uint32_t run = 0, h = 0;
 #pragma unroll
@@ -1458,7 +1464,7 @@ __global__ __launch_bounds__(256) void expand_kernel(TokParams P, SplitParams S)
           if (c > 3 && p + 3 < max_tok) o[p + 3] = (uint16_t)(rq[k].z >> 16);
           if (c > 4) {
             const uint16_t* pc =
-                reinterpret_cast<const uint16_t*>(S.rec + (size_t)(E.qb[jj] + (v[k] & 0xFFFu)) * 4);
+                reinterpret_cast<const uint16_t*>((TOK5_PCS ? S.pcs : S.rec) + (size_t)(E.qb[jj] + (v[k] & 0xFFFu)) * 4);
             for (uint32_t q = 4; q < c && p + q < max_tok; ++q) o[p + q] = pc[piece_at((int)q)];
           }
         }
