@@ -65,6 +65,9 @@ constexpr int KEYMAX = 56;               // key bytes a record holds
 #ifndef TOK5_PLANES
 #define TOK5_PLANES 1
 #endif
+#ifndef TOK5_WP_REGPCS
+#define TOK5_WP_REGPCS 1
+#endif
 #ifndef TOK5_PCS
 #define TOK5_PCS 1
 #endif
@@ -1150,10 +1153,32 @@ __global__ __launch_bounds__(64 * WAVES) void wp_kernel(TokParams P, SplitParams
   // record lines other lanes are still loading stay read-only)
   uint4* const outs = TOK5_PCS ? S.pcs : S.rec;
   auto rec16 = [&]() { return reinterpret_cast<uint16_t*>(outs + (size_t)r * 4); };
+#if TOK5_WP_REGPCS
+  // pieces 0-3 (nearly every word's all) held in two registers and stored
+  // with the count in one 12-B store at the end (what expand loads)
+  uint32_t pw01 = 0, pw23 = 0;
+  auto put_piece = [&](int k, uint32_t id) {
+    if (k < 4) {
+      const uint32_t sh = 16u * (uint32_t)(k & 1);
+      const uint32_t keep = ~(0xFFFFu << sh), val = id << sh;
+      if (k < 2) pw01 = (pw01 & keep) | val;
+      else pw23 = (pw23 & keep) | val;
+    } else {
+      rec16()[piece_at(k)] = (uint16_t)id;
+    }
+  };
+  auto finish = [&]() {
+    typedef uint32_t u32x3s __attribute__((ext_vector_type(3)));
+    *reinterpret_cast<u32x3s*>(reinterpret_cast<uint32_t*>(outs + (size_t)r * 4) + 1) = u32x3s{(uint32_t)np, pw01, pw23};
+    r = -1;
+  };
+#else
+  auto put_piece = [&](int k, uint32_t id) { rec16()[piece_at(k)] = (uint16_t)id; };
   auto finish = [&]() {
     reinterpret_cast<uint32_t*>(outs + (size_t)r * 4)[1] = (uint32_t)np;
     r = -1;
   };
+#endif
   // optional stamps (P.dbg, LDDL_TOK_DEBUG=1): A (Bloom scan + bucket
   // issue), B (refill issue), C (compare; waits for the loads), D (record
   // start), steps, lane-steps with a record
@@ -1258,7 +1283,7 @@ __global__ __launch_bounds__(64 * WAVES) void wp_kernel(TokParams P, SplitParams
     if (r >= 0) {
       if (fail) {  // some position has no match: the whole word is [UNK]
         np = 0;
-        rec16()[piece_at(0)] = (uint16_t)P.unk;
+        put_piece(0, (uint32_t)P.unk);
         np = 1;
         finish();
       } else {
@@ -1282,7 +1307,7 @@ __global__ __launch_bounds__(64 * WAVES) void wp_kernel(TokParams P, SplitParams
             for (int k = 24; k < len; ++k) m1 = m1 && kbyte(s + k) == P.pool[b1.w + k];
         }
         if (m0 || m1) {
-          rec16()[piece_at(np)] = (uint16_t)((m0 ? a1.z : b1.z) & 0xFFFFu);
+          put_piece(np, (m0 ? a1.z : b1.z) & 0xFFFFu);
           ++np;
           s = e;
           if (s >= we) {
