@@ -65,6 +65,9 @@ constexpr int KEYMAX = 56;               // key bytes a record holds
 #ifndef TOK5_PLANES
 #define TOK5_PLANES 1
 #endif
+#ifndef TOK5_WP_SHORTREF
+#define TOK5_WP_SHORTREF 1
+#endif
 #ifndef TOK5_WP_REGPCS
 #define TOK5_WP_REGPCS 1
 #endif
@@ -1097,6 +1100,7 @@ __global__ __launch_bounds__(64 * WAVES) void wp_kernel(TokParams P, SplitParams
   int r = -1;    // record slot being tokenised
   int pr = -1;   // record slot loaded, not begun
   uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0, q2 = q0, q3 = q0;
+  bool qlong = false;  // (TOK5_WP_SHORTREF) q2 / q3 of the pending record loaded
   int s = 0, we = 0, e = 0, np = 0, bslot = -1;
   uint32_t cont = 0;
   bool asc = false;
@@ -1271,8 +1275,15 @@ __global__ __launch_bounds__(64 * WAVES) void wp_kernel(TokParams P, SplitParams
           const uint4* rp = S.rec + (size_t)pr * 4;
           q0 = rp[0];
           q1 = rp[1];
+#if TOK5_WP_SHORTREF
+          // key bytes 24.. only for a longer key: loaded at its start (the
+          // record begins a step later); a key of <= 24 bytes is zero past them
+          q2 = q3 = make_uint4(0, 0, 0, 0);
+          qlong = false;
+#else
           q2 = rp[2];
           q3 = rp[3];
+#endif
         }
         off += min((uint32_t)__popcll(idle), avail);
         advance();
@@ -1329,6 +1340,13 @@ __global__ __launch_bounds__(64 * WAVES) void wp_kernel(TokParams P, SplitParams
     if (r < 0 && pr >= 0) {
       if (q0.x == 0u) {  // an extension slot
         pr = -1;
+#if TOK5_WP_SHORTREF
+      } else if ((q0.x & 0xFFu) > 24u && !qlong) {
+        const uint4* rp = S.rec + (size_t)pr * 4;
+        q2 = rp[2];
+        q3 = rp[3];
+        qlong = true;
+#endif
       } else {
         const int len = (int)(q0.x & 0xFFu);
         kb[0] = q0.z; kb[64] = q0.w;
@@ -1479,11 +1497,10 @@ __global__ __launch_bounds__(256) void expand_kernel(TokParams P, SplitParams S)
         uint16_t* o = P.out_ids + E.dst[jj];
         const uint32_t p = pre[k];
         const uint32_t max_tok = max_tok0 - E.f[jj];  // (entries are kept below max_tok: f < max_tok)
-        if (v[k] < SPLIT_EDEF) {
-          if (p < max_tok) o[p] = (uint16_t)v[k];
-        } else {
+        // (the first token of a direct id and of a record in one store)
+        if (p < max_tok) o[p] = (uint16_t)(v[k] < SPLIT_EDEF ? v[k] : rq[k].y & 0xFFFFu);
+        if (v[k] >= SPLIT_EDEF) {
           const uint32_t c = cnt[k];
-          if (p < max_tok) o[p] = (uint16_t)(rq[k].y & 0xFFFFu);
           if (c > 1 && p + 1 < max_tok) o[p + 1] = (uint16_t)(rq[k].y >> 16);
           if (c > 2 && p + 2 < max_tok) o[p + 2] = (uint16_t)(rq[k].z & 0xFFFFu);
           if (c > 3 && p + 3 < max_tok) o[p + 3] = (uint16_t)(rq[k].z >> 16);
