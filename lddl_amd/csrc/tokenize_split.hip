@@ -973,13 +973,15 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
           }
           if (ev[k] && (int)e < max_tok) {
             const int64_t at = (int64_t)L.sst[sj] + e;
+            // one store per unit: an id with no queued word before it is final
+            // (the output), everything else an entry for expand
+            const bool fin = idv[k] != U_DEFER && o == 0;
+            uint16_t* const dst = fin ? P.out_ids + (obase + at) : S.ent + (ent0 + at);
+            *dst = (uint16_t)(idv[k] != U_DEFER ? idv[k] : (SPLIT_EDEF | o));
             if (idv[k] != U_DEFER) {
-              if (o == 0) P.out_ids[obase + at] = (uint16_t)idv[k];  // no queued word before it: final
-              else S.ent[ent0 + at] = (uint16_t)idv[k];
               // ([CLS] / [SEP] come only from literal specials, never from WordPiece)
               if (idv[k] == P.special[2] || idv[k] == P.special[3]) atomicOr(&L.sspec[sj >> 5], 1u << (sj & 31));
             } else {
-              S.ent[ent0 + at] = (uint16_t)(SPLIT_EDEF | o);
               if (o == 0) {
                 L.sqb[sj] = gp;
                 L.sfdef[sj] = (uint16_t)e;
@@ -1006,24 +1008,37 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
           const int len = wlen(w), src = wsrc(w);
           const int a = src >> 2;
           const uint32_t sh = (uint32_t)(src & 3);
-          uint32_t x[15];
-#pragma unroll
-          for (int i = 0; i < 15; ++i) x[i] = L.nb[a + i];
-          uint32_t kd[14];
-#pragma unroll
-          for (int i = 0; i < 14; ++i) kd[i] = keep_bytes(__builtin_amdgcn_alignbyte(x[i + 1], x[i], sh), len - 4 * i);
           const uint32_t slots = len <= KEY1 ? 1u : 2u;
           uint4* rp = S.rec + (size_t)slot * 4;
-          rp[0] = make_uint4((uint32_t)len | (slots << 8) | 0x80000000u, 0u, kd[0], kd[1]);
-          rp[1] = make_uint4(kd[2], kd[3], kd[4], kd[5]);
-          rp[2] = make_uint4(kd[6], kd[7], kd[8], kd[9]);
-          rp[3] = make_uint4(kd[10], kd[11], kd[12], kd[13]);
-          if (slots == 2) {  // the extension slot: a zero header (skipped by wp_kernel), pieces 28..
+          {
+            uint32_t x[7];
+#pragma unroll
+            for (int i = 0; i < 7; ++i) x[i] = L.nb[a + i];
+            uint32_t kd[6];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) kd[i] = keep_bytes(__builtin_amdgcn_alignbyte(x[i + 1], x[i], sh), len - 4 * i);
+            rp[0] = make_uint4((uint32_t)len | (slots << 8) | 0x80000000u, 0u, kd[0], kd[1]);
+            rp[1] = make_uint4(kd[2], kd[3], kd[4], kd[5]);
+          }
+          // key bytes 24..55 (wp_kernel reads them only for a longer key)
+          if (!TOK5_WP_SHORTREF || len > 24) {
+            uint32_t x[9];
+#pragma unroll
+            for (int i = 0; i < 9; ++i) x[i] = L.nb[a + 6 + i];
+            uint32_t kd[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) kd[i] = keep_bytes(__builtin_amdgcn_alignbyte(x[i + 1], x[i], sh), len - 24 - 4 * i);
+            rp[2] = make_uint4(kd[0], kd[1], kd[2], kd[3]);
+            rp[3] = make_uint4(kd[4], kd[5], kd[6], kd[7]);
+          }
+          if (slots == 2) {  // the extension slot: a zero header (skipped by wp_kernel)
             const uint4 z = make_uint4(0, 0, 0, 0);
             rp[4] = z;
-            rp[5] = z;
-            rp[6] = z;
-            rp[7] = z;
+            if (!TOK5_PCS) {  // (pieces 28.. land in it)
+              rp[5] = z;
+              rp[6] = z;
+              rp[7] = z;
+            }
           }
         }
         cur += need;
