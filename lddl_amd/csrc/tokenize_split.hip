@@ -65,6 +65,9 @@ constexpr int KEYMAX = 56;               // key bytes a record holds
 #ifndef TOK5_PLANES
 #define TOK5_PLANES 1
 #endif
+#ifndef TOK5_REC_SOA
+#define TOK5_REC_SOA 1
+#endif
 #ifndef TOK5_WP_SHORTREF
 #define TOK5_WP_SHORTREF 1
 #endif
@@ -123,6 +126,12 @@ __device__ __forceinline__ void wsync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+// record slot k (of 4 16-B quarters) of slot i: quarter-major (TOK5_REC_SOA:
+// the lanes of a refill, on consecutive slots, load one contiguous run per
+// quarter) or slot-major
+__device__ __forceinline__ uint4* recq(const SplitParams& S, int k, uint64_t i) {
+  return TOK5_REC_SOA ? S.rec + (uint64_t)k * ((uint64_t)S.n_chunks * SPLIT_CHUNK) + i : S.rec + i * 4 + k;
 }
 __device__ __forceinline__ uint32_t rawb(const Lds& L, int p) { return reinterpret_cast<const uint8_t*>(L.rp)[p]; }
 __device__ __forceinline__ uint32_t nbyte(const uint32_t* nb, int p) { return reinterpret_cast<const uint8_t*>(nb)[p]; }
@@ -950,7 +959,8 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
             // (records this wave stored in an earlier round: drain its stores first)
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             const uint32_t from = L.sqb[first_sent];
-            for (uint32_t i = lane; i < carried * 4; i += 64) S.rec[(size_t)cur * 4 + i] = S.rec[(size_t)from * 4 + i];
+            for (int k = 0; k < 4; ++k)
+              for (uint32_t i = lane; i < carried; i += 64) *recq(S, k, cur + i) = *recq(S, k, from + i);
             if (lane == 0) L.sqb[first_sent] = cur;
             cur += carried;
           }
@@ -1009,7 +1019,6 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
           const int a = src >> 2;
           const uint32_t sh = (uint32_t)(src & 3);
           const uint32_t slots = len <= KEY1 ? 1u : 2u;
-          uint4* rp = S.rec + (size_t)slot * 4;
           {
             uint32_t x[7];
 #pragma unroll
@@ -1017,8 +1026,8 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
             uint32_t kd[6];
 #pragma unroll
             for (int i = 0; i < 6; ++i) kd[i] = keep_bytes(__builtin_amdgcn_alignbyte(x[i + 1], x[i], sh), len - 4 * i);
-            rp[0] = make_uint4((uint32_t)len | (slots << 8) | 0x80000000u, 0u, kd[0], kd[1]);
-            rp[1] = make_uint4(kd[2], kd[3], kd[4], kd[5]);
+            *recq(S, 0, slot) = make_uint4((uint32_t)len | (slots << 8) | 0x80000000u, 0u, kd[0], kd[1]);
+            *recq(S, 1, slot) = make_uint4(kd[2], kd[3], kd[4], kd[5]);
           }
           // key bytes 24..55 (wp_kernel reads them only for a longer key)
           if (!TOK5_WP_SHORTREF || len > 24) {
@@ -1028,16 +1037,16 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
             uint32_t kd[8];
 #pragma unroll
             for (int i = 0; i < 8; ++i) kd[i] = keep_bytes(__builtin_amdgcn_alignbyte(x[i + 1], x[i], sh), len - 24 - 4 * i);
-            rp[2] = make_uint4(kd[0], kd[1], kd[2], kd[3]);
-            rp[3] = make_uint4(kd[4], kd[5], kd[6], kd[7]);
+            *recq(S, 2, slot) = make_uint4(kd[0], kd[1], kd[2], kd[3]);
+            *recq(S, 3, slot) = make_uint4(kd[4], kd[5], kd[6], kd[7]);
           }
           if (slots == 2) {  // the extension slot: a zero header (skipped by wp_kernel)
             const uint4 z = make_uint4(0, 0, 0, 0);
-            rp[4] = z;
+            *recq(S, 0, slot + 1) = z;
             if (!TOK5_PCS) {  // (pieces 28.. land in it)
-              rp[5] = z;
-              rp[6] = z;
-              rp[7] = z;
+              *recq(S, 1, slot + 1) = z;
+              *recq(S, 2, slot + 1) = z;
+              *recq(S, 3, slot + 1) = z;
             }
           }
         }
@@ -1170,6 +1179,7 @@ __global__ __launch_bounds__(64 * WAVES) void wp_kernel(TokParams P, SplitParams
   };
   // (TOK5_PCS: the pieces and count go to a buffer of their own, so the
   // record lines other lanes are still loading stay read-only)
+  static_assert(!TOK5_REC_SOA || TOK5_PCS, "quarter-major records need the separate output buffer");
   uint4* const outs = TOK5_PCS ? S.pcs : S.rec;
   auto rec16 = [&]() { return reinterpret_cast<uint16_t*>(outs + (size_t)r * 4); };
 #if TOK5_WP_REGPCS
@@ -1287,17 +1297,16 @@ __global__ __launch_bounds__(64 * WAVES) void wp_kernel(TokParams P, SplitParams
         const int k = lane_rank(idle);
         if (r < 0 && pr < 0 && (uint32_t)k < avail) {
           pr = (int)(c * SPLIT_CHUNK + off + (uint32_t)k);
-          const uint4* rp = S.rec + (size_t)pr * 4;
-          q0 = rp[0];
-          q1 = rp[1];
+          q0 = *recq(S, 0, (uint32_t)pr);
+          q1 = *recq(S, 1, (uint32_t)pr);
 #if TOK5_WP_SHORTREF
           // key bytes 24.. only for a longer key: loaded at its start (the
           // record begins a step later); a key of <= 24 bytes is zero past them
           q2 = q3 = make_uint4(0, 0, 0, 0);
           qlong = false;
 #else
-          q2 = rp[2];
-          q3 = rp[3];
+          q2 = *recq(S, 2, (uint32_t)pr);
+          q3 = *recq(S, 3, (uint32_t)pr);
 #endif
         }
         off += min((uint32_t)__popcll(idle), avail);
@@ -1357,9 +1366,8 @@ __global__ __launch_bounds__(64 * WAVES) void wp_kernel(TokParams P, SplitParams
         pr = -1;
 #if TOK5_WP_SHORTREF
       } else if ((q0.x & 0xFFu) > 24u && !qlong) {
-        const uint4* rp = S.rec + (size_t)pr * 4;
-        q2 = rp[2];
-        q3 = rp[3];
+        q2 = *recq(S, 2, (uint32_t)pr);
+        q3 = *recq(S, 3, (uint32_t)pr);
         qlong = true;
 #endif
       } else {
