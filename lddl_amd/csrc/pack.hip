@@ -147,6 +147,9 @@ __global__ __launch_bounds__(256) void materialize_kernel(MatParams M) {
 constexpr int MAT_U = 4;         // chunks per lane per phase-1 iteration
 constexpr int MAT_SLOW = 512;    // slow-chunk list capacity per wave
 constexpr int MAT_PBITS = 26;    // slow entry: chunk start + 8 (26 bits) | row << 26
+#ifndef MAT_TWO
+#define MAT_TWO 1   // compaction: chunks across two rows blended from two source windows
+#endif
 struct RowDesc {
   int64_t src0, src1;       // source start of segment A / B
   int32_t l0, b1, l1, nt;   // |A|, first position of B, |B|, row length
@@ -252,6 +255,17 @@ __device__ __forceinline__ void mat_copy(MatWave& W, int64_t G0, int64_t G1, con
     int64_t sv[MAT_U];
     bool fast[MAT_U], slow[MAT_U];
     int rw[MAT_U];
+#if MAT_TWO
+    bool two[MAT_U];
+    int64_t sv2[MAT_U];
+    uint32_t spl[MAT_U];
+#pragma unroll
+    for (int u = 0; u < MAT_U; ++u) {
+      two[u] = false;
+      sv2[u] = 0;
+      spl[u] = 8;
+    }
+#endif
 #pragma unroll
     for (int u = 0; u < MAT_U; ++u) {
       const int64_t q = qb + u * 64 + lane;
@@ -270,8 +284,28 @@ __device__ __forceinline__ void mat_copy(MatWave& W, int64_t G0, int64_t G1, con
         inA = t0 >= 0 && t0 + 8 <= y.l0;
         inB = false;
         v = y.src0 + t0;
+#if MAT_TWO
+        // a chunk that runs from this row into the next one (compaction:
+        // rows back to back, ~34 tokens each) blends two source windows
+        // instead of going token by token through the slow list
+        two[u] = false;
+        if (q < q1 && !inA && t0 >= 0 && t0 < y.l0 && r < 63) {
+          const int32_t r2off = W.roff[r + 1];
+          const RowDesc y2 = W.row[r + 1];
+          const int64_t v2 = y2.src0 + (p0 - r2off);
+          if (r2off == p0 + (y.l0 - t0) && p0 + 8 <= r2off + y2.l0 && v2 >= 0 && (v >> 3) <= amax &&
+              (v2 >> 3) <= amax) {
+            two[u] = true;
+            sv2[u] = v2;
+            spl[u] = (uint32_t)(y.l0 - t0);
+          }
+        }
+#endif
       }
       fast[u] = q < q1 && (inA || inB) && (v >> 3) <= amax;
+#if MAT_TWO
+      if constexpr (!LEAD) fast[u] = fast[u] || two[u];
+#endif
       slow[u] = q < q1 && !fast[u];
       sv[u] = fast[u] ? v : 0;
     }
@@ -285,6 +319,28 @@ __device__ __forceinline__ void mat_copy(MatWave& W, int64_t G0, int64_t G1, con
         vb[u] = s4[a + 1];
       }
     }
+#if MAT_TWO
+    if constexpr (!LEAD) {
+#pragma unroll
+      for (int u = 0; u < MAT_U; ++u)
+        if (two[u]) {  // tokens [spl, 8) from the next row's window
+          const int64_t a2 = sv2[u] >> 3;
+          const uint4 vc = s4[a2], vd = s4[a2 + 1];
+          const uint4 w2 = funnel8(vc, vd, (uint32_t)(sv2[u] & 7));
+          const uint32_t sp = spl[u];
+          // keep token k of the first window iff k < sp: per dword, low / high halves
+          auto blend = [&](uint32_t x, uint32_t y2, uint32_t k0) {
+            const uint32_t lo = k0 < sp ? 0x0000FFFFu : 0u, hi = k0 + 1 < sp ? 0xFFFF0000u : 0u;
+            const uint32_t m = lo | hi;
+            return (x & m) | (y2 & ~m);
+          };
+          const uint4 w1 = funnel8(va[u], vb[u], (uint32_t)(sv[u] & 7));
+          va[u] = make_uint4(blend(w1.x, w2.x, 0), blend(w1.y, w2.y, 2), blend(w1.z, w2.z, 4), blend(w1.w, w2.w, 6));
+          vb[u] = va[u];
+          sv[u] &= ~(int64_t)7;  // (funnel8 at offset 0 below returns va unchanged)
+        }
+    }
+#endif
 #pragma unroll
     for (int u = 0; u < MAT_U; ++u)
       if (fast[u]) {
