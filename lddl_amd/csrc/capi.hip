@@ -478,8 +478,7 @@ extern "C" int lddl_tokenize(lddl_ctx* c, const uint8_t* d_bytes, int64_t nbytes
     if ((rc = ws_get(c, 19, nt + 1, &tile_sent)) || (rc = ws_get(c, 20, nt, &S.fb_list)) ||
         (rc = ws_get(c, 21, 16, &S.fb_count)) || (rc = ws_get(c, 34, (size_t)seg * 1024 + 4096, &S.ent)) ||
         (rc = ws_get(c, 35, (size_t)slots * 4, &S.rec)) || (rc = ws_get(c, 42, (size_t)slots * 4, &S.pcs)) || (rc = ws_get(c, 36, (size_t)n_chunks + 16, &S.chunk_fill)) ||
-        (rc = ws_get(c, 37, n_sent, &S.nent)) || (rc = ws_get(c, 38, n_sent, &S.nslot)) ||
-        (rc = ws_get(c, 39, n_sent, &S.qb)) || (rc = ws_get(c, 40, n_sent, &S.fdef)))
+        (rc = ws_get(c, 37, n_sent, &S.smeta)))
       return rc;
     S.chunk_ctr = S.chunk_fill + n_chunks;
     S.n_chunks = (uint32_t)n_chunks;

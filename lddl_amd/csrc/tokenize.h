@@ -61,7 +61,7 @@ hipError_t launch_tokenize_serial(const TokParams& P, int64_t nbytes, int64_t* t
 //          for a word of the queue; the ids before it are final and go
 //          straight to the output
 //   rec    64-B record slots in chunks of SPLIT_CHUNK, chunk_fill[c] used
-//   nent / nslot / qb / fdef per sentence
+//   smeta  per sentence: #entries, first queued entry (fdef), first record slot (qb)
 // 4 GiB of input per segment: 48 GB of scratch (entries 2 B/byte, record
 // slots and WordPiece outputs 64 B per 14 B each); fewer kernel boundaries
 // than 1 GiB segments (bench step 250.8 -> 246.7 ms; 2 GiB: 249.1).  The
@@ -81,12 +81,9 @@ struct SplitParams {
   uint32_t* chunk_fill;
   uint32_t* chunk_ctr;     // [0] chunks handed out
   uint32_t n_chunks;
-  uint16_t* nent;
-  uint16_t* nslot;
-  uint32_t* qb;
+  uint2* smeta;            // per sentence: #entries | first queued entry << 16, first record slot (~0: none)
   int32_t* fb_list;
   int32_t* fb_count;
-  uint16_t* fdef;          // entry index of the sentence's first queued word (nslot > 0)
   unsigned long long* n_rec;  // optional: records run by wp_kernel (summed over the call)
 };
 // optional per-kernel timing of a call: event pairs recorded around every

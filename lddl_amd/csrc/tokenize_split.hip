@@ -431,8 +431,7 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
         S.fb_list[at] = (int32_t)t;
       }
       for (int j = lane; j < ns; j += 64) {
-        S.nent[sa + j] = SPLIT_NENT_FB;
-        S.nslot[sa + j] = 0;
+        S.smeta[sa + j] = make_uint2(SPLIT_NENT_FB, 0xFFFFFFFFu);
       }
     };
     const int aoff = (int)(reinterpret_cast<uintptr_t>(P.bytes + A) & 15u);
@@ -1065,12 +1064,9 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
       const int64_t s = sa + lane;
       const int ne = min((int)L.sent_n[lane], max_tok);
       const int nsl = L.sslot[lane];
-      S.nent[s] = (uint16_t)ne;
-      S.nslot[s] = (uint16_t)nsl;
-      if (nsl) {
-        S.qb[s] = L.sqb[lane];
-        S.fdef[s] = (uint16_t)L.sfdef[lane];
-      }
+      // one 8-B record per sentence for expand: entries | first queued entry
+      // << 16, first record slot (~0: no queued word)
+      S.smeta[s] = make_uint2((uint32_t)ne | (nsl ? (uint32_t)L.sfdef[lane] << 16 : 0u), nsl ? L.sqb[lane] : 0xFFFFFFFFu);
       P.out_ntok[s] = ne - (int)L.sdef[lane];
       if (P.sent_spec) P.sent_spec[s] = (uint8_t)((L.sspec[lane >> 5] >> (lane & 31)) & 1u);
     }
@@ -1441,18 +1437,19 @@ __global__ __launch_bounds__(256) void expand_kernel(TokParams P, SplitParams S)
     if (s < sB) {
       // entries from the first queued word on (the ids before it are final;
       // a sentence without queued words or of a fallback tile is done)
-      ne = S.nent[s];
+      const uint2 m = S.smeta[s];
+      ne = m.x & 0xFFFFu;
       uint32_t f = 0;
-      if (ne == SPLIT_NENT_FB || S.nslot[s] == 0) {
+      if (ne == SPLIT_NENT_FB || m.y == 0xFFFFFFFFu) {
         ne = 0;
       } else {
-        f = S.fdef[s];
+        f = m.x >> 16;
         ne -= f;
       }
       const int64_t so = P.sent_off[s] - base + f;
       E.eoff[lane] = so - ebase;
       E.dst[lane] = so;
-      E.qb[lane] = ne ? S.qb[s] : 0u;
+      E.qb[lane] = ne ? m.y : 0u;
       E.f[lane] = f;
     }
     const uint32_t x = wave_incl_add(ne);
