@@ -144,7 +144,10 @@ __global__ __launch_bounds__(256) void materialize_kernel(MatParams M) {
 // Every other chunk ([CLS]/[SEP], a row boundary, or one of the two chunks
 // shared with the neighbouring waves) goes to a per-wave list that phase 2
 // drains token-parallel (one token per lane, u16 load + store).
-constexpr int MAT_U = 4;         // chunks per lane per phase-1 iteration
+#ifndef MAT_UNROLL
+#define MAT_UNROLL 2
+#endif
+constexpr int MAT_U = MAT_UNROLL;         // chunks per lane per phase-1 iteration
 constexpr int MAT_SLOW = 512;    // slow-chunk list capacity per wave
 constexpr int MAT_PBITS = 26;    // slow entry: chunk start + 8 (26 bits) | row << 26
 #ifndef MAT_TWO
