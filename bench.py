@@ -34,7 +34,7 @@ HBM_PEAK_GBS = 8000.0
 
 def parse():
   ap = argparse.ArgumentParser()
-  ap.add_argument('--gpus', type=int, default=1)
+  ap.add_argument('--gpus', type=int, default=None, help='ranks (default: WORLD_SIZE, else 1)')
   ap.add_argument('--steps', type=int, default=3)
   ap.add_argument('--warmup', type=int, default=1)
   ap.add_argument('--corpus-gb', type=float, default=20.0)
@@ -57,6 +57,9 @@ def parse():
   ap.add_argument('--parquet-parts', type=int, default=64,
                   help='after timing: write this many partitions as parquet shards and report the writer rate '
                        '(GPU string rendering + host Arrow/parquet encode; 0 = skip)')
+  ap.add_argument('--launch-check', action='store_true',
+                  help='multi-rank plumbing only (CPU, gloo, no GPU kernels): launch --gpus ranks, all-gather '
+                       'synthetic per-(partition, bin) counts and print the line fields that depend on the world')
   args = ap.parse_args()
   code = args.corpus == 'code'
   if args.unique_mb is None:
@@ -321,11 +324,72 @@ def parquet_sample(args, pk, res, sh):
     shutil.rmtree(d, ignore_errors=True)
 
 
+def launch_ranks(args):
+  """`--gpus N` without a launcher: start N rank processes (this process has
+  not touched the GPU: torch.cuda.device_count() does not initialise it) with
+  RANK / WORLD_SIZE / LOCAL_RANK / MASTER_* as torch.distributed.run sets them,
+  wait for all of them, and return the worst exit code.  Rank 0 prints the
+  line."""
+  import socket
+  import subprocess
+  if not args.launch_check:
+    have = torch.cuda.device_count()
+    if args.gpus > have:
+      print('bench.py: --gpus %d but %d GPU(s) visible' % (args.gpus, have), file=sys.stderr)
+      return 2
+  with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+  procs = []
+  for r in range(args.gpus):
+    env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus), LOCAL_WORLD_SIZE=str(args.gpus),
+               MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+  codes = [p.wait() for p in procs]
+  bad = [c for c in codes if c != 0]
+  return bad[0] if bad else 0
+
+
+def check_gather(gathered, own, rank, world):
+  """the all-gather saw every rank: world x the per-rank partitions, this
+  rank's block in its place"""
+  n_part = own.shape[0]
+  if gathered.shape[0] != world * n_part or not np.array_equal(gathered[rank * n_part:(rank + 1) * n_part], own):
+    raise RuntimeError('all-gather of bin counts: %d partitions gathered, expected %d x %d' % (
+        gathered.shape[0], world, n_part))
+  return int(gathered.shape[0])
+
+
+def launch_check(args, rank, world):
+  """--launch-check: the world-dependent part of a bench run on the CPU (gloo)"""
+  import torch.distributed as dist
+  from lddl_amd.balance import gather_bin_counts
+  if world > 1:
+    dist.init_process_group('gloo')
+  n_part, nbins = 7, args.target_seq_length // args.bin_size
+  own = torch.arange(n_part * nbins, dtype=torch.int64).view(n_part, nbins) + 1000 * rank
+  got = gather_bin_counts(own, rank * n_part) if world > 1 else own.numpy()
+  n = check_gather(got, own.numpy(), rank, world)
+  if rank == 0:
+    print(json.dumps({'metric': METRIC, 'check': 'launch', 'n_gpus': world, 'gathered_partitions': n,
+                      'partitions_per_rank': n_part, 'parallelism': 'shard%d' % world}), flush=True)
+  if world > 1:
+    dist.destroy_process_group()
+
+
 def main():
   args = parse()
+  if 'WORLD_SIZE' not in os.environ and (args.gpus or 1) > 1:
+    sys.exit(launch_ranks(args))
   rank = int(os.environ.get('RANK', 0))
   world = int(os.environ.get('WORLD_SIZE', 1))
   local = int(os.environ.get('LOCAL_RANK', 0))
+  if args.gpus is None:
+    args.gpus = world
+  if world != args.gpus:
+    raise SystemExit('bench.py: --gpus %d but WORLD_SIZE=%d' % (args.gpus, world))
+  if args.launch_check:
+    return launch_check(args, rank, world)
   torch.cuda.set_device(local)
   device = torch.device('cuda', local)
   dist = None
@@ -343,6 +407,7 @@ def main():
   kw = dict(target_seq_length=args.target_seq_length, short_seq_prob=0.1, duplicate_factor=args.duplicate_factor,
             seed=args.seed + rank * 10_000_000, bin_size=args.bin_size, masking=args.masking, codebert=code)
   tok_ms = []
+  gathered = []
 
   def step(timed):
     s = torch.cuda.current_stream()
@@ -355,7 +420,9 @@ def main():
       # per-(partition, bin) row counts of every rank: the load balancer's
       # input (lddl_amd/balance.py), one RCCL all-gather per step
       from lddl_amd.balance import gather_bin_counts
-      gather_bin_counts(res.bin_count, rank * sh.n_part)
+      g = gather_bin_counts(res.bin_count, rank * sh.n_part)
+      if timed:
+        gathered.append(g)
     if timed:
       tok_ms.append((e0, e1))
     return res, ntok
@@ -381,6 +448,11 @@ def main():
     raise RuntimeError('tokenize: replicas disagree: %s' % per_rep.tolist()[:16])
   tk = float(np.mean([a.elapsed_time(b) for a, b in tok_ms]))
   ks = pk.tok.stats()  # the last timed step's tokenize kernels
+  if not ks['launches'] or ks['scan_ms'] <= 0:
+    raise RuntimeError('bench: no tokenizer kernel events (the split tokenizer did not run: %s)' % ks)
+  n_gathered = None
+  if dist is not None:  # the last step's all-gather saw every rank
+    n_gathered = check_gather(gathered[-1], res.bin_count.cpu().numpy(), rank, world)
   if dist is not None:
     t = torch.tensor([el, float(n_tok)], dtype=torch.float64, device=device)
     mx = t.clone()
@@ -403,7 +475,7 @@ def main():
   # intermediates, not algorithmic (they show in roofline.traffic).  Divided
   # by the scan's HIP-event time inside the call (events on the launch
   # stream; one scan launch per segment of SPLIT_SEG_TILES KiB, 4 GiB).
-  nl = max(1, ks['launches'])
+  nl = ks['launches']
   alg_call = sh.nbytes + 12 * sh.n_sent + 2 * n_tok
   alg = alg_call / nl
   achieved = alg / (ks['scan_ms'] / nl * 1e-3) / 1e9
@@ -427,7 +499,7 @@ def main():
                  'partitions_per_gpu': sh.n_part, 'wordpiece_tokens_per_gpu': n_tok,
                  'pairs_per_gpu': res.n_pairs, 'packed_tokens_per_gpu': res.n_tokens,
                  'masked_positions_per_gpu': res.n_masked,
-                 'parallelism': 'shard%d' % world},
+                 'parallelism': 'shard%d' % world, 'gathered_partitions': n_gathered},
       'roofline': {'bound': 'hbm', 'kernel': 'lddl::tok5::scan_kernel', 'achieved': achieved, 'peak': HBM_PEAK_GBS,
                    'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS, 'traffic': None,
                    'algorithmic_bytes_per_launch': alg, 'avg_launch_ms': ks['scan_ms'] / nl,
