@@ -33,6 +33,7 @@ Where the reference cannot finish, this raises instead:
 import argparse
 import json
 import os
+import re
 import time
 
 import numpy as np
@@ -322,16 +323,79 @@ def rank_world():
   return 0, 1
 
 
-def _barrier(world):
-  """host barrier between the ranks (gloo; initialised from the launcher's
-  env, MASTER_ADDR / MASTER_PORT)"""
+_JOB_ENV = ('SLURM_JOB_ID', 'PMIX_NAMESPACE', 'OMPI_MCA_ess_base_jobid', 'OMPI_MCA_orte_ess_jobid', 'PMI_JOBID')
+
+
+def barrier_kind(world):
+  """How the ranks of this launch meet (checked BEFORE any shard is written):
+  'dist' (torch.distributed already up, or MASTER_ADDR / MASTER_PORT set, as
+  torch.distributed.run sets them), 'mpi4py' (importable under mpirun / srun),
+  'file' (a shared-file barrier in the output directory keyed by the
+  launcher's job id), or a ValueError: without any of them the reference's
+  MPI barrier (load_balance.py:442) has no counterpart here."""
   if world <= 1:
+    return 'none'
+  try:
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized():
+      return 'dist'
+  except ImportError:
+    pass
+  if os.environ.get('MASTER_ADDR') and os.environ.get('MASTER_PORT'):
+    return 'dist'
+  try:
+    import mpi4py  # noqa: F401
+    return 'mpi4py'
+  except ImportError:
+    pass
+  if job_id():
+    return 'file'
+  raise ValueError('%d ranks but no way to meet: set MASTER_ADDR / MASTER_PORT (torch.distributed.run), make mpi4py '
+                   'importable, or launch under mpirun / srun (a job id in %s)' % (world, '/'.join(_JOB_ENV)))
+
+
+def job_id():
+  for k in _JOB_ENV:
+    v = os.environ.get(k)
+    if v:
+      return '%s-%s' % (v, os.environ.get('SLURM_STEP_ID', ''))
+  return None
+
+
+def _file_barrier(outdir, rank, world, timeout=24 * 3600.0, poll=0.05):
+  """Every rank drops a marker file named by the job id; rank 0 waits for all
+  of them and removes them.  Only rank 0 acts after the barrier (it removes
+  the inputs and writes .num_samples.json), so the other ranks need not wait."""
+  tag = re.sub(r'[^A-Za-z0-9_.-]', '_', job_id() or 'nojob')
+  mk = lambda r: os.path.join(outdir, '.lddl_barrier.%s.%d' % (tag, r))
+  with open(mk(rank), 'w') as f:
+    f.write('done\n')
+  if rank != 0:
     return
-  import torch.distributed as dist
-  if not dist.is_initialized():
-    rank, world = rank_world()
-    dist.init_process_group('gloo', rank=rank, world_size=world)
-  dist.barrier()
+  t0 = time.time()
+  while not all(os.path.exists(mk(r)) for r in range(world)):
+    if time.time() - t0 > timeout:
+      raise RuntimeError('file barrier: ranks missing after %.0f s' % timeout)
+    time.sleep(poll)
+  for r in range(world):
+    os.remove(mk(r))
+
+
+def _barrier(world, kind='dist', outdir=None, rank=0):
+  """host barrier between the ranks (barrier_kind)"""
+  if world <= 1 or kind == 'none':
+    return
+  if kind == 'mpi4py':
+    from mpi4py import MPI
+    MPI.COMM_WORLD.Barrier()
+  elif kind == 'file':
+    _file_barrier(outdir, rank, world)
+  else:
+    import torch.distributed as dist
+    if not dist.is_initialized():
+      r, w = rank_world()
+      dist.init_process_group('gloo', rank=r, world_size=w)
+    dist.barrier()
 
 
 def main(args, rank=None, world=None):
@@ -343,13 +407,14 @@ def main(args, rank=None, world=None):
   if rank is None or world is None:
     rank, world = rank_world()
   outdir = args.indir if args.outdir is None else os.path.abspath(os.path.expanduser(args.outdir))
+  kind = barrier_kind(world)  # fail before writing when the ranks cannot meet
   os.makedirs(outdir, exist_ok=True)
   paths = sorted(os.path.join(r, f) for r, _, fs in os.walk(args.indir) for f in fs
                  if '.parquet' in os.path.splitext(f)[1])
   counts = [pq.ParquetFile(p).metadata.num_rows for p in paths]
   shards, ns = plan_files(paths, counts, args.num_shards, args.bin_ids)
   written = write_shards(shards, outdir, rank, world)
-  _barrier(world)
+  _barrier(world, kind, outdir, rank)
   if rank == 0:
     if not args.keep_orig:
       keep = set(os.path.abspath(p) for p in written) | {os.path.abspath(os.path.join(outdir, n)) for n, _, _ in shards}

@@ -73,6 +73,7 @@ struct lddl_ctx {
   // reused by a masked lddl_pack_bert over the same id / count buffers
   const void* spec_ids = nullptr;
   const void* spec_ntok = nullptr;
+  const void* spec_soff = nullptr;
   int64_t spec_nsent = -1;
   bool spec_flags = false;  // lddl_set_special_flags
   // pack workspace (grown on demand)
@@ -433,6 +434,7 @@ extern "C" int lddl_tokenize(lddl_ctx* c, const uint8_t* d_bytes, int64_t nbytes
     if ((rc = ws_get(c, 41, n_sent, &P.sent_spec))) return rc;
     c->spec_ids = d_out_ids;
     c->spec_ntok = d_out_ntok;
+    c->spec_soff = d_sent_off;
     c->spec_nsent = n_sent;
   }
   P.top = c->d_top;
@@ -643,7 +645,11 @@ static int pack_common(lddl_ctx* c, int codebert, const int32_t* d_ntok, const i
     P.ids = d_ids;
     uint8_t *sent_spec, *fs_spec;
     // the flags of the last lddl_tokenize into these buffers, else a pass over the ids
-    const bool spec_ok = c->spec_ids == d_ids && c->spec_ntok == d_ntok && c->spec_nsent == n_sent;
+    // (one pack consumes them: a later pack over recycled buffers at the same
+    // addresses recomputes the flags from the ids)
+    const bool spec_ok = c->spec_ids == d_ids && c->spec_ntok == d_ntok && c->spec_soff == d_sent_off &&
+                         c->spec_nsent == n_sent;
+    c->spec_ids = nullptr;
     if ((rc = ws_get(c, spec_ok ? 41 : 22, n_sent, &sent_spec)) || (rc = ws_get(c, 23, n_sent, &fs_spec)) ||
         (rc = ws_get(c, 24, npair_cap, &P.mref)) || (rc = ws_get(c, 25, npair_cap, &P.mloc)) ||
         (rc = ws_get(c, 26, n_part, &P.part_nmask)) || (rc = ws_get(c, 27, n_part + 1, &mask_base)) ||

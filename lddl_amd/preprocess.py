@@ -210,6 +210,15 @@ def partition_docs(corpus, block_size=None, num_blocks=None):
 
 
 # ------------------------------------------------------------------ CLI --
+def attach_bool_arg(parser, flag_name, default=False, help_str=None):
+  """--{flag} / --no-{flag} on one dest (lddl/utils.py:81-95)"""
+  attr = flag_name.replace('-', '_')
+  h = flag_name.replace('-', ' ') if help_str is None else help_str
+  parser.add_argument('--{}'.format(flag_name), dest=attr, action='store_true', help=h)
+  parser.add_argument('--no-{}'.format(flag_name), dest=attr, action='store_false', help=h)
+  parser.set_defaults(**{attr: default})
+
+
 def attach_args(parser=None, codebert=False):
   """The reference's flags (pretrain.py:618-880; pretrain_codebert.py's
   --code variant).  --schedule / --local-* are accepted for compatibility;
@@ -227,7 +236,9 @@ def attach_args(parser=None, codebert=False):
     p.add_argument('--common-crawl', type=str, default=None)
     p.add_argument('--wikipedia-lang', type=str, default='en')
   p.add_argument('--sink', type=str, required=True)
-  p.add_argument('--output-format', type=str, default='parquet', choices=['parquet'])
+  p.add_argument('--output-format', type=str, default='parquet', choices=['parquet', 'txt'],
+                 help='parquet (default) or txt, the reference\'s debugging text sink (pretrain.py:501-531): '
+                      '{i}.txt / {i}_{b}.txt per partition (and bin)')
   p.add_argument('--target-seq-length', type=int, default=128)
   p.add_argument('--short-seq-prob', type=float, default=0.1)
   p.add_argument('--block-size', type=lambda x: parse_str_of_num_bytes(x, return_str=False), default=None,
@@ -240,7 +251,7 @@ def attach_args(parser=None, codebert=False):
   p.add_argument('--vocab-file', type=str,
                  default=None, help='vocab.txt path (a local file: there is no hub access); default: the '
                  'bundled bert-base-uncased (BERT) or codebert_52000 (CodeBERT) vocab')
-  p.add_argument('--masking', action='store_true')
+  attach_bool_arg(p, 'masking', default=False, help_str='static masking (pretrain.py:859-866)')
   p.add_argument('--masked-lm-ratio', type=float, default=0.15)
   p.add_argument('--sentence-splitter', type=str, default='auto', choices=['auto', 'punkt', 'rules'])
   p.add_argument('--chunk-mb', type=float, default=64.0,
@@ -256,6 +267,8 @@ def attach_args(parser=None, codebert=False):
 
 
 def _check(args):
+  if args.output_format == 'txt' and getattr(args, 'num_shards', None):
+    raise ValueError('--num-shards balances parquet shards; it does not apply to --output-format txt')
   if args.bin_size is not None:
     if args.bin_size > args.target_seq_length:
       raise ValueError('Please provide a bin size that is <= target-seq-length')
@@ -412,8 +425,9 @@ def main(args, codebert=False):
       torch.cuda.synchronize()
       t['gpu_s'] += time.perf_counter() - t0
       t0 = time.perf_counter()
-      out += writer.write_shards(pk, res, sink, bin_size=args.bin_size, codebert=codebert,
-                                 masking=args.masking and not codebert, doc_ids=ids, part_base=a)
+      wr = writer.write_txt if args.output_format == 'txt' else writer.write_shards
+      out += wr(pk, res, sink, bin_size=args.bin_size, codebert=codebert, masking=args.masking and not codebert,
+                doc_ids=ids, part_base=a)
       t['write_s'] += time.perf_counter() - t0
       t['pairs'] += res.n_pairs
   finally:

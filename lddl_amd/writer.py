@@ -69,11 +69,12 @@ def render(packer, tokens, row_off, row0, n_rows, segment, len0=None, len1=None,
   return off.cpu().numpy(), data[:nb.value].cpu().numpy()
 
 
-def row_docs(packer, n_rows, stream=None):
-  """document index of every row of the last pack call (lddl_row_docs)"""
+def row_docs(packer, n_rows, n_copy=None, stream=None):
+  """document index of every row of the last pack call (lddl_row_docs, all
+  n_rows rows on the device); the first n_copy of them copied to the host"""
   out = torch.empty(max(n_rows, 1), dtype=torch.int64, device=packer.device)
   _lib.check(_lib.lib().lddl_row_docs(packer.tok.handle, _ptr(out), _stream(stream)))
-  return out[:n_rows].cpu().numpy()
+  return out[:n_rows if n_copy is None else min(n_copy, n_rows)].cpu().numpy()
 
 
 def _npy_header(k):
@@ -143,7 +144,7 @@ def write_shards(packer, res, out_dir, bin_size=None, codebert=False, masking=Fa
   if codebert:
     if doc_ids is None:
       raise ValueError('CodeBERT shards need doc_ids (the id column)')
-    docs = pa.array(row_docs(packer, res.n_pairs, stream)[:n_rows])
+    docs = pa.array(row_docs(packer, res.n_pairs, n_rows, stream))
     ids_col = pa.array(doc_ids, type=pa.string()).take(docs) if n_rows else pa.array([], pa.string())
   if masking and not codebert:
     moff_all = res.mlm_off[:n_rows + 1].cpu().numpy()
@@ -200,4 +201,81 @@ def write_shards(packer, res, out_dir, bin_size=None, codebert=False, masking=Fa
   for fu in pending:
     fu.result()
   pool.shutdown()
+  return files
+
+
+def write_txt(packer, res, out_dir, bin_size=None, codebert=False, masking=False, doc_ids=None, part_base=0,
+              batch_rows=1 << 20, max_parts=None, stream=None):
+  """The reference's txt sink (--output-format txt, pretrain.py:501-531,
+  pretrain_codebert.py:540-559): one line per row,
+
+    BERT      is_random_next: {b} - [CLS] {A} [SEP] {B} [SEP] - {num_tokens}
+    masking   is_random_next: {b} - [CLS] {A} [SEP] {B} [SEP] - masked_lm_positions: {str(np.array)}
+              - masked_lm_labels: {labels} - {num_tokens}
+    CodeBERT  {id} [CLS] {doc} [SEP] {code} [SEP] - {num_tokens}
+
+  joined by '\\n' with no final newline (dask's to_textfiles).  Files:
+  {p}.txt per partition (to_textfiles' default name), or {p}_{b}.txt for
+  every bin b (binning.py:439-476: the bin parsed back from the line's last
+  field, rows in shuffled order within a bin == this packer's row order).
+  Every file is created, empty ones included.  Returns the files."""
+  os.makedirs(out_dir, exist_ok=True)
+  binned = bin_size is not None
+  nbins = res.nbins if binned else 1
+  n_part = res.bin_count.shape[0]
+  counts = res.bin_count.cpu().numpy().reshape(n_part, res.nbins)
+  if not binned:
+    counts = counts.sum(axis=1, keepdims=True)
+  file_rows = counts.ravel()
+  file_start = np.zeros(len(file_rows) + 1, dtype=np.int64)
+  np.cumsum(file_rows, out=file_start[1:])
+  nfiles = len(file_rows) if max_parts is None else min(len(file_rows), max_parts * nbins)
+  n_rows = int(file_start[nfiles])
+  num_tokens = np.diff(res.tok_off[:n_rows + 1].cpu().numpy())
+  flags = res.flags[:n_rows].cpu().numpy()
+  if codebert:
+    if doc_ids is None:
+      raise ValueError('CodeBERT txt output needs doc_ids (the id field)')
+    docs = row_docs(packer, res.n_pairs, n_rows, stream)
+  if masking and not codebert:
+    moff_all = res.mlm_off[:n_rows + 1].cpu().numpy()
+    mpos_all = res.mlm_pos[:int(moff_all[-1])].cpu().numpy().view(np.uint16)
+  files = []
+  f = 0
+  while f < nfiles:
+    g = f + 1
+    while g < nfiles and file_start[g + 1] - file_start[f] <= batch_rows:
+      g += 1
+    r0, r1 = int(file_start[f]), int(file_start[g])
+    n = r1 - r0
+    kw = dict(len0=res.len0, len1=res.len1, flags=res.flags, codebert=codebert, stream=stream)
+    (o0, d0), (o1, d1) = (render(packer, res.tokens, res.tok_off, r0, n, SEG0, **kw),
+                          render(packer, res.tokens, res.tok_off, r0, n, SEG1, **kw))
+    if masking and not codebert:
+      ol, dl = render(packer, res.mlm_label, res.mlm_off, r0, n, ROW, stream=stream)
+    b0, b1 = d0.tobytes(), d1.tobytes()
+    bl = dl.tobytes() if masking and not codebert else b''
+    for fi in range(f, g):
+      lo, hi = int(file_start[fi] - r0), int(file_start[fi + 1] - r0)
+      p, b = divmod(fi, nbins)
+      lines = []
+      for i in range(lo, hi):
+        r = r0 + i
+        a, bb = b0[o0[i]:o0[i + 1]].decode(), b1[o1[i]:o1[i + 1]].decode()
+        if codebert:
+          lines.append('{} [CLS] {} [SEP] {} [SEP] - {}'.format(doc_ids[docs[r]], a, bb, int(num_tokens[r])))
+        elif masking:
+          pos = np.array(mpos_all[moff_all[r] - moff_all[0]:moff_all[r + 1] - moff_all[0]], dtype=np.uint16)
+          lines.append('is_random_next: {} - [CLS] {} [SEP] {} [SEP] - masked_lm_positions: {} - '
+                       'masked_lm_labels: {} - {}'.format(bool(flags[r] & 1), a, bb, pos,
+                                                          bl[ol[i]:ol[i + 1]].decode(), int(num_tokens[r])))
+        else:
+          lines.append('is_random_next: {} - [CLS] {} [SEP] {} [SEP] - {}'.format(bool(flags[r] & 1), a, bb,
+                                                                                 int(num_tokens[r])))
+      name = ('%d_%d.txt' % (part_base + p, b)) if binned else ('%d.txt' % (part_base + p))
+      path = os.path.join(out_dir, name)
+      with open(path, 'w', encoding='utf-8', newline='') as fh:
+        fh.write('\n'.join(lines))
+      files.append(path)
+    f = g
   return files

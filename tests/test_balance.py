@@ -125,3 +125,66 @@ def test_gather_and_ownership_gloo(tmp_path):
   for name, runs, n in shards:
     t = pq.read_table(os.path.join(d, 'out', name))
     assert t.num_rows == n
+
+
+def _clean_env(**kw):
+  env = {k: v for k, v in os.environ.items()
+         if k not in ('RANK', 'WORLD_SIZE', 'LOCAL_RANK', 'MASTER_ADDR', 'MASTER_PORT') and not k.startswith(
+             ('OMPI_', 'PMI', 'SLURM_'))}
+  env.update(kw)
+  return env
+
+
+def test_cli_under_mpirun_env_only(tmp_path):
+  """under mpirun the ranks have OMPI_COMM_WORLD_RANK / _SIZE and
+  a job id, no MASTER_ADDR: the balancer meets through the shared-file
+  barrier (or mpi4py when importable), rank 0 removes the inputs and writes
+  .num_samples.json once both ranks have written their shards -- the same
+  outputs as one rank"""
+  import subprocess
+  import sys
+  c = next(c for c in CASES if not c['error'])
+  ref_in, ref_out = tmp_path / 'ref_in', tmp_path / 'ref_out'
+  ref_in.mkdir()
+  _write_inputs(str(ref_in), c)
+  balance.main(balance.attach_args().parse_args(['--indir', str(ref_in), '--outdir', str(ref_out), '--num-shards',
+                                                 str(c['num_shards'])]), 0, 1)
+  ind, outd = tmp_path / 'in', tmp_path / 'out'
+  ind.mkdir()
+  _write_inputs(str(ind), c)
+  root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+  cmd = [sys.executable, '-m', 'lddl_amd.balance', '--indir', str(ind), '--outdir', str(outd), '--num-shards',
+         str(c['num_shards'])]
+  procs = [subprocess.Popen(cmd, cwd=root, env=_clean_env(OMPI_COMM_WORLD_RANK=str(r), OMPI_COMM_WORLD_SIZE='2',
+                                                          OMPI_MCA_ess_base_jobid='4242'),
+                            stdout=subprocess.PIPE, stderr=subprocess.PIPE) for r in range(2)]
+  outs = [p.communicate(timeout=240) for p in procs]
+  assert [p.returncode for p in procs] == [0, 0], outs
+  want = sorted(n for n in os.listdir(str(ref_out)))
+  assert sorted(os.listdir(str(outd))) == want  # no barrier markers left, inputs gone, .num_samples.json
+  for n in want:
+    if n.startswith('shard-'):
+      assert _runs_of(str(outd / n)) == _runs_of(str(ref_out / n))
+  with open(str(outd / '.num_samples.json')) as f, open(str(ref_out / '.num_samples.json')) as g:
+    assert json.load(f) == json.load(g)
+  assert not [n for n in os.listdir(str(ind)) if n.startswith('part.')]
+
+
+def test_ranks_without_a_meeting_point_fail_before_writing(tmp_path):
+  import subprocess
+  import sys
+  c = next(c for c in CASES if not c['error'])
+  ind, outd = tmp_path / 'in', tmp_path / 'out'
+  ind.mkdir()
+  _write_inputs(str(ind), c)
+  root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+  p = subprocess.run([sys.executable, '-m', 'lddl_amd.balance', '--indir', str(ind), '--outdir', str(outd),
+                      '--num-shards', str(c['num_shards'])], cwd=root, capture_output=True, text=True, timeout=120,
+                     env=_clean_env(OMPI_COMM_WORLD_RANK='1', OMPI_COMM_WORLD_SIZE='2'))
+  try:
+    import mpi4py  # noqa: F401
+    pytest.skip('mpi4py importable: the ranks meet through it')
+  except ImportError:
+    pass
+  assert p.returncode != 0 and 'no way to meet' in p.stderr
+  assert not outd.exists() or not os.listdir(str(outd))

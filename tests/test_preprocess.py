@@ -67,6 +67,27 @@ def test_flag_defaults_match_reference():
               'mpi', 128, 0.1, 0.9, 12345, 5, 0.15, None, None, None, 'en', 'parquet')
   c = preprocess.attach_args(codebert=True).parse_args(['--sink', 'x', '--code', 'y'])
   assert c.duplicate_factor == 1
+  assert a.masking is False
+
+
+def test_reference_full_flag_set_parses():
+  """every flag of the reference's attach_args (pretrain.py:618-880), incl.
+  attach_bool_arg's --masking / --no-masking pair (lddl/utils.py:81-95) and
+  --output-format txt"""
+  argv = ['--schedule', 'local', '--local-n-workers', '4', '--local-threads-per-worker', '1', '--wikipedia', 'w',
+          '--books', 'b', '--common-crawl', 'c', '--sink', 's', '--output-format', 'txt', '--wikipedia-lang', 'en',
+          '--target-seq-length', '512', '--short-seq-prob', '0.2', '--block-size', '64M', '--bin-size', '64',
+          '--sample-ratio', '0.5', '--seed', '7', '--duplicate-factor', '3', '--vocab-file', 'v.txt', '--masking',
+          '--masked-lm-ratio', '0.2']
+  a = preprocess.attach_args().parse_args(argv)
+  assert (a.output_format, a.masking, a.block_size, a.bin_size, a.masked_lm_ratio) == ('txt', True, 64 << 20, 64, 0.2)
+  assert preprocess.attach_args().parse_args(argv + ['--no-masking']).masking is False
+  assert preprocess.attach_args().parse_args(['--sink', 's', '--no-masking', '--masking']).masking is True
+  a = preprocess.attach_args().parse_args(['--sink', 's', '--num-blocks', '4096'])
+  assert a.num_blocks == 4096
+  with pytest.raises(ValueError):
+    preprocess._check(preprocess.attach_args().parse_args(['--sink', 's', '--output-format', 'txt',
+                                                             '--num-shards', '4']))
 
 
 def test_partition_docs():

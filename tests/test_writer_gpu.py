@@ -307,3 +307,71 @@ def test_cli_num_shards_all_gather_over_ranks(gpu, tmp_path):
   c3 = _read_dir(str(bal))
   for n in a:
     assert c3[n] == a[n], n
+
+
+def _txt_lines(path):
+  with open(path, encoding='utf-8', newline='') as f:
+    s = f.read()
+  return s.split('\n') if s else []
+
+
+@pytest.mark.parametrize('k', [0, 12, 24, 30])
+@pytest.mark.parametrize('binned', [False, True])
+def test_bert_txt_same_pairs_as_parquet(packer, tmp_path, k, binned):
+  """--output-format txt (pretrain.py:501-531): the same rows as the parquet
+  sink, in the reference's line format; {p}.txt / {p}_{b}.txt names
+  (to_textfiles, binning.py:439-476), every file created, '\\n'-joined"""
+  from lddl_amd import writer
+  case = BERT['cases'][k]
+  c = case['cfg']
+  if case['error']:
+    pytest.skip('reference raises for this case')
+  masking = c['masking']
+  sh, ids, ntok = shards_from_docs(case['docs'])
+  bin_size = case['bin_size'] if binned else None
+  res = packer.pack(sh, ids, ntok, target_seq_length=c['max_seq'], short_seq_prob=c['ssp'],
+                    duplicate_factor=c['dup'], seed=case['seed'], bin_size=bin_size, masking=masking)
+  pq_files = writer.write_shards(packer, res, str(tmp_path / 'pq'), bin_size=bin_size, masking=masking, part_base=3)
+  txt_files = writer.write_txt(packer, res, str(tmp_path / 'txt'), bin_size=bin_size, masking=masking, part_base=3,
+                               batch_rows=61)
+  nb = case['nbins'] if binned else 1
+  assert [os.path.basename(f) for f in txt_files] == (['3_%d.txt' % b for b in range(nb)] if binned else ['3.txt'])
+  for pf, tf in zip(pq_files, txt_files):
+    rows = _read(pf)
+    want = []
+    for i in range(len(rows['A'])):
+      if masking:
+        pos = np.load(__import__('io').BytesIO(rows['masked_lm_positions'][i]))
+        want.append('is_random_next: {} - [CLS] {} [SEP] {} [SEP] - masked_lm_positions: {} - masked_lm_labels: {} - {}'
+                    .format(rows['is_random_next'][i], rows['A'][i], rows['B'][i], pos, rows['masked_lm_labels'][i],
+                            rows['num_tokens'][i]))
+      else:
+        want.append('is_random_next: {} - [CLS] {} [SEP] {} [SEP] - {}'.format(
+            rows['is_random_next'][i], rows['A'][i], rows['B'][i], rows['num_tokens'][i]))
+    # (a masked_lm_positions array wider than numpy's 75-column line holds
+    # newlines, as the reference's str(np.ndarray) does: compare whole files)
+    with open(tf, encoding='utf-8', newline='') as f:
+      assert f.read() == '\n'.join(want)
+    if binned:  # binning.py:465-467: the bin is parsed back from each row's last field (num_tokens)
+      for w in want:
+        assert po.bin_of(int(w.split()[-1]), case['bin_size'], nb) == int(os.path.basename(tf)[:-4].split('_')[1])
+
+
+def test_cli_codebert_txt(gpu, tmp_path):
+  """--output-format txt for CodeBERT (pretrain_codebert.py:540-559): the
+  parquet run's rows as '{id} [CLS] {doc} [SEP] {code} [SEP] - {n}'"""
+  from lddl_amd import synth, preprocess
+  lines = synth.make_code_lines(120, seed=4)
+  (tmp_path / 'code').mkdir()
+  (tmp_path / 'code' / 'a.txt').write_bytes('\r\n'.join(lines).encode('utf-8'))
+  common = ['--code', str(tmp_path / 'code'), '--target-seq-length', '128', '--seed', '8', '--sample-ratio', '1.0',
+            '--split-workers', '0']
+  preprocess.main(preprocess.attach_args(codebert=True).parse_args(common + ['--sink', str(tmp_path / 'pq')]),
+                  codebert=True)
+  files, _ = preprocess.main(preprocess.attach_args(codebert=True).parse_args(
+      common + ['--sink', str(tmp_path / 'txt'), '--output-format', 'txt']), codebert=True)
+  assert [os.path.basename(f) for f in files] == ['0.txt']
+  rows = _read(str(tmp_path / 'pq' / 'part.0.parquet'))
+  want = ['{} [CLS] {} [SEP] {} [SEP] - {}'.format(i, d, c, n) for i, d, c, n in
+          zip(rows['id'], rows['doc'], rows['code'], rows['num_tokens'])]
+  assert want and _txt_lines(files[0]) == want
