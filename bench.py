@@ -413,9 +413,9 @@ def main():
     s = torch.cuda.current_stream()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(s)
-    ids, ntok = pk.tokenize(sh)
+    ids, ntok, toff = pk.tokenize(sh)
     e1.record(s)
-    res = pk.pack(sh, ids, ntok, **kw)
+    res = pk.pack(sh, ids, ntok, toff, **kw)
     if dist is not None:
       # per-(partition, bin) row counts of every rank: the load balancer's
       # input (lddl_amd/balance.py), one RCCL all-gather per step

@@ -60,20 +60,28 @@ int lddl_special_ids(const lddl_ctx *ctx, int32_t out[5]);
 /* NUL-terminated vocab entry `id` into buf; returns its length */
 int lddl_vocab_token(const lddl_ctx *ctx, int32_t id, char *buf, int64_t cap);
 
-/* Tokenise n_sent sentences (bytes [d_sent_off[s], d_sent_off[s+1])).
- * Sentence s's ids go to d_out_ids[d_sent_off[s] - d_sent_off[0] + k],
- * k < d_out_ntok[s] = min(#tokens, max_tok).  nbytes must be >=
- * d_sent_off[n_sent] - d_sent_off[0]; d_out_ids needs nbytes entries
- * (#tokens <= #bytes).  d_bytes: 4-byte aligned. */
+/* Tokenise n_sent sentences (bytes [d_sent_off[s], d_sent_off[s+1])) into
+ * the dense CSR layout: sentence s's ids are
+ * d_out_ids[d_out_tok_off[s] .. d_out_tok_off[s+1]), d_out_ntok[s] = their
+ * count = min(#tokens, max_tok), d_out_tok_off[n_sent] = the total
+ * (d_out_tok_off: n_sent + 1 entries).  out_cap = entries of d_out_ids: ids
+ * past it are not written, the offsets are still complete, so a caller that
+ * finds d_out_tok_off[n_sent] > out_cap calls again with a larger buffer;
+ * out_cap >= nbytes always suffices (#tokens <= #bytes).  nbytes must be >=
+ * d_sent_off[n_sent] - d_sent_off[0]; 1 <= max_tok <= 65534.  d_bytes:
+ * 4-byte aligned.  lddl_pack_* / lddl_materialize read d_out_ids with 16-B
+ * loads: keep it 16-B aligned with 16 entries of padding past the total. */
 int lddl_tokenize(lddl_ctx *ctx, const uint8_t *d_bytes, int64_t nbytes, const int64_t *d_sent_off,
-                  int64_t n_sent, int32_t max_tok, uint16_t *d_out_ids, int32_t *d_out_ntok, void *stream);
+                  int64_t n_sent, int32_t max_tok, uint16_t *d_out_ids, int64_t out_cap, int32_t *d_out_ntok,
+                  int64_t *d_out_tok_off, void *stream);
 
 /* Per-kernel timing of lddl_tokenize (diagnostics / bench): with timing on,
  * every call records HIP events around its kernels on the call's stream;
- * lddl_tokenize_stats (synchronises on them) returns out[0..4] = scan,
- * WordPiece and expand milliseconds of the last call (summed over its
- * segments), the number of WordPiece records it ran and the number of
- * segments (launches of each kernel). */
+ * lddl_tokenize_stats (synchronises on them) returns out[0..5] = scan,
+ * WordPiece and finish (serial-path tiles + counts + offset scan + dense
+ * expand) milliseconds of the last call (summed over its segments), the
+ * number of WordPiece records it ran, the number of segments (launches of
+ * each kernel) and the number of tiles sent to the serial path. */
 int lddl_set_timing(lddl_ctx *ctx, int on);
 int lddl_tokenize_stats(lddl_ctx *ctx, double *out, int n);
 
@@ -87,8 +95,8 @@ int lddl_set_special_flags(lddl_ctx *ctx, int on);
 /* Pack every partition of a tokenised shard set.
  * Partition p = docs [d_part_doc_off[p], d_part_doc_off[p+1]); doc d =
  * sentences [d_doc_sent_off[d], d_doc_sent_off[d+1]); d_ids / d_ntok /
- * d_sent_off are lddl_tokenize's output / input (d_ids may be NULL unless
- * masking).  Partition p is packed exactly like the reference's
+ * d_tok_off / d_sent_off are lddl_tokenize's output / input (d_ids may be
+ * NULL unless masking; all of them must stay live until lddl_materialize).  Partition p is packed exactly like the reference's
  * _to_partition_pairs (pretrain.py:386-402) after random.seed(seed + p):
  * duplicate_factor passes of create_pairs_from_document (:241-365), then
  * random.shuffle, then (bin_size > 0) the stable bin grouping of
@@ -98,22 +106,24 @@ int lddl_set_special_flags(lddl_ctx *ctx, int on);
  * (:182-238) with vocab_words = the vocab file's tokens in file order
  * (target_seq_length <= 1024); the rows are then written by
  * lddl_materialize and masked by lddl_masked_lm. */
-int lddl_pack_bert(lddl_ctx *ctx, const uint16_t *d_ids, const int32_t *d_ntok, const int64_t *d_sent_off,
-                   int64_t n_sent, const int64_t *d_doc_sent_off, int64_t n_doc, const int64_t *d_part_doc_off,
-                   int64_t n_part, int32_t target_seq_length, double short_seq_prob, int32_t duplicate_factor,
-                   int32_t masking, double masked_lm_ratio, uint64_t seed, int32_t bin_size, int64_t *out_totals,
+int lddl_pack_bert(lddl_ctx *ctx, const uint16_t *d_ids, const int32_t *d_ntok, const int64_t *d_tok_off,
+                   const int64_t *d_sent_off, int64_t n_sent, const int64_t *d_doc_sent_off, int64_t n_doc,
+                   const int64_t *d_part_doc_off, int64_t n_part, int32_t target_seq_length, double short_seq_prob,
+                   int32_t duplicate_factor, int32_t masking, double masked_lm_ratio, uint64_t seed, int32_t bin_size,
+                   int64_t *out_totals,
                    void *stream);
 
 /* CodeBERT docstring/code packing (pretrain_codebert.py:343-442, :460-477).
  * Doc d's first d_doc_nseg_doc[d] sentences are its docstring segments, the
  * rest its code segments (one per source line, pretrain_codebert.py:126-159). */
-int lddl_pack_codebert(lddl_ctx *ctx, const int32_t *d_ntok, const int64_t *d_sent_off, int64_t n_sent,
-                       const int64_t *d_doc_sent_off, const int32_t *d_doc_nseg_doc, int64_t n_doc,
+int lddl_pack_codebert(lddl_ctx *ctx, const int32_t *d_ntok, const int64_t *d_tok_off, const int64_t *d_sent_off,
+                       int64_t n_sent, const int64_t *d_doc_sent_off, const int32_t *d_doc_nseg_doc, int64_t n_doc,
                        const int64_t *d_part_doc_off, int64_t n_part, int32_t target_seq_length,
                        double short_seq_prob, int32_t duplicate_factor, uint64_t seed, int32_t bin_size,
                        int64_t *out_totals, void *stream);
 
-/* Write the rows of the last pack call in output order (partition-major,
+/* d_ids: the dense ids lddl_tokenize wrote (and the pack call read).
+ * Write the rows of the last pack call in output order (partition-major,
  * bin-major, shuffled order within a bin = the reference's part.{p}.parquet_{b}
  * row order).  Row g: d_out_tokens[d_out_tok_off[g] .. d_out_tok_off[g+1]) =
  * [CLS] A [SEP] B [SEP] (CodeBERT: [CLS] doc [SEP] code [SEP], or

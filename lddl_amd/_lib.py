@@ -24,15 +24,16 @@ SIGNATURES = {
     'lddl_vocab_size': (c_int, [c_void_p]),
     'lddl_special_ids': (c_int, [c_void_p, ctypes.POINTER(c_int32)]),
     'lddl_vocab_token': (c_int, [c_void_p, c_int32, c_char_p, c_int64]),
-    'lddl_tokenize': (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_int32, c_void_p, c_void_p,
-                              c_void_p]),
+    'lddl_tokenize': (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_int32, c_void_p, c_int64,
+                              c_void_p, c_void_p, c_void_p]),
     'lddl_set_timing': (c_int, [c_void_p, c_int]),
     'lddl_set_special_flags': (c_int, [c_void_p, c_int]),
     'lddl_tokenize_stats': (c_int, [c_void_p, ctypes.POINTER(c_double), c_int]),
-    'lddl_pack_bert': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p,
-                               c_int64, c_int32, c_double, c_int32, c_int32, c_double, c_uint64, c_int32,
+    'lddl_pack_bert': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_int64,
+                               c_void_p, c_int64, c_int32, c_double, c_int32, c_int32, c_double, c_uint64, c_int32,
                                ctypes.POINTER(c_int64), c_void_p]),
-    'lddl_pack_codebert': (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_void_p,
+    'lddl_pack_codebert': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int64,
+                                   c_void_p,
                                    c_int64, c_int32, c_double, c_int32, c_uint64, c_int32,
                                    ctypes.POINTER(c_int64), c_void_p]),
     'lddl_materialize': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

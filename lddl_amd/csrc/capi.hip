@@ -50,6 +50,7 @@ struct lddl_ctx {
   uint16_t* d_top = nullptr;
   uint32_t* d_pages = nullptr;
   uint32_t* d_bmp = nullptr;  // flat entries of the Basic Multilingual Plane (top/pages resolved)
+  uint32_t* d_xmap = nullptr;  // fast exception entries, one per code point (tokenize_split.hip XM_*)
   uint4* d_multi = nullptr;
   uint4* d_slots = nullptr;
   uint32_t* d_bloom = nullptr;
@@ -126,6 +127,7 @@ static void free_ctx(lddl_ctx* c) {
   (void)hipFree(c->d_top);
   (void)hipFree(c->d_pages);
   (void)hipFree(c->d_bmp);
+  (void)hipFree(c->d_xmap);
   (void)hipFree(c->d_multi);
   (void)hipFree(c->d_slots);
   (void)hipFree(c->d_bloom);
@@ -209,6 +211,37 @@ static int load_table(lddl_ctx* c, const char* path) {
   std::vector<uint32_t> bmp(0x10000);
   for (uint32_t cp = 0; cp < 0x10000; ++cp) bmp[cp] = pages[(size_t)top[cp >> 8] * 256 + (cp & 255)];
   if ((rc = upload(&c->d_bmp, bmp.data(), bmp.size() * 4))) return rc;
+  // the scan's fast exception entries (4.25 MiB, U+0000..U+10FFFF): what the
+  // full path would do with a code point, precomputed -- its pre-tokenizer
+  // action and, for a single-char mapping, the replacement's UTF-8 bytes;
+  // SLOW where the full path is needed (multi-char expansion, canonical
+  // reordering rank, a 4-byte replacement)
+  std::vector<uint32_t> xmap(0x110000);
+  for (uint32_t cp = 0; cp < 0x110000; ++cp) {
+    const uint32_t e = pages[(size_t)top[cp >> 8] * 256 + (cp & 255)];
+    const uint32_t kind = ent_kind(e), cls = ent_cls(e), pay = ent_payload(e);
+    uint32_t x = 0;
+    if (ent_rank(e) != 0) {
+      x = 0x80000000u;
+    } else if (kind == KIND_DROP_T || kind == KIND_DROP_D) {
+      x = 3u << 27;
+    } else if (cls == CLS_SPACE) {
+      x = 1u << 27;
+    } else {
+      x = (cls == CLS_ISOLATE ? 2u : 0u) << 27;
+      if (kind == KIND_MULTI || (kind != KIND_IDENT && pay >= 0x10000)) {
+        x = 0x80000000u;
+      } else if (kind != KIND_IDENT) {
+        uint32_t b = 0, t;
+        if (pay < 0x80) { b = pay; t = 1; }
+        else if (pay < 0x800) { b = (0xC0 | (pay >> 6)) | ((0x80 | (pay & 0x3F)) << 8); t = 2; }
+        else { b = (0xE0 | (pay >> 12)) | ((0x80 | ((pay >> 6) & 0x3F)) << 8) | ((0x80 | (pay & 0x3F)) << 16); t = 3; }
+        x |= 0x20000000u | (t << 24) | b;
+      }
+    }
+    xmap[cp] = x;
+  }
+  if ((rc = upload(&c->d_xmap, xmap.data(), xmap.size() * 4))) return rc;
   return 0;
 }
 
@@ -413,14 +446,21 @@ extern "C" int lddl_vocab_token(const lddl_ctx* c, int32_t id, char* buf, int64_
 }
 
 extern "C" int lddl_tokenize(lddl_ctx* c, const uint8_t* d_bytes, int64_t nbytes, const int64_t* d_sent_off,
-                             int64_t n_sent, int32_t max_tok, uint16_t* d_out_ids, int32_t* d_out_ntok, void* stream) {
+                             int64_t n_sent, int32_t max_tok, uint16_t* d_out_ids, int64_t out_cap,
+                             int32_t* d_out_ntok, int64_t* d_out_tok_off, void* stream) {
   if (!c) return set_err(LDDL_EINVAL, "null ctx");
-  if (n_sent < 0 || max_tok < 1 || nbytes < 0)
-    return set_err(LDDL_EINVAL, "n_sent %lld nbytes %lld max_tok %d", (long long)n_sent, (long long)nbytes, max_tok);
-  if (n_sent == 0) return 0;
-  if (!d_bytes || !d_sent_off || !d_out_ids || !d_out_ntok) return set_err(LDDL_EINVAL, "null device pointer");
+  if (n_sent < 0 || max_tok < 1 || max_tok > 65534 || nbytes < 0 || out_cap < 0)
+    return set_err(LDDL_EINVAL, "n_sent %lld nbytes %lld max_tok %d out_cap %lld", (long long)n_sent,
+                   (long long)nbytes, max_tok, (long long)out_cap);
+  if (!d_out_tok_off) return set_err(LDDL_EINVAL, "null device pointer");
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t st = (hipStream_t)stream;
+  if (n_sent == 0) {
+    HIP_TRY(hipMemsetAsync(d_out_tok_off, 0, sizeof(int64_t), st));
+    return 0;
+  }
+  if (!d_bytes || !d_sent_off || (!d_out_ids && out_cap > 0) || !d_out_ntok)
+    return set_err(LDDL_EINVAL, "null device pointer");
   TokParams P{};
   P.bytes = d_bytes;
   P.sent_off = d_sent_off;
@@ -428,6 +468,8 @@ extern "C" int lddl_tokenize(lddl_ctx* c, const uint8_t* d_bytes, int64_t nbytes
   P.max_tok = max_tok;
   P.out_ids = d_out_ids;
   P.out_ntok = d_out_ntok;
+  P.out_tok_off = d_out_tok_off;
+  P.out_cap = out_cap;
   c->spec_ids = nullptr;
   if (c->spec_flags) {
     int rc;
@@ -440,6 +482,7 @@ extern "C" int lddl_tokenize(lddl_ctx* c, const uint8_t* d_bytes, int64_t nbytes
   P.top = c->d_top;
   P.pages = c->d_pages;
   P.bmp = c->d_bmp;
+  P.xmap = c->d_xmap;
   P.multi = c->d_multi;
   P.slots = c->d_slots;
   P.slot_mask = c->slot_mask;
@@ -463,59 +506,55 @@ extern "C" int lddl_tokenize(lddl_ctx* c, const uint8_t* d_bytes, int64_t nbytes
     HIP_TRY(hipMemsetAsync(d_dbg, 0, 32 * 8, st));
     P.dbg = d_dbg;
   }
-  if (c->tok_algo == 5) {
-    const int64_t nt = tile_count(nbytes);
-    // LDDL_SPLIT_SEG (tiles per segment) / LDDL_SPLIT_CHUNKS (record chunks):
-    // tests force segment seams and record-capacity fallbacks at small sizes
-    const char* eseg = getenv("LDDL_SPLIT_SEG");
-    const char* ech = getenv("LDDL_SPLIT_CHUNKS");
-    const int64_t seg_max = eseg && atoll(eseg) > 0 ? atoll(eseg) : SPLIT_SEG_TILES;
-    const int64_t seg = nt < seg_max ? nt : seg_max;
-    int64_t n_chunks = split_seg_slots(seg) / SPLIT_CHUNK;
-    if (ech && atoll(ech) > 0) n_chunks = atoll(ech);
-    const int64_t slots = n_chunks * SPLIT_CHUNK;
-    int64_t* tile_sent;
-    SplitParams S{};
-    int rc;
-    if ((rc = ws_get(c, 19, nt + 1, &tile_sent)) || (rc = ws_get(c, 20, nt, &S.fb_list)) ||
-        (rc = ws_get(c, 21, 16, &S.fb_count)) || (rc = ws_get(c, 34, (size_t)seg * 1024 + 4096, &S.ent)) ||
-        (rc = ws_get(c, 35, (size_t)slots * 4, &S.rec)) || (rc = ws_get(c, 42, (size_t)slots * 4, &S.pcs)) || (rc = ws_get(c, 36, (size_t)n_chunks + 16, &S.chunk_fill)) ||
-        (rc = ws_get(c, 37, n_sent, &S.smeta)))
-      return rc;
-    S.chunk_ctr = S.chunk_fill + n_chunks;
-    S.n_chunks = (uint32_t)n_chunks;
-    S.seg_tiles = seg;
-    if (c->timing) {
-      S.n_rec = c->d_nrec;
-      HIP_TRY(hipMemsetAsync(c->d_nrec, 0, 8, st));
-    }
-    c->last_tok_bytes = nbytes;
-    c->last_tok_sent = n_sent;
+  const int64_t nt = tile_count(nbytes);
+  // LDDL_SPLIT_SEG (tiles per segment) / LDDL_SPLIT_CHUNKS (record chunks):
+  // tests force segment seams and record-capacity fallbacks at small sizes.
+  // The serial path (tok_algo 0) is one segment of fallback tiles.
+  const char* eseg = getenv("LDDL_SPLIT_SEG");
+  const char* ech = getenv("LDDL_SPLIT_CHUNKS");
+  const int64_t seg_max = c->tok_algo == 0 ? nt : eseg && atoll(eseg) > 0 ? atoll(eseg) : SPLIT_SEG_TILES;
+  const int64_t seg = nt < seg_max ? nt : seg_max;
+  int64_t n_chunks = c->tok_algo == 0 ? 1 : split_seg_slots(seg, c->n_cu) / SPLIT_CHUNK;
+  if (ech && atoll(ech) > 0 && c->tok_algo != 0) n_chunks = atoll(ech);
+  const int64_t slots = n_chunks * SPLIT_CHUNK;
+  int64_t* tile_sent;
+  SplitParams S{};
+  int rc;
+  if ((rc = ws_get(c, 19, nt + 1, &tile_sent)) || (rc = ws_get(c, 20, nt, &S.fb_list)) ||
+      (rc = ws_get(c, 21, 16, &S.fb_count)) || (rc = ws_get(c, 34, (size_t)seg * 1024 + 4096, &S.ent)) ||
+      (rc = ws_get(c, 35, (size_t)slots * 4, &S.rec)) || (rc = ws_get(c, 42, (size_t)slots * 4, &S.pcs)) ||
+      (rc = ws_get(c, 36, (size_t)n_chunks + 16, &S.chunk_fill)) || (rc = ws_get(c, 37, n_sent, &S.smeta)) ||
+      (rc = ws_get(c, 43, n_sent, &S.snslot)) || (rc = ws_get(c, 44, (size_t)slots, &S.cnt8)) ||
+      (rc = ws_get(c, 45, (size_t)scan_blocks(n_sent) + 1, &S.scan_bsum)))
+    return rc;
+  S.chunk_ctr = S.chunk_fill + n_chunks;
+  S.n_chunks = (uint32_t)n_chunks;
+  S.seg_tiles = seg;
+  S.seg_sent_cap = n_sent;
+  S.n_fallback = c->d_counter + 8;
+  if (c->timing) {
+    S.n_rec = c->d_nrec;
+    HIP_TRY(hipMemsetAsync(c->d_nrec, 0, 8, st));
+  }
+  c->last_tok_bytes = nbytes;
+  c->last_tok_sent = n_sent;
+  if (c->tok_algo == 0) {
+    HIP_TRY(launch_tokenize_serial_dense(P, nbytes, tile_sent, S, c->n_cu, c->tok_grid, st));
+  } else {
     HIP_TRY(launch_tokenize_split(P, nbytes, tile_sent, S, c->n_cu, c->tok_grid, c->tok5_cfg, st,
                                   c->timing ? c->tm : nullptr));
-    if (P.dbg) {
-      uint64_t h[18];
-      int32_t nfb = 0;
-      HIP_TRY(hipMemcpyAsync(h, P.dbg, sizeof h, hipMemcpyDeviceToHost, st));
-      HIP_TRY(hipMemcpyAsync(&nfb, S.fb_count, 4, hipMemcpyDeviceToHost, st));
-      HIP_TRY(hipStreamSynchronize(st));
-      const char* nm[12] = {"loop", "setup", "classify", "except", "units", "urec", "prep", "probe", "entries",
-                            "tile_end", "stages", "tiles"};
-      fprintf(stderr, "[lddl tok5 dbg] ntiles=%lld fallback=%d", (long long)nt, nfb);
-      for (int k = 0; k < 12; ++k) fprintf(stderr, " %s=%llu", nm[k], (unsigned long long)h[k]);
-      const char* wn[6] = {"wp_A", "wp_B", "wp_C", "wp_D", "wp_steps", "wp_lane_steps"};
-      for (int k = 0; k < 6; ++k) fprintf(stderr, " %s=%llu", wn[k], (unsigned long long)h[12 + k]);
-      fprintf(stderr, "\n");
-    }
-  } else {
-    const int64_t nt = tile_count(nbytes);
-    int64_t* tile_sent;
-    int32_t *fb_list, *fb_count;
-    int rc;
-    if ((rc = ws_get(c, 19, nt + 1, &tile_sent)) || (rc = ws_get(c, 20, nt, &fb_list)) ||
-        (rc = ws_get(c, 21, 16, &fb_count)))
-      return rc;
-    HIP_TRY(launch_tokenize_serial(P, nbytes, tile_sent, fb_list, fb_count, c->tok_grid, st));
+  }
+  if (P.dbg) {
+    uint64_t h[18];
+    HIP_TRY(hipMemcpyAsync(h, P.dbg, sizeof h, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    const char* nm[12] = {"loop", "setup", "classify", "except", "units", "urec", "prep", "probe", "entries",
+                          "tile_end", "stages", "tiles"};
+    fprintf(stderr, "[lddl tok5 dbg] ntiles=%lld", (long long)nt);
+    for (int k = 0; k < 12; ++k) fprintf(stderr, " %s=%llu", nm[k], (unsigned long long)h[k]);
+    const char* wn[6] = {"wp_A", "wp_B", "wp_C", "wp_D", "wp_steps", "wp_lane_steps"};
+    for (int k = 0; k < 6; ++k) fprintf(stderr, " %s=%llu", wn[k], (unsigned long long)h[12 + k]);
+    fprintf(stderr, "\n");
   }
   return 0;
 }
@@ -541,7 +580,7 @@ extern "C" int lddl_set_timing(lddl_ctx* c, int on) {
 }
 
 extern "C" int lddl_tokenize_stats(lddl_ctx* c, double* out, int n) {
-  if (!c || !out || n < 5) return set_err(LDDL_EINVAL, "need out[5]");
+  if (!c || !out || n < 6) return set_err(LDDL_EINVAL, "need out[6]");
   if (!c->timing || !c->tm) return set_err(LDDL_EINVAL, "timing is off (lddl_set_timing)");
   HIP_TRY(hipSetDevice(c->device));
   for (int k = 0; k < 3; ++k) {
@@ -558,10 +597,14 @@ extern "C" int lddl_tokenize_stats(lddl_ctx* c, double* out, int n) {
   HIP_TRY(hipMemcpy(&nrec, c->d_nrec, 8, hipMemcpyDeviceToHost));
   out[3] = (double)nrec;
   out[4] = (double)c->tm->n[0];
+  uint32_t nfb = 0;
+  HIP_TRY(hipMemcpy(&nfb, c->d_counter + 8, 4, hipMemcpyDeviceToHost));
+  out[5] = (double)nfb;
   return 0;
 }
 
-static int pack_common(lddl_ctx* c, int codebert, const int32_t* d_ntok, const int64_t* d_sent_off, int64_t n_sent,
+static int pack_common(lddl_ctx* c, int codebert, const int32_t* d_ntok, const int64_t* d_tok_off,
+                       const int64_t* d_sent_off, int64_t n_sent,
                        const int64_t* d_doc_sent_off, const int32_t* d_doc_nseg_doc, int64_t n_doc,
                        const int64_t* d_part_doc_off, int64_t n_part, int32_t target_seq_length,
                        double short_seq_prob, int32_t duplicate_factor, uint64_t seed, int32_t bin_size,
@@ -577,7 +620,7 @@ static int pack_common(lddl_ctx* c, int codebert, const int32_t* d_ntok, const i
     if (c->vocab_size > 65535) return set_err(LDDL_EINVAL, "masking: vocab larger than 65535");
   }
   if (n_part < 1 || n_doc < 0 || n_sent < 0) return set_err(LDDL_EINVAL, "bad sizes");
-  if (!d_ntok || !d_sent_off || !d_doc_sent_off || !d_part_doc_off || !out_totals)
+  if (!d_ntok || !d_tok_off || !d_sent_off || !d_doc_sent_off || !d_part_doc_off || !out_totals)
     return set_err(LDDL_EINVAL, "null pointer");
   if (codebert && !d_doc_nseg_doc) return set_err(LDDL_EINVAL, "codebert needs doc_nseg_doc");
   if (target_seq_length < 5 || target_seq_length > 32768)
@@ -622,12 +665,7 @@ static int pack_common(lddl_ctx* c, int codebert, const int32_t* d_ntok, const i
       (rc = ws_get(c, 14, n_part, &P.part_err)) || (rc = ws_get(c, 18, n_sent + n_part + 1, &P.kept)) ||
       (rc = ws_get(c, 33, n_sent, &P.fs_dense)))
     return rc;
-  {  // dense id offsets: tokoff = exclusive scan of the token counts
-    int64_t *tokoff, *bsum;
-    if ((rc = ws_get(c, 31, n_sent + 1, &tokoff)) || (rc = ws_get(c, 32, scan_blocks(n_sent) + 1, &bsum))) return rc;
-    HIP_TRY(launch_scan_ntok(d_ntok, n_sent, tokoff, bsum, st));
-    P.tokoff = tokoff;
-  }
+  P.tokoff = d_tok_off;  // the tokenizer's dense offsets (lddl_tokenize d_out_tok_off)
   int64_t *pair_base, *tok_base;
   int32_t* err_any;
   if ((rc = ws_get(c, 15, n_part + 1, &pair_base)) || (rc = ws_get(c, 16, n_part + 1, &tok_base)) ||
@@ -657,7 +695,7 @@ static int pack_common(lddl_ctx* c, int codebert, const int32_t* d_ntok, const i
       return rc;
     P.sent_spec = sent_spec;
     P.fs_spec = fs_spec;
-    if (!spec_ok) HIP_TRY(launch_sent_special(d_ids, d_sent_off, d_ntok, n_sent, P.cls_id, P.sep_id, sent_spec, st));
+    if (!spec_ok) HIP_TRY(launch_sent_special(d_ids, d_tok_off, d_ntok, n_sent, P.cls_id, P.sep_id, sent_spec, st));
     if (!c->mlm_cap) c->mlm_cap = (uint64_t)n_part * 4 * MLM_CHUNK + (uint64_t)duplicate_factor * n_sent * 4;
   }
   if (!codebert) {
@@ -742,23 +780,24 @@ static int pack_common(lddl_ctx* c, int codebert, const int32_t* d_ntok, const i
   return 0;
 }
 
-extern "C" int lddl_pack_bert(lddl_ctx* c, const uint16_t* d_ids, const int32_t* d_ntok, const int64_t* d_sent_off,
-                              int64_t n_sent, const int64_t* d_doc_sent_off, int64_t n_doc,
+extern "C" int lddl_pack_bert(lddl_ctx* c, const uint16_t* d_ids, const int32_t* d_ntok, const int64_t* d_tok_off,
+                              const int64_t* d_sent_off, int64_t n_sent, const int64_t* d_doc_sent_off, int64_t n_doc,
                               const int64_t* d_part_doc_off, int64_t n_part, int32_t target_seq_length,
                               double short_seq_prob, int32_t duplicate_factor, int32_t masking,
                               double masked_lm_ratio, uint64_t seed, int32_t bin_size, int64_t* out_totals,
                               void* stream) {
-  return pack_common(c, 0, d_ntok, d_sent_off, n_sent, d_doc_sent_off, nullptr, n_doc, d_part_doc_off, n_part,
+  return pack_common(c, 0, d_ntok, d_tok_off, d_sent_off, n_sent, d_doc_sent_off, nullptr, n_doc, d_part_doc_off, n_part,
                      target_seq_length, short_seq_prob, duplicate_factor, seed, bin_size, out_totals, stream, d_ids,
                      masking, masked_lm_ratio);
 }
 
-extern "C" int lddl_pack_codebert(lddl_ctx* c, const int32_t* d_ntok, const int64_t* d_sent_off, int64_t n_sent,
+extern "C" int lddl_pack_codebert(lddl_ctx* c, const int32_t* d_ntok, const int64_t* d_tok_off,
+                                  const int64_t* d_sent_off, int64_t n_sent,
                                   const int64_t* d_doc_sent_off, const int32_t* d_doc_nseg_doc, int64_t n_doc,
                                   const int64_t* d_part_doc_off, int64_t n_part, int32_t target_seq_length,
                                   double short_seq_prob, int32_t duplicate_factor, uint64_t seed, int32_t bin_size,
                                   int64_t* out_totals, void* stream) {
-  return pack_common(c, 1, d_ntok, d_sent_off, n_sent, d_doc_sent_off, d_doc_nseg_doc, n_doc, d_part_doc_off,
+  return pack_common(c, 1, d_ntok, d_tok_off, d_sent_off, n_sent, d_doc_sent_off, d_doc_nseg_doc, n_doc, d_part_doc_off,
                      n_part, target_seq_length, short_seq_prob, duplicate_factor, seed, bin_size, out_totals, stream);
 }
 
@@ -774,15 +813,10 @@ extern "C" int lddl_materialize(lddl_ctx* c, const uint16_t* d_ids, uint16_t* d_
   hipStream_t st = (hipStream_t)stream;
   const PackParams& P = c->pp;
   MatParams M{};
-  M.ids = d_ids;
-  uint16_t* dense;
-  int rc;
-  // LDDL_MAT_ALGO=1: the wave-per-partition materialize and per-sentence
-  // compaction kernels; otherwise the chunked v2 kernels
+  // LDDL_MAT_ALGO=1: the wave-per-partition materialize kernel (also taken
+  // for unaligned buffers); otherwise the chunked v2 kernel
   const int mat_algo = getenv("LDDL_MAT_ALGO") ? atoi(getenv("LDDL_MAT_ALGO")) : 2;
-  if ((rc = ws_get(c, 34, (size_t)c->last_ndense + 16, &dense))) return rc;
-  HIP_TRY(launch_compact_ids(d_ids, P.sent_off, P.ntok, P.tokoff, c->last_nsent, dense, mat_algo, st));
-  M.dense = dense;
+  M.dense = d_ids;
   M.fs_dense = P.fs_dense;
   M.sent_off = P.sent_off;
   M.doc_sent_off = P.doc_sent_off;

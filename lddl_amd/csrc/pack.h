@@ -37,7 +37,7 @@ struct PackParams {
   int32_t nbins;                // max_seq // bin_size (1 when unbinned)
   // scratch, indexed like the corpus (sentence / doc / partition slots)
   int32_t* fs_ntok;             // [n_sent]
-  int64_t* fs_base;             // [n_sent] sparse id offset (sent_off - base) per filtered slot
+  int64_t* fs_base;             // [n_sent] byte offset (sent_off - base) per filtered slot (row_docs)
   int64_t* fs_dense;            // [n_sent] dense id offset (tokoff) per filtered slot
   const int64_t* tokoff;        // [n_sent+1] exclusive scan of ntok: sentence s's ids in the dense array
   int64_t* fd_first;            // [n_doc]
@@ -61,7 +61,7 @@ struct PackParams {
   uint32_t n_vocab;             // len(vocab_words); vocab_words[i] = token id i
   uint32_t cls_id, sep_id, mask_id;
   const uint8_t* sent_spec;     // [n_sent] sentence holds a [CLS]/[SEP] token
-  const uint16_t* ids;          // tokenizer output (sparse)
+  const uint16_t* ids;          // tokenizer output (dense: sentence s at tokoff[s])
   uint8_t* fs_spec;             // [n_sent] sent_spec per filtered slot
   int64_t* mref;                // [dup*n_sent] per record: arena offset | #masked << 48
   int64_t* mloc;                // [dup*n_sent] per binned position: masked entries before it
@@ -95,8 +95,7 @@ struct MlmParams {
 };
 
 struct MatParams {
-  const uint16_t* ids;          // tokenizer output (sparse)
-  const uint16_t* dense;        // the same ids compacted per sentence (tokoff)
+  const uint16_t* dense;        // the tokenizer's dense ids (sentence s at tokoff[s])
   const int64_t* fs_dense;      // dense offset per filtered slot
   const int64_t* sent_off;
   const int64_t* doc_sent_off;
@@ -135,12 +134,13 @@ hipError_t launch_scan_parts(const int64_t* a, const int64_t* b, int64_t n, int6
 hipError_t launch_materialize(const MatParams& M, int64_t total_pairs, int64_t n_dense, int algo, hipStream_t s);
 // tokoff[0..n] = exclusive scan of ntok[0..n) (int64); blocksums: scratch of
 // scan_blocks(n) + 1 entries
-int64_t scan_blocks(int64_t n);
+__host__ __device__ int64_t scan_blocks(int64_t n);
 hipError_t launch_scan_ntok(const int32_t* ntok, int64_t n, int64_t* tokoff, int64_t* blocksums, hipStream_t s);
-// dense[tokoff[s] + k] = ids[sent_off[s] - sent_off[0] + k], k < ntok[s]
-hipError_t launch_compact_ids(const uint16_t* ids, const int64_t* sent_off, const int32_t* ntok,
-                              const int64_t* tokoff, int64_t n_sent, uint16_t* dense, int algo, hipStream_t s);
-hipError_t launch_sent_special(const uint16_t* ids, const int64_t* sent_off, const int32_t* ntok, int64_t n_sent,
+// the same over [*d_lo, *d_hi) (device values, at most max_items), continuing
+// from tokoff[*d_lo]; blocksums: scan_blocks(max_items) + 1
+hipError_t launch_scan_ntok_range(const int32_t* ntok, const int64_t* d_lo, const int64_t* d_hi, int64_t max_items,
+                                  int64_t* tokoff, int64_t* blocksums, hipStream_t s);
+hipError_t launch_sent_special(const uint16_t* ids, const int64_t* tok_off, const int32_t* ntok, int64_t n_sent,
                                uint32_t cls, uint32_t sep, uint8_t* out, hipStream_t s);
 hipError_t launch_masked_lm(const MlmParams& M, hipStream_t s);
 

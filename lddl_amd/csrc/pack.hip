@@ -15,7 +15,7 @@
 // it.  The packers (one wave per partition) are in pack_wave.hip; this file
 // holds the partition scans, materialisation (the bulk byte work: gathering
 // token ids into [CLS] A [SEP] B [SEP] rows, wave-parallel per 64 rows), the
-// dense id compaction and the static-masking kernels.
+// token offset scans and the static-masking kernels.
 #include "common.h"
 #include "pack.h"
 
@@ -132,10 +132,10 @@ __global__ __launch_bounds__(256) void materialize_kernel(MatParams M) {
   }
 }
 
-// ---- chunked row copy (materialize v2, dense compaction v2) ----------------
+// ---- chunked row copy (materialize v2) --------------------------------------
 // A wave owns 64 consecutive rows whose outputs form one contiguous range
-// [G0, G1).  Materialize: a row is [CLS] A [SEP] (B [SEP]) from the dense ids
-// (LEAD); compaction: a row is one sentence's ids.  Waves are dispatched in
+// [G0, G1); a row is [CLS] A [SEP] (B [SEP]) from the tokenizer's dense ids.
+// Waves are dispatched in
 // row order, so the resident waves touch only a narrow window of the source
 // (the dup-fold re-reads of a sentence's ids in materialize stay on-die).
 // The range is written in aligned 8-token (16-B) chunks.  Phase 1 is
@@ -144,15 +144,9 @@ __global__ __launch_bounds__(256) void materialize_kernel(MatParams M) {
 // Every other chunk ([CLS]/[SEP], a row boundary, or one of the two chunks
 // shared with the neighbouring waves) goes to a per-wave list that phase 2
 // drains token-parallel (one token per lane, u16 load + store).
-#ifndef MAT_UNROLL
-#define MAT_UNROLL 2
-#endif
-constexpr int MAT_U = MAT_UNROLL;         // chunks per lane per phase-1 iteration
+constexpr int MAT_U = 2;         // chunks per lane per phase-1 iteration (1 / 3 within noise, 8 slower)
 constexpr int MAT_SLOW = 512;    // slow-chunk list capacity per wave
 constexpr int MAT_PBITS = 26;    // slow entry: chunk start + 8 (26 bits) | row << 26
-#ifndef MAT_TWO
-#define MAT_TWO 1   // compaction: chunks across two rows blended from two source windows
-#endif
 struct RowDesc {
   int64_t src0, src1;       // source start of segment A / B
   int32_t l0, b1, l1, nt;   // |A|, first position of B, |B|, row length
@@ -192,22 +186,15 @@ __device__ __forceinline__ int mat_row(const MatWave& W, int32_t p) {
 }
 
 // token t of row x: the special it is (false) or its source index (true)
-template <bool LEAD>
 __device__ __forceinline__ bool mat_tok(const RowDesc& x, int32_t t, uint32_t cls, uint32_t& y, int64_t& src) {
-  if constexpr (LEAD) {
-    if (t == 0) { y = cls; return false; }
-    if (t <= x.l0) { src = x.src0 + (t - 1); return true; }
-    if (t >= x.b1 && t < x.b1 + x.l1) { src = x.src1 + (t - x.b1); return true; }
-    return false;  // [SEP]
-  } else {
-    src = x.src0 + t;
-    return true;
-  }
+  if (t == 0) { y = cls; return false; }
+  if (t <= x.l0) { src = x.src0 + (t - 1); return true; }
+  if (t >= x.b1 && t < x.b1 + x.l1) { src = x.src1 + (t - x.b1); return true; }
+  return false;  // [SEP]
 }
 
 // phase 2: tokens [0, ntok) of the listed chunks (or, with W == nullptr
 // semantics via plain, every position of the range), one token per lane
-template <bool LEAD>
 __device__ __forceinline__ void mat_drain(const MatWave& W, int ntok, bool listed, int64_t G0, int32_t G1r,
                                           const uint16_t* src, uint16_t* out, uint32_t cls, uint32_t sep,
                                           int lane) {
@@ -227,7 +214,7 @@ __device__ __forceinline__ void mat_drain(const MatWave& W, int ntok, bool liste
         if (p >= 0 && p < G1r) {
           const int r = mat_row(W, p);
           pos[m] = p;
-          ld = mat_tok<LEAD>(W.row[r], p - W.roff[r], cls, y[m], s);
+          ld = mat_tok(W.row[r], p - W.roff[r], cls, y[m], s);
         }
       }
       if (ld) y[m] = src[s];
@@ -241,12 +228,11 @@ __device__ __forceinline__ void mat_drain(const MatWave& W, int ntok, bool liste
 
 // rows published in W (roff, row) for nr rows spanning [G0, G1) of out;
 // src readable for n_src entries
-template <bool LEAD>
 __device__ __forceinline__ void mat_copy(MatWave& W, int64_t G0, int64_t G1, const uint16_t* src, int64_t n_src,
                                          uint16_t* out, uint32_t cls, uint32_t sep, int lane, bool no_drain = false) {
   const int32_t G1r = (int32_t)(G1 - G0);
   if (G1 - G0 >= (1 << MAT_PBITS) - 16) {  // (rows beyond any real max_tok) token by token
-    mat_drain<LEAD>(W, G1r, false, G0, G1r, src, out, cls, sep, lane);
+    mat_drain(W, G1r, false, G0, G1r, src, out, cls, sep, lane);
     return;
   }
   const int64_t q0 = G0 >> 3, q1 = (G1 + 7) >> 3;
@@ -258,17 +244,6 @@ __device__ __forceinline__ void mat_copy(MatWave& W, int64_t G0, int64_t G1, con
     int64_t sv[MAT_U];
     bool fast[MAT_U], slow[MAT_U];
     int rw[MAT_U];
-#if MAT_TWO
-    bool two[MAT_U];
-    int64_t sv2[MAT_U];
-    uint32_t spl[MAT_U];
-#pragma unroll
-    for (int u = 0; u < MAT_U; ++u) {
-      two[u] = false;
-      sv2[u] = 0;
-      spl[u] = 8;
-    }
-#endif
 #pragma unroll
     for (int u = 0; u < MAT_U; ++u) {
       const int64_t q = qb + u * 64 + lane;
@@ -279,36 +254,10 @@ __device__ __forceinline__ void mat_copy(MatWave& W, int64_t G0, int64_t G1, con
       const int32_t t0 = p0 - W.roff[r];
       bool inA, inB;
       int64_t v;
-      if constexpr (LEAD) {
-        inA = t0 >= 1 && t0 + 8 <= 1 + y.l0;
-        inB = t0 >= y.b1 && t0 + 8 <= y.b1 + y.l1;
-        v = inA ? y.src0 + (t0 - 1) : y.src1 + (t0 - y.b1);
-      } else {
-        inA = t0 >= 0 && t0 + 8 <= y.l0;
-        inB = false;
-        v = y.src0 + t0;
-#if MAT_TWO
-        // a chunk that runs from this row into the next one (compaction:
-        // rows back to back, ~34 tokens each) blends two source windows
-        // instead of going token by token through the slow list
-        two[u] = false;
-        if (q < q1 && !inA && t0 >= 0 && t0 < y.l0 && r < 63) {
-          const int32_t r2off = W.roff[r + 1];
-          const RowDesc y2 = W.row[r + 1];
-          const int64_t v2 = y2.src0 + (p0 - r2off);
-          if (r2off == p0 + (y.l0 - t0) && p0 + 8 <= r2off + y2.l0 && v2 >= 0 && (v >> 3) <= amax &&
-              (v2 >> 3) <= amax) {
-            two[u] = true;
-            sv2[u] = v2;
-            spl[u] = (uint32_t)(y.l0 - t0);
-          }
-        }
-#endif
-      }
+      inA = t0 >= 1 && t0 + 8 <= 1 + y.l0;
+      inB = t0 >= y.b1 && t0 + 8 <= y.b1 + y.l1;
+      v = inA ? y.src0 + (t0 - 1) : y.src1 + (t0 - y.b1);
       fast[u] = q < q1 && (inA || inB) && (v >> 3) <= amax;
-#if MAT_TWO
-      if constexpr (!LEAD) fast[u] = fast[u] || two[u];
-#endif
       slow[u] = q < q1 && !fast[u];
       sv[u] = fast[u] ? v : 0;
     }
@@ -322,44 +271,17 @@ __device__ __forceinline__ void mat_copy(MatWave& W, int64_t G0, int64_t G1, con
         vb[u] = s4[a + 1];
       }
     }
-#if MAT_TWO
-    if constexpr (!LEAD) {
-#pragma unroll
-      for (int u = 0; u < MAT_U; ++u)
-        if (two[u]) {  // tokens [spl, 8) from the next row's window
-          const int64_t a2 = sv2[u] >> 3;
-          const uint4 vc = s4[a2], vd = s4[a2 + 1];
-          const uint4 w2 = funnel8(vc, vd, (uint32_t)(sv2[u] & 7));
-          const uint32_t sp = spl[u];
-          // keep token k of the first window iff k < sp: per dword, low / high halves
-          auto blend = [&](uint32_t x, uint32_t y2, uint32_t k0) {
-            const uint32_t lo = k0 < sp ? 0x0000FFFFu : 0u, hi = k0 + 1 < sp ? 0xFFFF0000u : 0u;
-            const uint32_t m = lo | hi;
-            return (x & m) | (y2 & ~m);
-          };
-          const uint4 w1 = funnel8(va[u], vb[u], (uint32_t)(sv[u] & 7));
-          va[u] = make_uint4(blend(w1.x, w2.x, 0), blend(w1.y, w2.y, 2), blend(w1.z, w2.z, 4), blend(w1.w, w2.w, 6));
-          vb[u] = va[u];
-          sv[u] &= ~(int64_t)7;  // (funnel8 at offset 0 below returns va unchanged)
-        }
-    }
-#endif
 #pragma unroll
     for (int u = 0; u < MAT_U; ++u)
       if (fast[u]) {
         const uint4 v = funnel8(va[u], vb[u], (uint32_t)(sv[u] & 7));
-        if constexpr (LEAD) {
-          // the packed rows are written once and read next by the host copy:
-          // streaming stores keep L2 for the dup-fold re-reads of the dense
-          // ids (materialize 28.3 -> 25.0 ms).  Not for compaction, whose
-          // output materialize reads back (10.9 -> 12.4 ms with them).
-          typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-          u32x4 w;
-          w.x = v.x; w.y = v.y; w.z = v.z; w.w = v.w;
-          __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(out4) + (qb + u * 64 + lane));
-        } else {
-          out4[qb + u * 64 + lane] = v;
-        }
+        // the packed rows are written once and read next by the host copy:
+        // streaming stores keep L2 for the dup-fold re-reads of the dense ids
+        // (materialize 28.3 -> 25.0 ms)
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        u32x4 w;
+        w.x = v.x; w.y = v.y; w.z = v.z; w.w = v.w;
+        __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(out4) + (qb + u * 64 + lane));
       }
 #pragma unroll
     for (int u = 0; u < MAT_U; ++u) {
@@ -371,11 +293,11 @@ __device__ __forceinline__ void mat_copy(MatWave& W, int64_t G0, int64_t G1, con
       ns += __popcll(m);
     }
     if (ns > MAT_SLOW - MAT_U * 64) {
-      if (!no_drain) mat_drain<LEAD>(W, ns * 8, true, G0, G1r, src, out, cls, sep, lane);
+      if (!no_drain) mat_drain(W, ns * 8, true, G0, G1r, src, out, cls, sep, lane);
       ns = 0;
     }
   }
-  if (ns > 0 && !no_drain) mat_drain<LEAD>(W, ns * 8, true, G0, G1r, src, out, cls, sep, lane);
+  if (ns > 0 && !no_drain) mat_drain(W, ns * 8, true, G0, G1r, src, out, cls, sep, lane);
 }
 
 // workgroups are dealt round-robin to the 8 XCDs (one L2 each): block b runs
@@ -434,40 +356,13 @@ __global__ __launch_bounds__(256) void materialize2_kernel(MatParams M, int64_t 
   W.roff[lane] = lane < nr ? (int32_t)(off - G0) : 0x7FFFFFFF;
   W.row[lane] = x;
   mat_wsync();
-  mat_copy<true>(W, G0, G1, M.dense, n_src, M.out_tokens, M.cls_id, M.sep_id, lane, M.ablate == 1);
+  mat_copy(W, G0, G1, M.dense, n_src, M.out_tokens, M.cls_id, M.sep_id, lane, M.ablate == 1);
 }
 
-// dense[tokoff[s] + k] = ids[sent_off[s] - sent_off[0] + k]: wave per 64 sentences
-__global__ __launch_bounds__(256) void compact2_kernel(const uint16_t* ids, const int64_t* sent_off,
-                                                       const int32_t* ntok, const int64_t* tokoff, int64_t n_sent,
-                                                       uint16_t* dense) {
-  __shared__ MatWave mw[4];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int64_t sbase = ((int64_t)blockIdx.x * 4 + wv) * 64;
-  if (sbase >= n_sent) return;
-  const int nr = (int)min((int64_t)64, n_sent - sbase);
-  MatWave& W = mw[wv];
-  const int64_t base = sent_off[0], n_ids = sent_off[n_sent] - base;
-  int64_t off = 0, rend = 0;
-  RowDesc x{};
-  if (lane < nr) {
-    const int64_t s = sbase + lane;
-    off = tokoff[s];
-    x.l0 = x.nt = ntok[s];
-    x.src0 = sent_off[s] - base;
-    rend = off + x.nt;
-  }
-  const int64_t G0 = __shfl(off, 0), G1 = __shfl(rend, nr - 1);
-  W.roff[lane] = lane < nr ? (int32_t)(off - G0) : 0x7FFFFFFF;
-  W.row[lane] = x;
-  mat_wsync();
-  mat_copy<false>(W, G0, G1, ids, n_ids, dense, 0, 0, lane);
-}
-
-// ------------------------------------------------ dense id compaction ----
+// ------------------------------------------------- token offset scans ----
 constexpr int SCAN_ITEMS = 4096;  // ntok entries per scan block (256 x 16)
 
-int64_t scan_blocks(int64_t n) { return (n + SCAN_ITEMS - 1) / SCAN_ITEMS; }
+__host__ __device__ int64_t scan_blocks(int64_t n) { return (n + SCAN_ITEMS - 1) / SCAN_ITEMS; }
 
 __device__ __forceinline__ int64_t block_excl_scan256(int64_t v, int64_t* red, int64_t* total) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -490,21 +385,39 @@ __device__ __forceinline__ int64_t block_excl_scan256(int64_t v, int64_t* red, i
   return pre + x - v;
 }
 
-__global__ __launch_bounds__(256) void scan_reduce_kernel(const int32_t* ntok, int64_t n, int64_t* bsum) {
+// The scan's range [lo, hi) comes from the device (d_lo / d_hi, e.g. a
+// tokenizer segment's sentences) or is [0, n) (d_lo == nullptr); the grid is
+// sized for at most n items and blocks past the range exit.  With d_lo, the
+// scan continues from tokoff[lo] (the previous range's total).
+__device__ __forceinline__ void scan_range(const int64_t* d_lo, const int64_t* d_hi, int64_t n, int64_t& lo,
+                                           int64_t& hi) {
+  lo = d_lo ? *d_lo : 0;
+  hi = d_lo ? *d_hi : n;
+}
+
+__global__ __launch_bounds__(256) void scan_reduce_kernel(const int32_t* ntok, const int64_t* d_lo, const int64_t* d_hi,
+                                                          int64_t n, int64_t* bsum) {
   __shared__ int64_t red[4];
-  const int64_t b0 = (int64_t)blockIdx.x * SCAN_ITEMS;
+  int64_t lo, hi;
+  scan_range(d_lo, d_hi, n, lo, hi);
+  const int64_t b0 = lo + (int64_t)blockIdx.x * SCAN_ITEMS;
+  if (b0 >= hi) return;
   int64_t sum = 0;
   for (int k = threadIdx.x; k < SCAN_ITEMS; k += 256)
-    if (b0 + k < n) sum += ntok[b0 + k];
+    if (b0 + k < hi) sum += ntok[b0 + k];
   int64_t tot;
   block_excl_scan256(sum, red, &tot);
   if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
 }
 
 // exclusive scan of the block sums in place (one block), bsum[nb] = total
-__global__ __launch_bounds__(256) void scan_bsum_kernel(int64_t* bsum, int64_t nb) {
+__global__ __launch_bounds__(256) void scan_bsum_kernel(int64_t* bsum, const int64_t* d_lo, const int64_t* d_hi,
+                                                        int64_t n, const int64_t* tokoff) {
   __shared__ int64_t red[4];
-  int64_t carry = 0;
+  int64_t lo, hi;
+  scan_range(d_lo, d_hi, n, lo, hi);
+  const int64_t nb = scan_blocks(hi - lo);
+  int64_t carry = d_lo ? tokoff[lo] : 0;
   for (int64_t c = 0; c < nb; c += 256) {
     const int64_t i = c + threadIdx.x;
     const int64_t v = i < nb ? bsum[i] : 0;
@@ -516,85 +429,48 @@ __global__ __launch_bounds__(256) void scan_bsum_kernel(int64_t* bsum, int64_t n
   if (threadIdx.x == 0) bsum[nb] = carry;
 }
 
-__global__ __launch_bounds__(256) void scan_write_kernel(const int32_t* ntok, int64_t n, const int64_t* bsum,
-                                                         int64_t* tokoff) {
+__global__ __launch_bounds__(256) void scan_write_kernel(const int32_t* ntok, const int64_t* d_lo, const int64_t* d_hi,
+                                                         int64_t n, const int64_t* bsum, int64_t* tokoff) {
   __shared__ int64_t red[4];
-  const int64_t b0 = (int64_t)blockIdx.x * SCAN_ITEMS + threadIdx.x * 16;
+  int64_t lo, hi;
+  scan_range(d_lo, d_hi, n, lo, hi);
+  if (lo + (int64_t)blockIdx.x * SCAN_ITEMS >= hi) return;
+  const int64_t b0 = lo + (int64_t)blockIdx.x * SCAN_ITEMS + threadIdx.x * 16;
   int32_t v[16];
   int64_t sum = 0;
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
-    v[k] = b0 + k < n ? ntok[b0 + k] : 0;
+    v[k] = b0 + k < hi ? ntok[b0 + k] : 0;
     sum += v[k];
   }
   int64_t tot;
   int64_t run = bsum[blockIdx.x] + block_excl_scan256(sum, red, &tot);
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
-    if (b0 + k < n) tokoff[b0 + k] = run;
+    if (b0 + k < hi) tokoff[b0 + k] = run;
     run += v[k];
   }
-  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) tokoff[n] = bsum[gridDim.x];
+  if (lo + ((int64_t)blockIdx.x + 1) * SCAN_ITEMS >= hi && threadIdx.x == 0) tokoff[hi] = bsum[scan_blocks(hi - lo)];
+}
+
+static hipError_t scan_launch(const int32_t* ntok, const int64_t* d_lo, const int64_t* d_hi, int64_t n,
+                              int64_t* tokoff, int64_t* blocksums, hipStream_t s) {
+  const int64_t nb = scan_blocks(n);
+  if (nb == 0) return d_lo ? hipSuccess : hipMemsetAsync(tokoff, 0, sizeof(int64_t), s);
+  hipLaunchKernelGGL(scan_reduce_kernel, dim3((unsigned)nb), dim3(256), 0, s, ntok, d_lo, d_hi, n, blocksums);
+  hipLaunchKernelGGL(scan_bsum_kernel, dim3(1), dim3(256), 0, s, blocksums, d_lo, d_hi, n, (const int64_t*)tokoff);
+  hipLaunchKernelGGL(scan_write_kernel, dim3((unsigned)nb), dim3(256), 0, s, ntok, d_lo, d_hi, n,
+                     (const int64_t*)blocksums, tokoff);
+  return hipGetLastError();
 }
 
 hipError_t launch_scan_ntok(const int32_t* ntok, int64_t n, int64_t* tokoff, int64_t* blocksums, hipStream_t s) {
-  const int64_t nb = scan_blocks(n);
-  if (nb == 0) return hipMemsetAsync(tokoff, 0, sizeof(int64_t), s);
-  hipLaunchKernelGGL(scan_reduce_kernel, dim3((unsigned)nb), dim3(256), 0, s, ntok, n, blocksums);
-  hipLaunchKernelGGL(scan_bsum_kernel, dim3(1), dim3(256), 0, s, blocksums, nb);
-  hipLaunchKernelGGL(scan_write_kernel, dim3((unsigned)nb), dim3(256), 0, s, ntok, n, (const int64_t*)blocksums, tokoff);
-  return hipGetLastError();
+  return scan_launch(ntok, nullptr, nullptr, n, tokoff, blocksums, s);
 }
 
-// wave per 64 sentences, 8 sentences' copies in flight per step
-__global__ __launch_bounds__(256) void compact_ids_kernel(const uint16_t* ids, const int64_t* sent_off,
-                                                          const int32_t* ntok, const int64_t* tokoff, int64_t n_sent,
-                                                          uint16_t* dense) {
-  const int lane = threadIdx.x & 63;
-  const int64_t base = sent_off[0];
-  const int64_t nw = (int64_t)gridDim.x * 4;
-  for (int64_t s0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64; s0 < n_sent; s0 += nw * 64) {
-    const int64_t s = s0 + lane;
-    int64_t so = 0, to = 0;
-    int nt = 0;
-    if (s < n_sent) {
-      so = sent_off[s] - base;
-      to = tokoff[s];
-      nt = ntok[s];
-    }
-    for (int j0 = 0; j0 < 64; j0 += 8) {
-      uint16_t v[8];
-      int64_t dst[8];
-      int n[8];
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int64_t sq = __shfl(so, j0 + q), tq = __shfl(to, j0 + q);
-        n[q] = __shfl(nt, j0 + q);
-        dst[q] = tq;
-        v[q] = lane < n[q] ? ids[sq + lane] : (uint16_t)0;
-        for (int t = 64 + lane; t < n[q]; t += 64) dense[tq + t] = ids[sq + t];  // long sentences
-      }
-#pragma unroll
-      for (int q = 0; q < 8; ++q)
-        if (lane < n[q]) dense[dst[q] + lane] = v[q];
-    }
-  }
-}
-
-hipError_t launch_compact_ids(const uint16_t* ids, const int64_t* sent_off, const int32_t* ntok,
-                              const int64_t* tokoff, int64_t n_sent, uint16_t* dense, int algo, hipStream_t s) {
-  if (n_sent <= 0) return hipSuccess;
-  if (algo != 1 && ((reinterpret_cast<uintptr_t>(ids) | reinterpret_cast<uintptr_t>(dense)) & 15u) == 0) {
-    const int64_t items = (n_sent + 63) / 64;  // one wave per 64 sentences
-    hipLaunchKernelGGL(compact2_kernel, dim3((unsigned)((items + 3) / 4)), dim3(256), 0, s, ids, sent_off, ntok, tokoff,
-                       n_sent, dense);
-    return hipGetLastError();
-  }
-  int64_t grid = (n_sent + 255) / 256;
-  if (grid > 8192) grid = 8192;
-  hipLaunchKernelGGL(compact_ids_kernel, dim3((unsigned)grid), dim3(256), 0, s, ids, sent_off, ntok, tokoff, n_sent,
-                     dense);
-  return hipGetLastError();
+hipError_t launch_scan_ntok_range(const int32_t* ntok, const int64_t* d_lo, const int64_t* d_hi, int64_t max_items,
+                                  int64_t* tokoff, int64_t* blocksums, hipStream_t s) {
+  return scan_launch(ntok, d_lo, d_hi, max_items, tokoff, blocksums, s);
 }
 
 hipError_t launch_scan_parts(const int64_t* a, const int64_t* b, int64_t n, int64_t* sa, int64_t* sb,
@@ -608,12 +484,11 @@ hipError_t launch_scan_parts(const int64_t* a, const int64_t* b, int64_t n, int6
 // the text): create_masked_lm_predictions excludes those from the candidates
 // (pretrain.py:187-190), so pairs touching such a sentence build an explicit
 // candidate list; all others use the implicit one.
-__global__ __launch_bounds__(256) void sent_special_kernel(const uint16_t* ids, const int64_t* sent_off,
+__global__ __launch_bounds__(256) void sent_special_kernel(const uint16_t* ids, const int64_t* tok_off,
                                                            const int32_t* ntok, int64_t n_sent, uint32_t cls,
                                                            uint32_t sep, uint8_t* out) {
-  const int64_t base = sent_off[0];
   for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n_sent; s += (int64_t)gridDim.x * blockDim.x) {
-    const uint16_t* t = ids + (sent_off[s] - base);
+    const uint16_t* t = ids + tok_off[s];
     const int n = ntok[s];
     uint32_t f = 0;
     for (int k = 0; k < n; ++k) {
@@ -658,9 +533,9 @@ __global__ __launch_bounds__(256) void masked_lm_kernel(MlmParams M) {
   }
 }
 
-hipError_t launch_sent_special(const uint16_t* ids, const int64_t* sent_off, const int32_t* ntok, int64_t n_sent,
+hipError_t launch_sent_special(const uint16_t* ids, const int64_t* tok_off, const int32_t* ntok, int64_t n_sent,
                                uint32_t cls, uint32_t sep, uint8_t* out, hipStream_t s) {
-  hipLaunchKernelGGL(sent_special_kernel, dim3(4096), dim3(256), 0, s, ids, sent_off, ntok, n_sent, cls, sep, out);
+  hipLaunchKernelGGL(sent_special_kernel, dim3(4096), dim3(256), 0, s, ids, tok_off, ntok, n_sent, cls, sep, out);
   return hipGetLastError();
 }
 

@@ -725,7 +725,7 @@ __global__ __launch_bounds__(64, PACK_OCC) void pack_bert_wave_kernel(PackParams
               int acc = 0;
               for (int q = 0; q < ns && acc < hi; ++q) {
                 const int ln = len_at(fs + q);
-                const int64_t sb = P.fs_base[s0 + fs + q];
+                const int64_t sb = P.fs_dense[s0 + fs + q];
                 const int a0 = max(lo, acc), a1 = min(hi, acc + ln);
                 for (int t = a0; t < a1; t += 64) {
                   const int tt = t + lane;

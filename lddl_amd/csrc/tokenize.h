@@ -14,14 +14,17 @@ struct TokParams {
   const int64_t* sent_off;
   int64_t n_sent;
   int32_t max_tok;
-  uint16_t* out_ids;
+  uint16_t* out_ids;      // dense: sentence s's ids at out_tok_off[s] (split path; the serial kernel: see below)
   int32_t* out_ntok;
+  int64_t* out_tok_off;   // [n_sent + 1] exclusive scan of out_ntok
+  int64_t out_cap;        // entries of out_ids
   uint8_t* sent_spec;     // optional [n_sent]: the sentence's tokens include [CLS] / [SEP]
   // unicode table
   const uint16_t* top;
   const uint32_t* pages;
   const uint4* multi;
   const uint32_t* bmp;    // [0x10000] pages[top[cp >> 8] * 256 + (cp & 255)] for cp < U+10000
+  const uint32_t* xmap;   // [0x110000] the scan's fast exception entries (tokenize_split.hip XM_*)
   // vocab
   const uint4* slots;
   const uint32_t* bloom;  // [BLOOM_WORDS]
@@ -47,19 +50,18 @@ hipError_t launch_tile_bounds(const int64_t* sent_off, int64_t n_sent, int64_t n
 hipError_t launch_tokenize_fallback(const TokParams& P, const int64_t* tile_sent, const int32_t* fb_list,
                                     const int32_t* fb_count, int grid, hipStream_t s);
 const void* tokenize_fallback_kernel_ptr();
-// every tile through the exact serial path (tokenize_fallback.hip)
-hipError_t launch_tokenize_serial(const TokParams& P, int64_t nbytes, int64_t* tile_sent, int32_t* fb_list,
-                                  int32_t* fb_count, int fb_grid, hipStream_t s);
+// fb_list = every tile of [0, n_tiles), *fb_count = n_tiles
+hipError_t launch_list_all_tiles(int64_t n_tiles, int32_t* fb_list, int32_t* fb_count, hipStream_t s);
 
 // v5 (tokenize_split.hip): the tile scan resolves whole-word vocab hits and
 // hands every other word to a WordPiece record queue; a full-occupancy
-// WordPiece kernel runs the records, a count pass and an expand pass write
-// the ids.  Scratch per segment of tiles (SPLIT_SEG_TILES):
-//   ent    u16 per byte of the segment: sentence s's entries from its first
-//          queued word on (k >= fdef[s]) at sent_off[s] - sent_off[0] -
-//          t0 * 1 KiB + k: a vocab id, or SPLIT_EDEF | (record slot - qb[s])
-//          for a word of the queue; the ids before it are final and go
-//          straight to the output
+// WordPiece kernel runs the records, a count pass + scan give every
+// sentence's dense offset, and an expand pass writes the dense ids.  Scratch
+// per segment of tiles (SPLIT_SEG_TILES):
+//   ent    u16 per byte of the segment: sentence s's entries at
+//          sent_off[s] - sent_off[0] - t0 * 1 KiB + k: a vocab id, or
+//          SPLIT_EDEF | (record slot - qb[s]) for a word of the queue (the
+//          serial path's ids of a fallback tile land here too)
 //   rec    64-B record slots in chunks of SPLIT_CHUNK, chunk_fill[c] used
 //   smeta  per sentence: #entries, first queued entry (fdef), first record slot (qb)
 // 4 GiB of input per segment: 48 GB of scratch (entries 2 B/byte, record
@@ -82,8 +84,13 @@ struct SplitParams {
   uint32_t* chunk_ctr;     // [0] chunks handed out
   uint32_t n_chunks;
   uint2* smeta;            // per sentence: #entries | first queued entry << 16, first record slot (~0: none)
+  uint16_t* snslot;        // per sentence: its record slots (count_kernel sums their piece counts)
+  uint8_t* cnt8;           // per record slot: pieces of the word (0 for an extension slot)
+  int64_t* scan_bsum;      // scan_blocks(seg_sent_cap) + 1
+  int64_t seg_sent_cap;    // bound on the sentences of a segment (the count scan's grid)
   int32_t* fb_list;
-  int32_t* fb_count;
+  int32_t* fb_count;       // tiles listed for the serial path in this segment
+  uint32_t* n_fallback;    // tiles listed over the call (lddl_tokenize_stats)
   unsigned long long* n_rec;  // optional: records run by wp_kernel (summed over the call)
 };
 // optional per-kernel timing of a call: event pairs recorded around every
@@ -94,6 +101,12 @@ struct SplitTiming {
 };
 hipError_t launch_tokenize_split(const TokParams& P, int64_t nbytes, int64_t* tile_sent, SplitParams S, int n_cu,
                                  int fb_grid, int cfg, hipStream_t s, SplitTiming* tm = nullptr);
-int64_t split_seg_slots(int64_t seg_tiles);
+// every tile through the exact serial path, same dense output (tables the
+// split tokenizer does not model, LDDL_TOKENIZE_ALGO=0)
+hipError_t launch_tokenize_serial_dense(const TokParams& P, int64_t nbytes, int64_t* tile_sent, SplitParams S,
+                                        int n_cu, int fb_grid, hipStream_t s);
+// record slots for a segment: 1 per 14 input bytes + a partly used chunk per
+// scanning wave of the scan's real grid on n_cu CUs
+int64_t split_seg_slots(int64_t seg_tiles, int n_cu);
 
 }  // namespace lddl

@@ -11,9 +11,11 @@
 // tokenizer.tokenize(s, max_length=512, truncation=True),
 // lddl/dask/bert/pretrain.py:79-80, as oracle/tokenizer_oracle.c).  The
 // split tokenizer (tokenize_split.hip) lists the tiles it does not model;
-// launch_tokenize_serial lists every tile (vocabularies / unicode tables the
-// split tokenizer does not take: > 61440 ids, or an ASCII page with more
-// than the A-Z -> a-z mapping).
+// launch_tokenize_serial_dense lists every tile (vocabularies / unicode
+// tables the split tokenizer does not take: > 61440 ids, or an ASCII page
+// with more than the A-Z -> a-z mapping).  Its ids are written sparse by
+// byte offset (P.out_ids + sent_off[s] - sent_off[0]) into the split path's
+// entry buffer, from which expand_kernel writes the dense output.
 #include "common.h"
 #include "tokenize.h"
 #include "tokenize_serial.h"
@@ -75,14 +77,9 @@ __global__ void list_all_tiles_kernel(int64_t n_tiles, int32_t* fb_list, int32_t
   if (blockIdx.x == 0 && threadIdx.x == 0) *fb_count = (int32_t)n_tiles;
 }
 
-hipError_t launch_tokenize_serial(const TokParams& P, int64_t nbytes, int64_t* tile_sent, int32_t* fb_list,
-                                  int32_t* fb_count, int fb_grid, hipStream_t s) {
-  const int64_t n_tiles = tile_count(nbytes);
-  hipError_t e = launch_tile_bounds(P.sent_off, P.n_sent, n_tiles, tile_sent, s);
-  if (e != hipSuccess) return e;
+hipError_t launch_list_all_tiles(int64_t n_tiles, int32_t* fb_list, int32_t* fb_count, hipStream_t s) {
   hipLaunchKernelGGL(list_all_tiles_kernel, dim3(1024), dim3(256), 0, s, n_tiles, fb_list, fb_count);
-  if ((e = hipGetLastError()) != hipSuccess) return e;
-  return launch_tokenize_fallback(P, tile_sent, fb_list, fb_count, fb_grid, s);
+  return hipGetLastError();
 }
 
 hipError_t launch_tile_bounds(const int64_t* sent_off, int64_t n_sent, int64_t n_tiles, int64_t* tile_sent,

@@ -36,55 +36,27 @@
 #include "tokenize.h"
 #include "wave.h"
 #include "tokenize_serial.h"
+#include "pack.h"
 
 namespace lddl {
 namespace tok5 {
 
 constexpr int CAP = 2048;                // window bytes (32 per lane)
-#ifndef TOK5_DCAP
-#define TOK5_DCAP 256
-#endif
-#ifndef TOK5_XCAP
-#define TOK5_XCAP 32
-#endif
-constexpr int DCAP = TOK5_DCAP;          // side buffer for dirty words
+constexpr int DCAP = 256;                // side buffer for dirty words
 constexpr int NBUF = CAP + DCAP + 64;    // + over-read pad of the key loads
 constexpr int UCAP = 256;                // units per round
 constexpr int NSCAP = 64;                // sentences per tile
-constexpr int XCAP = TOK5_XCAP;          // expansion markers per tile
+constexpr int XCAP = 32;                 // expansion markers per tile
 constexpr int KEYMAX = 56;               // key bytes a record holds
-#ifndef TOK5_XB
-#define TOK5_XB 4
-#endif
-#ifndef TOK5_WP_GROUPS_ANY
-#define TOK5_WP_GROUPS_ANY 1
-#endif
-#ifndef TOK5_NB128
-#define TOK5_NB128 1
-#endif
-#ifndef TOK5_PLANES
-#define TOK5_PLANES 1
-#endif
-#ifndef TOK5_REC_SOA
-#define TOK5_REC_SOA 1
-#endif
-#ifndef TOK5_WP_SHORTREF
-#define TOK5_WP_SHORTREF 1
-#endif
-#ifndef TOK5_WP_REGPCS
-#define TOK5_WP_REGPCS 1
-#endif
-#ifndef TOK5_PCS
-#define TOK5_PCS 1
-#endif
-#ifndef TOK5_MERGED_PROBE
-#define TOK5_MERGED_PROBE 1
-#endif
-#ifndef TOK5_INPLACE
-#define TOK5_INPLACE 1
-#endif
 constexpr int KEY1 = 28;                 // keys up to 28 bytes take one slot (<= 28 pieces)
 constexpr uint32_t BF = 0xFFu, BX = 0xFDu, BS = 0xF8u;  // filler, expansion, special k = BS+k
+// fast exception entry (TokParams::xmap, one per code point; built by
+// lddl_create from the unicode table): replacement bytes 0-23, their count
+// 24-26, action 27-28, 29 write the replacement, 31 SLOW (the full path)
+constexpr uint32_t XM_SLOW = 0x80000000u, XM_WRITE = 0x20000000u;
+enum : uint32_t { XM_WORD = 0, XM_SPACE = 1, XM_ISOLATE = 2, XM_DROP = 3 };
+__device__ __forceinline__ uint32_t xm_len(uint32_t e) { return (e >> 24) & 7u; }
+__device__ __forceinline__ uint32_t xm_act(uint32_t e) { return (e >> 27) & 3u; }
 enum : uint32_t { C_W = 1, C_I = 2, C_S = 4, C_D = 8, C_UP = 16, C_X = 32, C_CS = 64 };
 constexpr uint16_t U_EMPTY = 0xFFFEu, U_DEFER = 0xFFFFu;
 
@@ -93,6 +65,14 @@ __device__ __forceinline__ uint32_t wmake(int u, int src, int len) {
   return (uint32_t)u | ((uint32_t)src << 8) | ((uint32_t)len << 20);
 }
 __device__ __forceinline__ int wsrc(uint32_t w) { return (int)((w >> 8) & 0xFFFu); }
+// unit record: window position (11 bits) | span length << 11 (12) | dirty << 23 | sentence << 24
+__device__ __forceinline__ uint32_t ur_make(int p, int len, bool dirty, int sent) {
+  return (uint32_t)p | ((uint32_t)len << 11) | ((uint32_t)dirty << 23) | ((uint32_t)sent << 24);
+}
+__device__ __forceinline__ int ur_p(uint32_t x) { return (int)(x & 0x7FFu); }
+__device__ __forceinline__ int ur_len(uint32_t x) { return (int)((x >> 11) & 0xFFFu); }
+__device__ __forceinline__ bool ur_dirty(uint32_t x) { return (x >> 23) & 1u; }
+__device__ __forceinline__ uint32_t ur_sent(uint32_t x) { return x >> 24; }
 __device__ __forceinline__ int wlen(uint32_t w) { return (int)(w >> 20); }
 
 struct alignas(16) Lds {
@@ -127,11 +107,10 @@ __device__ __forceinline__ void wsync() {
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
-// record slot k (of 4 16-B quarters) of slot i: quarter-major (TOK5_REC_SOA:
-// the lanes of a refill, on consecutive slots, load one contiguous run per
-// quarter) or slot-major
+// record slot k (of 4 16-B quarters) of slot i, quarter-major: the lanes of a
+// refill, on consecutive slots, load one contiguous run per quarter
 __device__ __forceinline__ uint4* recq(const SplitParams& S, int k, uint64_t i) {
-  return TOK5_REC_SOA ? S.rec + (uint64_t)k * ((uint64_t)S.n_chunks * SPLIT_CHUNK) + i : S.rec + i * 4 + k;
+  return S.rec + (uint64_t)k * ((uint64_t)S.n_chunks * SPLIT_CHUNK) + i;
 }
 __device__ __forceinline__ uint32_t rawb(const Lds& L, int p) { return reinterpret_cast<const uint8_t*>(L.rp)[p]; }
 __device__ __forceinline__ uint32_t nbyte(const uint32_t* nb, int p) { return reinterpret_cast<const uint8_t*>(nb)[p]; }
@@ -184,38 +163,23 @@ __device__ __forceinline__ int utf8_put(uint32_t* nb, int p, uint32_t c) {
   return 4;
 }
 
-// first break position > p (a unit's span end), at most nb
-__device__ __forceinline__ int span_end(const Lds& L, int p, int nb) {
-  int w = p >> 5;
-  uint32_t m = L.brk[w] & ~((2u << (p & 31)) - 1u);
-  while (m == 0) {
-    ++w;
-    if ((w << 5) >= nb) return nb;
-    m = L.brk[w];
-  }
-  return min((w << 5) + __ffs(m) - 1, nb);
-}
-
-__device__ __forceinline__ bool span_dirty(const Lds& L, int p, int q) {
-  for (int w = p >> 5; (w << 5) < q; ++w) {
-    const int lo = max(p - (w << 5), 0), hi = min(q - (w << 5), 32);
-    const uint32_t m = (hi >= 32 ? ~0u : ((1u << hi) - 1u)) & ~((1u << lo) - 1u);
-    if (L.dm[w] & m) return true;
-  }
-  return false;
-}
-
 // Compact / expand the dirty span [p, q).  Returns its normalised length
 // (source in *src), -1 on overflow (flagged in misc[2]).  Without expansion
 // markers in the tile (misc[1] == 0) a dirty span holds only fillers
 // (dropped / shortened chars): it compacts in place, one pass; otherwise it
 // goes to the side buffer (count pass, then the expansions written).
 __device__ int dirty_normalize(Lds& L, const TokParams& P, int p, int q, int* src) {
-  if (TOK5_INPLACE && L.misc[1] == 0) {
+  if (L.misc[1] == 0) {
+    // dword reads (no read waits on the previous byte's write: a byte is
+    // written at or below the position read, never into a later dword)
     int o = p;
-    for (int i = p; i < q; ++i) {
-      const uint32_t b = nbyte(L.nb, i);
-      if (b != BF) nput(L.nb, o++, b);
+    for (int a = p & ~3; a < q; a += 4) {
+      const uint32_t v = L.nb[a >> 2];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t b = (v >> (8 * k)) & 0xFFu;
+        if (a + k >= p && a + k < q && b != BF) nput(L.nb, o++, b);
+      }
     }
     *src = p;
     return o - p;
@@ -429,6 +393,7 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
       if (lane == 0) {
         const int at = atomicAdd(S.fb_count, 1);
         S.fb_list[at] = (int32_t)t;
+        atomicAdd(S.n_fallback, 1u);
       }
       for (int j = lane; j < ns; j += 64) {
         S.smeta[sa + j] = make_uint2(SPLIT_NENT_FB, 0xFFFFFFFFu);
@@ -473,7 +438,6 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
       if (p0 >= nb) v0 = make_uint4(0, 0, 0, 0);
       if (p0 + 16 >= nb) v1 = make_uint4(0, 0, 0, 0);
       const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-#if TOK5_PLANES
       // class bytes c[k] (byte j = position 4k + j), then the per-position
       // class bits as 32-bit planes without multiplies: 4x4 byte transposes
       // put position 4k + j at byte k of t[j]; a plane gathers bit q of the
@@ -487,15 +451,10 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
         const uint32_t dmk = (c[k] >> 3) & 0x01010101u;  // drop bytes -> filler 0xFF
         nv[k] = (x + ((c[k] & 0x10101010u) << 1)) | ((dmk << 8) - dmk);
       }
-#if TOK5_NB128
       // two 16-B stores per lane (8 dword stores at a 32-B lane stride hit
       // 1/8 of the banks)
       *reinterpret_cast<uint4*>(&L.nb[lane * 8]) = make_uint4(nv[0], nv[1], nv[2], nv[3]);
       *reinterpret_cast<uint4*>(&L.nb[lane * 8 + 4]) = make_uint4(nv[4], nv[5], nv[6], nv[7]);
-#else
-#pragma unroll
-      for (int k = 0; k < 8; ++k) L.nb[lane * 8 + k] = nv[k];
-#endif
       uint32_t t[8];
       byte_transpose4(c[0], c[1], c[2], c[3], t[0], t[1], t[2], t[3]);
       byte_transpose4(c[4], c[5], c[6], c[7], t[4], t[5], t[6], t[7]);
@@ -504,23 +463,6 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
       };
       const uint32_t Wh = plane(0), Ih = plane(1), Sh = plane(2), Dh = plane(3), Xh = plane(5);
       const uint32_t CSh = Wh | Ih | Sh | Xh;  // every byte but UTF-8 continuations (ctab)
-#else
-      uint32_t Wh = 0, Ih = 0, Sh = 0, CSh = 0, Dh = 0, Xh = 0;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const uint32_t x = w[k];
-        const uint32_t c = (uint32_t)ctab[x & 0xFFu] | ((uint32_t)ctab[(x >> 8) & 0xFFu] << 8) |
-                           ((uint32_t)ctab[(x >> 16) & 0xFFu] << 16) | ((uint32_t)ctab[x >> 24] << 24);
-        L.nb[lane * 8 + k] = (x + ((c & 0x10101010u) << 1)) | (((c >> 3) & 0x01010101u) * 0xFFu);
-        const int sh = 4 * k;
-        Wh |= gather4(c, 0) << sh;
-        Ih |= gather4(c, 1) << sh;
-        Sh |= gather4(c, 2) << sh;
-        Dh |= gather4(c, 3) << sh;
-        Xh |= gather4(c, 5) << sh;
-        CSh |= gather4(c, 6) << sh;
-      }
-#endif
       const int wlo = min(max(aoff - p0, 0), 32), whi = min(max(nb - p0, 0), 32);
       inwin = (whi >= 32 ? ~0u : ((1u << whi) - 1u)) & (wlo >= 32 ? 0u : ~((1u << wlo) - 1u));
       W = Wh; I = Ih; S_ = Sh; CS = CSh; D = Dh; X = Xh & inwin;
@@ -531,10 +473,98 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
     uint32_t sp_m = 0, sp_w = 0, sp_d = 0;  // this lane's last char / special running into the next lane
     {
       const int p0 = lane * 32;
-      // exceptions in batches of 4 per lane: the table lookups of a batch
-      // (code point -> page -> entry -> multi expansion) go out together
+      // Fast path, one exception byte per lane per step: '[' (a literal
+      // special token?) from the raw bytes and the sentence-start bits, a
+      // UTF-8 lead byte from ONE load of its code point's fast entry (xmap:
+      // class, replacement bytes, drop).  What it does not model (SLOW: multi-
+      // char expansions, canonical reordering, a replacement longer than the
+      // source) goes to the full path below.
+      uint32_t xslow = 0;
       for (uint32_t xm = X; __any(xm != 0);) {
-        constexpr int XB = TOK5_XB;
+        int i = -1;
+        if (xm) {
+          i = __ffs(xm) - 1;
+          xm &= xm - 1;
+        }
+        uint32_t e = XM_SLOW, n = 0;
+        bool brk = false;
+        if (i >= 0) {
+          const int p = p0 + i;
+          const uint32_t b = rawb(L, p);
+          if (b == '[') {
+            brk = true;
+          } else {
+            n = (uint32_t)utf8_len(b);
+            uint32_t cp = b & (0x3Fu >> (n - 1));
+            for (uint32_t q = 1; q < n; ++q) cp = (cp << 6) | (rawb(L, p + (int)q) & 0x3Fu);
+            if (cp > 0x10FFFF) cp = 0xFFFD;
+            e = P.xmap[cp];
+            if ((e & XM_SLOW) || xm_len(e) > n) xslow |= 1u << i;
+          }
+        }
+        if (brk) {  // [PAD] [UNK] [CLS] [SEP] [MASK] within p's sentence
+          const int p = p0 + i;
+          const int a = (p + 1) >> 2;
+          const uint32_t sh = (uint32_t)((p + 1) & 3);
+          const uint32_t w0 = __builtin_amdgcn_alignbyte(L.rp[a + 1], L.rp[a], sh);  // bytes p+1 .. p+4
+          const uint32_t w1 = __builtin_amdgcn_alignbyte(L.rp[a + 2], L.rp[a + 1], sh) & 0xFFu;  // byte p+5
+          // sentence starts at p+1 .. p+5 end p's sentence (no special crosses one)
+          const int wq = (p + 1) >> 5;
+          const uint64_t sbw = (uint64_t)L.sb[wq] | ((uint64_t)(wq + 1 < 64 ? L.sb[wq + 1] : 0u) << 32);
+          const uint32_t nxt = (uint32_t)(sbw >> ((p + 1) & 31)) & 0x1Fu;
+          int len = 0, sk = -1;
+          if (p + 5 <= nb && (nxt & 0xFu) == 0) {
+            if (w0 == 0x5D444150u) { sk = 0; len = 5; }         // PAD]
+            else if (w0 == 0x5D4B4E55u) { sk = 1; len = 5; }    // UNK]
+            else if (w0 == 0x5D534C43u) { sk = 2; len = 5; }    // CLS]
+            else if (w0 == 0x5D504553u) { sk = 3; len = 5; }    // SEP]
+            else if (w0 == 0x4B53414Du && w1 == ']' && p + 6 <= nb && (nxt & 0x10u) == 0) { sk = 4; len = 6; }  // MASK]
+          }
+          if (sk >= 0) {
+            nput(L.nb, p, BS + (uint32_t)sk);
+            const uint64_t cov = ((1ull << (len - 1)) - 1ull) << (i + 1);
+            const uint32_t cl = (uint32_t)cov;
+            W &= ~cl;
+            I &= ~cl;
+            S_ &= ~cl;
+            CS &= ~cl;
+            D &= ~cl;
+            sp_m |= (uint32_t)(cov >> 32);
+          }
+        } else if (i >= 0 && !((xslow >> i) & 1u)) {
+          const int p = p0 + i;
+          const uint32_t act = xm_act(e), T = xm_len(e);
+          const uint64_t span = ((1ull << n) - 1ull) << i;
+          bool dirty = false, wordc = false;
+          if (act == XM_DROP) {
+            for (uint32_t q = 0; q < n; ++q) nput(L.nb, p + (int)q, BF);
+            dirty = wordc = true;
+          } else if (act == XM_SPACE) {
+            S_ |= 1u << i;
+          } else {
+            if (act == XM_ISOLATE) I |= 1u << i;
+            else wordc = true;
+            if (e & XM_WRITE) {
+              for (uint32_t q = 0; q < n; ++q) nput(L.nb, p + (int)q, q < T ? (e >> (8 * q)) & 0xFFu : BF);
+              dirty = T < n;
+            }
+          }
+          const uint32_t slo = (uint32_t)span, shi = (uint32_t)(span >> 32);
+          if (wordc) {
+            W |= slo;
+            sp_w |= shi;
+          }
+          if (dirty) {
+            D |= slo;
+            sp_d |= shi;
+          }
+          sp_m |= shi;
+        }
+      }
+      // the full path: exceptions in batches of 4 per lane, the table lookups
+      // of a batch (code point -> page -> entry -> multi expansion) together
+      for (uint32_t xm = xslow; __any(xm != 0);) {
+        constexpr int XB = 4;
         int xi_[XB];
         uint32_t xcp[XB], xt[XB], xe[XB];
         uint4 xmul[XB];
@@ -694,6 +724,26 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
     // every sentence start distinct (no empty sentence shares one): a unit's
     // sentence is the number of starts at or before it, minus one
     const bool starts_distinct = nstarts == ns;
+    // the first break / dirty byte in a later lane (a unit's span end and its
+    // dirtiness come from the lane's own masks and these two positions,
+    // instead of a search of the LDS masks per unit)
+    int nxt_brk, nxt_dirty;
+    {
+      const uint32_t brk = U | (S_ & CS) | SBm;
+      const uint64_t later = lane < 63 ? ~0ull << (lane + 1) : 0ull;
+      const uint64_t mb = __ballot(brk != 0) & later, md = __ballot(D != 0) & later;
+      wsync();  // (L.brk / L.dm of every lane written)
+      nxt_brk = nb;
+      nxt_dirty = CAP;
+      if (mb) {
+        const int j = __ffsll((unsigned long long)mb) - 1;
+        nxt_brk = min(j * 32 + __ffs(L.brk[j]) - 1, nb);
+      }
+      if (md) {
+        const int j = __ffsll((unsigned long long)md) - 1;
+        nxt_dirty = j * 32 + __ffs(L.dm[j]) - 1;
+      }
+    }
     STAMP(4);
     if (wbad) {
       fallback();
@@ -724,15 +774,23 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
               else hi = mid - 1;
             }
           }
-          L.u.urec[u - rb] = (uint32_t)p | ((uint32_t)lo << 16);
+          // span end: the next break (own lane, else a later one); dirty:
+          // a filler / expansion byte in [p, q)
+          const uint32_t brk = U | (S_ & CS) | SBm;
+          const uint32_t rest = brk & ~((2u << b) - 1u);
+          const int q = rest ? min(p0 + __ffs(rest) - 1, nb) : nxt_brk;
+          uint32_t own = D & ~((1u << b) - 1u);
+          if (q < p0 + 32) own &= (1u << (q - p0)) - 1u;
+          const bool dirty = own != 0 || (q > p0 + 32 && nxt_dirty < q);
+          L.u.urec[u - rb] = ur_make(p, q - p, dirty, lo);
         }
       }
       wsync();
       STAMP(5);
-#if TOK5_MERGED_PROBE
-      // ---- 3: prep (spans, dirty words, specials, long words) + the
-      //      whole-word probe of each pending unit (slot 0 of its home
-      //      bucket), one unit per lane: the key is loaded and hashed once
+      // ---- 3: prep (dirty words, specials, long words) + the whole-word
+      //      probe of each pending unit (slot 0 of its home bucket), one
+      //      unit per lane: the key is loaded and hashed once; a special's
+      //      marker is its key's first byte
       {
         const int mb0 = (int)P.maxb[0];
         const uint32_t vmask = P.vt_mask;
@@ -740,29 +798,25 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
           const int u = r + lane;
           uint32_t w = 0;
           uint16_t id = U_EMPTY;
-          if (u < nr) {
-            const int p = (int)(L.u.urec[u] & 0xFFFFu);
-            const uint32_t b0 = nbyte(L.nb, p);
-            if (b0 >= BS && b0 < BS + 5) {
+          const uint32_t x = u < nr ? L.u.urec[u] : 0u;
+          int src = ur_p(x), len = ur_len(x);
+          const bool dirty = ur_dirty(x);
+          if (dirty) len = max(dirty_normalize(L, P, src, src + len, &src), 0);
+          Key6 key = {0, 0, 0, 0, 0, 0};
+          if (len > 0 && len <= 24) key = load_key(L.nb, src, len);
+          if (len > 0) {
+            const uint32_t b0 = key.d0 & 0xFFu;
+            if (!dirty && len <= 24 && b0 >= BS && b0 < BS + 5) {
               id = (uint16_t)P.special[b0 - BS];
+            } else if (len > 100 && count_chars(L.nb, src, len) > 100) {
+              id = (uint16_t)P.unk;
             } else {
-              const int q = span_end(L, p, nb);
-              int src = p, len = q - p;
-              if (span_dirty(L, p, q)) len = max(dirty_normalize(L, P, p, q, &src), 0);
-              if (len == 0) {
-                id = U_EMPTY;
-              } else if (len > 100 && count_chars(L.nb, src, len) > 100) {
-                id = (uint16_t)P.unk;
-              } else {
-                id = U_DEFER;
-                w = wmake(u, src, len);
-                if (len > KEYMAX) L.misc[2] = 1;  // too long for a record: the tile falls back
-              }
+              id = U_DEFER;
+              w = wmake(u, src, len);
+              if (len > KEYMAX) L.misc[2] = 1;  // too long for a record: the tile falls back
             }
           }
-          const int len = wlen(w);
           if (w != 0 && len <= 24 && len <= mb0) {
-            const Key6 key = load_key(L.nb, wsrc(w), len);
             const uint4* bk = P.vt + 4 * (key_hash(key, len, 0u) & vmask);
             const uint4 fa = bk[0], fb = bk[1];
             if (slot_eq(fa, fb, key, ((uint32_t)len << 16) | 0x80000000u)) {
@@ -783,88 +837,6 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
         ovf = true;
         break;
       }
-#else
-      // ---- 3: prep (spans, dirty words, specials, long words) ---------------
-      for (int r = 0; r < nr; r += 64) {
-        const int u = r + lane;
-        if (u < nr) {
-          const int p = (int)(L.u.urec[u] & 0xFFFFu);
-          const uint32_t b0 = nbyte(L.nb, p);
-          uint32_t w = 0;
-          uint16_t id;
-          if (b0 >= BS && b0 < BS + 5) {
-            id = (uint16_t)P.special[b0 - BS];
-          } else {
-            const int q = span_end(L, p, nb);
-            int src = p, len = q - p;
-            if (span_dirty(L, p, q)) len = max(dirty_normalize(L, P, p, q, &src), 0);
-            if (len == 0) {
-              id = U_EMPTY;
-            } else if (len > 100 && count_chars(L.nb, src, len) > 100) {
-              id = (uint16_t)P.unk;
-            } else {
-              id = U_DEFER;
-              w = wmake(u, src, len);
-              if (len > KEYMAX) L.misc[2] = 1;  // too long for a record: the tile falls back
-            }
-          }
-          L.uid[u] = id;
-          L.u.uwp[u] = w;
-        }
-      }
-      wsync();
-      STAMP(6);
-      // ---- 3b: whole-word probe of every pending unit, 4 bucket loads in
-      //      flight per lane; hits are resolved here
-      {
-        const int mb0 = (int)P.maxb[0];
-        const uint32_t vmask = P.vt_mask;
-#define TOK5_FP_ISSUE(k)                                                        \
-  uint4 fa##k = make_uint4(0, 0, 0, 0), fb##k = fa##k;                          \
-  bool fact##k = false;                                                         \
-  {                                                                             \
-    const int u = (k) * 64 + lane;                                              \
-    const uint32_t w = u < nr ? L.u.uwp[u] : 0u;                                \
-    const int len = wlen(w);                                                    \
-    if (w != 0 && len <= 24 && len <= mb0) {                                    \
-      const uint32_t h = key_hash(load_key(L.nb, wsrc(w), len), len, 0u);       \
-      const uint4* bk = P.vt + 4 * (h & vmask);                                 \
-      fa##k = bk[0];                                                            \
-      fb##k = bk[1];                                                            \
-      fact##k = true;                                                           \
-    }                                                                           \
-  }
-#define TOK5_FP_CHECK(k)                                                        \
-  if (fact##k) {                                                                \
-    const int u = (k) * 64 + lane;                                              \
-    const uint32_t w = L.u.uwp[u];                                              \
-    const int len = wlen(w);                                                    \
-    const Key6 key = load_key(L.nb, wsrc(w), len);                              \
-    if (slot_eq(fa##k, fb##k, key, ((uint32_t)len << 16) | 0x80000000u)) {       \
-      L.uid[u] = (uint16_t)(fb##k.z & 0xFFFFu);                                 \
-      L.u.uwp[u] = 0;                                                           \
-    }                                                                           \
-  }
-        // (slot 0 of the home bucket only: checking slot 1 too measured slower)
-        TOK5_FP_ISSUE(0)
-        TOK5_FP_ISSUE(1)
-        TOK5_FP_ISSUE(2)
-        TOK5_FP_ISSUE(3)
-        TOK5_FP_CHECK(0)
-        TOK5_FP_CHECK(1)
-        TOK5_FP_CHECK(2)
-        TOK5_FP_CHECK(3)
-#undef TOK5_FP_ISSUE
-#undef TOK5_FP_CHECK
-        static_assert(UCAP == 256, "first-probe batches are unrolled for 4 units per lane");
-      }
-      wsync();
-      if (L.misc[2]) {
-        ovf = true;
-        break;
-      }
-      STAMP(7);
-#endif
       // ---- 4: entries and records -------------------------------------------
       // Lane l holds units [l*per, l*per + per); segmented (by sentence)
       // exclusive prefix sums give each unit its entry index and its record
@@ -880,12 +852,12 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
         for (int k = 0; k < K; ++k) {
           const int uu = u0 + k;
           valid[k] = k < per && uu < nr;
-          sent[k] = valid[k] ? L.u.urec[uu] >> 16 : 0u;
+          sent[k] = valid[k] ? ur_sent(L.u.urec[uu]) : 0u;
           idv[k] = valid[k] ? (uint32_t)L.uid[uu] : (uint32_t)U_EMPTY;
           ev[k] = idv[k] != U_EMPTY ? 1u : 0u;
-          head[k] = valid[k] && (uu == 0 ? (int)sent[k] != prev_sent : (L.u.urec[uu - 1] >> 16) != sent[k]);
+          head[k] = valid[k] && (uu == 0 ? (int)sent[k] != prev_sent : ur_sent(L.u.urec[uu - 1]) != sent[k]);
         }
-        const int first_sent = (int)(L.u.urec[0] >> 16);
+        const int first_sent = (int)ur_sent(L.u.urec[0]);
         const bool cont = first_sent == prev_sent;
         auto seg_scan = [&](const uint32_t(&v)[K], uint32_t carry, uint32_t(&pre)[K]) {
           uint32_t run = 0, h = 0;
@@ -975,7 +947,7 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
           const int uu = u0 + k;
           const int sj = (int)sent[k];
           const uint32_t e = epre[k], o = spre[k] & 0xFFFFu;
-          if (uu == nr - 1 || (int)(L.u.urec[uu + 1] >> 16) != sj) {  // the sentence's last unit of the round
+          if (uu == nr - 1 || (int)ur_sent(L.u.urec[uu + 1]) != sj) {  // the sentence's last unit of the round
             L.sent_n[sj] = (uint16_t)min(e + ev[k], 65535u);
             L.sslot[sj] = (uint16_t)(o + nsl[k]);
             L.sdef[sj] = (uint16_t)((spre[k] >> 16) + (nsl[k] ? 1u : 0u));
@@ -984,8 +956,7 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
             const int64_t at = (int64_t)L.sst[sj] + e;
             // one store per unit: an id with no queued word before it is final
             // (the output), everything else an entry for expand
-            const bool fin = idv[k] != U_DEFER && o == 0;
-            uint16_t* const dst = fin ? P.out_ids + (obase + at) : S.ent + (ent0 + at);
+            uint16_t* const dst = S.ent + (ent0 + at);
             *dst = (uint16_t)(idv[k] != U_DEFER ? idv[k] : (SPLIT_EDEF | o));
             if (idv[k] != U_DEFER) {
               // ([CLS] / [SEP] come only from literal specials, never from WordPiece)
@@ -1029,7 +1000,7 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
             *recq(S, 1, slot) = make_uint4(kd[2], kd[3], kd[4], kd[5]);
           }
           // key bytes 24..55 (wp_kernel reads them only for a longer key)
-          if (!TOK5_WP_SHORTREF || len > 24) {
+          if (len > 24) {
             uint32_t x[9];
 #pragma unroll
             for (int i = 0; i < 9; ++i) x[i] = L.nb[a + 6 + i];
@@ -1042,17 +1013,13 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
           if (slots == 2) {  // the extension slot: a zero header (skipped by wp_kernel)
             const uint4 z = make_uint4(0, 0, 0, 0);
             *recq(S, 0, slot + 1) = z;
-            if (!TOK5_PCS) {  // (pieces 28.. land in it)
-              *recq(S, 1, slot + 1) = z;
-              *recq(S, 2, slot + 1) = z;
-              *recq(S, 3, slot + 1) = z;
-            }
+            S.cnt8[slot + 1] = 0;  // (its pieces buffer holds pieces 28.. of the word)
           }
         }
         cur += need;
       }
       wsync();
-      prev_sent = (int)(L.u.urec[nr - 1] >> 16);
+      prev_sent = (int)ur_sent(L.u.urec[nr - 1]);
       wsync();
       STAMP(8);
     }  // rounds
@@ -1067,6 +1034,7 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
       // one 8-B record per sentence for expand: entries | first queued entry
       // << 16, first record slot (~0: no queued word)
       S.smeta[s] = make_uint2((uint32_t)ne | (nsl ? (uint32_t)L.sfdef[lane] << 16 : 0u), nsl ? L.sqb[lane] : 0xFFFFFFFFu);
+      S.snslot[s] = (uint16_t)nsl;
       P.out_ntok[s] = ne - (int)L.sdef[lane];
       if (P.sent_spec) P.sent_spec[s] = (uint8_t)((L.sspec[lane >> 5] >> (lane & 31)) & 1u);
     }
@@ -1120,7 +1088,7 @@ __global__ __launch_bounds__(64 * WAVES) void wp_kernel(TokParams P, SplitParams
   int r = -1;    // record slot being tokenised
   int pr = -1;   // record slot loaded, not begun
   uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0, q2 = q0, q3 = q0;
-  bool qlong = false;  // (TOK5_WP_SHORTREF) q2 / q3 of the pending record loaded
+  bool qlong = false;  // q2 / q3 of the pending record loaded
   int s = 0, we = 0, e = 0, np = 0, bslot = -1;
   uint32_t cont = 0;
   bool asc = false;
@@ -1173,12 +1141,10 @@ __global__ __launch_bounds__(64 * WAVES) void wp_kernel(TokParams P, SplitParams
     if (e < we && !(asc && e - s < 24))
       while (e > s && (kbyte(e) & 0xC0u) == 0x80u) --e;
   };
-  // (TOK5_PCS: the pieces and count go to a buffer of their own, so the
+  // (the pieces and count go to a buffer of their own, so the
   // record lines other lanes are still loading stay read-only)
-  static_assert(!TOK5_REC_SOA || TOK5_PCS, "quarter-major records need the separate output buffer");
-  uint4* const outs = TOK5_PCS ? S.pcs : S.rec;
+  uint4* const outs = S.pcs;
   auto rec16 = [&]() { return reinterpret_cast<uint16_t*>(outs + (size_t)r * 4); };
-#if TOK5_WP_REGPCS
   // pieces 0-3 (nearly every word's all) held in two registers and stored
   // with the count in one 12-B store at the end (what expand loads)
   uint32_t pw01 = 0, pw23 = 0;
@@ -1195,15 +1161,9 @@ __global__ __launch_bounds__(64 * WAVES) void wp_kernel(TokParams P, SplitParams
   auto finish = [&]() {
     typedef uint32_t u32x3s __attribute__((ext_vector_type(3)));
     *reinterpret_cast<u32x3s*>(reinterpret_cast<uint32_t*>(outs + (size_t)r * 4) + 1) = u32x3s{(uint32_t)np, pw01, pw23};
+    S.cnt8[r] = (uint8_t)np;
     r = -1;
   };
-#else
-  auto put_piece = [&](int k, uint32_t id) { rec16()[piece_at(k)] = (uint16_t)id; };
-  auto finish = [&]() {
-    reinterpret_cast<uint32_t*>(outs + (size_t)r * 4)[1] = (uint32_t)np;
-    r = -1;
-  };
-#endif
   // optional stamps (P.dbg, LDDL_TOK_DEBUG=1): A (Bloom scan + bucket
   // issue), B (refill issue), C (compare; waits for the loads), D (record
   // start), steps, lane-steps with a record
@@ -1232,7 +1192,7 @@ __global__ __launch_bounds__(64 * WAVES) void wp_kernel(TokParams P, SplitParams
         // equals a vocab key, which is valid UTF-8: its Bloom false
         // positives only cost a failed probe, then shrink() steps back to a
         // character boundary)
-        if ((TOK5_WP_GROUPS_ANY || asc) && len <= 24) {
+        if (len <= 24) {
           int fl = 0;
           int ga = 0;
 #define TOK5_EXT(j, Hj1) \
@@ -1295,15 +1255,10 @@ __global__ __launch_bounds__(64 * WAVES) void wp_kernel(TokParams P, SplitParams
           pr = (int)(c * SPLIT_CHUNK + off + (uint32_t)k);
           q0 = *recq(S, 0, (uint32_t)pr);
           q1 = *recq(S, 1, (uint32_t)pr);
-#if TOK5_WP_SHORTREF
           // key bytes 24.. only for a longer key: loaded at its start (the
           // record begins a step later); a key of <= 24 bytes is zero past them
           q2 = q3 = make_uint4(0, 0, 0, 0);
           qlong = false;
-#else
-          q2 = *recq(S, 2, (uint32_t)pr);
-          q3 = *recq(S, 3, (uint32_t)pr);
-#endif
         }
         off += min((uint32_t)__popcll(idle), avail);
         advance();
@@ -1360,12 +1315,10 @@ __global__ __launch_bounds__(64 * WAVES) void wp_kernel(TokParams P, SplitParams
     if (r < 0 && pr >= 0) {
       if (q0.x == 0u) {  // an extension slot
         pr = -1;
-#if TOK5_WP_SHORTREF
       } else if ((q0.x & 0xFFu) > 24u && !qlong) {
         q2 = *recq(S, 2, (uint32_t)pr);
         q3 = *recq(S, 3, (uint32_t)pr);
         qlong = true;
-#endif
       } else {
         const int len = (int)(q0.x & 0xFFu);
         kb[0] = q0.z; kb[64] = q0.w;
@@ -1400,25 +1353,38 @@ __global__ __launch_bounds__(64 * WAVES) void wp_kernel(TokParams P, SplitParams
   }
 }
 
+// ---------------------------------------------------------------- count --
+// Final token count per sentence of the segment: its direct ids (the scan's
+// entries that are vocab ids) + the pieces of its queued words (wp_kernel's
+// per-slot counts over the sentence's contiguous record slots), capped at
+// max_tok; a fallback tile's sentences keep the count the serial path wrote.
+__global__ __launch_bounds__(256) void count_kernel(TokParams P, SplitParams S) {
+  const int64_t sA = S.tile_sent[S.t0], sB = S.tile_sent[S.t1];
+  for (int64_t s = sA + (int64_t)blockIdx.x * 256 + threadIdx.x; s < sB; s += (int64_t)gridDim.x * 256) {
+    const uint2 m = S.smeta[s];
+    int32_t t = P.out_ntok[s];
+    if ((m.x & 0xFFFFu) != SPLIT_NENT_FB && m.y != 0xFFFFFFFFu) {
+      const uint32_t n = S.snslot[s];
+      for (uint32_t k = 0; k < n; ++k) t += S.cnt8[m.y + k];
+      t = min(t, P.max_tok);
+    }
+    P.out_ntok[s] = t;
+  }
+}
+
 // --------------------------------------------------------------- expand --
-// A wave per group of 64 sentences; their entries in steps of 512 (8 per
-// lane, contiguous).  Per step, two rounds of loads: the entries, then the
-// records' count and first 4 pieces (one 12-B load); a segmented scan of the
-// token counts gives the positions; the sentence's last entry writes its
-// token count (a sentence with no queued word keeps the scan's count).
-#ifndef TOK5_EXP_BLOCKS
-#define TOK5_EXP_BLOCKS 8
-#endif
-#ifndef TOK5_EXP_PER
-#define TOK5_EXP_PER 1
-#endif
-constexpr int EXP_PER = TOK5_EXP_PER;
+// Dense output: a wave per group of 64 sentences; their entries (every one:
+// a vocab id, or a queued word's record) in steps of 64, one per lane.  Per
+// step, two rounds of loads: the entries, then the records' count and first 4
+// pieces (one 12-B load); a segmented scan of the token counts gives each
+// token's position in its sentence, written at out_tok_off[s] + position
+// while below the sentence's final count (count_kernel) and out_cap.
 struct ExpLds {
   uint32_t e0[65];      // group entry offsets
   int64_t eoff[64];     // entry index of the sentence's first entry
   int64_t dst[64];      // output index of its first token
   uint32_t qb[64];      // its first record slot
-  uint32_t f[64];       // entry index of its first queued word (the entries before it are done)
+  uint32_t lim[64];     // tokens it writes: min(final count, out_cap - dst)
 };
 
 __global__ __launch_bounds__(256) void expand_kernel(TokParams P, SplitParams S) {
@@ -1428,29 +1394,22 @@ __global__ __launch_bounds__(256) void expand_kernel(TokParams P, SplitParams S)
   ExpLds& E = X[wv];
   const int64_t sA = uni64(S.tile_sent[S.t0]), sB = uni64(S.tile_sent[S.t1]);
   const int64_t base = P.sent_off[0], ebase = S.t0 << 10;
-  const uint32_t max_tok0 = (uint32_t)P.max_tok;
   const int64_t nwaves = (int64_t)gridDim.x * 4;
   typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
+  const uint4* const pcs = S.pcs;
   for (int64_t g0 = sA + ((int64_t)blockIdx.x * 4 + wv) * 64; g0 < sB; g0 += nwaves * 64) {
     const int64_t s = g0 + lane;
     uint32_t ne = 0;
     if (s < sB) {
-      // entries from the first queued word on (the ids before it are final;
-      // a sentence without queued words or of a fallback tile is done)
       const uint2 m = S.smeta[s];
+      const int32_t nt = P.out_ntok[s];
       ne = m.x & 0xFFFFu;
-      uint32_t f = 0;
-      if (ne == SPLIT_NENT_FB || m.y == 0xFFFFFFFFu) {
-        ne = 0;
-      } else {
-        f = m.x >> 16;
-        ne -= f;
-      }
-      const int64_t so = P.sent_off[s] - base + f;
-      E.eoff[lane] = so - ebase;
-      E.dst[lane] = so;
-      E.qb[lane] = ne ? m.y : 0u;
-      E.f[lane] = f;
+      if (ne == SPLIT_NENT_FB) ne = (uint32_t)nt;  // the serial path's ids, all direct
+      const int64_t d = P.out_tok_off[s];
+      E.eoff[lane] = P.sent_off[s] - base - ebase;
+      E.dst[lane] = d;
+      E.qb[lane] = m.y == 0xFFFFFFFFu ? 0u : m.y;
+      E.lim[lane] = (uint32_t)max((int64_t)0, min((int64_t)nt, P.out_cap - d));
     }
     const uint32_t x = wave_incl_add(ne);
     E.e0[lane] = x - ne;
@@ -1458,10 +1417,10 @@ __global__ __launch_bounds__(256) void expand_kernel(TokParams P, SplitParams S)
     if (lane == 63) E.e0[64] = T;
     wsync();
     uint32_t carry = 0;
-    for (uint32_t st = 0; st < T; st += 64 * EXP_PER) {
-      const uint32_t g = st + (uint32_t)lane * EXP_PER;
+    for (uint32_t st = 0; st < T; st += 64) {
+      const uint32_t g = st + (uint32_t)lane;
       int j = 0;
-      if (g < T) {  // sentence of this lane's first entry: last j with e0[j] <= g
+      if (g < T) {  // sentence of this lane's entry: last j with e0[j] <= g
         int lo = 0, hi = 63;
         while (lo < hi) {
           const int mid = (lo + hi + 1) >> 1;
@@ -1470,76 +1429,36 @@ __global__ __launch_bounds__(256) void expand_kernel(TokParams P, SplitParams S)
         }
         j = lo;
       }
-      int js[EXP_PER];
-      uint32_t kk[EXP_PER], v[EXP_PER], cnt[EXP_PER], pre[EXP_PER];
-      u32x3 rq[EXP_PER];
-#pragma unroll
-      for (int k = 0; k < EXP_PER; ++k) {
-        const uint32_t gg = g + k;
-        while (gg < T && j < 63 && E.e0[j + 1] <= gg) ++j;
-        js[k] = j;
-        kk[k] = gg < T ? gg - E.e0[j] : 0xFFFFFFFFu;
-      }
-#pragma unroll
-      for (int k = 0; k < EXP_PER; ++k) v[k] = kk[k] != 0xFFFFFFFFu ? S.ent[E.eoff[js[k]] + kk[k]] : 0u;
-#pragma unroll
-      for (int k = 0; k < EXP_PER; ++k) {
-        rq[k] = u32x3{1u, 0u, 0u};
-        if (kk[k] != 0xFFFFFFFFu && v[k] >= SPLIT_EDEF)
-          rq[k] = *reinterpret_cast<const u32x3*>(reinterpret_cast<const uint32_t*>(
-                      (TOK5_PCS ? S.pcs : S.rec) + (size_t)(E.qb[js[k]] + (v[k] & 0xFFFu)) * 4) + 1);
-      }
-      uint32_t run = 0, h = 0;
-#pragma unroll
-      for (int k = 0; k < EXP_PER; ++k) {
-        cnt[k] = kk[k] != 0xFFFFFFFFu ? rq[k].x : 0u;
-        if (kk[k] == 0) {
-          run = 0;
-          h = 1;
-        }
-        pre[k] = run;
-        run += cnt[k];
-      }
-      uint32_t hv = h, sv = run;
+      const uint32_t kk = g < T ? g - E.e0[j] : 0xFFFFFFFFu;
+      const uint32_t v = kk != 0xFFFFFFFFu ? S.ent[E.eoff[j] + kk] : 0u;
+      u32x3 rq = u32x3{1u, 0u, 0u};
+      if (kk != 0xFFFFFFFFu && v >= SPLIT_EDEF)
+        rq = *reinterpret_cast<const u32x3*>(reinterpret_cast<const uint32_t*>(pcs + (size_t)(E.qb[j] + (v & 0xFFFu)) * 4) + 1);
+      const uint32_t cnt = kk != 0xFFFFFFFFu ? rq.x : 0u;
+      const uint32_t h = kk == 0 ? 1u : 0u;
+      uint32_t hv = h, sv = cnt;
       wave_seg_incl_add(hv, sv);
       uint32_t ex = wave_shr1(sv);
       if (!wave_shr1(hv)) ex += carry;
-      bool before = true;
-#pragma unroll
-      for (int k = 0; k < EXP_PER; ++k) {
-        if (kk[k] == 0) before = false;
-        if (before) pre[k] += ex;
-      }
-#pragma unroll
-      for (int k = 0; k < EXP_PER; ++k) {
-        if (kk[k] == 0xFFFFFFFFu) continue;
-        const int jj = js[k];
-        uint16_t* o = P.out_ids + E.dst[jj];
-        const uint32_t p = pre[k];
-        const uint32_t max_tok = max_tok0 - E.f[jj];  // (entries are kept below max_tok: f < max_tok)
+      const uint32_t p = h ? 0u : ex;  // tokens of the sentence before this entry
+      if (kk != 0xFFFFFFFFu) {
+        uint16_t* o = P.out_ids + E.dst[j];
+        const uint32_t lim = E.lim[j];
         // (the first token of a direct id and of a record in one store)
-        if (p < max_tok) o[p] = (uint16_t)(v[k] < SPLIT_EDEF ? v[k] : rq[k].y & 0xFFFFu);
-        if (v[k] >= SPLIT_EDEF) {
-          const uint32_t c = cnt[k];
-          if (c > 1 && p + 1 < max_tok) o[p + 1] = (uint16_t)(rq[k].y >> 16);
-          if (c > 2 && p + 2 < max_tok) o[p + 2] = (uint16_t)(rq[k].z & 0xFFFFu);
-          if (c > 3 && p + 3 < max_tok) o[p + 3] = (uint16_t)(rq[k].z >> 16);
-          if (c > 4) {
-            const uint16_t* pc =
-                reinterpret_cast<const uint16_t*>((TOK5_PCS ? S.pcs : S.rec) + (size_t)(E.qb[jj] + (v[k] & 0xFFFu)) * 4);
-            for (uint32_t q = 4; q < c && p + q < max_tok; ++q) o[p + q] = pc[piece_at((int)q)];
+        if (p < lim) o[p] = (uint16_t)(v < SPLIT_EDEF ? v : rq.y & 0xFFFFu);
+        if (v >= SPLIT_EDEF) {
+          if (cnt > 1 && p + 1 < lim) o[p + 1] = (uint16_t)(rq.y >> 16);
+          if (cnt > 2 && p + 2 < lim) o[p + 2] = (uint16_t)(rq.z & 0xFFFFu);
+          if (cnt > 3 && p + 3 < lim) o[p + 3] = (uint16_t)(rq.z >> 16);
+          if (cnt > 4) {
+            const uint16_t* pc = reinterpret_cast<const uint16_t*>(pcs + (size_t)(E.qb[j] + (v & 0xFFFu)) * 4);
+            for (uint32_t q = 4; q < cnt && p + q < lim; ++q) o[p + q] = pc[piece_at((int)q)];
           }
         }
-        if (kk[k] + 1 == E.e0[jj + 1] - E.e0[jj]) P.out_ntok[g0 + jj] = (int32_t)min(E.f[jj] + p + cnt[k], max_tok0);
       }
       // running total of the step's last entry (its sentence may continue)
-      const uint32_t lastg = min(T, st + 64 * EXP_PER) - 1 - st;
-      const int ll = (int)(lastg / EXP_PER), lk = (int)(lastg % EXP_PER);
-      uint32_t mytot = 0;
-#pragma unroll
-      for (int k = 0; k < EXP_PER; ++k)
-        if (k == lk) mytot = pre[k] + cnt[k];
-      carry = lane_get(mytot, ll);
+      const uint32_t ll = min(T, st + 64) - 1 - st;
+      carry = lane_get(p + cnt, (int)ll);
     }
     wsync();
   }
@@ -1576,14 +1495,39 @@ static hipError_t launch_wp(const TokParams& P, const SplitParams& S, int n_cu, 
 }  // namespace tok5
 
 constexpr int SCAN_WAVES = 4, WP_WAVES = 12;
+hipError_t finish_segment(TokParams P, const SplitParams& S, int n_cu, int fb_grid, hipStream_t s);
 
-int64_t split_seg_slots(int64_t seg_tiles) {
+int64_t split_seg_slots(int64_t seg_tiles, int n_cu) {
   // 1 slot per 14 input bytes (the synthetic Wikipedia corpus queues ~0.02
   // words per byte, the CodeSearchNet-style code corpus ~0.065) + one partly
-  // used chunk per scanning wave; past it tiles fall back to the serial path
-  const int64_t waves = 256 * 32;
+  // used chunk per scanning wave of the real grid; past it tiles fall back to
+  // the serial path (counted: lddl_tokenize_stats)
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, tok5::scan_kernel<SCAN_WAVES, false, 5>, 64 * SCAN_WAVES,
+                                                   0) != hipSuccess || per_cu < 1)
+    per_cu = 8;
+  const int64_t waves = (int64_t)n_cu * per_cu * SCAN_WAVES;
   const int64_t chunks = (seg_tiles * 1024 / 14 + SPLIT_CHUNK - 1) / SPLIT_CHUNK + std::min(waves, seg_tiles) + 16;
   return chunks * SPLIT_CHUNK;
+}
+
+__global__ void smeta_fallback_kernel(uint2* smeta, int64_t n_sent) {
+  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n_sent; s += (int64_t)gridDim.x * blockDim.x)
+    smeta[s] = make_uint2(SPLIT_NENT_FB, 0xFFFFFFFFu);
+}
+
+hipError_t launch_tokenize_serial_dense(const TokParams& P, int64_t nbytes, int64_t* tile_sent, SplitParams S,
+                                        int n_cu, int fb_grid, hipStream_t s) {
+  const int64_t n_tiles = tile_count(nbytes);
+  hipError_t e = launch_tile_bounds(P.sent_off, P.n_sent, n_tiles, tile_sent, s);
+  if (e != hipSuccess || (e = hipMemsetAsync(P.out_tok_off, 0, sizeof(int64_t), s)) != hipSuccess) return e;
+  S.tile_sent = tile_sent;
+  S.t0 = 0;
+  S.t1 = n_tiles;
+  if ((e = launch_list_all_tiles(n_tiles, S.fb_list, S.fb_count, s)) != hipSuccess) return e;
+  hipLaunchKernelGGL(smeta_fallback_kernel, dim3(1024), dim3(256), 0, s, S.smeta, P.n_sent);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  return finish_segment(P, S, n_cu, fb_grid, s);
 }
 
 hipError_t launch_tokenize_split(const TokParams& P, int64_t nbytes, int64_t* tile_sent, SplitParams S, int n_cu,
@@ -1598,13 +1542,14 @@ hipError_t launch_tokenize_split(const TokParams& P, int64_t nbytes, int64_t* ti
   const int64_t n_tiles = tile_count(nbytes);
   hipError_t e = launch_tile_bounds(P.sent_off, P.n_sent, n_tiles, tile_sent, s);
   if (e != hipSuccess) return e;
-  if ((e = hipMemsetAsync(S.fb_count, 0, 4, s)) != hipSuccess) return e;
+  if ((e = hipMemsetAsync(P.out_tok_off, 0, sizeof(int64_t), s)) != hipSuccess) return e;
   S.tile_sent = tile_sent;
   const int64_t seg = S.seg_tiles > 0 ? S.seg_tiles : SPLIT_SEG_TILES;
   for (int64_t t0 = 0; t0 < n_tiles; t0 += seg) {
     S.t0 = t0;
     S.t1 = std::min(n_tiles, t0 + seg);
     if ((e = hipMemsetAsync(S.chunk_ctr, 0, 4, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(S.fb_count, 0, 4, s)) != hipSuccess) return e;
     // cfg (LDDL_TOK5_CFG, tuning): 1 = registers unconstrained (4 waves/SIMD)
     if ((e = mark(0, 0)) != hipSuccess) return e;
     if (P.dbg) e = tok5::launch_scan<SCAN_WAVES, true, 5>(P, S, n_cu, s);
@@ -1613,10 +1558,27 @@ hipError_t launch_tokenize_split(const TokParams& P, int64_t nbytes, int64_t* ti
     if (e != hipSuccess || (e = mark(0, 1)) != hipSuccess || (e = mark(1, 0)) != hipSuccess) return e;
     if ((e = tok5::launch_wp<WP_WAVES>(P, S, n_cu, s)) != hipSuccess) return e;
     if ((e = mark(1, 1)) != hipSuccess || (e = mark(2, 0)) != hipSuccess) return e;
-    hipLaunchKernelGGL(tok5::expand_kernel, dim3((unsigned)std::max(1, n_cu * TOK5_EXP_BLOCKS)), dim3(256), 0, s, P, S);
-    if ((e = hipGetLastError()) != hipSuccess || (e = mark(2, 1)) != hipSuccess) return e;
+    if ((e = finish_segment(P, S, n_cu, fb_grid, s)) != hipSuccess || (e = mark(2, 1)) != hipSuccess) return e;
   }
-  return launch_tokenize_fallback(P, tile_sent, S.fb_list, S.fb_count, fb_grid, s);
+  return hipSuccess;
+}
+
+// The end of a segment: the serial path over the tiles the scan listed (its
+// ids into the segment's entry buffer, as direct ids), the final counts, their
+// exclusive scan continuing the previous segment's (out_tok_off), and the
+// dense ids.
+hipError_t finish_segment(TokParams P, const SplitParams& S, int n_cu, int fb_grid, hipStream_t s) {
+  TokParams F = P;
+  F.out_ids = S.ent - (S.t0 << 10);  // the serial path writes at sent_off[s] - sent_off[0]
+  hipError_t e = launch_tokenize_fallback(F, S.tile_sent, S.fb_list, S.fb_count, fb_grid, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(tok5::count_kernel, dim3((unsigned)std::max(1, n_cu * 8)), dim3(256), 0, s, P, S);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  if ((e = launch_scan_ntok_range(P.out_ntok, S.tile_sent + S.t0, S.tile_sent + S.t1, S.seg_sent_cap, P.out_tok_off,
+                                  S.scan_bsum, s)) != hipSuccess)
+    return e;
+  hipLaunchKernelGGL(tok5::expand_kernel, dim3((unsigned)std::max(1, n_cu * 8)), dim3(256), 0, s, P, S);
+  return hipGetLastError();
 }
 
 }  // namespace lddl

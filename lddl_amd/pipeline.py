@@ -100,8 +100,9 @@ class PackResult:
   bins: torch.Tensor       # uint8
   part: torch.Tensor       # int64
   bin_count: torch.Tensor  # int64 [n_part, nbins]
-  ids: torch.Tensor = None
+  ids: torch.Tensor = None       # the tokenizer's dense ids (sentence s at ids_off[s])
   ntok: torch.Tensor = None
+  ids_off: torch.Tensor = None
   n_masked: int = 0
   mlm_off: torch.Tensor = None    # int64 [n_pairs + 1] (masking only)
   mlm_pos: torch.Tensor = None    # int16 view of uint16 positions (row coordinates)
@@ -153,25 +154,34 @@ class Packer:
     return t
 
   def tokenize(self, shards, max_tok=512, stream=None):
-    ids = self._buf('ids', shards.nbytes, torch.int16)
+    """-> (ids, ntok, tok_off): the dense CSR ids (lddl_tokenize)"""
+    ids = self._buf('ids', shards.nbytes + 16, torch.int16)
     ntok = self._buf('ntok', shards.n_sent, torch.int32)
-    return self.tok.tokenize_device(shards.data, shards.sent_off, max_tok, ids, ntok, stream, nbytes=shards.nbytes)
+    toff = self._buf('tok_off_in', shards.n_sent + 1, torch.int64)
+    return self.tok.tokenize_device(shards.data, shards.sent_off, max_tok, ids, ntok, toff, stream,
+                                    nbytes=shards.nbytes)
 
-  def pack(self, shards, ids, ntok, target_seq_length=128, short_seq_prob=0.1, duplicate_factor=5,
+  def pack(self, shards, ids, ntok, tok_off=None, target_seq_length=128, short_seq_prob=0.1, duplicate_factor=5,
            seed=12345, bin_size=None, codebert=False, masking=False, masked_lm_ratio=0.15, stream=None):
+    """ids / ntok / tok_off: tokenize()'s dense CSR result (tok_off None:
+    the exclusive scan of ntok, for ids built by hand); ids must hold 16
+    entries of padding past the last id (lddl_materialize's 16-B loads)"""
     L = _lib.lib()
+    if tok_off is None:
+      tok_off = torch.zeros(shards.n_sent + 1, dtype=torch.int64, device=self.device)
+      torch.cumsum(ntok[:shards.n_sent].to(torch.int64), 0, out=tok_off[1:])
     tot = (ctypes.c_int64 * 4)()
     s = _stream(stream)
     if codebert:
       if shards.doc_nseg_doc is None:
         raise ValueError('CodeBERT packing needs doc_nseg_doc')
-      rc = L.lddl_pack_codebert(self.tok.handle, _ptr(ntok), _ptr(shards.sent_off), shards.n_sent,
+      rc = L.lddl_pack_codebert(self.tok.handle, _ptr(ntok), _ptr(tok_off), _ptr(shards.sent_off), shards.n_sent,
                                 _ptr(shards.doc_sent_off), _ptr(shards.doc_nseg_doc), shards.n_doc,
                                 _ptr(shards.part_doc_off), shards.n_part, target_seq_length, short_seq_prob,
                                 duplicate_factor, abs(int(seed)), bin_size or 0, tot, s)
     else:
-      rc = L.lddl_pack_bert(self.tok.handle, _ptr(ids) if masking else None, _ptr(ntok), _ptr(shards.sent_off),
-                            shards.n_sent,
+      rc = L.lddl_pack_bert(self.tok.handle, _ptr(ids) if masking else None, _ptr(ntok), _ptr(tok_off),
+                            _ptr(shards.sent_off), shards.n_sent,
                             _ptr(shards.doc_sent_off), shards.n_doc, _ptr(shards.part_doc_off), shards.n_part,
                             target_seq_length, short_seq_prob, duplicate_factor, 1 if masking else 0,
                             masked_lm_ratio, abs(int(seed)), bin_size or 0, tot, s)
@@ -191,7 +201,7 @@ class Packer:
                                   _ptr(res.len0), _ptr(res.len1), _ptr(res.flags), _ptr(res.bins),
                                   _ptr(res.part), _ptr(res.bin_count), s))
     res.bin_count = res.bin_count[:shards.n_part * nbins].view(shards.n_part, nbins)
-    res.ids, res.ntok = ids, ntok
+    res.ids, res.ntok, res.ids_off = ids, ntok, tok_off
     if masking and not codebert:
       res.n_masked = int(tot[3])
       res.mlm_off = self._buf('mlm_off', n_pairs + 1, torch.int64)
@@ -201,8 +211,7 @@ class Packer:
     return res
 
   def run(self, shards, **kw):
-    ids, ntok = self.tokenize(shards)
-    return self.pack(shards, ids, ntok, **kw)
+    return self.pack(shards, *self.tokenize(shards), **kw)
 
 
 def run_bert(corpus, vocab_file=VOCAB_BERT, target_seq_length=128, bin_size=None, n_partitions=1, seed=12345,

@@ -416,9 +416,9 @@ def main(args, codebert=False):
         futs[c + ahead] = submit(c + ahead)  # overlaps this chunk's GPU work and parquet writes
       t0 = time.perf_counter()
       sh = pipeline.upload(corpus, pro[a:b + 1] - pro[a], device)
-      ids_d, ntok = pk.tokenize(sh)
+      ids_d, ntok, toff = pk.tokenize(sh)
       # partition p packs after random.seed(args.seed + global p)
-      res = pk.pack(sh, ids_d, ntok, target_seq_length=args.target_seq_length, short_seq_prob=args.short_seq_prob,
+      res = pk.pack(sh, ids_d, ntok, toff, target_seq_length=args.target_seq_length, short_seq_prob=args.short_seq_prob,
                     duplicate_factor=args.duplicate_factor, seed=args.seed + a, bin_size=args.bin_size,
                     codebert=codebert, masking=args.masking and not codebert, masked_lm_ratio=args.masked_lm_ratio)
       counts[a - lo:b - lo] = res.bin_count.view(b - a, -1).to(torch.int64)

@@ -62,24 +62,31 @@ class Tokenizer:
     return self._h
 
   # ---- batched hot path -------------------------------------------------
-  def tokenize_device(self, data, sent_off, max_tok=512, out_ids=None, out_ntok=None, stream=None,
+  def tokenize_device(self, data, sent_off, max_tok=512, out_ids=None, out_ntok=None, out_tok_off=None, stream=None,
                       nbytes=None):
     """data: uint8 cuda tensor; sent_off: int64 cuda tensor [n_sent+1].
-    Returns (ids int16 view of uint16 [nbytes], ntok int32 [n_sent]); sentence
-    s's ids start at sent_off[s] - sent_off[0].  nbytes = sent_off[-1] -
-    sent_off[0] (default: data.numel(), i.e. data holds no padding)."""
+    Returns the dense CSR result (ids, ntok, tok_off): ids int16 view of
+    uint16, sentence s's ids at ids[tok_off[s]:tok_off[s+1]], ntok int32
+    [n_sent] = their counts, tok_off int64 [n_sent+1].  nbytes = sent_off[-1]
+    - sent_off[0] (default: data.numel(), i.e. data holds no padding).  The
+    default ids buffer holds nbytes + 16 entries (#tokens <= #bytes, plus the
+    16-entry pad lddl_materialize reads); a smaller out_ids must be checked
+    by the caller against tok_off[n_sent] (lddl_tokenize out_cap)."""
     n_sent = sent_off.numel() - 1
     if nbytes is None:
       nbytes = int(data.numel())
     if out_ids is None:
-      out_ids = torch.empty(max(nbytes, 1), dtype=torch.int16, device=self.device)
+      out_ids = torch.empty(max(nbytes, 1) + 16, dtype=torch.int16, device=self.device)
     if out_ntok is None:
       out_ntok = torch.empty(max(n_sent, 1), dtype=torch.int32, device=self.device)
+    if out_tok_off is None:
+      out_tok_off = torch.empty(n_sent + 1, dtype=torch.int64, device=self.device)
     assert data.dtype == torch.uint8 and sent_off.dtype == torch.int64
-    assert data.is_cuda and sent_off.is_cuda and out_ids.numel() >= nbytes
+    assert data.is_cuda and sent_off.is_cuda and out_tok_off.numel() >= n_sent + 1
+    cap = max(0, out_ids.numel() - 16)
     _lib.check(_lib.lib().lddl_tokenize(self._h, _ptr(data), nbytes, _ptr(sent_off), n_sent, max_tok,
-                                        _ptr(out_ids), _ptr(out_ntok), _stream(stream)))
-    return out_ids, out_ntok
+                                        _ptr(out_ids), cap, _ptr(out_ntok), _ptr(out_tok_off), _stream(stream)))
+    return out_ids, out_ntok, out_tok_off
 
   def set_special_flags(self, on=True):
     """following tokenize calls record per-sentence [CLS]/[SEP] flags for a
@@ -91,13 +98,14 @@ class Tokenizer:
     _lib.check(_lib.lib().lddl_set_timing(self.handle, 1 if on else 0))
 
   def stats(self):
-    """{'scan_ms', 'wordpiece_ms', 'expand_ms' (summed over the call's
-    segments), 'records', 'launches' (segments)} of the last call
+    """{'scan_ms', 'wordpiece_ms', 'expand_ms' (finish: serial-path tiles,
+    counts, offset scan, dense expand; summed over the call's segments),
+    'records', 'launches' (segments), 'fallback_tiles'} of the last call
     (synchronises on its events)"""
-    out = (ctypes.c_double * 5)()
-    _lib.check(_lib.lib().lddl_tokenize_stats(self.handle, out, 5))
+    out = (ctypes.c_double * 6)()
+    _lib.check(_lib.lib().lddl_tokenize_stats(self.handle, out, 6))
     return {'scan_ms': out[0], 'wordpiece_ms': out[1], 'expand_ms': out[2], 'records': int(out[3]),
-            'launches': int(out[4])}
+            'launches': int(out[4]), 'fallback_tiles': int(out[5])}
 
   def encode_batch(self, sentences, max_tok=512):
     """list[str] -> list[list[int]] (compact host result)."""
@@ -107,16 +115,16 @@ class Tokenizer:
     raw = np.frombuffer(b''.join(enc) + b'\0' * 16, dtype=np.uint8)
     d = torch.from_numpy(raw.copy()).to(self.device)
     o = torch.from_numpy(off).to(self.device)
-    ids, ntok = self.tokenize_device(d, o, max_tok)
+    ids, ntok, toff = self.tokenize_device(d, o, max_tok)
     ids = ids.cpu().numpy().view(np.uint16)
-    ntok = ntok.cpu().numpy()
-    return [ids[off[i]:off[i] + ntok[i]].astype(np.int64).tolist() for i in range(len(enc))]
+    toff = toff.cpu().numpy()
+    return [ids[toff[i]:toff[i + 1]].astype(np.int64).tolist() for i in range(len(enc))]
 
   # ---- reference-compatible surface --------------------------------------
   def tokenize(self, text, max_length=512, truncation=True, **kwargs):
     """Same result as BertTokenizerFast.tokenize as called at pretrain.py:79-80
     under transformers 4.16.2 (per-sentence truncation to max_length)."""
-    ids = self.encode_batch([text], max_length if truncation else 1 << 30)[0]
+    ids = self.encode_batch([text], max_length if truncation else 65534)[0]
     return [self.ids_to_tokens[i] for i in ids]
 
   def convert_tokens_to_ids(self, tokens):

@@ -18,7 +18,7 @@ def shards_from_docs(docs, nseg=None, part_doc_off=None, device='cuda'):
   ntok = np.array([len(s) for s in sents], dtype=np.int32)
   off = np.zeros(len(sents) + 1, dtype=np.int64)
   np.cumsum(ntok, out=off[1:])
-  ids = np.array([t for s in sents for t in s] + [0], dtype=np.uint16)
+  ids = np.array([t for s in sents for t in s] + [0] * 16, dtype=np.uint16)  # (+16: materialize's 16-B loads)
   dso = np.zeros(len(docs) + 1, dtype=np.int64)
   np.cumsum([len(d) for d in docs], out=dso[1:])
   pdo = np.array(part_doc_off if part_doc_off is not None else [0, len(docs)], dtype=np.int64)
@@ -354,8 +354,8 @@ def test_masked_special_flags_from_tokenizer(gpu):
   c = corpus_from_sentences(sents, dso)
   pk = pipeline.Packer(pipeline.VOCAB_BERT, 0, masking=True)
   sh = pipeline.upload(c, pipeline.partition_by_bytes(c, 3), torch.device('cuda', 0))
-  ids, ntok = pk.tokenize(sh)
+  ids, ntok, toff = pk.tokenize(sh)
   kw = dict(target_seq_length=128, duplicate_factor=2, seed=3, bin_size=32, masking=True)
-  a = pk.pack(sh, ids, ntok, **kw).rows()
-  b = pk.pack(sh, ids.clone(), ntok, **kw).rows()
+  a = pk.pack(sh, ids, ntok, toff, **kw).rows()
+  b = pk.pack(sh, ids.clone(), ntok, toff, **kw).rows()
   assert len(a) == len(b) and a == b

@@ -10,12 +10,28 @@ from test_oracle_golden import VOCABS
 pytestmark = pytest.mark.gpu
 
 
+def sparse_of_dense(ids, ntok, tok_off, sent_off, nbytes):
+  """the dense CSR ids placed at their sentences' byte offsets (the oracle's
+  layout, oracle.compact reads it), after checking the CSR invariants"""
+  assert tok_off[0] == 0 and np.array_equal(np.diff(tok_off), ntok)
+  total = int(tok_off[-1])
+  sp = np.zeros(nbytes + 16, dtype=np.uint16)
+  starts = np.asarray(sent_off[:-1]) - sent_off[0]
+  idx = np.repeat(starts, ntok) + (np.arange(total) - np.repeat(tok_off[:-1], ntok))
+  sp[idx] = ids[:total]
+  return sp
+
+
 def run_hip(tok, data, sent_off, max_tok=512):
+  """lddl_tokenize's dense output, in the oracle's sparse layout"""
   d = torch.from_numpy(np.concatenate([data, np.zeros(16, np.uint8)])).cuda()
   o = torch.from_numpy(np.ascontiguousarray(sent_off)).cuda()
-  ids, ntok = tok.tokenize_device(d, o, max_tok)
+  ids, ntok, toff = tok.tokenize_device(d, o, max_tok)
   torch.cuda.synchronize()
-  return ids.cpu().numpy().view(np.uint16), ntok.cpu().numpy()[:len(sent_off) - 1]
+  n = len(sent_off) - 1
+  ntok = ntok.cpu().numpy()[:n]
+  ids = ids.cpu().numpy().view(np.uint16)
+  return sparse_of_dense(ids, ntok, toff.cpu().numpy()[:n + 1], sent_off, len(data)), ntok
 
 
 @pytest.mark.parametrize('name', ['bert', 'codebert'])

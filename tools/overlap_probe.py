@@ -29,8 +29,8 @@ def main():
   kw = dict(target_seq_length=args.target_seq_length, short_seq_prob=0.1, duplicate_factor=args.duplicate_factor,
             seed=args.seed, bin_size=args.bin_size)
   s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
-  ids2, ntok2 = pk2.tokenize(sh, stream=s2)
-  pk2.pack(sh, ids2, ntok2, stream=s2, **kw)
+  ids2, ntok2, toff2 = pk2.tokenize(sh, stream=s2)
+  pk2.pack(sh, ids2, ntok2, toff2, stream=s2, **kw)
   pk1.tokenize(sh, stream=s1)
   torch.cuda.synchronize()
 
@@ -39,7 +39,7 @@ def main():
     s1.synchronize()
 
   def pack():
-    pk2.pack(sh, ids2, ntok2, stream=s2, **kw)
+    pk2.pack(sh, ids2, ntok2, toff2, stream=s2, **kw)
     s2.synchronize()
 
   def timed(fns, reps=3):

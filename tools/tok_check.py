@@ -38,14 +38,15 @@ def main():
     os.environ['LDDL_TOKENIZE_ALGO'] = algo
     os.environ['LDDL_TOK5_CFG'] = cfg or '0'
     tok = Tokenizer()
-    ids, ntok = tok.tokenize_device(d, o)
+    ids, ntok, toff = tok.tokenize_device(d, o)
     torch.cuda.synchronize()
     h_ntok = ntok.cpu().numpy()[:c.n_sent]
+    h_toff = toff.cpu().numpy()
     h_ids = ids.cpu().numpy().view(np.uint16)
     bad = np.nonzero(h_ntok[:ns_chk] != ontok)[0]
     nbad_ids = 0
     if len(bad) == 0:
-      for i, (a, b) in enumerate(zip(compact(h_ids, h_ntok[:ns_chk], c.sent_off[:ns_chk + 1]),
+      for i, (a, b) in enumerate(zip([h_ids[h_toff[k]:h_toff[k + 1]] for k in range(ns_chk)],
                                      compact(oids, ontok, c.sent_off[:ns_chk + 1]))):
         if not np.array_equal(a.astype(np.int64), b.astype(np.int64)):
           nbad_ids += 1
@@ -63,7 +64,7 @@ def main():
     for _ in range(3):
       s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
       s.record()
-      tok.tokenize_device(d, o, out_ids=ids, out_ntok=ntok)
+      tok.tokenize_device(d, o, out_ids=ids, out_ntok=ntok, out_tok_off=toff)
       e.record()
       torch.cuda.synchronize()
       times.append(s.elapsed_time(e))
@@ -71,9 +72,9 @@ def main():
         ks.append(tok.stats())
     ms = min(times)
     if ks:
-      print('  per kernel (min of 3): scan %.3f  wordpiece %.3f  expand %.3f ms; %d records' % (
+      print('  per kernel (min of 3): scan %.3f  wordpiece %.3f  finish %.3f ms; %d records, %d fallback tiles' % (
           min(k['scan_ms'] for k in ks), min(k['wordpiece_ms'] for k in ks), min(k['expand_ms'] for k in ks),
-          ks[0]['records']))
+          ks[0]['records'], ks[0]['fallback_tiles']))
     print('variant %s: parity(%d sents) %s (ntok bad %d, ids bad %d)  %.3f ms  %.1f GB/s  %.2f Gtok/s' % (
         v, ns_chk, 'OK' if ok else 'FAIL', len(bad), nbad_ids, ms, c.nbytes / ms / 1e6, ntoks / ms / 1e6),
           flush=True)
