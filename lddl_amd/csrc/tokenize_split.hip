@@ -932,6 +932,9 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
             const uint32_t from = L.sqb[first_sent];
             for (int k = 0; k < 4; ++k)
               for (uint32_t i = lane; i < carried; i += 64) *recq(S, k, cur + i) = *recq(S, k, from + i);
+            // (piece counts: wp_kernel writes the moved words' own; the moved
+            // extension slots count 0)
+            for (uint32_t i = lane; i < carried; i += 64) S.cnt8[cur + i] = 0;
             if (lane == 0) L.sqb[first_sent] = cur;
             cur += carried;
           }

@@ -174,3 +174,23 @@ def test_hip_tokenize_split_segments_and_capacity(gpu, monkeypatch, env, name):
     assert np.array_equal(ntok, ontok)
     for a, b in zip(compact(ids, ntok, c.sent_off), compact(oids, ontok, c.sent_off)):
       assert np.array_equal(a.astype(np.int64), b.astype(np.int64))
+
+
+def test_repeated_calls_reuse_scratch(gpu):
+  """one Tokenizer, scratch reused across calls: a second corpus after a
+  first one (record slots, piece counts and entry buffers hold the first
+  call's values) and the same corpus twice give the oracle's result -- a
+  word moved to a new record chunk with its sentence keeps no stale count"""
+  from lddl_amd import synth
+  from lddl_amd.tokenizer import Tokenizer
+  tok = Tokenizer(VOCABS['bert'])
+  a = synth.make_wiki(6_000_000, seed=21)
+  b = synth.make_wiki(5_000_000, seed=22)
+  run_hip(tok, a.data, a.sent_off)
+  oids, ontok = OracleTokenizer(VOCABS['bert']).run(b.data, b.sent_off, 512, nthreads=8)
+  for _ in range(2):
+    ids, ntok = run_hip(tok, b.data, b.sent_off)
+    assert np.array_equal(ntok, ontok)
+    starts = b.sent_off[:-1] - b.sent_off[0]
+    idx = np.repeat(starts, ntok) + (np.arange(ntok.sum()) - np.repeat(np.cumsum(ntok) - ntok, ntok))
+    assert np.array_equal(ids[idx].astype(np.int64), oids[idx].astype(np.int64))
