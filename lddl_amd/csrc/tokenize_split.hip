@@ -60,11 +60,6 @@ __device__ __forceinline__ uint32_t xm_act(uint32_t e) { return (e >> 27) & 3u; 
 enum : uint32_t { C_W = 1, C_I = 2, C_S = 4, C_D = 8, C_UP = 16, C_X = 32, C_CS = 64 };
 constexpr uint16_t U_EMPTY = 0xFFFEu, U_DEFER = 0xFFFFu;
 
-// work entry of a pending unit: unit | window position << 8 | byte length << 20
-__device__ __forceinline__ uint32_t wmake(int u, int src, int len) {
-  return (uint32_t)u | ((uint32_t)src << 8) | ((uint32_t)len << 20);
-}
-__device__ __forceinline__ int wsrc(uint32_t w) { return (int)((w >> 8) & 0xFFFu); }
 // unit record: window position (11 bits) | span length << 11 (12) | dirty << 23 | sentence << 24
 __device__ __forceinline__ uint32_t ur_make(int p, int len, bool dirty, int sent) {
   return (uint32_t)p | ((uint32_t)len << 11) | ((uint32_t)dirty << 23) | ((uint32_t)sent << 24);
@@ -73,26 +68,22 @@ __device__ __forceinline__ int ur_p(uint32_t x) { return (int)(x & 0x7FFu); }
 __device__ __forceinline__ int ur_len(uint32_t x) { return (int)((x >> 11) & 0xFFFu); }
 __device__ __forceinline__ bool ur_dirty(uint32_t x) { return (x >> 23) & 1u; }
 __device__ __forceinline__ uint32_t ur_sent(uint32_t x) { return x >> 24; }
-__device__ __forceinline__ int wlen(uint32_t w) { return (int)(w >> 20); }
 
 struct alignas(16) Lds {
   union {
     uint32_t rp[CAP / 4 + 4];  // phase 1: raw bytes of the tile (LDS-DMA)
     struct {
-      uint32_t urec[UCAP];     // window position | sentence << 16
-      uint32_t uwp[UCAP];      // pending unit (wmake), 0 once resolved
+      uint32_t urec[UCAP];     // unit records of the round (ur_make)
     } u;
   };
   uint32_t pb[8];              // the tile's bounds: tile_sent[t], tile_sent[t+1], sent_off of both (LDS-DMA)
   uint32_t nb[NBUF / 4];       // normalised bytes in window coordinates; side buffer at [CAP, CAP+DCAP)
   uint32_t brk[64];            // break bits: unit starts, spaces, sentence starts
+  uint32_t um[64];             // unit-start bits
   uint32_t dm[64];             // dirty bits: filler / expansion marker bytes
   uint32_t sb[64];             // sentence-start bits
-  uint16_t uid[UCAP];          // vocab id, U_EMPTY (no token) or U_DEFER (queued); in phase 4
-                               // (once read) the queued units of the round in unit order
   uint32_t sqb[NSCAP];         // record index of the sentence's first slot
   uint16_t sdef[NSCAP];        // queued entries below max_tok
-  uint16_t sfdef[NSCAP];       // entry index of the first queued word (< max_tok)
   uint16_t sst[NSCAP + 2];     // sentence starts (window coordinates)
   uint16_t sent_n[NSCAP];      // entries so far (uncapped)
   uint16_t sslot[NSCAP];       // record slots so far
@@ -711,6 +702,7 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
       const uint32_t pw = (W << 1) | (lane ? carry : 0u);
       U = CS & (I | (W & (~pw | SBm)));
       L.brk[lane] = U | (S_ & CS) | SBm;
+      L.um[lane] = U;
       L.dm[lane] = D;
       const uint32_t v = (uint32_t)__popc(U) | ((uint32_t)__popc(SBm) << 16);
       const uint32_t x = wave_incl_add(v);
@@ -757,14 +749,17 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
       const int nr = min(UCAP, n - rb);
       if (lane == 0) L.misc[0] = 0;
       {
+        // (the lane's masks from LDS: no register holds them across the
+        // per-unit work of the round)
+        const uint32_t Ul = L.um[lane], brk = L.brk[lane], Dl = L.dm[lane], SBl = L.sb[lane];
         const int p0 = lane * 32;
         int u = ub;
-        for (uint32_t m = U; m; m &= m - 1, ++u) {
+        for (uint32_t m = Ul; m; m &= m - 1, ++u) {
           if (u < rb || u >= rb + nr) continue;
           const int b = __ffs(m) - 1, p = p0 + b;
           int lo;
           if (starts_distinct) {
-            lo = sbb + __popc(SBm & ((2u << b) - 1u)) - 1;
+            lo = sbb + __popc(SBl & ((2u << b) - 1u)) - 1;
           } else {
             lo = 0;  // last sentence starting at or before p
             int hi = ns - 1;
@@ -776,10 +771,9 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
           }
           // span end: the next break (own lane, else a later one); dirty:
           // a filler / expansion byte in [p, q)
-          const uint32_t brk = U | (S_ & CS) | SBm;
           const uint32_t rest = brk & ~((2u << b) - 1u);
           const int q = rest ? min(p0 + __ffs(rest) - 1, nb) : nxt_brk;
-          uint32_t own = D & ~((1u << b) - 1u);
+          uint32_t own = Dl & ~((1u << b) - 1u);
           if (q < p0 + 32) own &= (1u << (q - p0)) - 1u;
           const bool dirty = own != 0 || (q > p0 + 32 && nxt_dirty < q);
           L.u.urec[u - rb] = ur_make(p, q - p, dirty, lo);
@@ -787,18 +781,24 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
       }
       wsync();
       STAMP(5);
-      // ---- 3: prep (dirty words, specials, long words) + the whole-word
-      //      probe of each pending unit (slot 0 of its home bucket), one
-      //      unit per lane: the key is loaded and hashed once; a special's
-      //      marker is its key's first byte
+      // ---- 3+4, 64 units per step (one per lane), in unit order: prep
+      //      (dirty words, specials, long words), the whole-word probe (slot 0
+      //      of the home bucket; the key loaded and hashed once, a special's
+      //      marker is its key's first byte), then the unit's entry and, for a
+      //      word the probe did not resolve, its WordPiece record from the key
+      //      still in registers.  Entry indices and record slots within a
+      //      sentence come from ballots (a sentence is a run of lanes; its
+      //      counts carry over from the previous step through LDS).
       {
         const int mb0 = (int)P.maxb[0];
         const uint32_t vmask = P.vt_mask;
+        const uint64_t lane_bit = 1ull << lane, below = lane_bit - 1ull;
         for (int r = 0; r < nr; r += 64) {
           const int u = r + lane;
+          const bool valid = u < nr;
           uint32_t w = 0;
           uint16_t id = U_EMPTY;
-          const uint32_t x = u < nr ? L.u.urec[u] : 0u;
+          const uint32_t x = valid ? L.u.urec[u] : 0u;
           int src = ur_p(x), len = ur_len(x);
           const bool dirty = ur_dirty(x);
           if (dirty) len = max(dirty_normalize(L, P, src, src + len, &src), 0);
@@ -812,7 +812,7 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
               id = (uint16_t)P.unk;
             } else {
               id = U_DEFER;
-              w = wmake(u, src, len);
+              w = 1;
               if (len > KEYMAX) L.misc[2] = 1;  // too long for a record: the tile falls back
             }
           }
@@ -824,206 +824,121 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
               w = 0;
             }
           }
-          if (u < nr) {
-            L.uid[u] = id;
-            L.u.uwp[u] = w;
+          wsync();
+          if (L.misc[2]) {
+            ovf = true;
+            break;
           }
-        }
-      }
-      wsync();
-      STAMP(6);
-      STAMP(7);
-      if (L.misc[2]) {
-        ovf = true;
-        break;
-      }
-      // ---- 4: entries and records -------------------------------------------
-      // Lane l holds units [l*per, l*per + per); segmented (by sentence)
-      // exclusive prefix sums give each unit its entry index and its record
-      // slot offset within the sentence; a sentence running on from the
-      // previous round continues its counts (carry).
-      {
-        constexpr int K = UCAP / 64;
-        const int per = (nr + 63) >> 6;
-        const int u0 = lane * per;
-        uint32_t sent[K], idv[K], ev[K], nsl[K], epre[K], spre[K];
-        bool valid[K], head[K];
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-          const int uu = u0 + k;
-          valid[k] = k < per && uu < nr;
-          sent[k] = valid[k] ? ur_sent(L.u.urec[uu]) : 0u;
-          idv[k] = valid[k] ? (uint32_t)L.uid[uu] : (uint32_t)U_EMPTY;
-          ev[k] = idv[k] != U_EMPTY ? 1u : 0u;
-          head[k] = valid[k] && (uu == 0 ? (int)sent[k] != prev_sent : ur_sent(L.u.urec[uu - 1]) != sent[k]);
-        }
-        const int first_sent = (int)ur_sent(L.u.urec[0]);
-        const bool cont = first_sent == prev_sent;
-        auto seg_scan = [&](const uint32_t(&v)[K], uint32_t carry, uint32_t(&pre)[K]) {
-          uint32_t run = 0, h = 0;
-#pragma unroll
-          for (int k = 0; k < K; ++k) {
-            pre[k] = 0;
-            if (valid[k]) {
-              if (head[k]) {
-                run = 0;
-                h = 1;
-              }
-              pre[k] = run;
-              run += v[k];
+          // ---- entries and records ----------------------------------------
+          const uint32_t sj = ur_sent(x);
+          const int last = min(64, nr - r) - 1;  // last valid lane
+          const uint32_t psj = wave_shr1(sj);  // (every lane active: DPP reads no disabled lane)
+          const bool head = valid && (lane == 0 ? (int)sj != prev_sent : psj != sj);
+          const uint64_t H = __ballot(head);
+          const uint64_t hb = H & (below | lane_bit);  // sentence starts at or before this lane
+          const uint64_t seg = hb ? below & ~((1ull << (63 - __clzll(hb))) - 1ull) : below;
+          const int first_sent = (int)lane_get(sj, 0);
+          const bool cont = !(H & 1ull);  // lane 0's sentence runs on from the previous step
+          uint32_t c_n = 0, c_s = 0, c_q = 0;
+          if (cont) {
+            c_n = L.sent_n[first_sent];
+            c_s = L.sslot[first_sent];
+            c_q = L.sdef[first_sent];
+          }
+          const bool inherit = hb == 0;  // this lane's sentence began in an earlier step
+          const bool ev = valid && id != U_EMPTY;
+          const uint64_t E = __ballot(ev);
+          const uint32_t e = (uint32_t)__popcll(E & seg) + (inherit ? c_n : 0u);
+          const uint32_t nsl = (ev && id == U_DEFER && (int)e < max_tok) ? (len <= KEY1 ? 1u : 2u) : 0u;
+          const uint64_t N1 = __ballot(nsl != 0), N2 = __ballot(nsl == 2);
+          const uint32_t qd = (uint32_t)__popcll(N1 & seg) + (inherit ? c_q : 0u);
+          const uint32_t o = qd - (inherit ? c_q : 0u) + (uint32_t)__popcll(N2 & seg) + (inherit ? c_s : 0u);
+          const uint32_t need = (uint32_t)(__popcll(N1) + __popcll(N2));
+          // this step's slots come from the wave's chunk; a sentence's slots
+          // stay contiguous: on a chunk switch, the slots the running sentence
+          // took in earlier steps move to the new chunk
+          if (need > 0 && cur + need > cend) {
+            const uint32_t carried = cont ? c_s : 0u;
+            if (carried + need > SPLIT_CHUNK) {  // (a sentence with > 1024 slots)
+              ovf = true;
+              break;
+            }
+            if (chunk >= 0 && lane == 0) S.chunk_fill[chunk] = cur - cbase;
+            int c = 0;
+            if (lane == 0) c = (int)atomicAdd(S.chunk_ctr, 1u);
+            c = __builtin_amdgcn_readfirstlane(c);
+            if ((uint32_t)c >= S.n_chunks) {  // record capacity exhausted
+              chunk = -1;
+              cur = cend = cbase = 0;
+              ovf = true;
+              break;
+            }
+            chunk = c;
+            cbase = cur = (uint32_t)c * SPLIT_CHUNK;
+            cend = cbase + SPLIT_CHUNK;
+            if (carried) {
+              // (records this wave stored in an earlier step: drain its stores first)
+              asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+              const uint32_t from = L.sqb[first_sent];
+              for (int k = 0; k < 4; ++k)
+                for (uint32_t i = lane; i < carried; i += 64) *recq(S, k, cur + i) = *recq(S, k, from + i);
+              // (piece counts: wp_kernel writes the moved words' own; the moved
+              // extension slots count 0)
+              for (uint32_t i = lane; i < carried; i += 64) S.cnt8[cur + i] = 0;
+              wsync();
+              if (lane == 0) L.sqb[first_sent] = cur;
+              cur += carried;
             }
           }
-          uint32_t hv = h, sv = run;
-          wave_seg_incl_add(hv, sv);
-          uint32_t ex = wave_shr1(sv);
-          if (!wave_shr1(hv)) ex += carry;  // no segment start before this lane
-          bool before = true;
-#pragma unroll
-          for (int k = 0; k < K; ++k) {
-            if (valid[k] && head[k]) before = false;
-            if (before) pre[k] += ex;
+          if (valid && (lane == last || ((H >> (lane + 1)) & 1ull))) {  // the sentence's last unit of the step
+            L.sent_n[sj] = (uint16_t)min(e + (ev ? 1u : 0u), 65535u);
+            L.sslot[sj] = (uint16_t)(o + nsl);
+            L.sdef[sj] = (uint16_t)(qd + (nsl ? 1u : 0u));
           }
-        };
-        seg_scan(ev, cont ? (uint32_t)L.sent_n[first_sent] : 0u, epre);
-        // record slots of queued units whose entry is kept (< max_tok)
-        uint32_t mine = 0;
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-          nsl[k] = 0;
-          if (valid[k] && idv[k] == U_DEFER && (int)epre[k] < max_tok)
-            nsl[k] = wlen(L.u.uwp[u0 + k]) <= KEY1 ? 1u : 2u;
-          mine += nsl[k];
-        }
-        // slots and queued entries per sentence in one scan (slots | count << 16)
-        uint32_t nsd[K], ndef = 0;
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-          nsd[k] = nsl[k] | (nsl[k] ? 0x10000u : 0u);
-          ndef += nsl[k] ? 1u : 0u;
-        }
-        seg_scan(nsd, cont ? ((uint32_t)L.sslot[first_sent] | ((uint32_t)L.sdef[first_sent] << 16)) : 0u, spre);
-        const uint32_t xs = wave_incl_add(mine | (ndef << 16));
-        const uint32_t need = lane_get(xs, 63) & 0xFFFFu;
-        // this round's slots come from the wave's chunk; a sentence's slots
-        // stay contiguous: on a chunk switch, the slots the running sentence
-        // took in earlier rounds move to the new chunk
-        if (need > 0 && cur + need > cend) {
-          const uint32_t carried = cont ? (uint32_t)L.sslot[first_sent] : 0u;
-          if (carried + need > SPLIT_CHUNK) {  // (a sentence with > 1024 slots)
-            ovf = true;
-            break;
-          }
-          if (chunk >= 0 && lane == 0) S.chunk_fill[chunk] = cur - cbase;
-          int c = 0;
-          if (lane == 0) c = (int)atomicAdd(S.chunk_ctr, 1u);
-          c = __builtin_amdgcn_readfirstlane(c);
-          if ((uint32_t)c >= S.n_chunks) {  // record capacity exhausted
-            chunk = -1;
-            cur = cend = cbase = 0;
-            ovf = true;
-            break;
-          }
-          chunk = c;
-          cbase = cur = (uint32_t)c * SPLIT_CHUNK;
-          cend = cbase + SPLIT_CHUNK;
-          if (carried) {
-            // (records this wave stored in an earlier round: drain its stores first)
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            const uint32_t from = L.sqb[first_sent];
-            for (int k = 0; k < 4; ++k)
-              for (uint32_t i = lane; i < carried; i += 64) *recq(S, k, cur + i) = *recq(S, k, from + i);
-            // (piece counts: wp_kernel writes the moved words' own; the moved
-            // extension slots count 0)
-            for (uint32_t i = lane; i < carried; i += 64) S.cnt8[cur + i] = 0;
-            if (lane == 0) L.sqb[first_sent] = cur;
-            cur += carried;
-          }
-        }
-        const uint32_t xpre = xs - (mine | (ndef << 16));
-        uint32_t gp = cur + (xpre & 0xFFFFu);  // global slot of this lane's first record
-        uint32_t qi = xpre >> 16;              // its rank among the round's queued units
-        uint16_t* qlist = L.uid;
-        wsync();  // (every lane has read its units' uid)
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-          if (!valid[k]) continue;
-          const int uu = u0 + k;
-          const int sj = (int)sent[k];
-          const uint32_t e = epre[k], o = spre[k] & 0xFFFFu;
-          if (uu == nr - 1 || (int)ur_sent(L.u.urec[uu + 1]) != sj) {  // the sentence's last unit of the round
-            L.sent_n[sj] = (uint16_t)min(e + ev[k], 65535u);
-            L.sslot[sj] = (uint16_t)(o + nsl[k]);
-            L.sdef[sj] = (uint16_t)((spre[k] >> 16) + (nsl[k] ? 1u : 0u));
-          }
-          if (ev[k] && (int)e < max_tok) {
+          if (ev && (int)e < max_tok) {
             const int64_t at = (int64_t)L.sst[sj] + e;
-            // one store per unit: an id with no queued word before it is final
-            // (the output), everything else an entry for expand
-            uint16_t* const dst = S.ent + (ent0 + at);
-            *dst = (uint16_t)(idv[k] != U_DEFER ? idv[k] : (SPLIT_EDEF | o));
-            if (idv[k] != U_DEFER) {
-              // ([CLS] / [SEP] come only from literal specials, never from WordPiece)
-              if (idv[k] == P.special[2] || idv[k] == P.special[3]) atomicOr(&L.sspec[sj >> 5], 1u << (sj & 31));
-            } else {
-              if (o == 0) {
-                L.sqb[sj] = gp;
-                L.sfdef[sj] = (uint16_t)e;
-              }
-              qlist[qi++] = (uint16_t)uu;
+            S.ent[ent0 + at] = (uint16_t)(id != U_DEFER ? id : (SPLIT_EDEF | o));
+            // ([CLS] / [SEP] come only from literal specials, never from WordPiece)
+            if (id == P.special[2] || id == P.special[3]) atomicOr(&L.sspec[sj >> 5], 1u << (sj & 31));
+          }
+          if (nsl) {
+            // the record {len | slots << 8 | valid, count, key bytes 0..55}
+            const uint32_t slot = cur + (uint32_t)(__popcll(N1 & below) + __popcll(N2 & below));
+            if (o == 0) L.sqb[sj] = slot;
+            uint32_t kd[6] = {key.d0, key.d1, key.d2, key.d3, key.d4, key.d5};
+            const int a = src >> 2;
+            const uint32_t sh = (uint32_t)(src & 3);
+            if (len > 24) {
+              uint32_t xx[7];
+#pragma unroll
+              for (int i = 0; i < 7; ++i) xx[i] = L.nb[a + i];
+#pragma unroll
+              for (int i = 0; i < 6; ++i) kd[i] = __builtin_amdgcn_alignbyte(xx[i + 1], xx[i], sh);
+            }
+            *recq(S, 0, slot) = make_uint4((uint32_t)len | (nsl << 8) | 0x80000000u, 0u, kd[0], kd[1]);
+            *recq(S, 1, slot) = make_uint4(kd[2], kd[3], kd[4], kd[5]);
+            // key bytes 24..55 (wp_kernel reads them only for a longer key)
+            if (len > 24) {
+              uint32_t xx[9];
+#pragma unroll
+              for (int i = 0; i < 9; ++i) xx[i] = L.nb[a + 6 + i];
+              uint32_t kq[8];
+#pragma unroll
+              for (int i = 0; i < 8; ++i) kq[i] = keep_bytes(__builtin_amdgcn_alignbyte(xx[i + 1], xx[i], sh), len - 24 - 4 * i);
+              *recq(S, 2, slot) = make_uint4(kq[0], kq[1], kq[2], kq[3]);
+              *recq(S, 3, slot) = make_uint4(kq[4], kq[5], kq[6], kq[7]);
+            }
+            if (nsl == 2) {  // the extension slot: a zero header (skipped by wp_kernel)
+              *recq(S, 0, slot + 1) = make_uint4(0, 0, 0, 0);
+              S.cnt8[slot + 1] = 0;  // (its pieces buffer holds pieces 28.. of the word)
             }
           }
-          gp += nsl[k];
+          cur += need;
+          prev_sent = (int)lane_get(sj, last);
+          wsync();
         }
-        wsync();
-        // the records, one queued unit per lane:
-        // {len | slots << 8 | valid, count, key bytes 0..55}
-        const uint32_t nq = lane_get(xs, 63) >> 16;
-        // (the list is in unit order, as the slots: a scan of the slot counts places them)
-        uint32_t qslot = cur;
-        for (uint32_t q0 = 0; q0 < nq; q0 += 64) {
-          const uint32_t q = q0 + lane;
-          const uint32_t w = q < nq ? L.u.uwp[qlist[q]] : 0u;
-          const uint32_t nslq = q < nq ? (wlen(w) <= KEY1 ? 1u : 2u) : 0u;
-          const uint32_t xq = wave_incl_add(nslq);
-          const uint32_t slot = qslot + xq - nslq;
-          qslot += lane_get(xq, 63);
-          if (q >= nq) continue;
-          const int len = wlen(w), src = wsrc(w);
-          const int a = src >> 2;
-          const uint32_t sh = (uint32_t)(src & 3);
-          const uint32_t slots = len <= KEY1 ? 1u : 2u;
-          {
-            uint32_t x[7];
-#pragma unroll
-            for (int i = 0; i < 7; ++i) x[i] = L.nb[a + i];
-            uint32_t kd[6];
-#pragma unroll
-            for (int i = 0; i < 6; ++i) kd[i] = keep_bytes(__builtin_amdgcn_alignbyte(x[i + 1], x[i], sh), len - 4 * i);
-            *recq(S, 0, slot) = make_uint4((uint32_t)len | (slots << 8) | 0x80000000u, 0u, kd[0], kd[1]);
-            *recq(S, 1, slot) = make_uint4(kd[2], kd[3], kd[4], kd[5]);
-          }
-          // key bytes 24..55 (wp_kernel reads them only for a longer key)
-          if (len > 24) {
-            uint32_t x[9];
-#pragma unroll
-            for (int i = 0; i < 9; ++i) x[i] = L.nb[a + 6 + i];
-            uint32_t kd[8];
-#pragma unroll
-            for (int i = 0; i < 8; ++i) kd[i] = keep_bytes(__builtin_amdgcn_alignbyte(x[i + 1], x[i], sh), len - 24 - 4 * i);
-            *recq(S, 2, slot) = make_uint4(kd[0], kd[1], kd[2], kd[3]);
-            *recq(S, 3, slot) = make_uint4(kd[4], kd[5], kd[6], kd[7]);
-          }
-          if (slots == 2) {  // the extension slot: a zero header (skipped by wp_kernel)
-            const uint4 z = make_uint4(0, 0, 0, 0);
-            *recq(S, 0, slot + 1) = z;
-            S.cnt8[slot + 1] = 0;  // (its pieces buffer holds pieces 28.. of the word)
-          }
-        }
-        cur += need;
       }
-      wsync();
-      prev_sent = (int)ur_sent(L.u.urec[nr - 1]);
-      wsync();
+      if (ovf) break;
       STAMP(8);
     }  // rounds
     if (ovf) {
@@ -1036,7 +951,7 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
       const int nsl = L.sslot[lane];
       // one 8-B record per sentence for expand: entries | first queued entry
       // << 16, first record slot (~0: no queued word)
-      S.smeta[s] = make_uint2((uint32_t)ne | (nsl ? (uint32_t)L.sfdef[lane] << 16 : 0u), nsl ? L.sqb[lane] : 0xFFFFFFFFu);
+      S.smeta[s] = make_uint2((uint32_t)ne, nsl ? L.sqb[lane] : 0xFFFFFFFFu);
       S.snslot[s] = (uint16_t)nsl;
       P.out_ntok[s] = ne - (int)L.sdef[lane];
       if (P.sent_spec) P.sent_spec[s] = (uint8_t)((L.sspec[lane >> 5] >> (lane & 31)) & 1u);
