@@ -80,6 +80,8 @@ struct alignas(16) Lds {
   uint32_t nb[NBUF / 4];       // normalised bytes in window coordinates; side buffer at [CAP, CAP+DCAP)
   uint32_t brk[64];            // break bits: unit starts, spaces, sentence starts
   uint32_t um[64];             // unit-start bits
+  uint32_t xm[5 * 64];         // exception pass: every lane's CS, D masks (W, I, S in brk, um, dm), its
+                               // SLOW bits, and 256 listed positions (u16)
   uint32_t dm[64];             // dirty bits: filler / expansion marker bytes
   uint32_t sb[64];             // sentence-start bits
   uint32_t sqb[NSCAP];         // record index of the sentence's first slot
@@ -464,93 +466,127 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
     uint32_t sp_m = 0, sp_w = 0, sp_d = 0;  // this lane's last char / special running into the next lane
     {
       const int p0 = lane * 32;
-      // Fast path, one exception byte per lane per step: '[' (a literal
-      // special token?) from the raw bytes and the sentence-start bits, a
-      // UTF-8 lead byte from ONE load of its code point's fast entry (xmap:
-      // class, replacement bytes, drop).  What it does not model (SLOW: multi-
-      // char expansions, canonical reordering, a replacement longer than the
-      // source) goes to the full path below.
+      // Fast path over the tile's exception bytes in ONE pass, one per lane
+      // (one table round trip for up to 64): the lanes list their exception
+      // positions, then lane k takes the k-th -- '[' (a literal special
+      // token?) from the raw bytes and the sentence-start bits, a UTF-8 lead
+      // byte from one load of its code point's fast entry (xmap: class,
+      // replacement bytes, drop) -- and applies it to the owner lanes' masks
+      // held in LDS (atomic or / and: a span may run into the next lane).
+      // What it does not model (SLOW: multi-char expansions, canonical
+      // reordering, a replacement longer than the source) goes back to the
+      // owner lane for the full path below.
       uint32_t xslow = 0;
-      for (uint32_t xm = X; __any(xm != 0);) {
-        int i = -1;
-        if (xm) {
-          i = __ffs(xm) - 1;
-          xm &= xm - 1;
-        }
-        uint32_t e = XM_SLOW, n = 0;
-        bool brk = false;
-        if (i >= 0) {
-          const int p = p0 + i;
-          const uint32_t b = rawb(L, p);
-          if (b == '[') {
-            brk = true;
-          } else {
-            n = (uint32_t)utf8_len(b);
-            uint32_t cp = b & (0x3Fu >> (n - 1));
-            for (uint32_t q = 1; q < n; ++q) cp = (cp << 6) | (rawb(L, p + (int)q) & 0x3Fu);
-            if (cp > 0x10FFFF) cp = 0xFFFD;
-            e = P.xmap[cp];
-            if ((e & XM_SLOW) || xm_len(e) > n) xslow |= 1u << i;
+      if (__any(X != 0)) {
+        // masks q = 0..4 (W, I, S, CS, D) of lane l at mw(q)[l]; the listed
+        // positions (u16) after the SLOW bits
+        auto mw = [&](int q) -> uint32_t* { return q == 0 ? L.brk : q == 1 ? L.um : q == 2 ? L.dm : L.xm + (q - 3) * 64; };
+        uint32_t* const slowm = L.xm + 128;
+        uint16_t* const xl = reinterpret_cast<uint16_t*>(L.xm + 192);
+        constexpr uint32_t XL = 256;
+        mw(0)[lane] = W;
+        mw(1)[lane] = I;
+        mw(2)[lane] = S_;
+        mw(3)[lane] = CS;
+        mw(4)[lane] = D;
+        slowm[lane] = 0;
+        const uint32_t cx = (uint32_t)__popc(X);
+        const uint32_t xi = wave_incl_add(cx);
+        const uint32_t nx = lane_get(xi, 63);
+        wsync();
+        auto mor = [&](int q, int pos, uint32_t nbits) {  // bits [pos, pos + nbits) of mask q
+          const int wq = pos >> 5, bq = pos & 31;
+          const uint64_t m = ((1ull << nbits) - 1ull) << bq;
+          atomicOr(&mw(q)[wq], (uint32_t)m);
+          if ((m >> 32) && wq < 63) atomicOr(&mw(q)[wq + 1], (uint32_t)(m >> 32));
+        };
+        auto mclr = [&](int q, int pos, uint32_t nbits) {
+          const int wq = pos >> 5, bq = pos & 31;
+          const uint64_t m = ((1ull << nbits) - 1ull) << bq;
+          atomicAnd(&mw(q)[wq], ~(uint32_t)m);
+          if ((m >> 32) && wq < 63) atomicAnd(&mw(q)[wq + 1], ~(uint32_t)(m >> 32));
+        };
+        bool any_slow = false;
+        for (uint32_t kb = 0; kb < nx; kb += XL) {
+          {  // list the exceptions kb .. kb + XL in lane order
+            uint32_t k = xi - cx;
+            for (uint32_t m = X; m; m &= m - 1, ++k)
+              if (k >= kb && k < kb + XL) xl[k - kb] = (uint16_t)(p0 + __ffs(m) - 1);
           }
-        }
-        if (brk) {  // [PAD] [UNK] [CLS] [SEP] [MASK] within p's sentence
-          const int p = p0 + i;
-          const int a = (p + 1) >> 2;
-          const uint32_t sh = (uint32_t)((p + 1) & 3);
-          const uint32_t w0 = __builtin_amdgcn_alignbyte(L.rp[a + 1], L.rp[a], sh);  // bytes p+1 .. p+4
-          const uint32_t w1 = __builtin_amdgcn_alignbyte(L.rp[a + 2], L.rp[a + 1], sh) & 0xFFu;  // byte p+5
-          // sentence starts at p+1 .. p+5 end p's sentence (no special crosses one)
-          const int wq = (p + 1) >> 5;
-          const uint64_t sbw = (uint64_t)L.sb[wq] | ((uint64_t)(wq + 1 < 64 ? L.sb[wq + 1] : 0u) << 32);
-          const uint32_t nxt = (uint32_t)(sbw >> ((p + 1) & 31)) & 0x1Fu;
-          int len = 0, sk = -1;
-          if (p + 5 <= nb && (nxt & 0xFu) == 0) {
-            if (w0 == 0x5D444150u) { sk = 0; len = 5; }         // PAD]
-            else if (w0 == 0x5D4B4E55u) { sk = 1; len = 5; }    // UNK]
-            else if (w0 == 0x5D534C43u) { sk = 2; len = 5; }    // CLS]
-            else if (w0 == 0x5D504553u) { sk = 3; len = 5; }    // SEP]
-            else if (w0 == 0x4B53414Du && w1 == ']' && p + 6 <= nb && (nxt & 0x10u) == 0) { sk = 4; len = 6; }  // MASK]
-          }
-          if (sk >= 0) {
-            nput(L.nb, p, BS + (uint32_t)sk);
-            const uint64_t cov = ((1ull << (len - 1)) - 1ull) << (i + 1);
-            const uint32_t cl = (uint32_t)cov;
-            W &= ~cl;
-            I &= ~cl;
-            S_ &= ~cl;
-            CS &= ~cl;
-            D &= ~cl;
-            sp_m |= (uint32_t)(cov >> 32);
-          }
-        } else if (i >= 0 && !((xslow >> i) & 1u)) {
-          const int p = p0 + i;
-          const uint32_t act = xm_act(e), T = xm_len(e);
-          const uint64_t span = ((1ull << n) - 1ull) << i;
-          bool dirty = false, wordc = false;
-          if (act == XM_DROP) {
-            for (uint32_t q = 0; q < n; ++q) nput(L.nb, p + (int)q, BF);
-            dirty = wordc = true;
-          } else if (act == XM_SPACE) {
-            S_ |= 1u << i;
-          } else {
-            if (act == XM_ISOLATE) I |= 1u << i;
-            else wordc = true;
-            if (e & XM_WRITE) {
-              for (uint32_t q = 0; q < n; ++q) nput(L.nb, p + (int)q, q < T ? (e >> (8 * q)) & 0xFFu : BF);
-              dirty = T < n;
+          wsync();
+          const uint32_t nl = min(nx - kb, XL);
+        for (uint32_t k0 = 0; k0 < nl; k0 += 64) {
+          const uint32_t k = k0 + lane;
+          const int p = k < nl ? (int)xl[k] : 0;
+          uint32_t e = XM_SLOW, n = 0;
+          bool brk = false;
+          if (k < nl) {
+            const uint32_t b = rawb(L, p);
+            if (b == '[') {
+              brk = true;
+            } else {
+              n = (uint32_t)utf8_len(b);
+              uint32_t cp = b & (0x3Fu >> (n - 1));
+              for (uint32_t q = 1; q < n; ++q) cp = (cp << 6) | (rawb(L, p + (int)q) & 0x3Fu);
+              if (cp > 0x10FFFF) cp = 0xFFFD;
+              e = P.xmap[cp];
             }
           }
-          const uint32_t slo = (uint32_t)span, shi = (uint32_t)(span >> 32);
-          if (wordc) {
-            W |= slo;
-            sp_w |= shi;
+          if (brk) {  // [PAD] [UNK] [CLS] [SEP] [MASK] within p's sentence
+            const int a = (p + 1) >> 2;
+            const uint32_t sh = (uint32_t)((p + 1) & 3);
+            const uint32_t w0 = __builtin_amdgcn_alignbyte(L.rp[a + 1], L.rp[a], sh);  // bytes p+1 .. p+4
+            const uint32_t w1 = __builtin_amdgcn_alignbyte(L.rp[a + 2], L.rp[a + 1], sh) & 0xFFu;  // byte p+5
+            // sentence starts at p+1 .. p+5 end p's sentence (no special crosses one)
+            const int wq = (p + 1) >> 5;
+            const uint64_t sbw = (uint64_t)L.sb[wq] | ((uint64_t)(wq + 1 < 64 ? L.sb[wq + 1] : 0u) << 32);
+            const uint32_t nxt = (uint32_t)(sbw >> ((p + 1) & 31)) & 0x1Fu;
+            int len = 0, sk = -1;
+            if (p + 5 <= nb && (nxt & 0xFu) == 0) {
+              if (w0 == 0x5D444150u) { sk = 0; len = 5; }         // PAD]
+              else if (w0 == 0x5D4B4E55u) { sk = 1; len = 5; }    // UNK]
+              else if (w0 == 0x5D534C43u) { sk = 2; len = 5; }    // CLS]
+              else if (w0 == 0x5D504553u) { sk = 3; len = 5; }    // SEP]
+              else if (w0 == 0x4B53414Du && w1 == ']' && p + 6 <= nb && (nxt & 0x10u) == 0) { sk = 4; len = 6; }  // MASK]
+            }
+            if (sk >= 0) {
+              nput(L.nb, p, BS + (uint32_t)sk);
+              for (int q = 0; q < 5; ++q) mclr(q, p + 1, (uint32_t)len - 1u);
+            }
+          } else if (k < nl) {
+            if ((e & XM_SLOW) || xm_len(e) > n) {
+              any_slow = true;  // (back to the owner lane: xslow)
+              atomicOr(&slowm[p >> 5], 1u << (p & 31));
+            } else {
+              const uint32_t act = xm_act(e), T = xm_len(e);
+              bool dirty = false, wordc = false;
+              if (act == XM_DROP) {
+                for (uint32_t q = 0; q < n; ++q) nput(L.nb, p + (int)q, BF);
+                dirty = wordc = true;
+              } else if (act == XM_SPACE) {
+                mor(2, p, 1);
+              } else {
+                if (act == XM_ISOLATE) mor(1, p, 1);
+                else wordc = true;
+                if (e & XM_WRITE) {
+                  for (uint32_t q = 0; q < n; ++q) nput(L.nb, p + (int)q, q < T ? (e >> (8 * q)) & 0xFFu : BF);
+                  dirty = T < n;
+                }
+              }
+              // (the continuation bytes past this lane carry no class bits)
+              if (wordc) mor(0, p, n);
+              if (dirty) mor(4, p, n);
+            }
           }
-          if (dirty) {
-            D |= slo;
-            sp_d |= shi;
-          }
-          sp_m |= shi;
         }
+          wsync();
+        }
+        W = mw(0)[lane];
+        I = mw(1)[lane];
+        S_ = mw(2)[lane];
+        CS = mw(3)[lane];
+        D = mw(4)[lane];
+        if (__any(any_slow)) xslow = slowm[lane];
       }
       // the full path: exceptions in batches of 4 per lane, the table lookups
       // of a batch (code point -> page -> entry -> multi expansion) together
