@@ -225,7 +225,18 @@ def cpu_baseline(args, base, pdo, seconds):
                      'tokenize and pack at %d cores in series' % (
                          ns, (base.sent_off[ns] - base.sent_off[0]) / 1e6, tok_s, tok_rate, threads, p, pack_s,
                          pack_rate or 0, threads)),
-          'tokenize_tokens_per_s': tok_rate, 'pack_tokens_per_s_per_thread': pack_rate}
+          'tokenize_tokens_per_s': tok_rate, 'pack_tokens_per_s_per_thread': pack_rate,
+          'host_cpus': host_cpus()}
+
+
+def host_cpus():
+  """The box's CPU count and this process's affinity beside the 16-thread cap
+  (the GPU box's CPU share; os.cpu_count() there shows the whole machine)."""
+  try:
+    aff = len(os.sched_getaffinity(0))
+  except (AttributeError, OSError):
+    aff = None
+  return {'os_cpu_count': os.cpu_count(), 'affinity': aff, 'cap': 16}
 
 
 def sample_partition_check(args, pk, res, base, pdo, reps, seed0):
@@ -467,17 +478,18 @@ def main():
     return
   value = tot_tok * args.steps / el
   # roofline of the dominant kernel, the tokenizer's tile scan
-  # (lddl::tok5::scan_kernel).  Algorithmic bytes = the
-  # tokenize call's own I/O (the corpus read once, 8 B sentence offset read
-  # + 4 B token count written per sentence, 2 B per token id written), all of
-  # it charged to the scan launch that reads the input; the WordPiece records
-  # and entries the scan hands to wp_kernel / expand_kernel are this design's
+  # (lddl::tok5::scan_kernel).  Algorithmic bytes of the
+  # scan = the part of the tokenize call's I/O it moves: the corpus read once,
+  # 8 B sentence offset read + 4 B token count written per sentence (the 2 B
+  # per token id are written by expand_kernel: charged to the whole call in
+  # roofline.tokenize_call, never to the scan).  The WordPiece records and
+  # entries the scan hands to wp_kernel / expand_kernel are this design's
   # intermediates, not algorithmic (they show in roofline.traffic).  Divided
   # by the scan's HIP-event time inside the call (events on the launch
   # stream; one scan launch per segment of SPLIT_SEG_TILES KiB, 4 GiB).
   nl = ks['launches']
   alg_call = sh.nbytes + 12 * sh.n_sent + 2 * n_tok
-  alg = alg_call / nl
+  alg = (sh.nbytes + 12 * sh.n_sent) / nl
   achieved = alg / (ks['scan_ms'] / nl * 1e-3) / 1e9
   tok_kernels_ms = ks['scan_ms'] + ks['wordpiece_ms'] + ks['expand_ms']
   line = {

@@ -63,7 +63,7 @@ struct lddl_ctx {
   uint4* d_vt = nullptr;         // v4 bucketed vocab table
   uint32_t vt_mask = 0;
   uint32_t* d_vbloom = nullptr;  // its Bloom filter
-  bool tok4_ok = false;          // the ASCII page fits tokenize_stream's class table
+  bool scan_ok = false;          // the ASCII page fits the split scan's per-byte class table
   int tok5_cfg = 0;
   // per-kernel timing of the split tokenizer (lddl_set_timing)
   bool timing = false;
@@ -191,18 +191,18 @@ static int load_table(lddl_ctx* c, const char* path) {
       if (ent_cls(multi[i * 4 + 1 + k]) != CLS_OTHER)
         return set_err(LDDL_EFORMAT, "unicode table multi entry %zu has a non-word char", i);
   }
-  // tokenize_stream derives its per-byte class table from the ASCII page: it
+  // the split scan (tokenize_split.hip) derives its per-byte class table from the ASCII page: it
   // needs rank-0, single-char entries whose only mapping is A-Z -> a-z
-  c->tok4_ok = true;
+  c->scan_ok = true;
   for (uint32_t b = 0; b < 128; ++b) {
     const uint32_t e = pages[(size_t)top[0] * 256 + b];
     const uint32_t kind = ent_kind(e), cls = ent_cls(e);
-    if (ent_rank(e) != 0 || kind == KIND_MULTI) c->tok4_ok = false;
-    if (kind == KIND_MAP && cls == CLS_ISOLATE) c->tok4_ok = false;
+    if (ent_rank(e) != 0 || kind == KIND_MULTI) c->scan_ok = false;
+    if (kind == KIND_MAP && cls == CLS_ISOLATE) c->scan_ok = false;
     if (kind == KIND_MAP && cls == CLS_OTHER && !(b >= 'A' && b <= 'Z' && ent_payload(e) == b + 32))
-      c->tok4_ok = false;
+      c->scan_ok = false;
   }
-  if (ent_cls(pages[(size_t)top[0] * 256 + '[']) != CLS_ISOLATE) c->tok4_ok = false;
+  if (ent_cls(pages[(size_t)top[0] * 256 + '[']) != CLS_ISOLATE) c->scan_ok = false;
   int rc;
   if ((rc = upload(&c->d_top, top.data(), top.size() * 2))) return rc;
   if ((rc = upload(&c->d_pages, pages.data(), pages.size() * 4))) return rc;
@@ -407,7 +407,7 @@ extern "C" int lddl_create(const char* vocab_path, const char* table_path, int d
   // SPLIT_EDEF; it derives a byte-class table from the ASCII page)
   const char* algo = getenv("LDDL_TOKENIZE_ALGO");
   c->tok_algo = (algo && algo[0] == '0') ? 0 : 5;
-  if (c->tok_algo == 5 && (!c->tok4_ok || c->vocab_size > (int)SPLIT_EDEF)) c->tok_algo = 0;
+  if (c->tok_algo == 5 && (!c->scan_ok || c->vocab_size > (int)SPLIT_EDEF)) c->tok_algo = 0;
   const char* cfg5 = getenv("LDDL_TOK5_CFG");  // split tokenizer variants (tokenize_split.hip)
   c->tok5_cfg = cfg5 ? atoi(cfg5) : 0;
   const char* mcap = getenv("LDDL_MLM_CAP");  // initial masking arena (tests force the regrow path)
@@ -548,8 +548,8 @@ extern "C" int lddl_tokenize(lddl_ctx* c, const uint8_t* d_bytes, int64_t nbytes
     uint64_t h[18];
     HIP_TRY(hipMemcpyAsync(h, P.dbg, sizeof h, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
-    const char* nm[12] = {"loop", "setup", "classify", "except", "units", "urec", "prep", "probe", "entries",
-                          "tile_end", "stages", "tiles"};
+    const char* nm[12] = {"loop", "setup", "classify", "except", "units", "urec", "prep", "probe", "records",
+                          "tile_end", "entries", "tiles"};
     fprintf(stderr, "[lddl tok5 dbg] ntiles=%lld", (long long)nt);
     for (int k = 0; k < 12; ++k) fprintf(stderr, " %s=%llu", nm[k], (unsigned long long)h[k]);
     const char* wn[6] = {"wp_A", "wp_B", "wp_C", "wp_D", "wp_steps", "wp_lane_steps"};

@@ -52,7 +52,7 @@ LDDL_HD uint32_t slot_info(uint32_t id, uint32_t len, uint32_t cont) {
   return id | (len << 16) | (cont << 24) | 0x80000000u;
 }
 
-// ---- v4 vocab table (tokenize_stream.hip) -----------------------------------
+// ---- vocab table (tokenize_split.hip, tokenize_serial.h) -----------------------------------
 // A candidate piece is hashed from its first 24 bytes held as six
 // little-endian dwords (bytes >= len zero), its byte length and the "##"
 // flag.  The table is an array of 64-byte buckets of two 32-byte slots

@@ -59,11 +59,14 @@ hipError_t launch_list_all_tiles(int64_t n_tiles, int32_t* fb_list, int32_t* fb_
 // sentence's dense offset, and an expand pass writes the dense ids.  Scratch
 // per segment of tiles (SPLIT_SEG_TILES):
 //   ent    u16 per byte of the segment: sentence s's entries at
-//          sent_off[s] - sent_off[0] - t0 * 1 KiB + k: a vocab id, or
-//          SPLIT_EDEF | (record slot - qb[s]) for a word of the queue (the
-//          serial path's ids of a fallback tile land here too)
-//   rec    64-B record slots in chunks of SPLIT_CHUNK, chunk_fill[c] used
-//   smeta  per sentence: #entries, first queued entry (fdef), first record slot (qb)
+//          sent_off[s] - sent_off[0] - t0 * 1 KiB + k, one per unit (k = its
+//          rank in the sentence): a vocab id, SPLIT_EHOLE for an empty unit,
+//          or SPLIT_EDEF | (record slot - the tile's first slot) for a word of
+//          the queue (the serial path's ids of a fallback tile land here too)
+//   rec    64-B record slots in chunks of SPLIT_CHUNK, chunk_fill[c] used;
+//          a tile's slots contiguous, in unit order
+//   smeta  per sentence: #entries | first slot relative to the tile's << 16,
+//          the tile's first slot
 // 4 GiB of input per segment: 48 GB of scratch (entries 2 B/byte, record
 // slots and WordPiece outputs 64 B per 14 B each); fewer kernel boundaries
 // than 1 GiB segments (bench step 250.8 -> 246.7 ms; 2 GiB: 249.1).  The
@@ -72,6 +75,7 @@ constexpr int64_t SPLIT_SEG_TILES = int64_t(1) << 22;
 constexpr uint32_t SPLIT_CHUNK = 1024;                 // record slots per allocation chunk (64 KiB)
 constexpr uint32_t SPLIT_EDEF = 0xF000u;               // entry >= EDEF: a queued word
 constexpr uint16_t SPLIT_NENT_FB = 0xFFFFu;            // nent of a sentence of a fallback tile
+constexpr uint16_t SPLIT_EHOLE = 0xFFFFu;              // entry of an empty unit (no token)
 
 struct SplitParams {
   int64_t seg_tiles;       // tiles per segment (SPLIT_SEG_TILES; tests force small ones)
@@ -79,11 +83,11 @@ struct SplitParams {
   const int64_t* tile_sent;
   uint16_t* ent;
   uint4* rec;              // 4 uint4 per slot
-  uint4* pcs;              // TOK5_PCS: WordPiece output (count + pieces) per slot, apart from the keys
+  uint4* pcs;              // WordPiece output (count + pieces) per slot, apart from the keys
   uint32_t* chunk_fill;
   uint32_t* chunk_ctr;     // [0] chunks handed out
   uint32_t n_chunks;
-  uint2* smeta;            // per sentence: #entries | first queued entry << 16, first record slot (~0: none)
+  uint2* smeta;            // per sentence: #entries | first slot - the tile's << 16, the tile's first slot
   uint16_t* snslot;        // per sentence: its record slots (count_kernel sums their piece counts)
   uint8_t* cnt8;           // per record slot: pieces of the word (0 for an extension slot)
   int64_t* scan_bsum;      // scan_blocks(seg_sent_cap) + 1

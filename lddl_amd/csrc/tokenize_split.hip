@@ -1,19 +1,19 @@
 // Tokenizer v5 (default): the per-tile scan and WordPiece are split into
 // separate kernels so that WordPiece runs at full lane occupancy.
 //
-// Same contract and results as tokenize_stream.hip (reference: HF
+// Contract: lddl_tokenize (include/lddl_amd.h); results those of HF
 // tokenizers' BertNormalizer / BertPreTokenizer / WordPiece behind
 // tokenizer.tokenize(s, max_length=512, truncation=True),
 // lddl/dask/bert/pretrain.py:79-80; restated in oracle/tokenizer_oracle.c).
 //
-// Why: in the one-kernel tile tokenizer (tok4) the WordPiece loop took ~60 %
+// Why: in round 1's one-kernel tile tokenizer (tok4, retired) the WordPiece loop took ~60 %
 // of the wave time at ~17 % lane occupancy -- a 1 KiB tile has ~20 words
 // that are not whole-word vocab hits, each needing a serial chain of Bloom
 // scans and dependent bucket loads, so the wave idled behind the longest
 // chain with most lanes masked off.
 //
 //  scan_kernel     wave per 1 KiB tile (sentences starting in it), persistent:
-//                  bytes -> normalised bytes + break masks (tok4 phases 1-2),
+//                  bytes -> normalised bytes + break masks (per-byte classes, exceptions),
 //                  units, dirty words normalised, specials, > 100-char words,
 //                  one whole-word bucket probe per unit.  Every unit that
 //                  yields tokens becomes an ENTRY of its sentence: a vocab id,
@@ -23,14 +23,14 @@
 //                  >= 1 token), #record slots, first slot, resolved count.
 //  wp_kernel       the records, one per lane with refill: greedy
 //                  longest-match-first (Bloom scan + 64-B bucket probe per
-//                  candidate, as tok4's loop), pieces and count written back
+//                  candidate), pieces and count written back
 //                  into the record.
 //  expand_kernel   per group of sentences: the entries from each sentence's
 //                  first queued word on -> ids (a record's pieces in place of
 //                  its entry) and the token count; the ids before it were
 //                  final and written by the scan.
 // Tiles the scan does not model (window > 2 KiB, > 64 sentences, > 256
-// units... as tok4, a queued word longer than 56 bytes, record capacity) are
+// units, a queued word longer than 56 bytes, record capacity) are
 // listed and re-run by tokenize_fallback_kernel (exact serial path).
 #include "common.h"
 #include "tokenize.h"
@@ -60,40 +60,38 @@ __device__ __forceinline__ uint32_t xm_act(uint32_t e) { return (e >> 27) & 3u; 
 enum : uint32_t { C_W = 1, C_I = 2, C_S = 4, C_D = 8, C_UP = 16, C_X = 32, C_CS = 64 };
 constexpr uint16_t U_EMPTY = 0xFFFEu, U_DEFER = 0xFFFFu;
 
-// unit record: window position (11 bits) | span length << 11 (12) | dirty << 23 | sentence << 24
-__device__ __forceinline__ uint32_t ur_make(int p, int len, bool dirty, int sent) {
-  return (uint32_t)p | ((uint32_t)len << 11) | ((uint32_t)dirty << 23) | ((uint32_t)sent << 24);
+// per lane of the window (LDS, for the unit steps): the first break / dirty
+// byte in a later lane and the sentence starts before the lane
+__device__ __forceinline__ uint32_t lx_make(int nxt_brk, int nxt_dirty, int sbb) {
+  return (uint32_t)nxt_brk | ((uint32_t)nxt_dirty << 12) | ((uint32_t)sbb << 24);
 }
-__device__ __forceinline__ int ur_p(uint32_t x) { return (int)(x & 0x7FFu); }
-__device__ __forceinline__ int ur_len(uint32_t x) { return (int)((x >> 11) & 0xFFFu); }
-__device__ __forceinline__ bool ur_dirty(uint32_t x) { return (x >> 23) & 1u; }
-__device__ __forceinline__ uint32_t ur_sent(uint32_t x) { return x >> 24; }
 
 struct alignas(16) Lds {
-  union {
-    uint32_t rp[CAP / 4 + 4];  // phase 1: raw bytes of the tile (LDS-DMA)
-    struct {
-      uint32_t urec[UCAP];     // unit records of the round (ur_make)
-    } u;
-  };
+  uint32_t rp[CAP / 4 + 4];    // raw bytes of the tile (LDS-DMA); free after the exception pass, when the
+                               // next tile's bytes are prefetched into it
   uint32_t pb[8];              // the tile's bounds: tile_sent[t], tile_sent[t+1], sent_off of both (LDS-DMA)
   uint32_t nb[NBUF / 4];       // normalised bytes in window coordinates; side buffer at [CAP, CAP+DCAP)
   uint32_t brk[64];            // break bits: unit starts, spaces, sentence starts
   uint32_t um[64];             // unit-start bits
   uint32_t xm[5 * 64];         // exception pass: every lane's CS, D masks (W, I, S in brk, um, dm), its
-                               // SLOW bits, and 256 listed positions (u16)
+                               // SLOW bits, and 256 listed positions (u16); then the unit start
+                               // positions of a round (u16, UCAP), lx_make per lane at [128, 192) and
+                               // the lanes' unit bases at [256, 320)
   uint32_t dm[64];             // dirty bits: filler / expansion marker bytes
   uint32_t sb[64];             // sentence-start bits
-  uint32_t sqb[NSCAP];         // record index of the sentence's first slot
-  uint16_t sdef[NSCAP];        // queued entries below max_tok
+  uint32_t sacc[NSCAP];        // per sentence: its record slots | (queued + empty units) << 16 (LDS atomics
+                               // of the rare lanes; direct ids = units - the high half)
   uint16_t sst[NSCAP + 2];     // sentence starts (window coordinates)
-  uint16_t sent_n[NSCAP];      // entries so far (uncapped)
-  uint16_t sslot[NSCAP];       // record slots so far
+  uint16_t ufirst[NSCAP + 2];  // index of the sentence's first unit in the tile ([ns] = #units)
+  uint16_t ebs[NSCAP];         // entry index base: unit u of sentence j has entry sst[j] + u - ufirst[j]
   uint32_t xent[XCAP];         // table entry of each expansion marker
   uint8_t xlen[XCAP];          // its normalised byte length
   int32_t misc[4];             // 0 side-buffer cursor, 1 #markers, 2 overflow
   uint32_t sspec[2];           // sentences holding a [CLS] / [SEP] token (P.sent_spec)
 };
+
+// five 4-wave blocks per CU (+ the 256-B class table): 5 waves per SIMD
+static_assert(4 * sizeof(Lds) + 256 <= 160 * 1024 / 5, "scan LDS no longer admits 5 waves per SIMD");
 
 __device__ __forceinline__ void wsync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -249,23 +247,29 @@ __device__ __forceinline__ Key6 load_key(const uint32_t* nb, int s, int len) {
   k.d5 = keep_bytes(__builtin_amdgcn_alignbyte(x6, x5, sh), lc - 20);
   return k;
 }
-// == vhash (common.h) of a loaded key
+// == vhash (common.h) of a loaded key; branch-free: the six mixes, then the
+// one of the key's length selected (a branch per dword diverges across lanes)
 __device__ __forceinline__ uint32_t key_hash(const Key6& k, int len, uint32_t cont) {
   const int lc = min(len, 24);
-  uint32_t h = VSEED;
-  if (lc > 0) h = vmix(h, k.d0);
-  if (lc > 4) h = vmix(h, k.d1);
-  if (lc > 8) h = vmix(h, k.d2);
-  if (lc > 12) h = vmix(h, k.d3);
-  if (lc > 16) h = vmix(h, k.d4);
-  if (lc > 20) h = vmix(h, k.d5);
+  const uint32_t h1 = vmix(VSEED, k.d0), h2 = vmix(h1, k.d1), h3 = vmix(h2, k.d2), h4 = vmix(h3, k.d3),
+                 h5 = vmix(h4, k.d4), h6 = vmix(h5, k.d5);
+  uint32_t h = lc > 20 ? h6 : lc > 16 ? h5 : lc > 12 ? h4 : lc > 8 ? h3 : lc > 4 ? h2 : h1;
+  if (lc <= 0) h = VSEED;
   return vfinal(h, (uint32_t)len, cont);
+}
+// a value the optimiser cannot see through: keeps the xor / or reduction
+// below (v_xor + v_or3) from being rewritten into one compare per dword,
+// materialised bools and 16-bit shifts
+__device__ __forceinline__ uint32_t opq(uint32_t x) {
+  asm("" : "+v"(x));
+  return x;
 }
 // branch-free (an && chain lets the compiler sink the slot's other loads
 // behind the first compare: a second dependent round trip on every hit)
 __device__ __forceinline__ bool slot_eq(const uint4& a, const uint4& b, const Key6& k, uint32_t want) {
-  return (((b.z & 0xFFFF0000u) ^ want) | (a.x ^ k.d0) | (a.y ^ k.d1) | (a.z ^ k.d2) | (a.w ^ k.d3) | (b.x ^ k.d4) |
-          (b.y ^ k.d5)) == 0u;
+  const uint32_t d = opq((b.z & 0xFFFF0000u) ^ want) | opq(a.x ^ k.d0) | opq(a.y ^ k.d1) | opq(a.z ^ k.d2) |
+                     opq(a.w ^ k.d3) | opq(b.x ^ k.d4) | opq(b.y ^ k.d5);
+  return d == 0u;
 }
 
 // DBG: phase stamps (s_memtime, diagnostics build only: LDDL_TOK_DEBUG=1)
@@ -316,7 +320,7 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
   const int64_t nwaves = (int64_t)gridDim.x * WAVES;
   const int max_tok = P.max_tok;
   // record chunk of this wave (wave-uniform): slots [cur, cend)
-  uint32_t cur = 0, cend = 0, cbase = 0;
+  uint32_t cur = 0, cend = 0, cbase = 0, tbase = 0, tsl = 0;
   int chunk = -1;
   // The tile's bounds (pb) and raw bytes (rp) arrive by LDS-DMA (no VGPRs,
   // no register-to-LDS copy of the bytes).  (A software-pipelined variant
@@ -331,9 +335,15 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
     __builtin_amdgcn_global_load_lds((const uint32_t*)g, (__attribute__((address_space(3))) uint32_t*)l, 4, 0, 0);
   };
   auto drain = [&]() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); };
+  // The next tile's staging runs inside the current one (stage1 after its
+  // sentence starts, stage2 after its exception pass, stage3 -- the raw
+  // bytes into rp, free by then -- before its unit steps), so that its three
+  // dependent round trips fly behind this tile's work; the loop top finishes
+  // whatever a tile that returned early left undone.
   auto stage1 = [&]() {
-    if (tn < S.t1 && lane < 4) dma4(reinterpret_cast<const uint32_t*>(S.tile_sent + tn) + lane, L.pb);
+    if (nst != 0) return;
     nst = 1;
+    if (tn < S.t1 && lane < 4) dma4(reinterpret_cast<const uint32_t*>(S.tile_sent + tn) + lane, L.pb);
   };
   auto stage2 = [&]() {
     if (nst != 1) return;
@@ -376,6 +386,7 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
     STAMP(0);
     if (dma_pending) drain();  // this tile's raw bytes
     dma_pending = false;
+    nst = 0;
     tn = t + nwaves;
     [&]() {
     if (sa >= sb) return;
@@ -409,17 +420,14 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
       L.sspec[0] = 0;
       L.sspec[1] = 0;
     }
-    if (lane < ns) {
-      L.sent_n[lane] = 0;
-      L.sslot[lane] = 0;
-      L.sdef[lane] = 0;
-    }
+    if (lane < ns) L.sacc[lane] = 0;
     wsync();
     if (lane < ns) {
       const int pos = (int)(spos - A) + aoff;
       L.sst[lane] = (uint16_t)pos;
       if (pos < nb) atomicOr(&L.sb[pos >> 5], 1u << (pos & 31));
     }
+    stage1();
     STAMP(1);
     // ---- 1: raw bytes -> masks + normalised bytes in place ------------------
     uint32_t W, I, S_, CS, D, X, inwin;
@@ -727,6 +735,7 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
       D = ((D & ~im) | id) & inwin;
     }
     const bool wbad = __any(bad);
+    stage2();
     STAMP(3);
     wsync();
     // ---- 2: units -----------------------------------------------------------
@@ -748,6 +757,7 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
       sbb = (int)(ex >> 16);
       n = (int)(tot & 0xFFFFu);
       nstarts = (int)(tot >> 16);
+      L.xm[256 + lane] = (uint32_t)ub;
     }
     // every sentence start distinct (no empty sentence shares one): a unit's
     // sentence is the number of starts at or before it, minus one
@@ -771,6 +781,17 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
         const int j = __ffsll((unsigned long long)md) - 1;
         nxt_dirty = j * 32 + __ffs(L.dm[j]) - 1;
       }
+      L.xm[128 + lane] = lx_make(nxt_brk, nxt_dirty, sbb);
+      // each sentence's first unit (units before its start: the owning lane's
+      // base + its unit bits below the start) and its entry base; a unit's
+      // entry is its rank in its sentence (an empty unit leaves a hole)
+      if (lane <= ns) {
+        const int pos = lane < ns ? (int)L.sst[lane] : nb;
+        int uf = n;
+        if (pos < nb) uf = (int)L.xm[256 + (pos >> 5)] + __popc(L.um[pos >> 5] & ((1u << (pos & 31)) - 1u));
+        L.ufirst[lane] = (uint16_t)uf;
+        if (lane < ns) L.ebs[lane] = (uint16_t)(pos - uf);
+      }
     }
     STAMP(4);
     if (wbad) {
@@ -779,64 +800,68 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
     }
     const int64_t obase = (A - base) - aoff;  // output index of window position 0
     const int64_t ent0 = obase - ebase;       // entry index of window position 0
-    int prev_sent = -1;
     bool ovf = false;
+    tbase = cur;  // the tile's first record slot (it moves with a chunk switch)
+    tsl = 0;      // record slots the tile took so far
     for (int rb = 0; rb < n; rb += UCAP) {
       const int nr = min(UCAP, n - rb);
       if (lane == 0) L.misc[0] = 0;
       {
-        // (the lane's masks from LDS: no register holds them across the
-        // per-unit work of the round)
-        const uint32_t Ul = L.um[lane], brk = L.brk[lane], Dl = L.dm[lane], SBl = L.sb[lane];
+        // the round's unit start positions in unit order (each lane its own
+        // bits: the loop runs the wave's largest count at about half the
+        // lanes busy, so a unit's span end, dirtiness and sentence are
+        // derived in the unit step below, one unit per lane)
+        uint16_t* const up = reinterpret_cast<uint16_t*>(L.xm);
+        const uint32_t Ul = L.um[lane];
         const int p0 = lane * 32;
         int u = ub;
-        for (uint32_t m = Ul; m; m &= m - 1, ++u) {
-          if (u < rb || u >= rb + nr) continue;
-          const int b = __ffs(m) - 1, p = p0 + b;
-          int lo;
-          if (starts_distinct) {
-            lo = sbb + __popc(SBl & ((2u << b) - 1u)) - 1;
-          } else {
-            lo = 0;  // last sentence starting at or before p
-            int hi = ns - 1;
-            while (lo < hi) {
-              const int mid = (lo + hi + 1) >> 1;
-              if ((int)L.sst[mid] <= p) lo = mid;
-              else hi = mid - 1;
-            }
-          }
-          // span end: the next break (own lane, else a later one); dirty:
-          // a filler / expansion byte in [p, q)
-          const uint32_t rest = brk & ~((2u << b) - 1u);
-          const int q = rest ? min(p0 + __ffs(rest) - 1, nb) : nxt_brk;
-          uint32_t own = Dl & ~((1u << b) - 1u);
-          if (q < p0 + 32) own &= (1u << (q - p0)) - 1u;
-          const bool dirty = own != 0 || (q > p0 + 32 && nxt_dirty < q);
-          L.u.urec[u - rb] = ur_make(p, q - p, dirty, lo);
-        }
+        for (uint32_t m = Ul; m; m &= m - 1, ++u)
+          if (u >= rb && u < rb + nr) up[u - rb] = (uint16_t)(p0 + __ffs(m) - 1);
       }
       wsync();
+      stage3();  // (rp is free: the next tile's bytes fly behind the unit steps)
       STAMP(5);
       // ---- 3+4, 64 units per step (one per lane), in unit order: prep
       //      (dirty words, specials, long words), the whole-word probe (slot 0
       //      of the home bucket; the key loaded and hashed once, a special's
       //      marker is its key's first byte), then the unit's entry and, for a
       //      word the probe did not resolve, its WordPiece record from the key
-      //      still in registers.  Entry indices and record slots within a
-      //      sentence come from ballots (a sentence is a run of lanes; its
-      //      counts carry over from the previous step through LDS).
+      //      still in registers.  A unit's entry index is its rank in its
+      //      sentence (ebs); record slots are tile-relative, in unit order,
+      //      from two ballots (a sentence's slots are then contiguous and its
+      //      first is the exclusive sum of the earlier sentences' at the end).
       {
         const int mb0 = (int)P.maxb[0];
         const uint32_t vmask = P.vt_mask;
-        const uint64_t lane_bit = 1ull << lane, below = lane_bit - 1ull;
         for (int r = 0; r < nr; r += 64) {
           const int u = r + lane;
           const bool valid = u < nr;
           uint32_t w = 0;
           uint16_t id = U_EMPTY;
-          const uint32_t x = valid ? L.u.urec[u] : 0u;
-          int src = ur_p(x), len = ur_len(x);
-          const bool dirty = ur_dirty(x);
+          // the unit: start p (window position), span end q = the next break
+          // (the owning lane's own bits, else its later-lane position), dirty
+          // (a filler / expansion byte in [p, q)) and sentence sj
+          const int p = valid ? (int)reinterpret_cast<const uint16_t*>(L.xm)[u] : 0;
+          const int wl = p >> 5, b = p & 31, p0 = p & ~31;
+          const uint32_t brk = L.brk[wl], Dl = L.dm[wl], SBl = L.sb[wl], lx = L.xm[128 + wl];
+          const uint32_t rest = brk & ~((2u << b) - 1u);
+          const int q = rest ? min(p0 + __ffs(rest) - 1, nb) : (int)(lx & 0xFFFu);
+          uint32_t own = Dl & ~((1u << b) - 1u);
+          if (q < p0 + 32) own &= (1u << (q - p0)) - 1u;
+          const bool dirty = valid && (own != 0 || (q > p0 + 32 && (int)((lx >> 12) & 0xFFFu) < q));
+          uint32_t sj;
+          if (starts_distinct) {
+            sj = (lx >> 24) + (uint32_t)__popc(SBl & ((2u << b) - 1u)) - 1u;
+          } else {
+            int lo = 0, hi = ns - 1;  // last sentence starting at or before p
+            while (lo < hi) {
+              const int mid = (lo + hi + 1) >> 1;
+              if ((int)L.sst[mid] <= p) lo = mid;
+              else hi = mid - 1;
+            }
+            sj = (uint32_t)lo;
+          }
+          int src = p, len = valid ? q - p : 0;
           if (dirty) len = max(dirty_normalize(L, P, src, src + len, &src), 0);
           Key6 key = {0, 0, 0, 0, 0, 0};
           if (len > 0 && len <= 24) key = load_key(L.nb, src, len);
@@ -852,6 +877,7 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
               if (len > KEYMAX) L.misc[2] = 1;  // too long for a record: the tile falls back
             }
           }
+          STAMP(6);
           if (w != 0 && len <= 24 && len <= mb0) {
             const uint4* bk = P.vt + 4 * (key_hash(key, len, 0u) & vmask);
             const uint4 fa = bk[0], fb = bk[1];
@@ -865,82 +891,58 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
             ovf = true;
             break;
           }
+          STAMP(7);
           // ---- entries and records ----------------------------------------
-          const uint32_t sj = ur_sent(x);
-          const int last = min(64, nr - r) - 1;  // last valid lane
-          const uint32_t psj = wave_shr1(sj);  // (every lane active: DPP reads no disabled lane)
-          const bool head = valid && (lane == 0 ? (int)sj != prev_sent : psj != sj);
-          const uint64_t H = __ballot(head);
-          const uint64_t hb = H & (below | lane_bit);  // sentence starts at or before this lane
-          const uint64_t seg = hb ? below & ~((1ull << (63 - __clzll(hb))) - 1ull) : below;
-          const int first_sent = (int)lane_get(sj, 0);
-          const bool cont = !(H & 1ull);  // lane 0's sentence runs on from the previous step
-          uint32_t c_n = 0, c_s = 0, c_q = 0;
-          if (cont) {
-            c_n = L.sent_n[first_sent];
-            c_s = L.sslot[first_sent];
-            c_q = L.sdef[first_sent];
-          }
-          const bool inherit = hb == 0;  // this lane's sentence began in an earlier step
-          const bool ev = valid && id != U_EMPTY;
-          const uint64_t E = __ballot(ev);
-          const uint32_t e = (uint32_t)__popcll(E & seg) + (inherit ? c_n : 0u);
-          const uint32_t nsl = (ev && id == U_DEFER && (int)e < max_tok) ? (len <= KEY1 ? 1u : 2u) : 0u;
+          const uint32_t nsl = (valid && id == U_DEFER) ? (len <= KEY1 ? 1u : 2u) : 0u;
           const uint64_t N1 = __ballot(nsl != 0), N2 = __ballot(nsl == 2);
-          const uint32_t qd = (uint32_t)__popcll(N1 & seg) + (inherit ? c_q : 0u);
-          const uint32_t o = qd - (inherit ? c_q : 0u) + (uint32_t)__popcll(N2 & seg) + (inherit ? c_s : 0u);
           const uint32_t need = (uint32_t)(__popcll(N1) + __popcll(N2));
-          // this step's slots come from the wave's chunk; a sentence's slots
-          // stay contiguous: on a chunk switch, the slots the running sentence
-          // took in earlier steps move to the new chunk
+          // this step's slots come from the wave's chunk; the tile's slots stay
+          // contiguous: on a chunk switch, the ones it took in earlier steps
+          // move to the new chunk (entries hold tile-relative slots)
           if (need > 0 && cur + need > cend) {
-            const uint32_t carried = cont ? c_s : 0u;
-            if (carried + need > SPLIT_CHUNK) {  // (a sentence with > 1024 slots)
+            if (tsl + need > SPLIT_CHUNK) {  // (a tile with > 1024 slots)
               ovf = true;
               break;
             }
-            if (chunk >= 0 && lane == 0) S.chunk_fill[chunk] = cur - cbase;
+            if (chunk >= 0 && lane == 0) S.chunk_fill[chunk] = tbase - cbase;  // (the moved ones not run)
             int c = 0;
             if (lane == 0) c = (int)atomicAdd(S.chunk_ctr, 1u);
             c = __builtin_amdgcn_readfirstlane(c);
             if ((uint32_t)c >= S.n_chunks) {  // record capacity exhausted
               chunk = -1;
-              cur = cend = cbase = 0;
+              cur = cend = cbase = tbase = 0;
               ovf = true;
               break;
             }
             chunk = c;
-            cbase = cur = (uint32_t)c * SPLIT_CHUNK;
+            cbase = (uint32_t)c * SPLIT_CHUNK;
             cend = cbase + SPLIT_CHUNK;
-            if (carried) {
+            if (tsl) {
               // (records this wave stored in an earlier step: drain its stores first)
               asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-              const uint32_t from = L.sqb[first_sent];
               for (int k = 0; k < 4; ++k)
-                for (uint32_t i = lane; i < carried; i += 64) *recq(S, k, cur + i) = *recq(S, k, from + i);
+                for (uint32_t i = lane; i < tsl; i += 64) *recq(S, k, cbase + i) = *recq(S, k, tbase + i);
               // (piece counts: wp_kernel writes the moved words' own; the moved
               // extension slots count 0)
-              for (uint32_t i = lane; i < carried; i += 64) S.cnt8[cur + i] = 0;
-              wsync();
-              if (lane == 0) L.sqb[first_sent] = cur;
-              cur += carried;
+              for (uint32_t i = lane; i < tsl; i += 64) S.cnt8[cbase + i] = 0;
             }
+            tbase = cbase;
+            cur = cbase + tsl;
           }
-          if (valid && (lane == last || ((H >> (lane + 1)) & 1ull))) {  // the sentence's last unit of the step
-            L.sent_n[sj] = (uint16_t)min(e + (ev ? 1u : 0u), 65535u);
-            L.sslot[sj] = (uint16_t)(o + nsl);
-            L.sdef[sj] = (uint16_t)(qd + (nsl ? 1u : 0u));
-          }
-          if (ev && (int)e < max_tok) {
-            const int64_t at = (int64_t)L.sst[sj] + e;
-            S.ent[ent0 + at] = (uint16_t)(id != U_DEFER ? id : (SPLIT_EDEF | o));
-            // ([CLS] / [SEP] come only from literal specials, never from WordPiece)
-            if (id == P.special[2] || id == P.special[3]) atomicOr(&L.sspec[sj >> 5], 1u << (sj & 31));
+          STAMP(10);
+          const uint32_t o = tsl + (uint32_t)(lane_rank(N1) + lane_rank(N2));  // tile-relative slot
+          if (valid) {
+            S.ent[ent0 + (int)L.ebs[sj] + rb + u] =
+                (uint16_t)(id == U_EMPTY ? SPLIT_EHOLE : id != U_DEFER ? id : (SPLIT_EDEF | o));
+            if (id == U_EMPTY || id == U_DEFER) atomicAdd(&L.sacc[sj], nsl | 0x10000u);
+            // ([CLS] / [SEP] come only from literal specials, never from WordPiece;
+            // a flag past the sentence's max_tok cut is harmless: the masked
+            // packer then checks the ids themselves)
+            else if (id == P.special[2] || id == P.special[3]) atomicOr(&L.sspec[sj >> 5], 1u << (sj & 31));
           }
           if (nsl) {
             // the record {len | slots << 8 | valid, count, key bytes 0..55}
-            const uint32_t slot = cur + (uint32_t)(__popcll(N1 & below) + __popcll(N2 & below));
-            if (o == 0) L.sqb[sj] = slot;
+            const uint32_t slot = tbase + o;
             uint32_t kd[6] = {key.d0, key.d1, key.d2, key.d3, key.d4, key.d5};
             const int a = src >> 2;
             const uint32_t sh = (uint32_t)(src & 3);
@@ -969,33 +971,37 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
               S.cnt8[slot + 1] = 0;  // (its pieces buffer holds pieces 28.. of the word)
             }
           }
+          tsl += need;
           cur += need;
-          prev_sent = (int)lane_get(sj, last);
           wsync();
+          STAMP(8);
         }
       }
       if (ovf) break;
-      STAMP(8);
     }  // rounds
     if (ovf) {
       fallback();
       return;
     }
-    if (lane < ns) {
-      const int64_t s = sa + lane;
-      const int ne = min((int)L.sent_n[lane], max_tok);
-      const int nsl = L.sslot[lane];
-      // one 8-B record per sentence for expand: entries | first queued entry
-      // << 16, first record slot (~0: no queued word)
-      S.smeta[s] = make_uint2((uint32_t)ne, nsl ? L.sqb[lane] : 0xFFFFFFFFu);
-      S.snslot[s] = (uint16_t)nsl;
-      P.out_ntok[s] = ne - (int)L.sdef[lane];
-      if (P.sent_spec) P.sent_spec[s] = (uint8_t)((L.sspec[lane >> 5] >> (lane & 31)) & 1u);
+    {
+      // one 8-B record per sentence for expand / count: entries (units, holes
+      // included) | its first slot relative to the tile's << 16, the tile's
+      // first slot; the direct ids so far (count_kernel adds the pieces)
+      const uint32_t acc = lane < ns ? L.sacc[lane] : 0u;
+      const uint32_t nsl = acc & 0xFFFFu;
+      const uint32_t sq0 = wave_incl_add(nsl) - nsl;
+      if (lane < ns) {
+        const int64_t s = sa + lane;
+        const uint32_t ne = (uint32_t)L.ufirst[lane + 1] - (uint32_t)L.ufirst[lane];
+        S.smeta[s] = make_uint2(ne | (sq0 << 16), tbase);
+        S.snslot[s] = (uint16_t)nsl;
+        P.out_ntok[s] = (int)(ne - (acc >> 16));
+        if (P.sent_spec) P.sent_spec[s] = (uint8_t)((L.sspec[lane >> 5] >> (lane & 31)) & 1u);
+      }
     }
   
     }();
     STAMP(9);
-    STAMP(10);
     if (DBG) acc[11] += 1;
   }
   if (DBG && lane == 0)
@@ -1317,9 +1323,9 @@ __global__ __launch_bounds__(256) void count_kernel(TokParams P, SplitParams S) 
   for (int64_t s = sA + (int64_t)blockIdx.x * 256 + threadIdx.x; s < sB; s += (int64_t)gridDim.x * 256) {
     const uint2 m = S.smeta[s];
     int32_t t = P.out_ntok[s];
-    if ((m.x & 0xFFFFu) != SPLIT_NENT_FB && m.y != 0xFFFFFFFFu) {
-      const uint32_t n = S.snslot[s];
-      for (uint32_t k = 0; k < n; ++k) t += S.cnt8[m.y + k];
+    if ((m.x & 0xFFFFu) != SPLIT_NENT_FB) {
+      const uint32_t n = S.snslot[s], q = m.y + (m.x >> 16);
+      for (uint32_t k = 0; k < n; ++k) t += S.cnt8[q + k];
       t = min(t, P.max_tok);
     }
     P.out_ntok[s] = t;
@@ -1362,7 +1368,7 @@ __global__ __launch_bounds__(256) void expand_kernel(TokParams P, SplitParams S)
       const int64_t d = P.out_tok_off[s];
       E.eoff[lane] = P.sent_off[s] - base - ebase;
       E.dst[lane] = d;
-      E.qb[lane] = m.y == 0xFFFFFFFFu ? 0u : m.y;
+      E.qb[lane] = (m.x & 0xFFFFu) == SPLIT_NENT_FB ? 0u : m.y;
       E.lim[lane] = (uint32_t)max((int64_t)0, min((int64_t)nt, P.out_cap - d));
     }
     const uint32_t x = wave_incl_add(ne);
@@ -1385,8 +1391,8 @@ __global__ __launch_bounds__(256) void expand_kernel(TokParams P, SplitParams S)
       }
       const uint32_t kk = g < T ? g - E.e0[j] : 0xFFFFFFFFu;
       const uint32_t v = kk != 0xFFFFFFFFu ? S.ent[E.eoff[j] + kk] : 0u;
-      u32x3 rq = u32x3{1u, 0u, 0u};
-      if (kk != 0xFFFFFFFFu && v >= SPLIT_EDEF)
+      u32x3 rq = u32x3{v == SPLIT_EHOLE ? 0u : 1u, 0u, 0u};  // (a hole: an empty unit, no token)
+      if (kk != 0xFFFFFFFFu && v >= SPLIT_EDEF && v != SPLIT_EHOLE)
         rq = *reinterpret_cast<const u32x3*>(reinterpret_cast<const uint32_t*>(pcs + (size_t)(E.qb[j] + (v & 0xFFFu)) * 4) + 1);
       const uint32_t cnt = kk != 0xFFFFFFFFu ? rq.x : 0u;
       const uint32_t h = kk == 0 ? 1u : 0u;
@@ -1399,8 +1405,8 @@ __global__ __launch_bounds__(256) void expand_kernel(TokParams P, SplitParams S)
         uint16_t* o = P.out_ids + E.dst[j];
         const uint32_t lim = E.lim[j];
         // (the first token of a direct id and of a record in one store)
-        if (p < lim) o[p] = (uint16_t)(v < SPLIT_EDEF ? v : rq.y & 0xFFFFu);
-        if (v >= SPLIT_EDEF) {
+        if (cnt && p < lim) o[p] = (uint16_t)(v < SPLIT_EDEF ? v : rq.y & 0xFFFFu);
+        if (v >= SPLIT_EDEF && v != SPLIT_EHOLE) {
           if (cnt > 1 && p + 1 < lim) o[p + 1] = (uint16_t)(rq.y >> 16);
           if (cnt > 2 && p + 2 < lim) o[p + 2] = (uint16_t)(rq.z & 0xFFFFu);
           if (cnt > 3 && p + 3 < lim) o[p + 3] = (uint16_t)(rq.z >> 16);
