@@ -46,7 +46,7 @@ struct TokParams {
 
 int64_t tile_count(int64_t nbytes);
 hipError_t launch_tile_bounds(const int64_t* sent_off, int64_t n_sent, int64_t n_tiles, int64_t* tile_sent,
-                              hipStream_t s);
+                              int64_t* tile_off, hipStream_t s);
 hipError_t launch_tokenize_fallback(const TokParams& P, const int64_t* tile_sent, const int32_t* fb_list,
                                     const int32_t* fb_count, int grid, hipStream_t s);
 const void* tokenize_fallback_kernel_ptr();
@@ -81,6 +81,7 @@ struct SplitParams {
   int64_t seg_tiles;       // tiles per segment (SPLIT_SEG_TILES; tests force small ones)
   int64_t t0, t1;          // the segment's tiles
   const int64_t* tile_sent;
+  const int64_t* tile_off;  // sent_off[tile_sent[t]] (the scan stages a tile's bounds in one round trip)
   uint16_t* ent;
   uint4* rec;              // 4 uint4 per slot
   uint4* pcs;              // WordPiece output (count + pieces) per slot, apart from the keys

@@ -25,7 +25,8 @@ namespace lddl {
 constexpr int TILE_SHIFT = 10;  // nominal tile: sentences starting in 1 KiB
 
 // tile_sent[t] = first sentence whose start (relative) >= t * TILE
-__global__ void tile_bounds_kernel(const int64_t* sent_off, int64_t n_sent, int64_t n_tiles, int64_t* tile_sent) {
+__global__ void tile_bounds_kernel(const int64_t* sent_off, int64_t n_sent, int64_t n_tiles, int64_t* tile_sent,
+                                   int64_t* tile_off) {
   const int64_t base = sent_off[0];
   for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s <= n_sent; s += (int64_t)gridDim.x * blockDim.x) {
     // tiles t with off[s-1] < t*TILE <= off[s] map to s (s = n_sent: the rest)
@@ -34,7 +35,10 @@ __global__ void tile_bounds_kernel(const int64_t* sent_off, int64_t n_sent, int6
     int64_t t0 = (lo >> TILE_SHIFT) + 1;  // first t with t*TILE > lo
     if (lo < 0) t0 = 0;
     const int64_t t1 = hi >> TILE_SHIFT;  // last t with t*TILE <= hi
-    for (int64_t t = t0; t <= t1 && t <= n_tiles; ++t) tile_sent[t] = s;
+    for (int64_t t = t0; t <= t1 && t <= n_tiles; ++t) {
+      tile_sent[t] = s;
+      if (tile_off) tile_off[t] = sent_off[s];
+    }
   }
 }
 
@@ -83,8 +87,8 @@ hipError_t launch_list_all_tiles(int64_t n_tiles, int32_t* fb_list, int32_t* fb_
 }
 
 hipError_t launch_tile_bounds(const int64_t* sent_off, int64_t n_sent, int64_t n_tiles, int64_t* tile_sent,
-                              hipStream_t s) {
-  hipLaunchKernelGGL(tile_bounds_kernel, dim3(4096), dim3(256), 0, s, sent_off, n_sent, n_tiles, tile_sent);
+                              int64_t* tile_off, hipStream_t s) {
+  hipLaunchKernelGGL(tile_bounds_kernel, dim3(4096), dim3(256), 0, s, sent_off, n_sent, n_tiles, tile_sent, tile_off);
   return hipGetLastError();
 }
 

@@ -86,7 +86,7 @@ struct alignas(16) Lds {
   uint16_t ebs[NSCAP];         // entry index base: unit u of sentence j has entry sst[j] + u - ufirst[j]
   uint32_t xent[XCAP];         // table entry of each expansion marker
   uint8_t xlen[XCAP];          // its normalised byte length
-  int32_t misc[4];             // 0 side-buffer cursor, 1 #markers, 2 overflow
+  int32_t misc[4];             // 0 side-buffer cursor, 1 #markers
   uint32_t sspec[2];           // sentences holding a [CLS] / [SEP] token (P.sent_spec)
 };
 
@@ -155,7 +155,7 @@ __device__ __forceinline__ int utf8_put(uint32_t* nb, int p, uint32_t c) {
 }
 
 // Compact / expand the dirty span [p, q).  Returns its normalised length
-// (source in *src), -1 on overflow (flagged in misc[2]).  Without expansion
+// (source in *src), -1 on overflow (the tile falls back).  Without expansion
 // markers in the tile (misc[1] == 0) a dirty span holds only fillers
 // (dropped / shortened chars): it compacts in place, one pass; otherwise it
 // goes to the side buffer (count pass, then the expansions written).
@@ -190,10 +190,7 @@ __device__ int dirty_normalize(Lds& L, const TokParams& P, int p, int q, int* sr
   }
   if (len == 0) return 0;
   const int off = atomicAdd(&L.misc[0], len);
-  if (off + len > DCAP) {
-    L.misc[2] = 1;
-    return -1;
-  }
+  if (off + len > DCAP) return -1;
   int o = CAP + off;
   *src = o;
   for (int i = p; i < q;) {
@@ -335,15 +332,18 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
     __builtin_amdgcn_global_load_lds((const uint32_t*)g, (__attribute__((address_space(3))) uint32_t*)l, 4, 0, 0);
   };
   auto drain = [&]() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); };
-  // The next tile's staging runs inside the current one (stage1 after its
-  // sentence starts, stage2 after its exception pass, stage3 -- the raw
-  // bytes into rp, free by then -- before its unit steps), so that its three
-  // dependent round trips fly behind this tile's work; the loop top finishes
-  // whatever a tile that returned early left undone.
+  // The next tile's staging runs inside the current one: stage1 (its bounds
+  // and byte offsets, tile_sent / tile_off, by LDS-DMA) right after this
+  // tile's own arrived, stage2 (its raw bytes into rp -- free after this
+  // tile's exception pass -- and its sentence starts) before this tile's
+  // unit steps, so both round trips fly behind this tile's work; the loop
+  // top finishes whatever a tile that returned early left undone.
   auto stage1 = [&]() {
     if (nst != 0) return;
     nst = 1;
-    if (tn < S.t1 && lane < 4) dma4(reinterpret_cast<const uint32_t*>(S.tile_sent + tn) + lane, L.pb);
+    // (lanes 0-3: tile_sent[tn], [tn + 1] -> pb[0..3]; lanes 4-7: tile_off -> pb[4..7])
+    if (tn < S.t1 && lane < 8)
+      dma4(reinterpret_cast<const uint32_t*>(lane < 4 ? S.tile_sent + tn : S.tile_off + tn) + (lane & 3), L.pb);
   };
   auto stage2 = [&]() {
     if (nst != 1) return;
@@ -354,17 +354,9 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
     n_sa = uni64(*reinterpret_cast<const int64_t*>(&L.pb[0]));
     n_sb = uni64(*reinterpret_cast<const int64_t*>(&L.pb[2]));
     if (n_sa >= n_sb) return;
-    if (lane < 2) dma4(reinterpret_cast<const uint32_t*>(P.sent_off + n_sa) + lane, L.pb + 4);
-    if (lane < 2) dma4(reinterpret_cast<const uint32_t*>(P.sent_off + n_sb) + lane, L.pb + 6);
-    if (lane < n_sb - n_sa) n_spos = P.sent_off[n_sa + lane];
-  };
-  auto stage3 = [&]() {
-    if (nst != 2) return;
-    nst = 3;
-    if (n_sa >= n_sb) return;
-    drain();
     n_A = uni64(*reinterpret_cast<const int64_t*>(&L.pb[4]));
     n_B = uni64(*reinterpret_cast<const int64_t*>(&L.pb[6]));
+    if (lane < n_sb - n_sa) n_spos = P.sent_off[n_sa + lane];
     const int aoff = (int)(reinterpret_cast<uintptr_t>(P.bytes + n_A) & 15u);
     const int64_t nb64 = (n_B - n_A) + aoff;
     if (nb64 > CAP || n_sb - n_sa > NSCAP) return;  // the tile falls back: no bytes needed
@@ -381,13 +373,13 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
     wsync();
     stage1();
     stage2();
-    stage3();
     const int64_t sa = n_sa, sb = n_sb, A = n_A, B = n_B, spos = n_spos;
     STAMP(0);
     if (dma_pending) drain();  // this tile's raw bytes
     dma_pending = false;
     nst = 0;
     tn = t + nwaves;
+    stage1();
     [&]() {
     if (sa >= sb) return;
     const int ns = (int)(sb - sa);
@@ -416,7 +408,6 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
     if (lane == 0) {
       L.misc[0] = 0;
       L.misc[1] = 0;
-      L.misc[2] = 0;
       L.sspec[0] = 0;
       L.sspec[1] = 0;
     }
@@ -427,7 +418,6 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
       L.sst[lane] = (uint16_t)pos;
       if (pos < nb) atomicOr(&L.sb[pos >> 5], 1u << (pos & 31));
     }
-    stage1();
     STAMP(1);
     // ---- 1: raw bytes -> masks + normalised bytes in place ------------------
     uint32_t W, I, S_, CS, D, X, inwin;
@@ -735,7 +725,6 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
       D = ((D & ~im) | id) & inwin;
     }
     const bool wbad = __any(bad);
-    stage2();
     STAMP(3);
     wsync();
     // ---- 2: units -----------------------------------------------------------
@@ -819,7 +808,7 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
           if (u >= rb && u < rb + nr) up[u - rb] = (uint16_t)(p0 + __ffs(m) - 1);
       }
       wsync();
-      stage3();  // (rp is free: the next tile's bytes fly behind the unit steps)
+      stage2();  // (rp is free: the next tile's bytes fly behind the unit steps)
       STAMP(5);
       // ---- 3+4, 64 units per step (one per lane), in unit order: prep
       //      (dirty words, specials, long words), the whole-word probe (slot 0
@@ -862,7 +851,12 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
             sj = (uint32_t)lo;
           }
           int src = p, len = valid ? q - p : 0;
-          if (dirty) len = max(dirty_normalize(L, P, src, src + len, &src), 0);
+          bool lovf = false;  // the tile falls back: side buffer full, or a queued word too long for a record
+          if (dirty) {
+            len = dirty_normalize(L, P, src, src + len, &src);
+            lovf = len < 0;
+            len = max(len, 0);
+          }
           Key6 key = {0, 0, 0, 0, 0, 0};
           if (len > 0 && len <= 24) key = load_key(L.nb, src, len);
           if (len > 0) {
@@ -874,7 +868,7 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
             } else {
               id = U_DEFER;
               w = 1;
-              if (len > KEYMAX) L.misc[2] = 1;  // too long for a record: the tile falls back
+              lovf |= len > KEYMAX;
             }
           }
           STAMP(6);
@@ -886,8 +880,7 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
               w = 0;
             }
           }
-          wsync();
-          if (L.misc[2]) {
+          if (__any(lovf)) {
             ovf = true;
             break;
           }
@@ -1479,7 +1472,7 @@ __global__ void smeta_fallback_kernel(uint2* smeta, int64_t n_sent) {
 hipError_t launch_tokenize_serial_dense(const TokParams& P, int64_t nbytes, int64_t* tile_sent, SplitParams S,
                                         int n_cu, int fb_grid, hipStream_t s) {
   const int64_t n_tiles = tile_count(nbytes);
-  hipError_t e = launch_tile_bounds(P.sent_off, P.n_sent, n_tiles, tile_sent, s);
+  hipError_t e = launch_tile_bounds(P.sent_off, P.n_sent, n_tiles, tile_sent, nullptr, s);
   if (e != hipSuccess || (e = hipMemsetAsync(P.out_tok_off, 0, sizeof(int64_t), s)) != hipSuccess) return e;
   S.tile_sent = tile_sent;
   S.t0 = 0;
@@ -1500,7 +1493,7 @@ hipError_t launch_tokenize_split(const TokParams& P, int64_t nbytes, int64_t* ti
     return e;
   };
   const int64_t n_tiles = tile_count(nbytes);
-  hipError_t e = launch_tile_bounds(P.sent_off, P.n_sent, n_tiles, tile_sent, s);
+  hipError_t e = launch_tile_bounds(P.sent_off, P.n_sent, n_tiles, tile_sent, const_cast<int64_t*>(S.tile_off), s);
   if (e != hipSuccess) return e;
   if ((e = hipMemsetAsync(P.out_tok_off, 0, sizeof(int64_t), s)) != hipSuccess) return e;
   S.tile_sent = tile_sent;
