@@ -1326,18 +1326,25 @@ __global__ __launch_bounds__(256) void count_kernel(TokParams P, SplitParams S) 
 }
 
 // --------------------------------------------------------------- expand --
-// Dense output: a wave per group of 64 sentences; their entries (every one:
-// a vocab id, or a queued word's record) in steps of 64, one per lane.  Per
-// step, two rounds of loads: the entries, then the records' count and first 4
-// pieces (one 12-B load); a segmented scan of the token counts gives each
+// Dense output: a wave per group of 64 sentences; their entries (a vocab id,
+// a hole, or a queued word's record) in steps of 64, one per lane.  An entry's
+// sentence comes from a scatter of the sentences' first entries (LDS max) and
+// a wave max-scan; the step's entries are loaded one step ahead, so each
+// step's record loads (count + first 4 pieces, one 12-B load) fly with the
+// next step's entry loads.  A segmented scan of the token counts gives each
 // token's position in its sentence, written at out_tok_off[s] + position
 // while below the sentence's final count (count_kernel) and out_cap.
+struct ExpSent {
+  int64_t eb;    // entry index of the sentence's entry g (group numbering) = eb + g
+  int64_t dst;   // output index of its first token
+  uint32_t qb;   // the tile's first record slot
+  uint32_t lim;  // tokens it writes: min(final count, out_cap - dst)
+  uint32_t e0;   // its first entry (group numbering)
+  uint32_t pad;
+};
 struct ExpLds {
-  uint32_t e0[65];      // group entry offsets
-  int64_t eoff[64];     // entry index of the sentence's first entry
-  int64_t dst[64];      // output index of its first token
-  uint32_t qb[64];      // its first record slot
-  uint32_t lim[64];     // tokens it writes: min(final count, out_cap - dst)
+  ExpSent sn[64];
+  uint32_t own[64];  // scatter: the sentence whose first entry is the step's entry k
 };
 
 __global__ __launch_bounds__(256) void expand_kernel(TokParams P, SplitParams S) {
@@ -1353,59 +1360,80 @@ __global__ __launch_bounds__(256) void expand_kernel(TokParams P, SplitParams S)
   for (int64_t g0 = sA + ((int64_t)blockIdx.x * 4 + wv) * 64; g0 < sB; g0 += nwaves * 64) {
     const int64_t s = g0 + lane;
     uint32_t ne = 0;
+    int64_t eoff = 0, d = 0;
+    uint32_t qb = 0, lim = 0;
     if (s < sB) {
       const uint2 m = S.smeta[s];
       const int32_t nt = P.out_ntok[s];
       ne = m.x & 0xFFFFu;
       if (ne == SPLIT_NENT_FB) ne = (uint32_t)nt;  // the serial path's ids, all direct
-      const int64_t d = P.out_tok_off[s];
-      E.eoff[lane] = P.sent_off[s] - base - ebase;
-      E.dst[lane] = d;
-      E.qb[lane] = (m.x & 0xFFFFu) == SPLIT_NENT_FB ? 0u : m.y;
-      E.lim[lane] = (uint32_t)max((int64_t)0, min((int64_t)nt, P.out_cap - d));
+      d = P.out_tok_off[s];
+      eoff = P.sent_off[s] - base - ebase;
+      qb = (m.x & 0xFFFFu) == SPLIT_NENT_FB ? 0u : m.y;
+      lim = (uint32_t)max((int64_t)0, min((int64_t)nt, P.out_cap - d));
     }
     const uint32_t x = wave_incl_add(ne);
-    E.e0[lane] = x - ne;
+    const uint32_t e0 = x - ne;
     const uint32_t T = lane_get(x, 63);
-    if (lane == 63) E.e0[64] = T;
-    wsync();
+    ExpSent es;
+    es.eb = eoff - (int64_t)e0;
+    es.dst = d;
+    es.qb = qb;
+    es.lim = lim;
+    es.e0 = e0;
+    es.pad = 0;
+    E.sn[lane] = es;
+    // the sentence of each entry of step st (entries st + lane)
+    uint32_t own_carry = 0;
+    auto owner = [&](uint32_t st) -> uint32_t {
+      E.own[lane] = 0u;
+      wsync();
+      if (ne != 0 && e0 >= st && e0 < st + 64) atomicMax(&E.own[e0 - st], (uint32_t)lane);
+      wsync();
+      const uint32_t o = max(wave_incl_max(E.own[lane]), own_carry);
+      own_carry = lane_get(o, 63);
+      return o;
+    };
+    // step st's entry: sentence j, entry value v (loaded), head (first entry of j)
+    uint32_t j = 0, v = 0;
+    bool in = false, head = false;
+    auto load_step = [&](uint32_t st) {
+      const uint32_t g = st + (uint32_t)lane;
+      j = owner(st);
+      in = g < T;
+      const ExpSent sj = E.sn[j];
+      head = in && g == sj.e0;
+      v = in ? S.ent[sj.eb + g] : 0u;
+    };
+    if (T > 0) load_step(0);
     uint32_t carry = 0;
     for (uint32_t st = 0; st < T; st += 64) {
-      const uint32_t g = st + (uint32_t)lane;
-      int j = 0;
-      if (g < T) {  // sentence of this lane's entry: last j with e0[j] <= g
-        int lo = 0, hi = 63;
-        while (lo < hi) {
-          const int mid = (lo + hi + 1) >> 1;
-          if (E.e0[mid] <= g) lo = mid;
-          else hi = mid - 1;
-        }
-        j = lo;
-      }
-      const uint32_t kk = g < T ? g - E.e0[j] : 0xFFFFFFFFu;
-      const uint32_t v = kk != 0xFFFFFFFFu ? S.ent[E.eoff[j] + kk] : 0u;
-      u32x3 rq = u32x3{v == SPLIT_EHOLE ? 0u : 1u, 0u, 0u};  // (a hole: an empty unit, no token)
-      if (kk != 0xFFFFFFFFu && v >= SPLIT_EDEF && v != SPLIT_EHOLE)
-        rq = *reinterpret_cast<const u32x3*>(reinterpret_cast<const uint32_t*>(pcs + (size_t)(E.qb[j] + (v & 0xFFFu)) * 4) + 1);
-      const uint32_t cnt = kk != 0xFFFFFFFFu ? rq.x : 0u;
-      const uint32_t h = kk == 0 ? 1u : 0u;
-      uint32_t hv = h, sv = cnt;
+      const uint32_t cj = j, cv = v;
+      const bool cin = in, chead = head;
+      const bool rec = cin && cv >= SPLIT_EDEF && cv != SPLIT_EHOLE;
+      const ExpSent sj = E.sn[cj];
+      const size_t ri = (size_t)(sj.qb + (cv & 0xFFFu)) * 4;
+      u32x3 rq = u32x3{cin && cv != SPLIT_EHOLE ? 1u : 0u, 0u, 0u};  // (a hole: an empty unit, no token)
+      if (rec) rq = *reinterpret_cast<const u32x3*>(reinterpret_cast<const uint32_t*>(pcs + ri) + 1);
+      if (st + 64 < T) load_step(st + 64);  // (the next step's entries fly with these record loads)
+      const uint32_t cnt = rq.x;
+      uint32_t hv = chead ? 1u : 0u, sv = cnt;
       wave_seg_incl_add(hv, sv);
       uint32_t ex = wave_shr1(sv);
       if (!wave_shr1(hv)) ex += carry;
-      const uint32_t p = h ? 0u : ex;  // tokens of the sentence before this entry
-      if (kk != 0xFFFFFFFFu) {
-        uint16_t* o = P.out_ids + E.dst[j];
-        const uint32_t lim = E.lim[j];
+      const uint32_t p = chead ? 0u : ex;  // tokens of the sentence before this entry
+      if (cin) {
+        uint16_t* o = P.out_ids + sj.dst;
+        const uint32_t lm = sj.lim;
         // (the first token of a direct id and of a record in one store)
-        if (cnt && p < lim) o[p] = (uint16_t)(v < SPLIT_EDEF ? v : rq.y & 0xFFFFu);
-        if (v >= SPLIT_EDEF && v != SPLIT_EHOLE) {
-          if (cnt > 1 && p + 1 < lim) o[p + 1] = (uint16_t)(rq.y >> 16);
-          if (cnt > 2 && p + 2 < lim) o[p + 2] = (uint16_t)(rq.z & 0xFFFFu);
-          if (cnt > 3 && p + 3 < lim) o[p + 3] = (uint16_t)(rq.z >> 16);
+        if (cnt && p < lm) o[p] = (uint16_t)(cv < SPLIT_EDEF ? cv : rq.y & 0xFFFFu);
+        if (rec) {
+          if (cnt > 1 && p + 1 < lm) o[p + 1] = (uint16_t)(rq.y >> 16);
+          if (cnt > 2 && p + 2 < lm) o[p + 2] = (uint16_t)(rq.z & 0xFFFFu);
+          if (cnt > 3 && p + 3 < lm) o[p + 3] = (uint16_t)(rq.z >> 16);
           if (cnt > 4) {
-            const uint16_t* pc = reinterpret_cast<const uint16_t*>(pcs + (size_t)(E.qb[j] + (v & 0xFFFu)) * 4);
-            for (uint32_t q = 4; q < cnt && p + q < lim; ++q) o[p + q] = pc[piece_at((int)q)];
+            const uint16_t* pc = reinterpret_cast<const uint16_t*>(pcs + ri);
+            for (uint32_t q = 4; q < cnt && p + q < lm; ++q) o[p + q] = pc[piece_at((int)q)];
           }
         }
       }

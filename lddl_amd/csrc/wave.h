@@ -39,6 +39,17 @@ __device__ __forceinline__ uint32_t wave_incl_add(uint32_t x) {
 }
 __device__ __forceinline__ int wave_incl_add(int x) { return (int)wave_incl_add((uint32_t)x); }
 
+// inclusive max-scan over the wave (unsigned; the out-of-range reads give 0)
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {
+  x = max(x, dpp0<DPP_ROW_SHR1>(x));
+  x = max(x, dpp0<DPP_ROW_SHR2>(x));
+  x = max(x, dpp0<DPP_ROW_SHR4>(x));
+  x = max(x, dpp0<DPP_ROW_SHR8>(x));
+  x = max(x, dpp0<DPP_ROW_BCAST15, 0xA>(x));
+  x = max(x, dpp0<DPP_ROW_BCAST31, 0xC>(x));
+  return x;
+}
+
 // lane l receives lane l-1's value, lane 0 receives 0
 __device__ __forceinline__ uint32_t wave_shr1(uint32_t x) { return dpp0<DPP_WAVE_SHR1>(x); }
 __device__ __forceinline__ int wave_shr1(int x) { return (int)dpp0<DPP_WAVE_SHR1>((uint32_t)x); }
