@@ -1197,14 +1197,16 @@ __global__ __launch_bounds__(64 * WAVES) void wp_kernel(TokParams P, SplitParams
       }
     }
     WP_STAMP(0)
-    // ---- B: idle lanes take the next slots of the stream; their record
-    //      loads fly together with the bucket loads
+    // ---- B: lanes without a loaded record take the next slots of the
+    //      stream, working lanes included (one record ahead: a lane that
+    //      finishes its word in C begins the next one in D of the same step
+    //      instead of idling a step); their loads fly with the bucket loads
     {
-      const uint64_t idle = __ballot(r < 0 && pr < 0);
+      const uint64_t idle = __ballot(pr < 0);
       if (idle != 0 && c < nch) {
         const uint32_t avail = fill - off;
         const int k = lane_rank(idle);
-        if (r < 0 && pr < 0 && (uint32_t)k < avail) {
+        if (pr < 0 && (uint32_t)k < avail) {
           pr = (int)(c * SPLIT_CHUNK + off + (uint32_t)k);
           q0 = *recq(S, 0, (uint32_t)pr);
           q1 = *recq(S, 1, (uint32_t)pr);
@@ -1264,15 +1266,17 @@ __global__ __launch_bounds__(64 * WAVES) void wp_kernel(TokParams P, SplitParams
       }
     }
     WP_STAMP(2)
-    // ---- D: lanes with a loaded record begin it
-    if (r < 0 && pr >= 0) {
+    // ---- D: an extension slot is dropped (refilled in the next B), a long
+    //      key's bytes 24.. are loaded (working lanes too: ready when their
+    //      word ends), idle lanes with a loaded record begin it
+    if (pr >= 0) {
       if (q0.x == 0u) {  // an extension slot
         pr = -1;
       } else if ((q0.x & 0xFFu) > 24u && !qlong) {
         q2 = *recq(S, 2, (uint32_t)pr);
         q3 = *recq(S, 3, (uint32_t)pr);
         qlong = true;
-      } else {
+      } else if (r < 0) {
         const int len = (int)(q0.x & 0xFFu);
         kb[0] = q0.z; kb[64] = q0.w;
         kb[128] = q1.x; kb[192] = q1.y; kb[256] = q1.z; kb[320] = q1.w;
@@ -1535,6 +1539,7 @@ hipError_t launch_tokenize_split(const TokParams& P, int64_t nbytes, int64_t* ti
     if ((e = mark(0, 0)) != hipSuccess) return e;
     if (P.dbg) e = tok5::launch_scan<SCAN_WAVES, true, 5>(P, S, n_cu, s);
     else if (cfg == 1) e = tok5::launch_scan<SCAN_WAVES, false, 1>(P, S, n_cu, s);
+    else if (cfg == 6) e = tok5::launch_scan<SCAN_WAVES, false, 6>(P, S, n_cu, s);
     else e = tok5::launch_scan<SCAN_WAVES, false, 5>(P, S, n_cu, s);
     if (e != hipSuccess || (e = mark(0, 1)) != hipSuccess || (e = mark(1, 0)) != hipSuccess) return e;
     if ((e = tok5::launch_wp<WP_WAVES>(P, S, n_cu, s)) != hipSuccess) return e;
