@@ -147,7 +147,15 @@ def _strip_spans(buf, starts, ends):
   e = np.where(keep, nz[np.maximum(i1, 0)] + 1 if len(nz) else 0, 0)
   off, ln = s[keep].astype(np.int64), (e - s)[keep].astype(np.int64)
   if len(off):
-    hi = (buf[off] >= 0x80) | (buf[off + ln - 1] >= 0x80)
+    # a line may start or end with a Unicode space (str.isspace beyond ASCII:
+    # U+0085, U+00A0 lead 0xC2; U+1680, U+2000-U+205F, U+3000 lead 0xE1-0xE3)
+    # only if its first byte or its last character's lead byte is one of
+    # those: only such lines are decoded (not every CJK line)
+    end = off + ln
+    f0 = buf[off]
+    l2 = np.where(ln >= 2, buf[np.maximum(end - 2, off)], 0)
+    l3 = np.where(ln >= 3, buf[np.maximum(end - 3, off)], 0)
+    hi = ((f0 == 0xC2) | ((f0 >= 0xE1) & (f0 <= 0xE3)) | (l2 == 0xC2) | ((l3 >= 0xE1) & (l3 <= 0xE3)))
     for k in np.flatnonzero(hi):
       raw = bytes(buf[off[k]:off[k] + ln[k]])
       t = raw.decode('utf-8')
@@ -158,6 +166,9 @@ def _strip_spans(buf, starts, ends):
     nonempty = ln > 0
     off, ln = off[nonempty], ln[nonempty]
   return off, ln
+
+
+INDEX_WINDOW = 64 << 20  # bytes of a file indexed at a time
 
 
 class RecordIndex:
@@ -183,8 +194,38 @@ class RecordIndex:
     if size == 0:
       return np.zeros(0, np.int64), np.zeros(0, np.int64)
     buf = np.memmap(path, dtype=np.uint8, mode='r')
-    s, e = _line_spans(buf, linedelimiter == '\r\n')
-    return _strip_spans(buf, s, e)
+    # windows of ~INDEX_WINDOW bytes, each cut right after a line feed (a
+    # window starts a line; a \r\n pair never splits), so the per-byte masks
+    # and indices live for one window at a time, not the whole file
+    crlf = linedelimiter == '\r\n'
+
+    def cuts(lo, hi):  # line feeds in [lo, hi) that end a line (\r\n only: after a \r)
+      w = buf[lo:hi]
+      lf = np.flatnonzero(w == 10)
+      if crlf and len(lf):
+        prev = np.where(lf > 0, w[np.maximum(lf - 1, 0)], buf[lo - 1] if lo > 0 else 0)
+        lf = lf[prev == 13]
+      return lf + lo
+
+    offs, lns = [], []
+    a = 0
+    while a < size:
+      b = min(size, a + INDEX_WINDOW)
+      if b < size:
+        lf = cuts(a, b)
+        while len(lf) == 0 and b < size:  # a line longer than the window
+          b2 = min(size, b + INDEX_WINDOW)
+          lf = cuts(b, b2)
+          b = b2
+        if len(lf):
+          b = int(lf[-1]) + 1
+      w = buf[a:b]
+      s, e = _line_spans(w, linedelimiter == '\r\n')
+      o, l = _strip_spans(w, s, e)
+      offs.append(o + a)
+      lns.append(l)
+      a = b
+    return np.concatenate(offs), np.concatenate(lns)
 
   @classmethod
   def build(cls, files, linedelimiter=None, file_ids=None):

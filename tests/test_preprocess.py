@@ -155,13 +155,17 @@ def test_reader_code_records_split_on_crlf_only(tmp_path):
   assert idx.texts(range(len(idx))) == want
 
 
-def test_reader_index_matches_text_mode_on_random_bytes(tmp_path):
+@pytest.mark.parametrize('window', [None, 5, 37])
+def test_reader_index_matches_text_mode_on_random_bytes(tmp_path, monkeypatch, window):
   """RecordIndex (vectorised, bytes) == Python text mode + strip + filter on
-  random mixtures of terminators, ASCII / Unicode spaces and text."""
+  random mixtures of terminators, ASCII / Unicode spaces and text, also with
+  tiny file windows (cut after a line feed) that split runs every way."""
   from lddl_amd import readers
+  if window:
+    monkeypatch.setattr(readers, 'INDEX_WINDOW', window)
   rng = np.random.default_rng(3)
   atoms = ['a', 'bc', ' ', '\t', '\n', '\r', '\r\n', '\x0b', '\x0c', '\x1c', '\x1f', '\x85', '\xa0', ' ',
-           '　', 'é', '中', '😀', '​']
+           '　', 'é', '中', '😀', '​', '\u2028', '\u1680', '\u205f', '\u3000', 'ア']
   for k in range(6):
     s = ''.join(atoms[i] for i in rng.integers(0, len(atoms), 3000))
     f = _write(tmp_path / ('r%d.txt' % k), s.encode('utf-8'))
