@@ -54,6 +54,9 @@ def parse():
   ap.add_argument('--no-sample-check', action='store_true',
                   help='skip the oracle comparison of one full-size partition after the timed steps')
   ap.add_argument('--cpu-seconds', type=float, default=12.0)
+  ap.add_argument('--frontend-mb', type=float, default=100.0,
+                  help='MB of raw input for the front-end leg (the preprocessor CLI end to end on BASELINE '
+                       'configs[0]: seq 128, no binning; rank 0 at N=1, before the bench touches the GPU; 0: off)')
   ap.add_argument('--parquet-parts', type=int, default=64,
                   help='after timing: write this many partitions as parquet shards and report the writer rate '
                        '(GPU string rendering + host Arrow/parquet encode; 0 = skip)')
@@ -335,6 +338,42 @@ def parquet_sample(args, pk, res, sh):
     shutil.rmtree(d, ignore_errors=True)
 
 
+def frontend_leg(mb):
+  """The preprocessor CLI end to end (lddl_amd.preprocess.main, the
+  reference's preprocess_bert_pretrain) on BASELINE.json configs[0]: mb MB of
+  synthetic Wikipedia-style raw input (one ``wiki-<id> <text>`` document per
+  line), seq 128, no static masking, unbinned parquet.  Runs first in the
+  process (its split workers fork before anything touches the GPU); wall,
+  host read / sentence split / GPU / parquet write seconds and the split time
+  hidden behind the GPU and the writer, as preprocess.main reports them."""
+  import shutil
+  import tempfile
+  from lddl_amd import preprocess, synth
+  d = tempfile.mkdtemp(prefix='lddl_bench_fe_')
+  try:
+    t0 = time.perf_counter()
+    c = synth.make_wiki(int(mb * (1 << 20)), seed=11)
+    os.makedirs(os.path.join(d, 'wiki', 'en'))
+    with open(os.path.join(d, 'wiki', 'en', 'a.txt'), 'w', encoding='utf-8') as f:
+      for i, doc in enumerate(c.documents()):
+        f.write('wiki-%d %s\n' % (i, ' '.join(doc)))
+    gen_s = time.perf_counter() - t0
+    raw = os.path.getsize(os.path.join(d, 'wiki', 'en', 'a.txt'))
+    a = preprocess.attach_args().parse_args(
+        ['--wikipedia', os.path.join(d, 'wiki'), '--sentence-splitter', 'rules', '--sink', os.path.join(d, 'out'),
+         '--target-seq-length', '128', '--block-size', str(1 << 20), '--chunk-mb', '16', '--seed', '7'])
+    t0 = time.perf_counter()
+    files, t = preprocess.main(a)
+    el = time.perf_counter() - t0
+    t.pop('partitions', None)
+    out = {'what': 'preprocess CLI end to end, BERT seq 128 unbinned (BASELINE configs[0])', 'raw_mb': raw / 1e6,
+           'files': len(files), 'seconds': el, 'raw_mb_per_s': raw / 1e6 / el, 'gen_s': gen_s}
+    out.update({k: v for k, v in t.items() if isinstance(v, (int, float, str))})
+    return out
+  finally:
+    shutil.rmtree(d, ignore_errors=True)
+
+
 def launch_ranks(args):
   """`--gpus N` without a launcher: start N rank processes (this process has
   not touched the GPU: torch.cuda.device_count() does not initialise it) with
@@ -401,6 +440,7 @@ def main():
     raise SystemExit('bench.py: --gpus %d but WORLD_SIZE=%d' % (args.gpus, world))
   if args.launch_check:
     return launch_check(args, rank, world)
+  fe = frontend_leg(args.frontend_mb) if world == 1 and args.frontend_mb > 0 else None
   torch.cuda.set_device(local)
   device = torch.device('cuda', local)
   dist = None
@@ -522,7 +562,8 @@ def main():
                                      'frac': alg_call / (tok_kernels_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}},
       'tokenize_ms': tk, 'tokenize_kernels_ms': {'scan': ks['scan_ms'], 'wordpiece': ks['wordpiece_ms'],
                                                  'expand': ks['expand_ms']},
-      'wordpiece_records_per_gpu': ks['records'], 'gen_s': gen_s,
+      'wordpiece_records_per_gpu': ks['records'], 'tokenizer_fallback_tiles': ks['fallback_tiles'],
+      'gen_s': gen_s,
   }
   # HBM traffic of the tokenize call from the committed PMC passes of this
   # same workload (rocprofv3 cannot run inside the timed process)
@@ -537,6 +578,8 @@ def main():
     pass
   if args.parquet_parts > 0:
     line['parquet_writer'] = parquet_sample(args, pk, res, sh)
+  if fe is not None:
+    line['frontend'] = fe
   if not args.no_cpu_baseline and world == 1:  # the host leg (the oracle): rank 0 at N=1 only
     line['cpu_baseline'] = cpu_baseline(args, base, pdo, args.cpu_seconds)
     if not args.no_sample_check:  # the oracle as the checker of one full-size partition of the timed run

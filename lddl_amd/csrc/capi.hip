@@ -64,7 +64,6 @@ struct lddl_ctx {
   uint32_t vt_mask = 0;
   uint32_t* d_vbloom = nullptr;  // its Bloom filter
   bool scan_ok = false;          // the ASCII page fits the split scan's per-byte class table
-  int tok5_cfg = 0;
   // per-kernel timing of the split tokenizer (lddl_set_timing)
   bool timing = false;
   SplitTiming* tm = nullptr;
@@ -408,8 +407,6 @@ extern "C" int lddl_create(const char* vocab_path, const char* table_path, int d
   const char* algo = getenv("LDDL_TOKENIZE_ALGO");
   c->tok_algo = (algo && algo[0] == '0') ? 0 : 5;
   if (c->tok_algo == 5 && (!c->scan_ok || c->vocab_size > (int)SPLIT_EDEF)) c->tok_algo = 0;
-  const char* cfg5 = getenv("LDDL_TOK5_CFG");  // split tokenizer variants (tokenize_split.hip)
-  c->tok5_cfg = cfg5 ? atoi(cfg5) : 0;
   const char* mcap = getenv("LDDL_MLM_CAP");  // initial masking arena (tests force the regrow path)
   c->mlm_cap = mcap ? (uint64_t)atoll(mcap) : 0;
   int per_cu = 0;
@@ -544,11 +541,11 @@ extern "C" int lddl_tokenize(lddl_ctx* c, const uint8_t* d_bytes, int64_t nbytes
   if (c->tok_algo == 0) {
     HIP_TRY(launch_tokenize_serial_dense(P, nbytes, tile_sent, S, c->n_cu, c->tok_grid, st));
   } else {
-    HIP_TRY(launch_tokenize_split(P, nbytes, tile_sent, S, c->n_cu, c->tok_grid, c->tok5_cfg, st,
+    HIP_TRY(launch_tokenize_split(P, nbytes, tile_sent, S, c->n_cu, c->tok_grid, st,
                                   c->timing ? c->tm : nullptr));
   }
   if (P.dbg) {
-    uint64_t h[18];
+    uint64_t h[20];
     HIP_TRY(hipMemcpyAsync(h, P.dbg, sizeof h, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     const char* nm[12] = {"loop", "setup", "classify", "except", "units", "urec", "prep", "probe", "records",
@@ -557,6 +554,7 @@ extern "C" int lddl_tokenize(lddl_ctx* c, const uint8_t* d_bytes, int64_t nbytes
     for (int k = 0; k < 12; ++k) fprintf(stderr, " %s=%llu", nm[k], (unsigned long long)h[k]);
     const char* wn[6] = {"wp_A", "wp_B", "wp_C", "wp_D", "wp_steps", "wp_lane_steps"};
     for (int k = 0; k < 6; ++k) fprintf(stderr, " %s=%llu", wn[k], (unsigned long long)h[12 + k]);
+    fprintf(stderr, " prep_decode=%llu prep_dirty=%llu", (unsigned long long)h[18], (unsigned long long)h[19]);
     fprintf(stderr, "\n");
   }
   return 0;
@@ -839,7 +837,6 @@ extern "C" int lddl_materialize(lddl_ctx* c, const uint16_t* d_ids, uint16_t* d_
   M.cls_id = c->special[2];
   M.sep_id = c->special[3];
   M.codebert = c->pack_codebert;
-  M.ablate = getenv("LDDL_MAT_ABLATE") ? atoi(getenv("LDDL_MAT_ABLATE")) : 0;
   M.out_tokens = d_out_tokens;
   M.out_tok_off = d_out_tok_off;
   M.out_len0 = d_out_len0;

@@ -113,7 +113,6 @@ struct MatParams {
   int32_t bin_size, nbins;
   uint32_t cls_id, sep_id;
   int32_t codebert;
-  int32_t ablate;               // LDDL_MAT_ABLATE=1 (diagnostics only): skip the edge-chunk drain
   // outputs, global final order (partition-major, bin-major, shuffled)
   uint16_t* out_tokens;         // [total tokens]  [CLS] A [SEP] B [SEP]
   int64_t* out_tok_off;         // [n_pairs + 1]

@@ -229,7 +229,7 @@ __device__ __forceinline__ void mat_drain(const MatWave& W, int ntok, bool liste
 // rows published in W (roff, row) for nr rows spanning [G0, G1) of out;
 // src readable for n_src entries
 __device__ __forceinline__ void mat_copy(MatWave& W, int64_t G0, int64_t G1, const uint16_t* src, int64_t n_src,
-                                         uint16_t* out, uint32_t cls, uint32_t sep, int lane, bool no_drain = false) {
+                                         uint16_t* out, uint32_t cls, uint32_t sep, int lane) {
   const int32_t G1r = (int32_t)(G1 - G0);
   if (G1 - G0 >= (1 << MAT_PBITS) - 16) {  // (rows beyond any real max_tok) token by token
     mat_drain(W, G1r, false, G0, G1r, src, out, cls, sep, lane);
@@ -293,11 +293,11 @@ __device__ __forceinline__ void mat_copy(MatWave& W, int64_t G0, int64_t G1, con
       ns += __popcll(m);
     }
     if (ns > MAT_SLOW - MAT_U * 64) {
-      if (!no_drain) mat_drain(W, ns * 8, true, G0, G1r, src, out, cls, sep, lane);
+      mat_drain(W, ns * 8, true, G0, G1r, src, out, cls, sep, lane);
       ns = 0;
     }
   }
-  if (ns > 0 && !no_drain) mat_drain(W, ns * 8, true, G0, G1r, src, out, cls, sep, lane);
+  if (ns > 0) mat_drain(W, ns * 8, true, G0, G1r, src, out, cls, sep, lane);
 }
 
 // workgroups are dealt round-robin to the 8 XCDs (one L2 each): block b runs
@@ -356,7 +356,7 @@ __global__ __launch_bounds__(256) void materialize2_kernel(MatParams M, int64_t 
   W.roff[lane] = lane < nr ? (int32_t)(off - G0) : 0x7FFFFFFF;
   W.row[lane] = x;
   mat_wsync();
-  mat_copy(W, G0, G1, M.dense, n_src, M.out_tokens, M.cls_id, M.sep_id, lane, M.ablate == 1);
+  mat_copy(W, G0, G1, M.dense, n_src, M.out_tokens, M.cls_id, M.sep_id, lane);
 }
 
 // ------------------------------------------------- token offset scans ----

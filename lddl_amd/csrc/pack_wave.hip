@@ -30,18 +30,8 @@ namespace lddl {
 // partition (PackParams cap_*); a partition that does not fit runs the same
 // code on global memory (wave-uniform branch).
 constexpr int PW_DOCS = 512;    // documents held in static LDS by the global-only variant
-#ifndef PACK_OCC
-#define PACK_OCC 8              // BERT packer held to 8 waves/SIMD (78 SGPRs; 7 at 106): pack 36.7 -> 35.6 ms
-#endif
-#ifndef PACK_CHOICE_JUMP
-#define PACK_CHOICE_JUMP 1      // mlm_choices: the picks of a window by pointer doubling, not a scalar walk
-#endif
-#ifndef PACK_TRACE_ONE
-#define PACK_TRACE_ONE 1        // pick trace: one pick per lane, passes of 64 (not two picks per lane)
-#endif
-#ifndef PACK_DRAW_ROUNDS
-#define PACK_DRAW_ROUNDS 3      // shuffle_draws: bound-propagation rounds before the ordered walk
-#endif
+constexpr int PACK_OCC = 8;          // BERT packer held to 8 waves/SIMD (78 SGPRs; 7 at 106): pack 36.7 -> 35.6 ms
+constexpr int PACK_DRAW_ROUNDS = 3;  // shuffle_draws: bound-propagation rounds before the ordered walk
 struct PackWaveLds {
   uint32_t mt[MT_N];            // MT19937 state; draws temper on the fly
   uint16_t dfirst[PW_DOCS];     // global-only variant: the partition's documents
@@ -309,7 +299,6 @@ struct WaveRng {
       uint64_t chosen = 0;
       int pos = 0;
       const int pk0 = pk;
-#if PACK_CHOICE_JUMP
       // the walk 0 -> nx[0] -> ... over resolved words (nx = l + len; it
       // stops at an unresolved word), found by pointer doubling: round i
       // marks the 2^i-step successors J of the chain words found so far
@@ -339,13 +328,6 @@ struct WaveRng {
         pos = __builtin_amdgcn_readlane(nx, last);
         pk += __popcll(chosen);
       }
-#else
-      while (pk < nm && pos < lim && (resm >> pos & 1ull)) {
-        chosen |= 1ull << pos;
-        ++pk;
-        pos += __builtin_amdgcn_readlane(len, pos);
-      }
-#endif
       if (chosen >> lane & 1ull) mid[pk0 + __popcll(chosen & ((1ull << lane) - 1ull))] = (uint16_t)nid;
       if (pos == 0) {  // the pick does not fit before the state's end: sequential
         uint32_t v;
@@ -453,18 +435,20 @@ __device__ __forceinline__ int range_sum(const GET& len_at, int k0, int k1, int 
   return wsum(s);
 }
 
-// find_fill / range_sum over a document of <= 64 sentences whose lengths are
-// held one per lane in dl (lane k = sentence k, 0 beyond): no memory access
-__device__ __forceinline__ int find_fill_reg(int dl, int k0, int n, int target, int lane, int* sum_out) {
+// find_fill / range_sum over a document of <= 64 sentences whose lengths'
+// inclusive prefix sums are held one per lane in dps (lane k = sentence k,
+// flat beyond; one wave scan per document visit): a chunk is a ballot and two
+// lane reads, no scan per chunk
+__device__ __forceinline__ int find_fill_reg(int dps, int k0, int n, int target, int lane, int* sum_out) {
+  const int base = k0 > 0 ? __builtin_amdgcn_readlane(dps, k0 - 1) : 0;
   const bool in = lane >= k0 && lane < n;
-  const int ps = wscan_incl(in ? dl : 0, lane);
-  const uint64_t m = __ballot(in && (lane == n - 1 || ps >= target));  // lane n-1 always qualifies
+  const uint64_t m = __ballot(in && (lane == n - 1 || dps - base >= target));  // lane n-1 always qualifies
   const int j = __ffsll((unsigned long long)m) - 1;
-  *sum_out = lane_get(ps, j);
+  *sum_out = __builtin_amdgcn_readlane(dps, j) - base;
   return j;
 }
-__device__ __forceinline__ int range_sum_reg(int dl, int k0, int k1, int lane) {
-  return wsum(lane >= k0 && lane < k1 ? dl : 0);
+__device__ __forceinline__ int range_sum_reg(int dps, int k0, int k1) {
+  return __builtin_amdgcn_readlane(dps, k1 - 1) - (k0 > 0 ? __builtin_amdgcn_readlane(dps, k0 - 1) : 0);
 }
 
 // LDSOK = false: every LDS capacity is 0 (the default), the arrays are in
@@ -627,6 +611,7 @@ __global__ __launch_bounds__(64, PACK_OCC) void pack_bert_wave_kernel(PackParams
       const int first = doc_first(di), len = doc_n(di);
       const bool dreg = len <= 64;
       const int dl = dl_next;
+      const int dps = dreg ? wave_incl_add(dl) : 0;  // (dl is 0 past the document)
       if (di + 1 < nd) dl_next = doc_lens(di + 1);
       else if (dup + 1 < P.dup) dl_next = doc_lens(0);
       int target = max_num;
@@ -636,13 +621,13 @@ __global__ __launch_bounds__(64, PACK_OCC) void pack_bert_wave_kernel(PackParams
       while (i < len) {
         const int cs = i;
         int cur;
-        const int j = dreg ? find_fill_reg(dl, cs, len, target, lane, &cur)
+        const int j = dreg ? find_fill_reg(dps, cs, len, target, lane, &cur)
                            : find_fill([&](int k) { return len_at(first + k); }, cs, len, target, lane, &cur);
         const int nchunk = j - cs + 1;
         int a_end = 1;
         if (nchunk >= 2) a_end = (int)rng.randint(1, nchunk - 1);
         const int la = a_end == nchunk ? cur
-                       : dreg ? range_sum_reg(dl, cs, cs + a_end, lane)
+                       : dreg ? range_sum_reg(dps, cs, cs + a_end)
                               : range_sum([&](int k) { return len_at(first + k); }, cs, cs + a_end, lane);
         PW_GSTAMP(7)
         PairRec r;
@@ -797,7 +782,6 @@ __global__ __launch_bounds__(64, PACK_OCC) void pack_bert_wave_kernel(PackParams
             wsync();
             const uint4* jb4 = reinterpret_cast<const uint4*>(ML.jb);
             auto elem = [&](int q) { return split ? (int)ML.jb[nm8 + q] : q; };
-#if PACK_TRACE_ONE
             // one pick per lane, 64 picks per pass: swaps below a pass's first
             // pick leave its picks in place, so pass k traces [64k, tr8)
             for (int pb0 = 0; pb0 < nm; pb0 += 64) {
@@ -816,39 +800,6 @@ __global__ __launch_bounds__(64, PACK_OCC) void pack_bert_wave_kernel(PackParams
               wsync();  // (mpos overlaps F: every lane has read its chains)
               if (pk < nm) ML.mpos[pk] = pick_pos(ea);
             }
-#else
-            for (int pb0 = 0; pb0 < nm; pb0 += 128) {
-              const int pk = pb0 + lane, pk2 = pk + 64;
-              int qa = pk, qb = pk2;
-              // swaps q < pb0 leave picks >= pb0 in place (j_q <= q)
-              if (nm - pb0 <= 64) {  // one pick per lane (seq 128: always)
-                for (int c = pb0; c < tr8; c += 8) {
-                  const uint4 w = jb4[c >> 3];
-                  const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-                  for (int t = 0; t < 8; ++t) {
-                    const int i2 = c + t, j = (int)((ww[t >> 1] >> (16 * (t & 1))) & 0xFFFFu);
-                    qa = qa == i2 ? j : (qa == j ? i2 : qa);
-                  }
-                }
-              } else {
-                for (int c = pb0; c < tr8; c += 8) {
-                  const uint4 w = jb4[c >> 3];
-                  const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-                  for (int t = 0; t < 8; ++t) {
-                    const int i2 = c + t, j = (int)((ww[t >> 1] >> (16 * (t & 1))) & 0xFFFFu);
-                    qa = qa == i2 ? j : (qa == j ? i2 : qa);
-                    qb = qb == i2 ? j : (qb == j ? i2 : qb);
-                  }
-                }
-              }
-              const int ea = pk < nm ? elem(qa) : 0, eb = pk2 < nm ? elem(qb) : 0;
-              wsync();  // (mpos overlaps F: every lane has read its chains)
-              if (pk < nm) ML.mpos[pk] = pick_pos(ea);
-              if (pk2 < nm) ML.mpos[pk2] = pick_pos(eb);
-            }
-#endif
           }
           // 80% [MASK], 10% keep, 10% random word, in pick order
           PW_STAMP(8)

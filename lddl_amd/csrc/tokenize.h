@@ -105,7 +105,7 @@ struct SplitTiming {
   int n[3];
 };
 hipError_t launch_tokenize_split(const TokParams& P, int64_t nbytes, int64_t* tile_sent, SplitParams S, int n_cu,
-                                 int fb_grid, int cfg, hipStream_t s, SplitTiming* tm = nullptr);
+                                 int fb_grid, hipStream_t s, SplitTiming* tm = nullptr);
 // every tile through the exact serial path, same dense output (tables the
 // split tokenizer does not model, LDDL_TOKENIZE_ALGO=0)
 hipError_t launch_tokenize_serial_dense(const TokParams& P, int64_t nbytes, int64_t* tile_sent, SplitParams S,

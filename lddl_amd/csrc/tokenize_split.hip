@@ -38,11 +38,16 @@
 #include "tokenize_serial.h"
 #include "pack.h"
 
+
 namespace lddl {
 namespace tok5 {
 
+// (a 1.5 KiB window for 6 waves/SIMD measured slower: 0.2 % of the tiles fall
+// back to the serial path, finish 0.97 -> 3.2 ms per GiB, and the 80-VGPR
+// scan spills: 3.80 vs 3.49)
 constexpr int CAP = 2048;                // window bytes (32 per lane)
 constexpr int DCAP = 256;                // side buffer for dirty words
+constexpr int SCAN_OCC = 5;              // waves per SIMD the scan's LDS admits (4 measured 5 % slower)
 constexpr int NBUF = CAP + DCAP + 64;    // + over-read pad of the key loads
 constexpr int UCAP = 256;                // units per round
 constexpr int NSCAP = 64;                // sentences per tile
@@ -90,8 +95,8 @@ struct alignas(16) Lds {
   uint32_t sspec[2];           // sentences holding a [CLS] / [SEP] token (P.sent_spec)
 };
 
-// five 4-wave blocks per CU (+ the 256-B class table): 5 waves per SIMD
-static_assert(4 * sizeof(Lds) + 256 <= 160 * 1024 / 5, "scan LDS no longer admits 5 waves per SIMD");
+// SCAN_OCC 4-wave blocks per CU (+ the 256-B class table): SCAN_OCC waves per SIMD
+static_assert(4 * sizeof(Lds) + 256 <= 160 * 1024 / SCAN_OCC, "scan LDS no longer admits SCAN_OCC waves per SIMD");
 
 __device__ __forceinline__ void wsync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -133,6 +138,15 @@ __device__ __forceinline__ uint32_t class_plane16(uint32_t t0, uint32_t t1, uint
   return (m | (m >> 8)) & 0xFFFFu;
 }
 
+// the lane index, re-materialised where it is used: per-lane 64-bit address
+// offsets (lane * 8 ...) derived from it are otherwise hoisted out of the
+// tile loop and spilled, and a spill reload's vmcnt(0) then waits for the
+// next tile's prefetched bytes as well
+__device__ __forceinline__ int lane_here() {
+  int l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+}
 __device__ __forceinline__ int64_t uni64(int64_t x) {
   const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)(uint64_t)x);
   const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)x >> 32));
@@ -244,22 +258,24 @@ __device__ __forceinline__ Key6 load_key(const uint32_t* nb, int s, int len) {
   k.d5 = keep_bytes(__builtin_amdgcn_alignbyte(x6, x5, sh), lc - 20);
   return k;
 }
-// == vhash (common.h) of a loaded key; branch-free: the six mixes, then the
-// one of the key's length selected (a branch per dword diverges across lanes)
-__device__ __forceinline__ uint32_t key_hash(const Key6& k, int len, uint32_t cont) {
-  const int lc = min(len, 24);
-  const uint32_t h1 = vmix(VSEED, k.d0), h2 = vmix(h1, k.d1), h3 = vmix(h2, k.d2), h4 = vmix(h3, k.d3),
-                 h5 = vmix(h4, k.d4), h6 = vmix(h5, k.d5);
-  uint32_t h = lc > 20 ? h6 : lc > 16 ? h5 : lc > 12 ? h4 : lc > 8 ? h3 : lc > 4 ? h2 : h1;
-  if (lc <= 0) h = VSEED;
-  return vfinal(h, (uint32_t)len, cont);
-}
 // a value the optimiser cannot see through: keeps the xor / or reduction
 // below (v_xor + v_or3) from being rewritten into one compare per dword,
 // materialised bools and 16-bit shifts
 __device__ __forceinline__ uint32_t opq(uint32_t x) {
   asm("" : "+v"(x));
   return x;
+}
+// == vhash (common.h) of a loaded key; branch-free: the six mixes, then the
+// one of the key's length selected (a branch per dword diverges across lanes)
+__device__ __forceinline__ uint32_t key_hash(const Key6& k, int len, uint32_t cont) {
+  const int lc = min(len, 24);
+  // (opaque: LLVM otherwise sinks each mix into a branch on lc, divergent
+  // across the step's lanes: scan 3.49 -> 3.46 ms per GiB)
+  const uint32_t h1 = opq(vmix(VSEED, k.d0)), h2 = opq(vmix(h1, k.d1)), h3 = opq(vmix(h2, k.d2)),
+                 h4 = opq(vmix(h3, k.d3)), h5 = opq(vmix(h4, k.d4)), h6 = opq(vmix(h5, k.d5));
+  uint32_t h = lc > 20 ? h6 : lc > 16 ? h5 : lc > 12 ? h4 : lc > 8 ? h3 : lc > 4 ? h2 : h1;
+  if (lc <= 0) h = VSEED;
+  return vfinal(h, (uint32_t)len, cont);
 }
 // branch-free (an && chain lets the compiler sink the slot's other loads
 // behind the first compare: a second dependent round trip on every hit)
@@ -273,7 +289,7 @@ __device__ __forceinline__ bool slot_eq(const uint4& a, const uint4& b, const Ke
 // OCC: the waves per SIMD the register allocation is held to (LDS admits 5)
 template <int WAVES, bool DBG, int OCC>
 __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, SplitParams S) {
-  uint64_t acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t acc[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t tprev = 0;
 #define STAMP(k)                                                                   \
   if (DBG) {                                                                       \
@@ -356,16 +372,17 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
     if (n_sa >= n_sb) return;
     n_A = uni64(*reinterpret_cast<const int64_t*>(&L.pb[4]));
     n_B = uni64(*reinterpret_cast<const int64_t*>(&L.pb[6]));
-    if (lane < n_sb - n_sa) n_spos = P.sent_off[n_sa + lane];
+    const int ln = lane_here();
+    if (ln < n_sb - n_sa) n_spos = P.sent_off[n_sa + ln];
     const int aoff = (int)(reinterpret_cast<uintptr_t>(P.bytes + n_A) & 15u);
     const int64_t nb64 = (n_B - n_A) + aoff;
     if (nb64 > CAP || n_sb - n_sa > NSCAP) return;  // the tile falls back: no bytes needed
     dma_pending = true;
     // streamed once: non-temporal (aux bit 1), keep L2 for the vocab table
-    const uint8_t* g = P.bytes + (n_A - aoff) + 16 * lane;
-    if (16 * lane < nb64)
+    const uint8_t* g = P.bytes + (n_A - aoff) + 16 * ln;
+    if (16 * ln < nb64)
       __builtin_amdgcn_global_load_lds((const uint32_t*)g, (__attribute__((address_space(3))) uint32_t*)L.rp, 16, 0, 2);
-    if (1024 + 16 * lane < nb64)
+    if (1024 + 16 * ln < nb64)
       __builtin_amdgcn_global_load_lds((const uint32_t*)(g + 1024), (__attribute__((address_space(3))) uint32_t*)(L.rp + 256), 16, 0, 2);
   };
   if (DBG) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(tprev)::"memory");
@@ -391,7 +408,7 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
         S.fb_list[at] = (int32_t)t;
         atomicAdd(S.n_fallback, 1u);
       }
-      for (int j = lane; j < ns; j += 64) {
+      for (int j = lane_here(); j < ns; j += 64) {
         S.smeta[sa + j] = make_uint2(SPLIT_NENT_FB, 0xFFFFFFFFu);
       }
     };
@@ -424,8 +441,11 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
     {
       const int p0 = lane * 32;
       (void)wbase;  // the raw bytes came with the prefetch (stage3), bytes >= nb zero
-      uint4 v0 = *reinterpret_cast<const uint4*>(&L.rp[lane * 8]);
-      uint4 v1 = *reinterpret_cast<const uint4*>(&L.rp[lane * 8 + 4]);
+      uint4 v0 = make_uint4(0, 0, 0, 0), v1 = v0;
+      if (p0 < CAP) {
+        v0 = *reinterpret_cast<const uint4*>(&L.rp[lane * 8]);
+        v1 = *reinterpret_cast<const uint4*>(&L.rp[lane * 8 + 4]);
+      }
       if (p0 >= nb) v0 = make_uint4(0, 0, 0, 0);
       if (p0 + 16 >= nb) v1 = make_uint4(0, 0, 0, 0);
       const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
@@ -444,8 +464,10 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
       }
       // two 16-B stores per lane (8 dword stores at a 32-B lane stride hit
       // 1/8 of the banks)
-      *reinterpret_cast<uint4*>(&L.nb[lane * 8]) = make_uint4(nv[0], nv[1], nv[2], nv[3]);
-      *reinterpret_cast<uint4*>(&L.nb[lane * 8 + 4]) = make_uint4(nv[4], nv[5], nv[6], nv[7]);
+      if (p0 < CAP) {
+        *reinterpret_cast<uint4*>(&L.nb[lane * 8]) = make_uint4(nv[0], nv[1], nv[2], nv[3]);
+        *reinterpret_cast<uint4*>(&L.nb[lane * 8 + 4]) = make_uint4(nv[4], nv[5], nv[6], nv[7]);
+      }
       uint32_t t[8];
       byte_transpose4(c[0], c[1], c[2], c[3], t[0], t[1], t[2], t[3]);
       byte_transpose4(c[4], c[5], c[6], c[7], t[4], t[5], t[6], t[7]);
@@ -850,6 +872,7 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
             }
             sj = (uint32_t)lo;
           }
+          STAMP(12);
           int src = p, len = valid ? q - p : 0;
           bool lovf = false;  // the tile falls back: side buffer full, or a queued word too long for a record
           if (dirty) {
@@ -857,6 +880,7 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
             lovf = len < 0;
             len = max(len, 0);
           }
+          STAMP(13);
           Key6 key = {0, 0, 0, 0, 0, 0};
           if (len > 0 && len <= 24) key = load_key(L.nb, src, len);
           if (len > 0) {
@@ -984,7 +1008,7 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
       const uint32_t nsl = acc & 0xFFFFu;
       const uint32_t sq0 = wave_incl_add(nsl) - nsl;
       if (lane < ns) {
-        const int64_t s = sa + lane;
+        const int64_t s = sa + lane_here();
         const uint32_t ne = (uint32_t)L.ufirst[lane + 1] - (uint32_t)L.ufirst[lane];
         S.smeta[s] = make_uint2(ne | (sq0 << 16), tbase);
         S.snslot[s] = (uint16_t)nsl;
@@ -999,6 +1023,8 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
   }
   if (DBG && lane == 0)
     for (int k = 0; k < 12; ++k) atomicAdd((unsigned long long*)&P.dbg[k], (unsigned long long)acc[k]);
+  if (DBG && lane == 0)
+    for (int k = 12; k < 14; ++k) atomicAdd((unsigned long long*)&P.dbg[6 + k], (unsigned long long)acc[k]);
 #undef STAMP
   if (chunk >= 0 && lane == 0) S.chunk_fill[chunk] = cur - cbase;
 }
@@ -1398,52 +1424,76 @@ __global__ __launch_bounds__(256) void expand_kernel(TokParams P, SplitParams S)
       own_carry = lane_get(o, 63);
       return o;
     };
-    // step st's entry: sentence j, entry value v (loaded), head (first entry of j)
-    uint32_t j = 0, v = 0;
-    bool in = false, head = false;
-    auto load_step = [&](uint32_t st) {
-      const uint32_t g = st + (uint32_t)lane;
-      j = owner(st);
-      in = g < T;
-      const ExpSent sj = E.sn[j];
-      head = in && g == sj.e0;
-      v = in ? S.ent[sj.eb + g] : 0u;
-    };
-    if (T > 0) load_step(0);
+    // EXP_K steps at a time, in three phases: the entry loads of all of them,
+    // then their record loads, then their tokens -- every load of a phase in
+    // flight together (the compiler drains the vector memory counter before
+    // the first use of a load whenever stores are pending, so a pipeline
+    // across loop iterations would wait at every step; here it waits twice
+    // per EXP_K steps)
+    constexpr int EXP_K = 4;  // 46 VGPRs, 8 waves per SIMD (8 steps: 86 VGPRs, 5 waves, slower)
     uint32_t carry = 0;
-    for (uint32_t st = 0; st < T; st += 64) {
-      const uint32_t cj = j, cv = v;
-      const bool cin = in, chead = head;
-      const bool rec = cin && cv >= SPLIT_EDEF && cv != SPLIT_EHOLE;
-      const ExpSent sj = E.sn[cj];
-      const size_t ri = (size_t)(sj.qb + (cv & 0xFFFu)) * 4;
-      u32x3 rq = u32x3{cin && cv != SPLIT_EHOLE ? 1u : 0u, 0u, 0u};  // (a hole: an empty unit, no token)
-      if (rec) rq = *reinterpret_cast<const u32x3*>(reinterpret_cast<const uint32_t*>(pcs + ri) + 1);
-      if (st + 64 < T) load_step(st + 64);  // (the next step's entries fly with these record loads)
-      const uint32_t cnt = rq.x;
-      uint32_t hv = chead ? 1u : 0u, sv = cnt;
-      wave_seg_incl_add(hv, sv);
-      uint32_t ex = wave_shr1(sv);
-      if (!wave_shr1(hv)) ex += carry;
-      const uint32_t p = chead ? 0u : ex;  // tokens of the sentence before this entry
-      if (cin) {
-        uint16_t* o = P.out_ids + sj.dst;
-        const uint32_t lm = sj.lim;
-        // (the first token of a direct id and of a record in one store)
-        if (cnt && p < lm) o[p] = (uint16_t)(cv < SPLIT_EDEF ? cv : rq.y & 0xFFFFu);
-        if (rec) {
-          if (cnt > 1 && p + 1 < lm) o[p + 1] = (uint16_t)(rq.y >> 16);
-          if (cnt > 2 && p + 2 < lm) o[p + 2] = (uint16_t)(rq.z & 0xFFFFu);
-          if (cnt > 3 && p + 3 < lm) o[p + 3] = (uint16_t)(rq.z >> 16);
-          if (cnt > 4) {
-            const uint16_t* pc = reinterpret_cast<const uint16_t*>(pcs + ri);
-            for (uint32_t q = 4; q < cnt && p + q < lm; ++q) o[p + q] = pc[piece_at((int)q)];
-          }
+    for (uint32_t st0 = 0; st0 < T; st0 += 64 * EXP_K) {
+      uint32_t xj[EXP_K], xv[EXP_K];
+      bool xin[EXP_K], xhead[EXP_K];
+#pragma unroll
+      for (int k = 0; k < EXP_K; ++k) {
+        const uint32_t st = st0 + 64 * k;
+        xj[k] = 0;
+        xv[k] = 0;
+        xin[k] = xhead[k] = false;
+        if (st < T) {
+          const uint32_t g = st + (uint32_t)lane;
+          xj[k] = owner(st);
+          xin[k] = g < T;
+          const ExpSent sj = E.sn[xj[k]];
+          xhead[k] = xin[k] && g == sj.e0;
+          xv[k] = S.ent[xin[k] ? sj.eb + g : 0];  // (every lane loads: no branch around the load)
         }
       }
-      // running total of the step's last entry (its sentence may continue)
-      const uint32_t ll = min(T, st + 64) - 1 - st;
-      carry = lane_get(p + cnt, (int)ll);
+      u32x3 xr[EXP_K];
+#pragma unroll
+      for (int k = 0; k < EXP_K; ++k) {
+        const bool r = xin[k] && xv[k] >= SPLIT_EDEF && xv[k] != SPLIT_EHOLE;
+        xr[k] = u32x3{0u, 0u, 0u};
+        if (st0 + 64 * k < T)
+          xr[k] = *reinterpret_cast<const u32x3*>(reinterpret_cast<const uint32_t*>(
+                                                     pcs + (r ? (size_t)(E.sn[xj[k]].qb + (xv[k] & 0xFFFu)) * 4 : 0)) + 1);
+      }
+#pragma unroll
+      for (int k = 0; k < EXP_K; ++k) {
+        const uint32_t st = st0 + 64 * k;
+        if (st >= T) break;
+        const uint32_t cj = xj[k], cv = xin[k] ? xv[k] : 0u;
+        const bool cin = xin[k], chead = xhead[k], rec = cin && cv >= SPLIT_EDEF && cv != SPLIT_EHOLE;
+        // (a hole: an empty unit, no token; a direct id: one)
+        const u32x3 rq = rec ? xr[k] : u32x3{cin && cv != SPLIT_EHOLE ? 1u : 0u, 0u, 0u};
+        const ExpSent sj = E.sn[cj];
+        const size_t ri = (size_t)(sj.qb + (cv & 0xFFFu)) * 4;
+        const uint32_t cnt = rq.x;
+        uint32_t hv = chead ? 1u : 0u, sv = cnt;
+        wave_seg_incl_add(hv, sv);
+        uint32_t ex = wave_shr1(sv);
+        if (!wave_shr1(hv)) ex += carry;
+        const uint32_t p = chead ? 0u : ex;  // tokens of the sentence before this entry
+        if (cin) {
+          uint16_t* o = P.out_ids + sj.dst;
+          const uint32_t lm = sj.lim;
+          // (the first token of a direct id and of a record in one store)
+          if (cnt && p < lm) o[p] = (uint16_t)(cv < SPLIT_EDEF ? cv : rq.y & 0xFFFFu);
+          if (rec) {
+            if (cnt > 1 && p + 1 < lm) o[p + 1] = (uint16_t)(rq.y >> 16);
+            if (cnt > 2 && p + 2 < lm) o[p + 2] = (uint16_t)(rq.z & 0xFFFFu);
+            if (cnt > 3 && p + 3 < lm) o[p + 3] = (uint16_t)(rq.z >> 16);
+            if (cnt > 4) {
+              const uint16_t* pc = reinterpret_cast<const uint16_t*>(pcs + ri);
+              for (uint32_t q = 4; q < cnt && p + q < lm; ++q) o[p + q] = pc[piece_at((int)q)];
+            }
+          }
+        }
+        // running total of the step's last entry (its sentence may continue)
+        const uint32_t ll = min(T, st + 64) - 1 - st;
+        carry = lane_get(p + cnt, (int)ll);
+      }
     }
     wsync();
   }
@@ -1488,7 +1538,7 @@ int64_t split_seg_slots(int64_t seg_tiles, int n_cu) {
   // used chunk per scanning wave of the real grid; past it tiles fall back to
   // the serial path (counted: lddl_tokenize_stats)
   int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, tok5::scan_kernel<SCAN_WAVES, false, 5>, 64 * SCAN_WAVES,
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, tok5::scan_kernel<SCAN_WAVES, false, tok5::SCAN_OCC>, 64 * SCAN_WAVES,
                                                    0) != hipSuccess || per_cu < 1)
     per_cu = 8;
   const int64_t waves = (int64_t)n_cu * per_cu * SCAN_WAVES;
@@ -1516,7 +1566,7 @@ hipError_t launch_tokenize_serial_dense(const TokParams& P, int64_t nbytes, int6
 }
 
 hipError_t launch_tokenize_split(const TokParams& P, int64_t nbytes, int64_t* tile_sent, SplitParams S, int n_cu,
-                                 int fb_grid, int cfg, hipStream_t s, SplitTiming* tm) {
+                                 int fb_grid, hipStream_t s, SplitTiming* tm) {
   if (tm) tm->n[0] = tm->n[1] = tm->n[2] = 0;
   auto mark = [&](int k, int side) -> hipError_t {  // (at most 64 segments timed per kernel)
     if (!tm || tm->n[k] >= 64) return hipSuccess;
@@ -1535,12 +1585,9 @@ hipError_t launch_tokenize_split(const TokParams& P, int64_t nbytes, int64_t* ti
     S.t1 = std::min(n_tiles, t0 + seg);
     if ((e = hipMemsetAsync(S.chunk_ctr, 0, 4, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(S.fb_count, 0, 4, s)) != hipSuccess) return e;
-    // cfg (LDDL_TOK5_CFG, tuning): 1 = registers unconstrained (4 waves/SIMD)
     if ((e = mark(0, 0)) != hipSuccess) return e;
-    if (P.dbg) e = tok5::launch_scan<SCAN_WAVES, true, 5>(P, S, n_cu, s);
-    else if (cfg == 1) e = tok5::launch_scan<SCAN_WAVES, false, 1>(P, S, n_cu, s);
-    else if (cfg == 6) e = tok5::launch_scan<SCAN_WAVES, false, 6>(P, S, n_cu, s);
-    else e = tok5::launch_scan<SCAN_WAVES, false, 5>(P, S, n_cu, s);
+    if (P.dbg) e = tok5::launch_scan<SCAN_WAVES, true, tok5::SCAN_OCC>(P, S, n_cu, s);
+    else e = tok5::launch_scan<SCAN_WAVES, false, tok5::SCAN_OCC>(P, S, n_cu, s);
     if (e != hipSuccess || (e = mark(0, 1)) != hipSuccess || (e = mark(1, 0)) != hipSuccess) return e;
     if ((e = tok5::launch_wp<WP_WAVES>(P, S, n_cu, s)) != hipSuccess) return e;
     if ((e = mark(1, 1)) != hipSuccess || (e = mark(2, 0)) != hipSuccess) return e;

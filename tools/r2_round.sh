@@ -19,7 +19,7 @@ if [ -z "$SKIP_BENCH" ]; then
   tail -1 $OUT/bench.log > $OUT/bench.json
   cat $OUT/bench.json
 fi
-B="bench.py --no-cpu-baseline --parquet-parts 0 ${BENCH_ARGS}"
+B="bench.py --no-cpu-baseline --parquet-parts 0 --frontend-mb 0 ${BENCH_ARGS}"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/kt -o kt --output-format csv -- python -u $B --steps 2 --warmup 1 > $OUT/kt.log 2>&1 || { echo "kernel trace failed"; tail -20 $OUT/kt.log; exit 1; }
 f=$(find $OUT/kt -name '*kernel_stats.csv' | head -1); cp $f $OUT/kernel_stats.csv; cut -d, -f1-4 $f | head -16
 [ -n "$SKIP_PMC" ] && exit 0

@@ -1,6 +1,6 @@
 """GPU tokenizer check + timing for the kernel variants (GPU box tool).
 
-    python tools/tok_check.py [MB] [algo[:cfg] ...]   (algo 5: split tokenizer, 0: serial path)
+    python tools/tok_check.py [MB] [algo ...]   (algo 5: split tokenizer, 0: serial path)
 
 Tokenizes a synthetic Wikipedia-style corpus of MB megabytes with each
 variant, compares ids / counts with the oracle (first MB only, for speed)
@@ -35,9 +35,8 @@ def main():
   oids, ontok = OracleTokenizer(VOCAB_BERT).run(
       c.data, c.sent_off[:ns_chk + 1], 512, nthreads=8)
   for v in variants:
-    algo, _, cfg = v.partition(':')
+    algo = v
     os.environ['LDDL_TOKENIZE_ALGO'] = algo
-    os.environ['LDDL_TOK5_CFG'] = cfg or '0'
     tok = Tokenizer()
     ids, ntok, toff = tok.tokenize_device(d, o)
     torch.cuda.synchronize()
