@@ -89,8 +89,8 @@ struct alignas(16) Lds {
   uint16_t sst[NSCAP + 2];     // sentence starts (window coordinates)
   uint16_t ufirst[NSCAP + 2];  // index of the sentence's first unit in the tile ([ns] = #units)
   uint16_t ebs[NSCAP];         // entry index base: unit u of sentence j has entry sst[j] + u - ufirst[j]
-  uint32_t xent[XCAP];         // table entry of each expansion marker
-  uint8_t xlen[XCAP];          // its normalised byte length
+  uint32_t xrep[XCAP * 3];     // each expansion marker's normalised bytes (<= 12: up to three chars)
+  uint8_t xlen[XCAP];          // their number
   int32_t misc[4];             // 0 side-buffer cursor, 1 #markers
   uint32_t sspec[2];           // sentences holding a [CLS] / [SEP] token (P.sent_spec)
 };
@@ -212,15 +212,10 @@ __device__ int dirty_normalize(Lds& L, const TokParams& P, int p, int q, int* sr
     if (b == BF) {
       ++i;
     } else if (b == BX) {
-      const uint32_t e = L.xent[nbyte(L.nb, i + 1)];
-      if (ent_kind(e) == KIND_MULTI) {
-        const uint4 m = P.multi[ent_payload(e)];
-        o += utf8_put(L.nb, o, ent_payload(m.y));
-        o += utf8_put(L.nb, o, ent_payload(m.z));
-        if (m.x > 2) o += utf8_put(L.nb, o, ent_payload(m.w));
-      } else {
-        o += utf8_put(L.nb, o, ent_payload(e));
-      }
+      // (the marker's bytes, encoded when the exception pass placed it: no
+      // table load here)
+      const int x = (int)nbyte(L.nb, i + 1), nx = L.xlen[x];
+      for (int t = 0; t < nx; ++t) nput(L.nb, o++, nbyte(L.xrep, 12 * x + t));
       i += 2;
     } else {
       nput(L.nb, o++, b);
@@ -715,7 +710,10 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
                 if (xi >= XCAP) {
                   bad = true;
                 } else {
-                  L.xent[xi] = e;
+                  int ox = 12 * xi;
+                  ox += utf8_put(L.xrep, ox, c0);
+                  if (nc > 1) ox += utf8_put(L.xrep, ox, c1);
+                  if (nc > 2) ox += utf8_put(L.xrep, ox, c2);
                   L.xlen[xi] = (uint8_t)T;
                   nput(L.nb, p, BX);
                   nput(L.nb, p + 1, (uint32_t)xi);
