@@ -323,6 +323,10 @@ def parquet_sample(args, pk, res, sh):
     nd = int(sh.part_doc_off[min(args.parquet_parts, sh.n_part)].item())
     doc_ids = ['python_%d' % i for i in range(nd)]
   try:
+    # one untimed partition first: pyarrow's lazily imported modules (compute,
+    # pandas compat: ~0.55 s once per process) stay out of the rate
+    writer.write_shards(pk, res, os.path.join(d, 'warm'), bin_size=args.bin_size, masking=args.masking,
+                        codebert=args.corpus == 'code', doc_ids=doc_ids, max_parts=1)
     torch.cuda.synchronize()
     t = time.perf_counter()
     files = writer.write_shards(pk, res, d, bin_size=args.bin_size, masking=args.masking,

@@ -53,8 +53,18 @@ create_pairs_from_document would draw them after that seed.
 Multi-GPU: launch under torch.distributed.run; rank r preprocesses the
 contiguous partition range r of world (LPT would also do: partitions are
 independent, pretrain.py:304,387) with no data-path collective.
+
+Restart (``--resume``; the reference has none): after a chunk's
+files are written, a marker ``<sink>/.lddl_done/chunk_<a>_<b>.json`` records
+its files, per-(partition, bin) row counts and a key of every flag and input
+file (name, size, mtime) the chunk's output depends on.  A rerun skips each
+chunk whose marker carries the same key and whose files all exist; chunk
+(a, b)'s output does not depend on the world size (partition p draws from
+seed + p), so a restart may use another rank count.
 """
 import argparse
+import hashlib
+import json
 import os
 import re
 import sys
@@ -263,7 +273,54 @@ def attach_args(parser=None, codebert=False):
                  help='balance the output into this many shard-{k}.parquet[_b] files (balance_dask_output, '
                       'load_balance.py) with counts all-gathered from the packer')
   p.add_argument('--keep-orig', action='store_true', help='with --num-shards: keep the part files')
+  p.add_argument('--resume', action='store_true',
+                 help='write a completion marker per chunk and skip chunks an earlier run with the same flags '
+                      'and inputs completed')
   return p
+
+
+DONE_DIR = '.lddl_done'
+
+
+def run_key(args, codebert, files, vocab, how, n_part):
+  """Digest of everything a chunk's output depends on: the flags that reach
+  the pipeline, the vocab and the input files (path, size, mtime)."""
+  keys = ['target_seq_length', 'short_seq_prob', 'block_size', 'num_blocks', 'bin_size', 'sample_ratio', 'seed',
+          'duplicate_factor', 'masking', 'masked_lm_ratio', 'output_format', 'wikipedia_lang']
+  d = {k: getattr(args, k, None) for k in keys}
+  d.update(codebert=codebert, splitter=how, n_part=n_part, vocab=os.path.abspath(vocab),
+           vocab_size=os.path.getsize(vocab),
+           files=[(os.path.abspath(f), os.path.getsize(f), os.stat(f).st_mtime_ns) for f in files])
+  return hashlib.sha256(json.dumps(d, sort_keys=True).encode()).hexdigest()
+
+
+def _marker(sink, a, b):
+  return os.path.join(sink, DONE_DIR, 'chunk_%d_%d.json' % (a, b))
+
+
+def load_marker(sink, a, b, key):
+  """The marker of chunk [a, b) if it belongs to this run key and its files
+  are all present, else None."""
+  try:
+    with open(_marker(sink, a, b)) as f:
+      m = json.load(f)
+  except (OSError, ValueError):
+    return None
+  if m.get('key') != key or not all(os.path.isfile(os.path.join(sink, f)) for f in m.get('files', [])):
+    return None
+  return m
+
+
+def save_marker(sink, a, b, key, files, counts, n_pairs):
+  """Written after the chunk's files (tmp + rename, so a crash leaves either
+  no marker or a whole one)."""
+  p = _marker(sink, a, b)
+  os.makedirs(os.path.dirname(p), exist_ok=True)
+  tmp = p + '.tmp%d' % os.getpid()
+  with open(tmp, 'w') as f:
+    json.dump({'key': key, 'files': sorted(os.path.relpath(x, sink) for x in files), 'counts': counts,
+               'n_pairs': int(n_pairs)}, f)
+  os.replace(tmp, p)
 
 
 def _check(args):
@@ -373,10 +430,20 @@ def main(args, codebert=False):
       acc0 = part_end[p - lo]
   bounds.append(hi)
   chunks = [(a, b) for a, b in zip(bounds[:-1], bounds[1:]) if b > a]
+  sink = os.path.abspath(os.path.expanduser(args.sink))
+  nbins = args.target_seq_length // args.bin_size if args.bin_size else 1
+  done, key = {}, None
+  if args.resume:
+    key = run_key(args, codebert, input_files(args, codebert)[0], vocab, how, n_part)
+    for c, (a, b) in enumerate(chunks):
+      m = load_marker(sink, a, b, key)
+      if m is not None and np.asarray(m['counts']).shape == (b - a, nbins):
+        done[c] = m
+  todo = [c for c in range(len(chunks)) if c not in done]
 
   # split workers: forked here, before anything touches the GPU; they read
   # their records from the index (integers only are inherited)
-  nw = min(max(0, args.split_workers), len(chunks)) if len(chunks) > 1 else 0
+  nw = min(max(0, args.split_workers), len(todo)) if len(todo) > 1 else 0
   pool = None
   if nw > 0:
     import multiprocessing
@@ -399,21 +466,26 @@ def main(args, codebert=False):
   device = torch.device('cuda', local)
   torch.cuda.set_device(device)
   pk = pipeline.Packer(vocab, local, masking=args.masking and not codebert)
-  sink = os.path.abspath(os.path.expanduser(args.sink))
   out = []
-  nbins = args.target_seq_length // args.bin_size if args.bin_size else 1
   counts = torch.zeros(hi - lo, nbins, dtype=torch.int64, device=device)  # rows per (partition, bin)
-  t.update(host_split_s=0.0, split_wait_s=0.0, gpu_s=0.0, write_s=0.0, pairs=0, split_workers=nw)
+  t.update(host_split_s=0.0, split_wait_s=0.0, gpu_s=0.0, write_s=0.0, pairs=0, split_workers=nw,
+           chunks_skipped=len(done))
+  for c, m in done.items():
+    a, b = chunks[c]
+    counts[a - lo:b - lo] = torch.tensor(m['counts'], dtype=torch.int64)
+    out += [os.path.join(sink, f) for f in m['files']]
+    t['pairs'] += m['n_pairs']
   try:
     ahead = max(1, nw)
-    futs = {c: submit(c) for c in range(min(ahead, len(chunks)))} if pool is not None else {}
-    for c, (a, b) in enumerate(chunks):
+    futs = {c: submit(c) for c in todo[:ahead]} if pool is not None else {}
+    for i, c in enumerate(todo):
+      a, b = chunks[c]
       tw = time.perf_counter()
       corpus, ids, ts = (futs.pop(c) if c in futs else submit(c)).get()
       t['split_wait_s'] += time.perf_counter() - tw
       t['host_split_s'] += ts
-      if pool is not None and c + ahead < len(chunks):
-        futs[c + ahead] = submit(c + ahead)  # overlaps this chunk's GPU work and parquet writes
+      if pool is not None and i + ahead < len(todo):
+        futs[todo[i + ahead]] = submit(todo[i + ahead])  # overlaps this chunk's GPU work and parquet writes
       t0 = time.perf_counter()
       sh = pipeline.upload(corpus, pro[a:b + 1] - pro[a], device)
       ids_d, ntok, toff = pk.tokenize(sh)
@@ -426,8 +498,11 @@ def main(args, codebert=False):
       t['gpu_s'] += time.perf_counter() - t0
       t0 = time.perf_counter()
       wr = writer.write_txt if args.output_format == 'txt' else writer.write_shards
-      out += wr(pk, res, sink, bin_size=args.bin_size, codebert=codebert, masking=args.masking and not codebert,
-                doc_ids=ids, part_base=a)
+      wrote = wr(pk, res, sink, bin_size=args.bin_size, codebert=codebert, masking=args.masking and not codebert,
+                 doc_ids=ids, part_base=a)
+      out += wrote
+      if args.resume:
+        save_marker(sink, a, b, key, wrote, counts[a - lo:b - lo].tolist(), res.n_pairs)
       t['write_s'] += time.perf_counter() - t0
       t['pairs'] += res.n_pairs
   finally:
@@ -457,6 +532,9 @@ def main(args, codebert=False):
         for p in out_all_parts(sink, allc.shape[0], nbins, args.bin_size is not None):
           if os.path.exists(p):
             os.remove(p)
+        if args.resume:  # the markers name the part files just removed
+          import shutil
+          shutil.rmtree(os.path.join(sink, DONE_DIR), ignore_errors=True)
     t['balance_s'] = time.perf_counter() - t0
     t['shards'] = len(written)
     out = written

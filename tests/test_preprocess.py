@@ -243,3 +243,37 @@ def test_plan_input_sharded_over_ranks_matches_one_rank(tmp_path):
   for _, fid, off, ln, od, pr in got:
     assert fid == idx.fid.tolist() and off == idx.off.tolist() and ln == idx.len.tolist()
     assert od == order.tolist() and pr == pro.tolist()
+
+
+def test_resume_markers(tmp_path):
+  """--resume: a chunk's marker is trusted only with the same run key and
+  with all its files present; the key follows flags and input files"""
+  src = tmp_path / 'wiki' / 'en'
+  src.mkdir(parents=True)
+  (src / 'a.txt').write_text('wiki-1 Hello there.\n')
+  vocab = tmp_path / 'vocab.txt'
+  vocab.write_text('[PAD]\n')
+  sink = tmp_path / 'out'
+  sink.mkdir()
+  args = preprocess.attach_args().parse_args(['--wikipedia', str(tmp_path / 'wiki'), '--sink', str(sink), '--resume'])
+  assert args.resume
+  files = preprocess.input_files(args)[0]
+  key = preprocess.run_key(args, False, files, str(vocab), 'rules', 1)
+  assert key == preprocess.run_key(args, False, files, str(vocab), 'rules', 1)
+  args2 = preprocess.attach_args().parse_args(['--wikipedia', str(tmp_path / 'wiki'), '--sink', str(sink),
+                                               '--seed', '7'])
+  assert preprocess.run_key(args2, False, files, str(vocab), 'rules', 1) != key
+  assert preprocess.run_key(args, True, files, str(vocab), 'rules', 1) != key
+  part = sink / 'part.0.parquet'
+  part.write_bytes(b'x')
+  assert preprocess.load_marker(str(sink), 0, 1, key) is None
+  preprocess.save_marker(str(sink), 0, 1, key, [str(part)], [[3]], 3)
+  m = preprocess.load_marker(str(sink), 0, 1, key)
+  assert m == {'key': key, 'files': ['part.0.parquet'], 'counts': [[3]], 'n_pairs': 3}
+  assert preprocess.load_marker(str(sink), 0, 1, 'other') is None
+  assert preprocess.load_marker(str(sink), 0, 2, key) is None
+  part.unlink()
+  assert preprocess.load_marker(str(sink), 0, 1, key) is None
+  # an input file that changed changes the key
+  (src / 'a.txt').write_text('wiki-1 Hello there, again.\n')
+  assert preprocess.run_key(args, False, files, str(vocab), 'rules', 1) != key

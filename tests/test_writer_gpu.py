@@ -375,3 +375,34 @@ def test_cli_codebert_txt(gpu, tmp_path):
   want = ['{} [CLS] {} [SEP] {} [SEP] - {}'.format(i, d, c, n) for i, d, c, n in
           zip(rows['id'], rows['doc'], rows['code'], rows['num_tokens'])]
   assert want and _txt_lines(files[0]) == want
+
+
+def test_cli_resume_skips_completed_chunks(gpu, tmp_path):
+  """--resume: a rerun skips every chunk with a marker of the same run and
+  redoes a chunk whose file went missing, with the same bytes; a rerun with
+  other flags trusts no marker"""
+  from lddl_amd import synth, preprocess
+  c = synth.make_wiki(200_000, seed=9)
+  docs = c.documents()
+  src = tmp_path / 'wiki' / 'en'
+  src.mkdir(parents=True)
+  for k in range(3):
+    with open(str(src / ('wiki_%d.txt' % k)), 'w', encoding='utf-8') as f:
+      for d in range(k, len(docs), 3):
+        f.write('wiki-%d %s\n' % (d, ' '.join(docs[d])))
+  sink = tmp_path / 'out'
+  common = ['--wikipedia', str(tmp_path / 'wiki'), '--sink', str(sink), '--target-seq-length', '128',
+            '--bin-size', '64', '--sentence-splitter', 'rules', '--seed', '3', '--chunk-mb', '0.02',
+            '--split-workers', '0', '--resume']
+  files, t = preprocess.main(preprocess.attach_args().parse_args(common))
+  assert t['chunks'] == 3 and t['chunks_skipped'] == 0
+  blobs = {f: open(f, 'rb').read() for f in files}
+  files2, t2 = preprocess.main(preprocess.attach_args().parse_args(common))
+  assert t2['chunks_skipped'] == 3 and t2['pairs'] == t['pairs'] and sorted(files2) == sorted(files)
+  gone = sorted(files)[0]
+  os.remove(gone)
+  files3, t3 = preprocess.main(preprocess.attach_args().parse_args(common))
+  assert t3['chunks_skipped'] == 2 and sorted(files3) == sorted(files)
+  assert all(open(f, 'rb').read() == blobs[f] for f in files)
+  _, t4 = preprocess.main(preprocess.attach_args().parse_args(common + ['--duplicate-factor', '2']))
+  assert t4['chunks_skipped'] == 0
