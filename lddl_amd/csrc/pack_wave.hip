@@ -34,8 +34,14 @@ constexpr int PACK_OCC = 8;          // BERT packer held to 8 waves/SIMD (78 SGP
 constexpr int PACK_DRAW_ROUNDS = 3;  // shuffle_draws: bound-propagation rounds before the ordered walk
 struct PackWaveLds {
   uint32_t mt[MT_N];            // MT19937 state; draws temper on the fly
-  uint16_t dfirst[PW_DOCS];     // global-only variant: the partition's documents
-  uint16_t dn[PW_DOCS];         //   (first kept slot relative to s0, #kept sentences)
+};
+// global-only unmasked variant: the partition's documents (first kept slot
+// relative to s0, #kept sentences) for the random-next lookups.  The masked
+// variants read them from global memory: their LDS bounds the resident waves
+// (mt + MaskLds), and the document lookups are a small part of their time.
+struct PackDocLds {
+  uint16_t dfirst[PW_DOCS];
+  uint16_t dn[PW_DOCS];
 };
 struct PackDyn {                // views into the dynamic LDS region
   uint16_t* lens;               // [cap_lens] filtered sentence lengths
@@ -209,11 +215,12 @@ struct WaveRng {
       const int n_lo = max(n_hi - 63, 1 << (k - 1));
       const int dmax = n_hi - n_lo + 1;  // draws this batch may complete (<= q)
       const int lim = min(MT_N - idx, 64);
-      const bool valid = lane < lim;
-      const uint32_t r = valid ? temper(L.mt[idx + lane]) >> (32 - k) : 0xFFFFFFFFu;
-      const uint64_t defm = __ballot(valid && r < (uint32_t)n_lo);
-      uint64_t ambm = __ballot(valid && r >= (uint32_t)n_lo && r < (uint32_t)n_hi);
-      const uint64_t lt = (1ull << lane) - 1ull;
+      const uint64_t vm = lim >= 64 ? ~0ull : (1ull << lim) - 1ull;  // words before the state's end
+      const uint32_t r = temper(L.mt[min(idx + lane, MT_N - 1)]) >> (32 - k);
+      // (masks as wave-uniform values: every per-lane test of them below is
+      // an exec mask or a v_mbcnt, no per-lane bit extraction)
+      uint64_t accm = __ballot(r < (uint32_t)n_lo) & vm;
+      uint64_t ambm = __ballot(r - (uint32_t)n_lo < (uint32_t)(n_hi - n_lo)) & vm;
       // bound propagation first: the words accepted before ambiguous word a
       // number at least L_a (decided accepts before a) and at most U_a (L_a +
       // undecided before a), so r < n_hi - U_a accepts it and r >= n_hi - L_a
@@ -221,15 +228,14 @@ struct WaveRng {
       // practice, most of the others: three rounds leave ~0.5 of a seq-512
       // shuffle's ~150 ambiguous words to the ordered walk below (simulated;
       // 1 / 2 / 3 rounds measured 2.11 / 1.91 / 1.87 e12 draw ticks per step).
-      uint64_t accm = defm;
 #pragma unroll
       for (int it = 0; it < PACK_DRAW_ROUNDS; ++it) {
         if (!ambm) break;
-        const bool und = (ambm >> lane) & 1ull;
-        const int Lc = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(accm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)accm, 0u));
-        const int Uc = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(ambm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ambm, (uint32_t)Lc));
-        const uint64_t acc_new = __ballot(und && (int)r < n_hi - Uc);
-        const uint64_t rej_new = __ballot(und && (int)r >= n_hi - Lc);
+        const int Lc = bits_below(accm);
+        const int Uc = bits_below(ambm, Lc);
+        // (r < 2^k <= 2^31 on the ambiguous lanes: no wrap there)
+        const uint64_t acc_new = __ballot(r + (uint32_t)Uc < (uint32_t)n_hi) & ambm;
+        const uint64_t rej_new = __ballot(r + (uint32_t)Lc >= (uint32_t)n_hi) & ambm;
         accm |= acc_new;
         ambm &= ~(acc_new | rej_new);
       }
@@ -237,17 +243,19 @@ struct WaveRng {
       // it, D_a decided + A earlier accepted ambiguous, leave its bound above
       // r: A < n_hi - r - D_a =: u_a.  Lanes past the batch's last draw are
       // resolved too and cut below (their outcome never feeds back).
-      const int u = n_hi - (int)r - __popcll(accm & lt);
-      int A = 0;
-      while (ambm) {
-        const int a = __ffsll((unsigned long long)ambm) - 1;
-        ambm &= ambm - 1;
-        const int ok = A < __builtin_amdgcn_readlane(u, a) ? 1 : 0;  // (scalar select, no branch)
-        A += ok;
-        accm |= (uint64_t)ok << a;
+      if (ambm) {
+        const int u = n_hi - (int)r - bits_below(accm);
+        int A = 0;
+        while (ambm) {
+          const int a = __ffsll((unsigned long long)ambm) - 1;
+          ambm &= ambm - 1;
+          const int ok = A < __builtin_amdgcn_readlane(u, a) ? 1 : 0;  // (scalar select, no branch)
+          A += ok;
+          accm |= (uint64_t)ok << a;
+        }
       }
-      const int pre = __popcll(accm & lt);
-      const uint64_t hit = __ballot((accm >> lane & 1ull) && pre == dmax - 1);
+      const int pre = bits_below(accm);
+      const uint64_t hit = __ballot(pre == dmax - 1) & accm;
       int end, s;
       if (hit) {
         end = __ffsll((unsigned long long)hit) - 1;
@@ -256,7 +264,7 @@ struct WaveRng {
         end = lim - 1;
         s = __popcll(accm);
       }
-      if (lane <= end && (accm >> lane & 1ull)) jb[q - pre] = (T)r;
+      if (lane_in(accm & (end >= 63 ? ~0ull : (2ull << end) - 1ull))) jb[q - pre] = (T)r;
       idx += end + 1;
       q -= s;
     }
@@ -457,6 +465,7 @@ template <int MASK, bool LDSOK>
 __global__ __launch_bounds__(64, PACK_OCC) void pack_bert_wave_kernel(PackParams P) {
   __shared__ PackWaveLds L;
   __shared__ typename std::conditional<MASK != 0, MaskLds<MASK == 1 ? 512 : MLM_MAX_SEQ>, NoMaskLds>::type ML;
+  __shared__ typename std::conditional<MASK != 0, NoMaskLds, PackDocLds>::type DL;
   PackDyn D;
   D.lens = reinterpret_cast<uint16_t*>(pw_dyn);
   D.dfirst = D.lens + P.cap_lens;
@@ -561,19 +570,29 @@ __global__ __launch_bounds__(64, PACK_OCC) void pack_bert_wave_kernel(PackParams
   PW_STAMP(1)
   // slot-relative accessors
   // global-only variant: the documents (the random-next lookups) in static LDS
-  const bool dres = !LDSOK && nd <= PW_DOCS && nfs < 65536;
-  if (dres) {
-    for (int k = lane; k < nd; k += 64) {
-      L.dfirst[k] = (uint16_t)(P.fd_first[d0 + k] - s0);
-      L.dn[k] = (uint16_t)P.fd_n[d0 + k];
+  const bool dres = !MASK && !LDSOK && nd <= PW_DOCS && nfs < 65536;
+  if constexpr (!MASK) {
+    if (dres) {
+      for (int k = lane; k < nd; k += 64) {
+        DL.dfirst[k] = (uint16_t)(P.fd_first[d0 + k] - s0);
+        DL.dn[k] = (uint16_t)P.fd_n[d0 + k];
+      }
+      wsync();
     }
-    wsync();
   }
   auto len_at = [&](int k) -> int { return lres ? (int)D.lens[k] : P.fs_ntok[s0 + k]; };
   auto doc_first = [&](int d) -> int {
-    return lres ? (int)D.dfirst[d] : dres ? (int)L.dfirst[d] : (int)(P.fd_first[d0 + d] - s0);
+    if constexpr (!MASK) {
+      if (dres) return (int)DL.dfirst[d];
+    }
+    return lres ? (int)D.dfirst[d] : (int)(P.fd_first[d0 + d] - s0);
   };
-  auto doc_n = [&](int d) -> int { return lres ? (int)D.dn[d] : dres ? (int)L.dn[d] : P.fd_n[d0 + d]; };
+  auto doc_n = [&](int d) -> int {
+    if constexpr (!MASK) {
+      if (dres) return (int)DL.dn[d];
+    }
+    return lres ? (int)D.dn[d] : P.fd_n[d0 + d];
+  };
 
   WaveRng rng{L, lane, MT_N};
   rng.seed(P.seed + (uint64_t)p);

@@ -58,6 +58,14 @@ __device__ __forceinline__ int wave_shr1(int x) { return (int)dpp0<DPP_WAVE_SHR1
 __device__ __forceinline__ uint32_t lane_get(uint32_t x, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)x, l); }
 __device__ __forceinline__ int lane_get(int x, int l) { return __builtin_amdgcn_readlane(x, l); }
 
+// this lane's bit of a wave-uniform mask: the mask becomes exec directly
+// (s_and_saveexec), where (m >> lane) & 1 costs a 64-bit shift + compare
+__device__ __forceinline__ bool lane_in(uint64_t m) { return __builtin_amdgcn_inverse_ballot_w64(m); }
+// set bits of a wave-uniform mask below this lane (v_mbcnt)
+__device__ __forceinline__ int bits_below(uint64_t m, int base = 0) {
+  return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, (uint32_t)base));
+}
+
 // segmented inclusive sum: a lane with h != 0 starts a segment; returns the
 // sum from the segment start (or lane 0) to this lane, h becomes "a segment
 // start at or before this lane"
