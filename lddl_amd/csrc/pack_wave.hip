@@ -62,7 +62,6 @@ struct MaskLds {
   alignas(16) uint16_t jb[CAP + 8];  // shuffle draws: swap x[i] <-> x[jb[i]]
   uint16_t mpos[CAP];           // picked positions in pick order
   uint16_t mid[CAP];            // their replacement ids (MLM_KEEP = unchanged)
-  uint32_t mark[16];            // mlm_choices: chain marks (one byte per word of a window)
 };
 struct NoMaskLds {};
 
@@ -276,11 +275,10 @@ struct WaveRng {
   // keep; else vocab_words[randint(0, V-1)]), the same words consumed as the
   // sequential calls.  Every lane decides the pick that would start at its
   // word (its length 2 / 4 / 4 + randbelow's words and its id) from the next
-  // <= 64 words; the scalar walk then hops from pick to pick.  A pick that
+  // <= 64 words; the walk from pick to pick is then read off jump tables.  A pick that
   // runs past the window starts the next window; one that cannot fit before
   // the state's end is drawn sequentially.
-  __device__ __forceinline__ void mlm_choices(int nm, uint32_t V, uint32_t mask_id, uint32_t keep_id, uint16_t* mid,
-                                              uint32_t* mark) {
+  __device__ __forceinline__ void mlm_choices(int nm, uint32_t V, uint32_t mask_id, uint32_t keep_id, uint16_t* mid) {
     const int kV = 32 - __clz(V);
     int pk = 0;
     while (pk < nm) {
@@ -304,39 +302,33 @@ struct WaveRng {
         res = true; len = p - lane + 1; nid = rv;
       }
       const uint64_t resm = __ballot(res);
-      uint64_t chosen = 0;
       int pos = 0;
-      const int pk0 = pk;
       // the walk 0 -> nx[0] -> ... over resolved words (nx = l + len; it
-      // stops at an unresolved word), found by pointer doubling: round i
-      // marks the 2^i-step successors J of the chain words found so far
-      // (LDS byte marks), then J = J[J].  len >= 2, so five rounds reach
-      // every chain word of a 64-word window; the first nm - pk are picks.
-      // (A scalar walk cost ~10 scalar instructions per pick on the CU's
-      // one scalar unit, the packer's bottleneck.)
+      // stops at an unresolved word): lane d finds the walk's d-th word
+      // c_d = nx^d(0) by the bits of d from jump tables J_i = nx^(2^i)
+      // (J_{i+1} = J_i[J_i], one ds_bpermute each, built alongside the
+      // walk's own gathers: ~5 dependent bpermutes per window, no LDS
+      // stores or wave syncs).  len >= 2, so a window holds <= 32 picks,
+      // and the members are a prefix of the lanes.  (A scalar walk cost ~10
+      // scalar instructions per pick on the CU's one scalar unit; LDS-mark
+      // pointer doubling 4 dependent LDS round trips per round.)
       if (resm & 1ull) {
         const int nx = res ? lane + len : 64;
-        int J = nx;
-        uint64_t on = 1ull;
-        uint8_t* mk = reinterpret_cast<uint8_t*>(mark);
+        int J = min(nx, 64), c = 0;
 #pragma unroll
         for (int i = 0; i < 5; ++i) {
-          mk[lane] = 0;
-          wsync();
-          if ((on >> lane & 1ull) && J < 64) mk[J] = 1;
-          wsync();
-          on |= __ballot(mk[lane] != 0) & resm;
-          const int JJ = __shfl(J, J < 64 ? J : 0);
-          J = J < 64 ? JJ : 64;
+          const int gc = __shfl(J, min(c, 63));  // J_i[c]
+          const int gj = __shfl(J, min(J, 63));  // J_i[J_i]
+          if ((lane >> i) & 1) c = c >= 64 ? 64 : gc;
+          J = J >= 64 ? 64 : gj;
         }
-        const int K = nm - pk;
-        const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(on >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)on, 0u));
-        chosen = __ballot((on >> lane & 1ull) && rank < K);
-        const int last = 63 - __clzll((long long)chosen);
-        pos = __builtin_amdgcn_readlane(nx, last);
-        pk += __popcll(chosen);
+        const bool member = lane < 32 && c < 64 && ((resm >> (c & 63)) & 1ull);
+        const int cnt = min(__popcll(__ballot(member)), nm - pk);
+        const uint32_t ng = (uint32_t)__shfl((int)nid, min(c, 63));
+        if (lane < cnt) mid[pk + lane] = (uint16_t)ng;
+        pos = __builtin_amdgcn_readlane(nx, __builtin_amdgcn_readlane(c, cnt - 1));
+        pk += cnt;
       }
-      if (chosen >> lane & 1ull) mid[pk0 + __popcll(chosen & ((1ull << lane) - 1ull))] = (uint16_t)nid;
       if (pos == 0) {  // the pick does not fit before the state's end: sequential
         uint32_t v;
         if (random() < 0.8) v = mask_id;
@@ -822,7 +814,7 @@ __global__ __launch_bounds__(64, PACK_OCC) void pack_bert_wave_kernel(PackParams
           }
           // 80% [MASK], 10% keep, 10% random word, in pick order
           PW_STAMP(8)
-          rng.mlm_choices(nm, P.n_vocab, P.mask_id, MLM_KEEP, ML.mid, ML.mark);
+          rng.mlm_choices(nm, P.n_vocab, P.mask_id, MLM_KEEP, ML.mid);
           PW_STAMP(9)
           if (mcur + nm > mend) {
             unsigned long long b0 = 0;
