@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "../../include/lddl_amd.h"
+#include "tok_tables.h"
 #include "collate.h"
 #include "common.h"
 #include "pack.h"
@@ -164,225 +165,39 @@ static int upload(T** dst, const void* src, size_t bytes) {
 }
 
 static int load_table(lddl_ctx* c, const char* path) {
-  FILE* f = fopen(path, "rb");
-  if (!f) return set_err(LDDL_EIO, "cannot open unicode table %s", path);
-  char magic[8];
-  uint32_t hdr[3];
-  std::vector<uint16_t> top(0x1100);
-  if (fread(magic, 1, 8, f) != 8 || memcmp(magic, "LDDLUNI1", 8) != 0 || fread(hdr, 4, 3, f) != 3) {
-    fclose(f);
-    return set_err(LDDL_EFORMAT, "bad unicode table header in %s", path);
-  }
-  std::vector<uint32_t> pages((size_t)hdr[0] * 256);
-  std::vector<uint32_t> multi((size_t)hdr[1] * 4);
-  bool ok = fread(top.data(), 2, top.size(), f) == top.size() &&
-            fread(pages.data(), 4, pages.size(), f) == pages.size() &&
-            fread(multi.data(), 4, multi.size(), f) == multi.size();
-  fclose(f);
-  if (!ok) return set_err(LDDL_EFORMAT, "truncated unicode table %s", path);
-  for (size_t i = 0; i < top.size(); ++i)
-    if (top[i] >= hdr[0]) return set_err(LDDL_EFORMAT, "unicode table page index out of range");
-  // the kernel assumes multi-char expansions are plain word chars (checked)
-  for (size_t i = 0; i < hdr[1]; ++i) {
-    uint32_t n = multi[i * 4];
-    if (n < 2 || n > 3) return set_err(LDDL_EFORMAT, "unicode table multi entry %zu has %u chars", i, n);
-    for (uint32_t k = 0; k < n; ++k)
-      if (ent_cls(multi[i * 4 + 1 + k]) != CLS_OTHER)
-        return set_err(LDDL_EFORMAT, "unicode table multi entry %zu has a non-word char", i);
-  }
-  // the split scan (tokenize_split.hip) derives its per-byte class table from the ASCII page: it
-  // needs rank-0, single-char entries whose only mapping is A-Z -> a-z
-  c->scan_ok = true;
-  for (uint32_t b = 0; b < 128; ++b) {
-    const uint32_t e = pages[(size_t)top[0] * 256 + b];
-    const uint32_t kind = ent_kind(e), cls = ent_cls(e);
-    if (ent_rank(e) != 0 || kind == KIND_MULTI) c->scan_ok = false;
-    if (kind == KIND_MAP && cls == CLS_ISOLATE) c->scan_ok = false;
-    if (kind == KIND_MAP && cls == CLS_OTHER && !(b >= 'A' && b <= 'Z' && ent_payload(e) == b + 32))
-      c->scan_ok = false;
-  }
-  if (ent_cls(pages[(size_t)top[0] * 256 + '[']) != CLS_ISOLATE) c->scan_ok = false;
-  int rc;
-  if ((rc = upload(&c->d_top, top.data(), top.size() * 2))) return rc;
-  if ((rc = upload(&c->d_pages, pages.data(), pages.size() * 4))) return rc;
-  if ((rc = upload(&c->d_multi, multi.data(), multi.size() * 4))) return rc;
-  // the BMP flattened (256 KiB, L2-resident): one load per code point < U+10000
-  std::vector<uint32_t> bmp(0x10000);
-  for (uint32_t cp = 0; cp < 0x10000; ++cp) bmp[cp] = pages[(size_t)top[cp >> 8] * 256 + (cp & 255)];
-  if ((rc = upload(&c->d_bmp, bmp.data(), bmp.size() * 4))) return rc;
-  // the scan's fast exception entries (4.25 MiB, U+0000..U+10FFFF): what the
-  // full path would do with a code point, precomputed -- its pre-tokenizer
-  // action and, for a single-char mapping, the replacement's UTF-8 bytes;
-  // SLOW where the full path is needed (multi-char expansion, canonical
-  // reordering rank, a 4-byte replacement)
-  std::vector<uint32_t> xmap(0x110000);
-  for (uint32_t cp = 0; cp < 0x110000; ++cp) {
-    const uint32_t e = pages[(size_t)top[cp >> 8] * 256 + (cp & 255)];
-    const uint32_t kind = ent_kind(e), cls = ent_cls(e), pay = ent_payload(e);
-    uint32_t x = 0;
-    if (ent_rank(e) != 0) {
-      x = 0x80000000u;
-    } else if (kind == KIND_DROP_T || kind == KIND_DROP_D) {
-      x = 3u << 27;
-    } else if (cls == CLS_SPACE) {
-      x = 1u << 27;
-    } else {
-      x = (cls == CLS_ISOLATE ? 2u : 0u) << 27;
-      if (kind == KIND_MULTI || (kind != KIND_IDENT && pay >= 0x10000)) {
-        x = 0x80000000u;
-      } else if (kind != KIND_IDENT) {
-        uint32_t b = 0, t;
-        if (pay < 0x80) { b = pay; t = 1; }
-        else if (pay < 0x800) { b = (0xC0 | (pay >> 6)) | ((0x80 | (pay & 0x3F)) << 8); t = 2; }
-        else { b = (0xE0 | (pay >> 12)) | ((0x80 | ((pay >> 6) & 0x3F)) << 8) | ((0x80 | (pay & 0x3F)) << 16); t = 3; }
-        x |= 0x20000000u | (t << 24) | b;
-      }
-    }
-    xmap[cp] = x;
-  }
-  if ((rc = upload(&c->d_xmap, xmap.data(), xmap.size() * 4))) return rc;
+  UniTables T;
+  std::string err;
+  int rc = build_uni_tables(path, T, err);
+  if (rc) return set_err(rc, "%s", err.c_str());
+  c->scan_ok = T.scan_ok;
+  if ((rc = upload(&c->d_top, T.top.data(), T.top.size() * 2))) return rc;
+  if ((rc = upload(&c->d_pages, T.pages.data(), T.pages.size() * 4))) return rc;
+  if ((rc = upload(&c->d_multi, T.multi.data(), T.multi.size() * 4))) return rc;
+  if ((rc = upload(&c->d_bmp, T.bmp.data(), T.bmp.size() * 4))) return rc;
+  if ((rc = upload(&c->d_xmap, T.xmap.data(), T.xmap.size() * 4))) return rc;
   return 0;
 }
 
 static int load_vocab(lddl_ctx* c, const char* path) {
-  FILE* f = fopen(path, "rb");
-  if (!f) return set_err(LDDL_EIO, "cannot open vocab %s", path);
-  std::string cur;
-  int ch;
-  while ((ch = fgetc(f)) != EOF) {
-    if (ch == '\n') {
-      while (!cur.empty() && cur.back() == '\r') cur.pop_back();
-      c->vocab.push_back(cur);
-      cur.clear();
-    } else {
-      cur.push_back((char)ch);
-    }
-  }
-  if (!cur.empty()) c->vocab.push_back(cur);
-  fclose(f);
-  int rc0;
-  const size_t V = c->vocab.size();
-  if (V == 0 || V > 65536) return set_err(LDDL_EFORMAT, "vocab size %zu not in [1, 65536]", V);
-  c->vocab_size = (int)V;
-  const char* sp[5] = {"[PAD]", "[UNK]", "[CLS]", "[SEP]", "[MASK]"};
-  for (int k = 0; k < 5; ++k) {
-    int found = -1;
-    for (size_t i = 0; i < V; ++i)
-      if (c->vocab[i] == sp[k]) found = (int)i;  // last occurrence wins
-    if (found < 0) return set_err(LDDL_EFORMAT, "vocab %s lacks %s", path, sp[k]);
-    c->special[k] = (uint32_t)found;
-  }
-  // pool of (cont, bytes) keys; "##x" -> cont=1 "x"; every key 4-aligned
-  std::vector<uint8_t> pool;
-  std::vector<uint32_t> voff(V), vlen(V), vcont(V);
-  for (size_t i = 0; i < V; ++i) {
-    const std::string& w = c->vocab[i];
-    uint32_t cont = (w.size() >= 2 && w[0] == '#' && w[1] == '#') ? 1u : 0u;
-    const char* s = w.data() + 2 * cont;
-    uint32_t n = (uint32_t)w.size() - 2 * cont;
-    if (n > 255) return set_err(LDDL_EFORMAT, "vocab entry %zu longer than 255 bytes", i);
-    voff[i] = (uint32_t)pool.size();
-    vlen[i] = n;
-    vcont[i] = cont;
-    pool.insert(pool.end(), s, s + n);
-    pool.resize((pool.size() + 3) & ~(size_t)3, 0);
-    if (n > c->maxb[cont]) c->maxb[cont] = n;
-  }
-  pool.resize(pool.size() + 16, 0);
-  uint32_t cap = 1;
-  while (cap < V * 2) cap <<= 1;
-  std::vector<uint4> slots(cap, make_uint4(0, 0, 0, 0));
-  for (size_t i = 0; i < V; ++i) {
-    if (vlen[i] == 0) continue;  // "##" alone: unreachable
-    uint64_t h = 0;
-    for (uint32_t k = 0; k < vlen[i]; ++k) h = hash_push(h, pool[voff[i] + k]);
-    uint64_t key = hash_key(h, vlen[i], vcont[i]);
-    uint32_t idx = (uint32_t)key & (cap - 1), fp = (uint32_t)(key >> 32);
-    uint32_t pre[2] = {0, 0};
-    memcpy(pre, &pool[voff[i]], vlen[i] < 8 ? vlen[i] : 8);
-    for (;;) {
-      uint4& s = slots[idx];
-      if (!(s.y & 0x80000000u)) { s = make_uint4(fp, slot_info((uint32_t)i, vlen[i], vcont[i]), pre[0], pre[1]); break; }
-      uint32_t j = s.y & 0xFFFFu;
-      if (vlen[j] == vlen[i] && vcont[j] == vcont[i] && memcmp(&pool[voff[j]], &pool[voff[i]], vlen[i]) == 0) {
-        s.y = slot_info((uint32_t)i, vlen[i], vcont[i]);  // duplicate line: last id wins
-        break;
-      }
-      idx = (idx + 1) & (cap - 1);
-    }
-  }
-  c->slot_mask = cap - 1;
-  // blocked Bloom filter over the same keys: word = key bits 40..52, two bit
-  // positions from key bits 0..9.  A clear bit proves absence (exact negative).
-  std::vector<uint32_t> bloom(BLOOM_WORDS, 0);
-  for (size_t i = 0; i < V; ++i) {
-    if (vlen[i] == 0) continue;
-    uint64_t h = 0;
-    for (uint32_t k = 0; k < vlen[i]; ++k) h = hash_push(h, pool[voff[i] + k]);
-    const uint64_t key = hash_key(h, vlen[i], vcont[i]);
-    bloom[(uint32_t)(key >> 40) & (BLOOM_WORDS - 1)] |= (1u << (key & 31)) | (1u << ((key >> 5) & 31));
-  }
-  if ((rc0 = upload(&c->d_bloom, bloom.data(), bloom.size() * 4))) return rc0;
-  // v4 table: >= 2V buckets of two 32-B slots (load <= 1/4: a key outside
-  // its home bucket costs the WordPiece loop a dependent probe; tools/wp_sim.py),
-  // linear probing over buckets; Bloom filter over the same hashes (common.h vhash)
-  {
-    uint32_t nbk = 1;
-    while (nbk < 2 * V) nbk <<= 1;
-    std::vector<uint32_t> vt((size_t)nbk * 16, 0u);
-    std::vector<uint32_t> vbl(BLOOM_WORDS, 0u);
-    for (size_t i = 0; i < V; ++i) {
-      if (vlen[i] == 0) continue;
-      uint32_t d[VKEY_DW] = {0, 0, 0, 0, 0, 0};
-      memcpy(d, &pool[voff[i]], vlen[i] < 24 ? vlen[i] : 24);
-      const uint32_t h = vhash(d, vlen[i], vcont[i]), bk = vbkey_of(d, vlen[i], vcont[i]);
-      vbl[vbloom_word(bk)] |= vbloom_bits(bk);
-      {  // extension keys of its 4-, 8-, .. 24-byte prefixes shorter than it
-        uint32_t hp = VSEED;
-        for (uint32_t j = 0; j < VKEY_DW && 4 * (j + 1) < vlen[i]; ++j) {
-          hp = vmix(hp, d[j]);
-          const uint32_t ek = vbkey_ext(hp, 4 * (j + 1), vcont[i]);
-          vbl[vbloom_word(ek)] |= vbloom_bits(ek);
-        }
-      }
-      bool done = false;
-      for (uint32_t b = h & (nbk - 1); !done; b = (b + 1) & (nbk - 1)) {
-        for (int sl = 0; sl < 2 && !done; ++sl) {
-          uint32_t* s = &vt[((size_t)b * 2 + sl) * 8];
-          if (s[6] != 0) {
-            const uint32_t j = s[6] & 0xFFFFu;
-            if (!(vlen[j] == vlen[i] && vcont[j] == vcont[i] && memcmp(&pool[voff[j]], &pool[voff[i]], vlen[i]) == 0))
-              continue;  // occupied by another key
-          }
-          memcpy(s, d, sizeof d);  // empty slot, or a duplicate line: last id wins
-          s[6] = slot_info((uint32_t)i, vlen[i], vcont[i]);
-          s[7] = voff[i];
-          done = true;
-        }
-      }
-    }
-    c->vt_mask = nbk - 1;
-    if ((rc0 = upload(&c->d_vt, vt.data(), vt.size() * 4))) return rc0;
-    if ((rc0 = upload(&c->d_vbloom, vbl.data(), vbl.size() * 4))) return rc0;
-  }
-  int rc;
-  if ((rc = upload(&c->d_slots, slots.data(), slots.size() * sizeof(uint4)))) return rc;
-  if ((rc = upload(&c->d_pool, pool.data(), pool.size()))) return rc;
-  if ((rc = upload(&c->d_voff, voff.data(), voff.size() * 4))) return rc;
-  {  // rendering tables: the vocab entries verbatim (pretrain.py:348-353 joins them)
-    std::vector<uint8_t> rpool;
-    std::vector<uint32_t> rinfo(V);
-    for (size_t i = 0; i < V; ++i) {
-      const std::string& w = c->vocab[i];
-      if (rpool.size() >= (1u << 24)) return set_err(LDDL_EFORMAT, "vocab text larger than 16 MiB");
-      rinfo[i] = (uint32_t)rpool.size() << 8 | (uint32_t)w.size();  // size <= 255, checked above
-      rpool.insert(rpool.end(), w.begin(), w.end());
-      rpool.resize((rpool.size() + 3) & ~(size_t)3, 0);
-    }
-    rpool.resize(rpool.size() + 16, 0);
-    if ((rc = upload(&c->d_rpool, rpool.data(), rpool.size()))) return rc;
-    if ((rc = upload(&c->d_rinfo, rinfo.data(), rinfo.size() * 4))) return rc;
-  }
+  VocabTables V;
+  std::string err;
+  int rc = build_vocab_tables(path, V, err);
+  if (rc) return set_err(rc, "%s", err.c_str());
+  c->vocab_size = (int)V.vocab.size();
+  for (int k = 0; k < 5; ++k) c->special[k] = V.special[k];
+  c->maxb[0] = V.maxb[0];
+  c->maxb[1] = V.maxb[1];
+  c->slot_mask = V.slot_mask;
+  c->vt_mask = V.vt_mask;
+  if ((rc = upload(&c->d_bloom, V.bloom.data(), V.bloom.size() * 4))) return rc;
+  if ((rc = upload(&c->d_vt, V.vt.data(), V.vt.size() * 4))) return rc;
+  if ((rc = upload(&c->d_vbloom, V.vbloom.data(), V.vbloom.size() * 4))) return rc;
+  if ((rc = upload(&c->d_slots, V.slots.data(), V.slots.size() * sizeof(uint4)))) return rc;
+  if ((rc = upload(&c->d_pool, V.pool.data(), V.pool.size()))) return rc;
+  if ((rc = upload(&c->d_voff, V.voff.data(), V.voff.size() * 4))) return rc;
+  if ((rc = upload(&c->d_rpool, V.rpool.data(), V.rpool.size()))) return rc;
+  if ((rc = upload(&c->d_rinfo, V.rinfo.data(), V.rinfo.size() * 4))) return rc;
+  c->vocab = std::move(V.vocab);
   return 0;
 }
 

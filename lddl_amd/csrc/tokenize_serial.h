@@ -11,6 +11,9 @@ namespace lddl {
 constexpr int WB_LDS = 64;    // bytes of word buffer per lane held in LDS
 constexpr int BLOCK = 256;
 
+// The functions below are host + device: tests/host_serial.cpp builds them
+// for the host (g++, AddressSanitizer) over the same tables.
+#ifdef __HIP__
 // per-lane word buffer: bytes [0, WB_LDS) in LDS, dword-interleaved across
 // the block's lanes (byte i of lane t in word [i>>2][t]: conflict-free when
 // lanes touch the same i), the rest in a per-lane global overflow slab.
@@ -33,11 +36,13 @@ struct LdsWordBuf {
   }
 };
 
-// all bytes in a global slab (v2's single-lane fallback)
+#endif
+
+// all bytes in one slab (the host build's word buffer)
 struct GlobalWordBuf {
   uint8_t* ovf;  // WB_LDS + WB_OVF bytes
-  __device__ __forceinline__ uint32_t get(int i) const { return ovf[i]; }
-  __device__ __forceinline__ void put(int i, uint32_t v) const { ovf[i] = (uint8_t)v; }
+  LDDL_HD uint32_t get(int i) const { return ovf[i]; }
+  LDDL_HD void put(int i, uint32_t v) const { ovf[i] = (uint8_t)v; }
 };
 
 struct SentState {
@@ -46,16 +51,16 @@ struct SentState {
   int32_t ntok;
 };
 
-__device__ __forceinline__ void emit(const TokParams& P, SentState& st, uint32_t id) {
+LDDL_HD void emit(const TokParams& P, SentState& st, uint32_t id) {
   if (st.ntok < P.max_tok) P.out_ids[st.obase + st.ntok] = (uint16_t)id;
   st.ntok++;
 }
 
-__device__ __forceinline__ int utf8_len(uint32_t b) { return b < 0x80 ? 1 : b >= 0xF0 ? 4 : b >= 0xE0 ? 3 : 2; }
-__device__ __forceinline__ int utf8_enc_len(uint32_t c) { return c < 0x80 ? 1 : c < 0x800 ? 2 : c < 0x10000 ? 3 : 4; }
+LDDL_HD int utf8_len(uint32_t b) { return b < 0x80 ? 1 : b >= 0xF0 ? 4 : b >= 0xE0 ? 3 : 2; }
+LDDL_HD int utf8_enc_len(uint32_t c) { return c < 0x80 ? 1 : c < 0x800 ? 2 : c < 0x10000 ? 3 : 4; }
 
 template <class WB>
-__device__ __forceinline__ int put_utf8(const WB& wb, int at, uint32_t c) {
+LDDL_HD int put_utf8(const WB& wb, int at, uint32_t c) {
   if (at > WB_LDS + WB_OVF - 4) return 0;  // never reached for words <= 100 chars
   if (c < 0x80) { wb.put(at, c); return 1; }
   if (c < 0x800) { wb.put(at, 0xC0 | (c >> 6)); wb.put(at + 1, 0x80 | (c & 0x3F)); return 2; }
@@ -68,12 +73,12 @@ __device__ __forceinline__ int put_utf8(const WB& wb, int at, uint32_t c) {
   return 4;
 }
 
-__device__ __forceinline__ uint32_t table_entry(const TokParams& P, uint32_t cp) {
+LDDL_HD uint32_t table_entry(const TokParams& P, uint32_t cp) {
   return P.pages[(uint32_t)P.top[cp >> 8] * 256u + (cp & 255u)];
 }
 
 // literal [PAD] [UNK] [CLS] [SEP] [MASK] starting at p (byte p is '[')
-__device__ __forceinline__ int match_special(const uint8_t* s, int64_t p, int64_t e, int* len) {
+LDDL_HD int match_special(const uint8_t* s, int64_t p, int64_t e, int* len) {
   if (p + 5 > e) return -1;
   uint32_t c1 = s[p + 1], c2 = s[p + 2], c3 = s[p + 3], c4 = s[p + 4];
   if (c1 == 'P' && c2 == 'A' && c3 == 'D' && c4 == ']') { *len = 5; return 0; }
@@ -89,11 +94,11 @@ __device__ __forceinline__ int match_special(const uint8_t* s, int64_t p, int64_
 // slot's prefix, longer ones additionally against the 4-aligned pool (all
 // dword loads issued together, no per-byte dependent chain).
 struct NoFilter {
-  __device__ __forceinline__ bool operator()(uint64_t) const { return true; }
+  LDDL_HD bool operator()(uint64_t) const { return true; }
 };
 
 template <class GET, class FILT>
-__device__ __forceinline__ int probe(const TokParams& P, const GET& get, int s, int len, uint32_t cont, uint64_t h,
+LDDL_HD int probe(const TokParams& P, const GET& get, int s, int len, uint32_t cont, uint64_t h,
                                      const FILT& filt) {
   const uint64_t key = hash_key(h, (uint32_t)len, cont);
   if (!filt(key)) return -1;  // exact negative
@@ -130,12 +135,13 @@ __device__ __forceinline__ int probe(const TokParams& P, const GET& get, int s, 
 // EMIT(n, id) is called per piece; returns #pieces, or -1 when some position
 // has no match (the caller then emits the single [UNK]).
 template <class GET, class EMIT, class FILT = NoFilter>
-__device__ __forceinline__ int wordpiece_core(const TokParams& P, const GET& get, int nb, const EMIT& emit_fn,
+LDDL_HD int wordpiece_core(const TokParams& P, const GET& get, int nb, const EMIT& emit_fn,
                                               const FILT& filt = FILT()) {
   int s = 0, n = 0;
   uint32_t cont = 0;
   while (s < nb) {
-    int e = min(nb, s + (int)P.maxb[cont]);
+    int e = s + (int)P.maxb[cont];
+    if (e > nb) e = nb;
     while (e < nb && e > s && (get(e) & 0xC0u) == 0x80u) --e;
     uint64_t h = 0;
     for (int k = s; k < e; ++k) h = hash_push(h, get(k));
@@ -156,7 +162,7 @@ __device__ __forceinline__ int wordpiece_core(const TokParams& P, const GET& get
 
 // WordPiece over the buffered normalised word (nb bytes, nch chars).
 template <class WB>
-__device__ void wordpiece(const TokParams& P, SentState& st, const WB& wb, int nb, int nch) {
+__host__ __device__ void wordpiece(const TokParams& P, SentState& st, const WB& wb, int nb, int nch) {
   if (nch > 100) { emit(P, st, P.unk); return; }
   const int32_t mark = st.ntok;
   auto get = [&](int i) { return wb.get(i); };
@@ -167,7 +173,7 @@ __device__ void wordpiece(const TokParams& P, SentState& st, const WB& wb, int n
 // Append one normalised char; keeps each run of ccc>0 chars stably sorted by
 // rank (NFD canonical ordering).  Rare path only for chars with rank > 0.
 template <class WB>
-__device__ __forceinline__ void append_char(const TokParams& P, const WB& wb, int& nb, int& nch,
+LDDL_HD void append_char(const TokParams& P, const WB& wb, int& nb, int& nch,
                                             uint32_t c, uint32_t rank, uint32_t& prev_rank, int& run_start) {
   ++nch;
   if (nch > 100) return;  // word becomes [UNK]; stop buffering
@@ -192,7 +198,7 @@ __device__ __forceinline__ void append_char(const TokParams& P, const WB& wb, in
 
 // One step: the next word (or special token / isolated char) of the sentence.
 template <class WB>
-__device__ void step(const TokParams& P, SentState& st, const WB& wb, const uint32_t* ascii_tab) {
+__host__ __device__ void step(const TokParams& P, SentState& st, const WB& wb, const uint32_t* ascii_tab) {
   int nb = 0, nch = 0, run_start = 0;
   uint32_t prev_rank = 0;
   const uint8_t* bytes = P.bytes;
