@@ -321,7 +321,8 @@ def parquet_sample(args, pk, res, sh):
   doc_ids = None
   if args.corpus == 'code':  # the CodeBERT 'id' column of the documents written
     nd = int(sh.part_doc_off[min(args.parquet_parts, sh.n_part)].item())
-    doc_ids = ['python_%d' % i for i in range(nd)]
+    import pyarrow as pa  # (as the CLI's split workers hand it over: an Arrow column)
+    doc_ids = pa.array(['python_%d' % i for i in range(nd)], type=pa.string())
   try:
     # one untimed partition first: pyarrow's lazily imported modules (compute,
     # pandas compat: ~0.55 s once per process) stay out of the rate

@@ -340,6 +340,9 @@ def _split_worker(a, b):
   ts = time.perf_counter()
   recs = _FE['index'].texts(_FE['order'][a:b])
   corpus, ids = split_records(recs, _FE['codebert'], _FE['split'])
+  if _FE['codebert']:  # the writer's id column, built here in the worker, off the writer's path
+    import pyarrow as pa
+    ids = pa.array(ids, type=pa.string())
   return corpus, ids, time.perf_counter() - ts
 
 

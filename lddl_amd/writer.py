@@ -120,7 +120,7 @@ def write_shards(packer, res, out_dir, bin_size=None, codebert=False, masking=Fa
   """Write the rows of ``res`` (a pipeline.PackResult) as the reference's
   parquet files under out_dir.  Partition p of this pack call is file
   ``part.{part_base + p}.parquet`` (unbinned) or ``part.{..}.parquet_{b}``
-  for every bin b (binned).  doc_ids: CodeBERT 'id' strings per document of
+  for every bin b (binned).  doc_ids: CodeBERT 'id' strings (list or Arrow array) per document of
   the packed corpus.  max_parts: only the first max_parts partitions.
   Returns the list of files written."""
   os.makedirs(out_dir, exist_ok=True)
@@ -145,7 +145,8 @@ def write_shards(packer, res, out_dir, bin_size=None, codebert=False, masking=Fa
     if doc_ids is None:
       raise ValueError('CodeBERT shards need doc_ids (the id column)')
     docs = pa.array(row_docs(packer, res.n_pairs, n_rows, stream))
-    ids_col = pa.array(doc_ids, type=pa.string()).take(docs) if n_rows else pa.array([], pa.string())
+    ids_arr = doc_ids if isinstance(doc_ids, pa.Array) else pa.array(doc_ids, type=pa.string())
+    ids_col = ids_arr.take(docs) if n_rows else pa.array([], pa.string())
   if masking and not codebert:
     moff_all = res.mlm_off[:n_rows + 1].cpu().numpy()
     mpos_all = res.mlm_pos[:int(moff_all[-1])].cpu().numpy().view(np.uint16)
@@ -236,6 +237,8 @@ def write_txt(packer, res, out_dir, bin_size=None, codebert=False, masking=False
   if codebert:
     if doc_ids is None:
       raise ValueError('CodeBERT txt output needs doc_ids (the id field)')
+    if isinstance(doc_ids, pa.Array):
+      doc_ids = doc_ids.to_pylist()
     docs = row_docs(packer, res.n_pairs, n_rows, stream)
   if masking and not codebert:
     moff_all = res.mlm_off[:n_rows + 1].cpu().numpy()
