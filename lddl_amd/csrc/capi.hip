@@ -507,7 +507,8 @@ static int pack_common(lddl_ctx* c, int codebert, const int32_t* d_ntok, const i
     if ((rc = ws_get(c, spec_ok ? 41 : 22, n_sent, &sent_spec)) || (rc = ws_get(c, 23, n_sent, &fs_spec)) ||
         (rc = ws_get(c, 24, npair_cap, &P.mref)) || (rc = ws_get(c, 25, npair_cap, &P.mloc)) ||
         (rc = ws_get(c, 26, n_part, &P.part_nmask)) || (rc = ws_get(c, 27, n_part + 1, &mask_base)) ||
-        (rc = ws_get(c, 28, n_part + 1, &mask_base2)) || (rc = ws_get(c, 29, 1, &P.mcounter)))
+        (rc = ws_get(c, 28, n_part + 1, &mask_base2)) || (rc = ws_get(c, 29, 1, &P.mcounter)) ||
+        (rc = ws_get(c, 31, (size_t)n_part * MLM_MAX_SEQ, &P.mcand)))
       return rc;
     P.sent_spec = sent_spec;
     P.fs_spec = fs_spec;

@@ -69,6 +69,7 @@ struct PackParams {
   uint32_t* marena;             // masked entries: position | (new id or 0xFFFF = keep) << 16
   uint64_t mcap;                // arena capacity (entries)
   unsigned long long* mcounter; // arena bump allocator (entries handed out)
+  uint16_t* mcand;              // [n_part * MLM_MAX_SEQ] masking: candidate list scratch per partition
 };
 
 constexpr int MLM_CHUNK = 1024;     // arena entries grabbed per allocation

@@ -58,7 +58,6 @@ extern __shared__ __attribute__((aligned(16))) uint8_t pw_dyn[];
 // LDS for more resident waves
 template <int CAP>
 struct MaskLds {
-  uint16_t cand[CAP];   // explicit candidate positions (pairs with [CLS]/[SEP] tokens)
   alignas(16) uint16_t jb[CAP + 8];  // shuffle draws: swap x[i] <-> x[jb[i]]
   uint16_t mpos[CAP];           // picked positions in pick order
   uint16_t mid[CAP];            // their replacement ids (MLM_KEEP = unchanged)
@@ -202,9 +201,10 @@ struct WaveRng {
   // is already decided for every draw the batch could give it (r < n_lo:
   // accepted, r >= n_hi: rejected); only the words with r in [n_lo, n_hi) are
   // walked in order, one ballot step each.
-  template <class T>
-  __device__ __forceinline__ void shuffle_draws(int m, T* jb) { shuffle_draws_inl(m, jb); }
-  template <class T>
+  // REL: jb[q] holds j - (q & ~7) (signed 16-bit; the pick trace's chunk-relative form)
+  template <bool REL = false, class T>
+  __device__ __forceinline__ void shuffle_draws(int m, T* jb) { shuffle_draws_inl<REL>(m, jb); }
+  template <bool REL = false, class T>
   __device__ __forceinline__ void shuffle_draws_inl(int m, T* jb) {
     int q = m - 1;
     while (q >= 1) {
@@ -263,7 +263,10 @@ struct WaveRng {
         end = lim - 1;
         s = __popcll(accm);
       }
-      if (lane_in(accm & (end >= 63 ? ~0ull : (2ull << end) - 1ull))) jb[q - pre] = (T)r;
+      if (lane_in(accm & (end >= 63 ? ~0ull : (2ull << end) - 1ull))) {
+        const int qq = q - pre;
+        jb[qq] = REL ? (T)((int)r - (qq & ~7)) : (T)r;
+      }
       idx += end + 1;
       q -= s;
     }
@@ -714,6 +717,10 @@ __global__ __launch_bounds__(64, PACK_OCC) void pack_bert_wave_kernel(PackParams
           const int ntp = max(1, (int)rint((double)(la2 + lb2 + 3) * P.mlm_ratio));
           const int fa = first + cs, fb = (int)(r.fs1 - s0);
           const bool expl = any_spec(fa, a_end) || any_spec(fb, r.n1);
+          // explicit candidate positions (pairs holding [CLS]/[SEP] tokens,
+          // rare): global scratch of this partition, keeping the LDS lists
+          // small for more resident waves
+          uint16_t* const mcand = P.mcand + p * MLM_MAX_SEQ;
           int m = la2 + lb2;
           if (expl) {  // candidates = positions whose token is not [CLS]/[SEP]
             m = 0;
@@ -731,7 +738,7 @@ __global__ __launch_bounds__(64, PACK_OCC) void pack_bert_wave_kernel(PackParams
                     keep = v != P.cls_id && v != P.sep_id;
                   }
                   const uint64_t bm = __ballot(keep);
-                  if (keep) ML.cand[m + __popcll(bm & ((1ull << lane) - 1ull))] = (uint16_t)(pos0 + tt - lo);
+                  if (keep) mcand[m + bits_below(bm)] = (uint16_t)(pos0 + tt - lo);
                   m += __popcll(bm);
                 }
                 acc += ln;
@@ -739,18 +746,19 @@ __global__ __launch_bounds__(64, PACK_OCC) void pack_bert_wave_kernel(PackParams
             };
             seg(fa, a_end, alo, ahi, 1);
             seg(fb, r.n1, blo, bhi, 2 + la2);
+            gsync();  // the list's global writes visible to the trace's reads (other lanes)
           }
           // random.shuffle(cand_indexes): record the swaps, then undo them
           // per picked slot (lane per pick) instead of permuting the list
           PW_STAMP(6)
-          rng.shuffle_draws(m, ML.jb);
+          rng.shuffle_draws<true>(m, ML.jb);
           PW_STAMP(7)
           const int nm = min(ntp, m);
           // pick pk's candidate = the slot that the swaps (q, jb[q]), applied
           // for q = m-1 .. 1, move to pk: traced back over q = 1 .. m-1.
           // Picks pk, pk + 64 per lane; 8 swaps per 16-B LDS read (measured
           // against u16 reads / readlane swaps: 2.87 vs 3.82 / 3.23 s per step)
-          auto pick_pos = [&](int q) { return (uint16_t)(expl ? (int)ML.cand[q] : (q < la2 ? 1 + q : 2 + q)); };
+          auto pick_pos = [&](int q) { return (uint16_t)(expl ? (int)mcand[q] : (q < la2 ? 1 + q : 2 + q)); };
           // Final position pk < nm of the shuffled list = the element the
           // swaps move there.  Split the swaps at nm: the late ones
           // (q = nm-1 .. 1, all j_q <= q < nm) only permute positions < nm
@@ -771,7 +779,7 @@ __global__ __launch_bounds__(64, PACK_OCC) void pack_bert_wave_kernel(PackParams
             for (int k = lane; k < m; k += 64) F[k] = 0xFFFFFFFFu;
             wsync();
             for (int q = nm + lane; q < m; q += 64) {
-              const uint32_t j = ML.jb[q];
+              const uint32_t j = (uint32_t)((int)(int16_t)ML.jb[q] + (q & ~7));
               if ((uint32_t)q > j) atomicMin(&F[j], (uint32_t)q);
             }
             wsync();
@@ -786,10 +794,11 @@ __global__ __launch_bounds__(64, PACK_OCC) void pack_bert_wave_kernel(PackParams
             }
           }
           {
-            // identity swaps pad the traced list: jb[0] = 0, jb[q] = q for q in [end, tr8)
+            // identity swaps pad the traced list: jb[0] = 0, jb[q] = q for q in
+            // [end, tr8) (chunk-relative: q & 7)
             const int end = split ? nm : m;
             if (lane == 0) ML.jb[0] = 0;
-            if (end + lane < tr8) ML.jb[end + lane] = (uint16_t)(end + lane);
+            if (end + lane < tr8) ML.jb[end + lane] = (uint16_t)((end + lane) & 7);
             wsync();
             const uint4* jb4 = reinterpret_cast<const uint4*>(ML.jb);
             auto elem = [&](int q) { return split ? (int)ML.jb[nm8 + q] : q; };
@@ -797,16 +806,20 @@ __global__ __launch_bounds__(64, PACK_OCC) void pack_bert_wave_kernel(PackParams
             // pick leave its picks in place, so pass k traces [64k, tr8)
             for (int pb0 = 0; pb0 < nm; pb0 += 64) {
               const int pk = pb0 + lane;
-              int qa = pk;
+              // chunk-relative: d = qa - c against swap (t, j - c), t and the
+              // chunk's j - c as stored: no per-swap index materialisation
+              int d = pk - pb0;
               for (int c = pb0; c < tr8; c += 8) {
                 const uint4 w = jb4[c >> 3];
                 const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
                 for (int t = 0; t < 8; ++t) {
-                  const int i2 = c + t, j = (int)((ww[t >> 1] >> (16 * (t & 1))) & 0xFFFFu);
-                  qa = qa == i2 ? j : (qa == j ? i2 : qa);
+                  const int jc = (t & 1) ? (int)ww[t >> 1] >> 16 : (int)(int16_t)(ww[t >> 1] & 0xFFFFu);
+                  d = d == t ? jc : (d == jc ? t : d);
                 }
+                d -= 8;
               }
+              const int qa = d + tr8;
               const int ea = pk < nm ? elem(qa) : 0;
               wsync();  // (mpos overlaps F: every lane has read its chains)
               if (pk < nm) ML.mpos[pk] = pick_pos(ea);
