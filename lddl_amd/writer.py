@@ -88,7 +88,11 @@ def npy_positions(mlm_off, mlm_pos):
   (header + 2k bytes), built vectorised.  mlm_off: int64[n+1] (from 0),
   mlm_pos: uint16[mlm_off[-1]].  Returns (int64 offsets, uint8 data)."""
   k = np.diff(mlm_off)
-  hdr = {int(v): _npy_header(int(v)) for v in np.unique(k)} if len(k) else {}
+  uk, inv = np.unique(k, return_inverse=True)
+  hdr = [_npy_header(int(v)) for v in uk]
+  if len(k) and len({len(h) for h in hdr}) == 1 and len(hdr[0]) % 2 == 0:
+    return _npy_positions_u16(k, inv, hdr, mlm_pos)
+  hdr = dict(zip((int(v) for v in uk), hdr))
   hlen = np.array([len(hdr[int(v)]) for v in k], dtype=np.int64) if len(k) else np.zeros(0, np.int64)
   sizes = hlen + 2 * k
   off = np.zeros(len(k) + 1, dtype=np.int64)
@@ -103,6 +107,26 @@ def npy_positions(mlm_off, mlm_pos):
     within = np.arange(int(2 * k.sum())) - np.repeat(2 * mlm_off[:-1], 2 * k)
     data[off[rix] + hlen[rix] + within] = np.ascontiguousarray(mlm_pos, dtype='<u2').view(np.uint8)
   return off, data
+
+
+def _npy_positions_u16(k, inv, hdr, mlm_pos):
+  """npy_positions when every row's header has one even length H (np.save
+  pads its v1.0 header to 128 bytes for any 1-D uint16 shape): the column is
+  a u16 stream whose header slots are H/2 values at each row start, filled
+  by two boolean-mask assignments instead of index arrays per byte."""
+  h2 = len(hdr[0]) // 2
+  sizes = h2 + k  # u16 units
+  off16 = np.zeros(len(k) + 1, dtype=np.int64)
+  np.cumsum(sizes, out=off16[1:])
+  data = np.empty(int(off16[-1]), dtype='<u2')
+  is_hdr = np.zeros(int(off16[-1]) + 1, dtype=np.int8)
+  is_hdr[off16[:-1]] += 1  # (starts distinct, ends distinct: each pass has no repeated index)
+  is_hdr[off16[:-1] + h2] -= 1
+  is_hdr = np.cumsum(is_hdr[:-1], dtype=np.int8).view(bool)
+  table = np.stack([np.frombuffer(h.tobytes(), dtype='<u2') for h in hdr])
+  data[is_hdr] = table[inv].ravel()
+  data[~is_hdr] = np.ascontiguousarray(mlm_pos, dtype='<u2')
+  return off16 * 2, data.view(np.uint8)
 
 
 def _arrow(typ, off, data, lo, hi):
