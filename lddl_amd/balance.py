@@ -323,13 +323,28 @@ def rank_world():
   return 0, 1
 
 
-_JOB_ENV = ('SLURM_JOB_ID', 'PMIX_NAMESPACE', 'OMPI_MCA_ess_base_jobid', 'OMPI_MCA_orte_ess_jobid', 'PMI_JOBID')
+# per-launch ids first: SLURM_JOB_ID is shared by every launch inside one
+# allocation (mpirun under salloc often leaves SLURM_STEP_ID unset)
+_JOB_ENV = ('PMIX_NAMESPACE', 'OMPI_MCA_ess_base_jobid', 'OMPI_MCA_orte_ess_jobid', 'PMI_JOBID', 'SLURM_JOB_ID')
 
 
-def barrier_kind(world):
+def _mpi_joins(rank, world):
+  """mpi4py is usable only when its COMM_WORLD is this launch's world: under
+  srun without PMI wiring, or with an mpi4py built against another MPI, every
+  process is a singleton and Barrier() would return at once."""
+  try:
+    from mpi4py import MPI
+    c = MPI.COMM_WORLD
+    return c.Get_size() == world and (rank is None or c.Get_rank() == rank)
+  except Exception:  # ImportError, or an MPI that fails to initialise
+    return False
+
+
+def barrier_kind(world, rank=None):
   """How the ranks of this launch meet (checked BEFORE any shard is written):
   'dist' (torch.distributed already up, or MASTER_ADDR / MASTER_PORT set, as
-  torch.distributed.run sets them), 'mpi4py' (importable under mpirun / srun),
+  torch.distributed.run sets them), 'mpi4py' (importable under mpirun / srun
+  AND its COMM_WORLD has this world's size and rank),
   'file' (a shared-file barrier in the output directory keyed by the
   launcher's job id), or a ValueError: without any of them the reference's
   MPI barrier (load_balance.py:442) has no counterpart here."""
@@ -343,11 +358,8 @@ def barrier_kind(world):
     pass
   if os.environ.get('MASTER_ADDR') and os.environ.get('MASTER_PORT'):
     return 'dist'
-  try:
-    import mpi4py  # noqa: F401
+  if _mpi_joins(rank, world):
     return 'mpi4py'
-  except ImportError:
-    pass
   if job_id():
     return 'file'
   raise ValueError('%d ranks but no way to meet: set MASTER_ADDR / MASTER_PORT (torch.distributed.run), make mpi4py '
@@ -358,8 +370,21 @@ def job_id():
   for k in _JOB_ENV:
     v = os.environ.get(k)
     if v:
-      return '%s-%s' % (v, os.environ.get('SLURM_STEP_ID', ''))
+      return '%s-%s' % (v, os.environ.get('SLURM_STEP_ID', '')) if k == 'SLURM_JOB_ID' else v
   return None
+
+
+def _launch_start():
+  """This process' start time: barrier markers older than it belong to an
+  earlier launch with the same job id (e.g. one that crashed)."""
+  try:
+    import psutil
+    return psutil.Process().create_time()
+  except Exception:
+    return _T_IMPORT
+
+
+_T_IMPORT = time.time()
 
 
 def _file_barrier(outdir, rank, world, timeout=24 * 3600.0, poll=0.05):
@@ -372,8 +397,14 @@ def _file_barrier(outdir, rank, world, timeout=24 * 3600.0, poll=0.05):
     f.write('done\n')
   if rank != 0:
     return
-  t0 = time.time()
-  while not all(os.path.exists(mk(r)) for r in range(world)):
+  t0, start = time.time(), _launch_start() - 2.0
+
+  def fresh(p):
+    try:
+      return os.stat(p).st_mtime >= start
+    except OSError:
+      return False
+  while not all(fresh(mk(r)) for r in range(world)):
     if time.time() - t0 > timeout:
       raise RuntimeError('file barrier: ranks missing after %.0f s' % timeout)
     time.sleep(poll)
@@ -407,7 +438,7 @@ def main(args, rank=None, world=None):
   if rank is None or world is None:
     rank, world = rank_world()
   outdir = args.indir if args.outdir is None else os.path.abspath(os.path.expanduser(args.outdir))
-  kind = barrier_kind(world)  # fail before writing when the ranks cannot meet
+  kind = barrier_kind(world, rank)  # fail before writing when the ranks cannot meet
   os.makedirs(outdir, exist_ok=True)
   paths = sorted(os.path.join(r, f) for r, _, fs in os.walk(args.indir) for f in fs
                  if '.parquet' in os.path.splitext(f)[1])

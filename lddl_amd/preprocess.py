@@ -311,6 +311,26 @@ def load_marker(sink, a, b, key):
   return m
 
 
+def clear_markers(sink, a, b):
+  """Remove every marker whose partition range overlaps [a, b): called before
+  a chunk's files are (re)written, on every run with or without --resume, so
+  no marker -- of this run key, an older one or other chunk bounds -- vouches
+  for files that are about to change (a crash before save_marker then leaves
+  the chunk without a marker)."""
+  d = os.path.join(sink, DONE_DIR)
+  try:
+    names = os.listdir(d)
+  except OSError:
+    return
+  for n in names:
+    m = re.match(r'chunk_(\d+)_(\d+)\.json$', n)
+    if m and int(m.group(1)) < b and a < int(m.group(2)):
+      try:
+        os.remove(os.path.join(d, n))
+      except OSError:
+        pass
+
+
 def save_marker(sink, a, b, key, files, counts, n_pairs):
   """Written after the chunk's files (tmp + rename, so a crash leaves either
   no marker or a whole one)."""
@@ -501,6 +521,7 @@ def main(args, codebert=False):
       t['gpu_s'] += time.perf_counter() - t0
       t0 = time.perf_counter()
       wr = writer.write_txt if args.output_format == 'txt' else writer.write_shards
+      clear_markers(sink, a, b)
       wrote = wr(pk, res, sink, bin_size=args.bin_size, codebert=codebert, masking=args.masking and not codebert,
                  doc_ids=ids, part_base=a)
       out += wrote

@@ -188,3 +188,52 @@ def test_ranks_without_a_meeting_point_fail_before_writing(tmp_path):
     pass
   assert p.returncode != 0 and 'no way to meet' in p.stderr
   assert not outd.exists() or not os.listdir(str(outd))
+
+
+def test_mpi4py_singleton_world_is_not_a_barrier(monkeypatch):
+  """an mpi4py whose COMM_WORLD is a singleton (srun without PMI,
+  another MPI) must not be taken as the launch's barrier"""
+  import sys
+  import types
+
+  class _W:
+    def __init__(self, size, rank):
+      self.s, self.r = size, rank
+
+    def Get_size(self):
+      return self.s
+
+    def Get_rank(self):
+      return self.r
+
+  for k in ('MASTER_ADDR', 'MASTER_PORT') + balance._JOB_ENV:
+    monkeypatch.delenv(k, raising=False)
+  mod, mpi = types.ModuleType('mpi4py'), types.ModuleType('mpi4py.MPI')
+  mod.MPI = mpi
+  monkeypatch.setitem(sys.modules, 'mpi4py', mod)
+  monkeypatch.setitem(sys.modules, 'mpi4py.MPI', mpi)
+  mpi.COMM_WORLD = _W(1, 0)
+  with pytest.raises(ValueError):
+    balance.barrier_kind(2, 1)
+  monkeypatch.setenv('PMIX_NAMESPACE', 'ns7')
+  assert balance.barrier_kind(2, 1) == 'file'
+  mpi.COMM_WORLD = _W(2, 1)
+  assert balance.barrier_kind(2, 1) == 'mpi4py'
+
+
+def test_file_barrier_ignores_markers_of_an_earlier_launch(tmp_path, monkeypatch):
+  """a crashed earlier launch with the same job id left rank 1's
+  marker; rank 0 must not pass the barrier on it"""
+  for k in balance._JOB_ENV:
+    monkeypatch.delenv(k, raising=False)
+  monkeypatch.setenv('SLURM_JOB_ID', '77')
+  monkeypatch.setenv('PMIX_NAMESPACE', 'launch-b')
+  assert balance.job_id() == 'launch-b'  # the per-launch id wins over the allocation's
+  stale = tmp_path / '.lddl_barrier.launch-b.1'
+  stale.write_text('done\n')
+  os.utime(str(stale), (1e9, 1e9))
+  with pytest.raises(RuntimeError):
+    balance._file_barrier(str(tmp_path), 0, 2, timeout=0.3)
+  stale.write_text('done\n')  # a marker of this launch
+  balance._file_barrier(str(tmp_path), 0, 2, timeout=5)
+  assert not [n for n in os.listdir(str(tmp_path)) if n.startswith('.lddl_barrier')]

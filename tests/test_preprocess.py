@@ -277,3 +277,18 @@ def test_resume_markers(tmp_path):
   # an input file that changed changes the key
   (src / 'a.txt').write_text('wiki-1 Hello there, again.\n')
   assert preprocess.run_key(args, False, files, str(vocab), 'rules', 1) != key
+
+
+def test_clear_markers_removes_overlapping_chunks(tmp_path):
+  """a chunk's markers (any run key, any chunk bounds overlapping it) go
+  before its files are rewritten (a stale marker vouched for
+  overwritten files)"""
+  from lddl_amd import preprocess
+  sink = str(tmp_path)
+  for a, b in [(0, 4), (4, 8), (8, 12), (2, 6)]:
+    preprocess.save_marker(sink, a, b, 'k', [], [[0]] * (b - a), 0)
+  preprocess.clear_markers(sink, 4, 8)
+  left = sorted(os.listdir(os.path.join(sink, preprocess.DONE_DIR)))
+  assert left == ['chunk_0_4.json', 'chunk_8_12.json']
+  assert preprocess.load_marker(sink, 0, 4, 'k') is not None
+  preprocess.clear_markers(str(tmp_path / 'nothing'), 0, 1)  # no marker dir: no error

@@ -404,5 +404,12 @@ def test_cli_resume_skips_completed_chunks(gpu, tmp_path):
   files3, t3 = preprocess.main(preprocess.attach_args().parse_args(common))
   assert t3['chunks_skipped'] == 2 and sorted(files3) == sorted(files)
   assert all(open(f, 'rb').read() == blobs[f] for f in files)
+  # a run without --resume and other flags rewrites the part files: the old
+  # markers must not vouch for them afterwards
+  plain = [a for a in common if a != '--resume'] + ['--duplicate-factor', '3']
+  preprocess.main(preprocess.attach_args().parse_args(plain))
+  files5, t5 = preprocess.main(preprocess.attach_args().parse_args(common))
+  assert t5['chunks_skipped'] == 0 and sorted(files5) == sorted(files)
+  assert all(open(f, 'rb').read() == blobs[f] for f in files)
   _, t4 = preprocess.main(preprocess.attach_args().parse_args(common + ['--duplicate-factor', '2']))
   assert t4['chunks_skipped'] == 0
