@@ -178,19 +178,33 @@ def cpu_baseline(args, base, pdo, seconds):
   from oracle import pack_oracle as po
   from lddl_amd.pipeline import VOCAB_BERT, VOCAB_CODEBERT
   code = args.corpus == 'code'
-  threads = min(os.cpu_count() or 1, 16)
+  hc = host_cpus()
+  threads = hc['share']
   ot = OracleTokenizer(VOCAB_CODEBERT if code else VOCAB_BERT)
   # calibrate on ~1 MB, then size the sample to ~seconds of work
   ns = int(np.searchsorted(base.sent_off, base.sent_off[0] + (1 << 20)))
+  # output buffers allocated and touched outside the timed calls (page faults
+  # of a fresh 4-B-per-byte array otherwise serialise the threads)
+  out = (np.zeros(base.nbytes + 16, np.int32), np.zeros(base.n_sent + 1, np.int32))
+  out[0].fill(1)
+  out[1].fill(1)
   t = time.time()
-  ot.run(base.data, base.sent_off[:ns + 1], 512, nthreads=threads)
+  ot.run(base.data, base.sent_off[:ns + 1], 512, nthreads=threads, out=out)
   rate = (base.sent_off[ns] - base.sent_off[0]) / max(1e-6, time.time() - t)
+  # one thread on ~1 s of the same text: the per-core rate and how the
+  # tokenizer scales from 1 to `threads` cores (the box projection's basis)
+  n1 = int(np.searchsorted(base.sent_off, base.sent_off[0] + int(rate / max(1, threads))))
+  n1 = max(1, min(n1, base.n_sent))
+  t = time.time()
+  ot.run(base.data, base.sent_off[:n1 + 1], 512, nthreads=1, out=out)
+  rate1 = float(out[1][:n1].sum()) / max(1e-6, time.time() - t)
   want = min(base.nbytes, int(rate * seconds * 0.7))
   ns = int(np.searchsorted(base.sent_off, base.sent_off[0] + want))
   ns = max(1, min(ns, base.n_sent))
   t = time.time()
-  ids, ntok = ot.run(base.data, base.sent_off[:ns + 1], 512, nthreads=threads)
+  ids, ntok = ot.run(base.data, base.sent_off[:ns + 1], 512, nthreads=threads, out=out)
   tok_s = time.time() - t
+  ntok = ntok[:ns]
   tok_rate = float(ntok.sum()) / tok_s
   # pack+bin (pure-Python restatement, 1 thread) on the first partitions
   t = time.time()
@@ -221,7 +235,20 @@ def cpu_baseline(args, base, pdo, seconds):
   if pack_rate:
     e2e = 1.0 / (1.0 / tok_rate + 1.0 / (pack_rate * threads))
   ref = reference_tokenizer_rate(args, base, min(3.0, seconds * 0.25), threads)
+  eff = tok_rate / (threads * rate1) if rate1 > 0 else None
+  box = hc['affinity'] or threads
+  proj = None
+  if box > threads and eff:
+    # NOT measured: this harness caps a GPU command's worker pools at the box's
+    # CPU share (16 per GPU); the whole box's rate is the measured rate at
+    # `threads` cores scaled linearly to the affinity count
+    proj = {'cores': box, 'tokenize_tokens_per_s': tok_rate * box / threads,
+            'value': (e2e if e2e else tok_rate) * box / threads,
+            'basis': 'measured at %d cores (%.2f of linear from 1 core), scaled linearly to the %d-CPU affinity; '
+                     'not measured (worker pools are capped at the box CPU share)' % (threads, eff, box)}
   return {'value': e2e if e2e else tok_rate, 'unit': 'tokens/s', 'cores': threads, 'kind': 'port',
+          'tokenize_scaling_1_to_%d' % threads: eff, 'tokenize_tokens_per_s_1_core': rate1,
+          'projected_box': proj,
           'reference_library': ref,
           'sample': ('oracle/tokenizer_oracle.c on %d sentences (%.1f MB, %.1f s, %.3g tok/s at %d threads) + '
                      'oracle/pack_oracle.py on %d partitions (%.1f s, %.3g input tok/s/thread); value = '
@@ -229,17 +256,23 @@ def cpu_baseline(args, base, pdo, seconds):
                          ns, (base.sent_off[ns] - base.sent_off[0]) / 1e6, tok_s, tok_rate, threads, p, pack_s,
                          pack_rate or 0, threads)),
           'tokenize_tokens_per_s': tok_rate, 'pack_tokens_per_s_per_thread': pack_rate,
-          'host_cpus': host_cpus()}
+          'host_cpus': hc}
+
+
+CPU_SHARE = 16  # host cores per GPU this harness lets a GPU command's worker pools use
 
 
 def host_cpus():
-  """The box's CPU count and this process's affinity beside the 16-thread cap
-  (the GPU box's CPU share; os.cpu_count() there shows the whole machine)."""
+  """The box's CPU count, this process's affinity and the share the CPU legs
+  run at: min(affinity, LDDL_CPU_SHARE or 16).  The GPU boxes of this harness
+  show the whole machine in os.cpu_count() / the affinity (256) but allot one
+  GPU's command a share of 16 cores for its worker pools."""
   try:
     aff = len(os.sched_getaffinity(0))
   except (AttributeError, OSError):
     aff = None
-  return {'os_cpu_count': os.cpu_count(), 'affinity': aff, 'cap': 16}
+  share = int(os.environ.get('LDDL_CPU_SHARE', CPU_SHARE))
+  return {'os_cpu_count': os.cpu_count(), 'affinity': aff, 'share': max(1, min(aff or share, share))}
 
 
 def sample_partition_check(args, pk, res, base, pdo, reps, seed0):
@@ -283,7 +316,7 @@ def sample_partition_check(args, pk, res, base, pdo, reps, seed0):
                base.doc_sent_off[d0:d1 + 1] - s0,
                None if base.doc_nseg_doc is None else base.doc_nseg_doc[d0:d1])
   oids, ontok = OracleTokenizer(pk.tok.vocab_file).run(sub.data, sub.sent_off, 512,
-                                                        nthreads=min(os.cpu_count() or 1, 16))
+                                                        nthreads=host_cpus()['share'])
   nbins = args.target_seq_length // args.bin_size
   if code:
     docs, nd = _code_docs(sub, oids, ontok, 0, d1 - d0)

@@ -153,13 +153,30 @@ class Packer:
       self._out[name] = t
     return t
 
+  @staticmethod
+  def ids_estimate(nbytes):
+    """ids buffer entries for a corpus of nbytes: WordPiece averages
+    0.23 (Wikipedia-style) to 0.26 (code) tokens per byte; a denser input
+    re-runs with the exact total (tokenize).  #tokens <= #bytes always."""
+    return min(nbytes, nbytes * 3 // 8 + (1 << 16))
+
   def tokenize(self, shards, max_tok=512, stream=None):
-    """-> (ids, ntok, tok_off): the dense CSR ids (lddl_tokenize)"""
-    ids = self._buf('ids', shards.nbytes + 16, torch.int16)
+    """-> (ids, ntok, tok_off): the dense CSR ids (lddl_tokenize).  The ids
+    buffer is sized by ids_estimate, not by the byte count (20 GB of corpus:
+    ~8 GB instead of 43 GB); the total is read back (one stream sync) and a
+    corpus with more tokens runs again into a buffer of exactly its size."""
+    from .tokenizer import CapacityError
     ntok = self._buf('ntok', shards.n_sent, torch.int32)
     toff = self._buf('tok_off_in', shards.n_sent + 1, torch.int64)
-    return self.tok.tokenize_device(shards.data, shards.sent_off, max_tok, ids, ntok, toff, stream,
-                                    nbytes=shards.nbytes)
+    cap = self.ids_estimate(shards.nbytes)
+    for _ in range(2):
+      ids = self._buf('ids', cap + 16, torch.int16)
+      try:
+        return self.tok.tokenize_device(shards.data, shards.sent_off, max_tok, ids, ntok, toff, stream,
+                                        nbytes=shards.nbytes)
+      except CapacityError as e:
+        cap = e.total
+    raise RuntimeError('lddl_amd: tokenize did not fit its exact total')
 
   def pack(self, shards, ids, ntok, tok_off=None, target_seq_length=128, short_seq_prob=0.1, duplicate_factor=5,
            seed=12345, bin_size=None, codebert=False, masking=False, masked_lm_ratio=0.15, stream=None):

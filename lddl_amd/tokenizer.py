@@ -13,6 +13,8 @@ import torch
 
 from . import _lib
 
+TOKENS_MAX = 65534  # lddl_tokenize's max_tok bound (u16 per-sentence counts)
+
 
 def _ptr(t):
   return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
@@ -21,6 +23,14 @@ def _ptr(t):
 def _stream(stream=None):
   s = stream if stream is not None else torch.cuda.current_stream()
   return ctypes.c_void_p(s.cuda_stream)
+
+
+class CapacityError(RuntimeError):
+  """lddl_tokenize's ids did not fit out_cap (LDDL_ECAPACITY): .total ids needed"""
+
+  def __init__(self, total, cap):
+    super().__init__('lddl_amd: %d token ids do not fit the %d-entry ids buffer' % (total, cap))
+    self.total, self.cap = total, cap
 
 
 class Tokenizer:
@@ -70,8 +80,10 @@ class Tokenizer:
     [n_sent] = their counts, tok_off int64 [n_sent+1].  nbytes = sent_off[-1]
     - sent_off[0] (default: data.numel(), i.e. data holds no padding).  The
     default ids buffer holds nbytes + 16 entries (#tokens <= #bytes, plus the
-    16-entry pad lddl_materialize reads); a smaller out_ids must be checked
-    by the caller against tok_off[n_sent] (lddl_tokenize out_cap)."""
+    16-entry pad lddl_materialize reads).  With a smaller out_ids the total
+    tok_off[n_sent] is read back (one stream sync) and a total past its
+    capacity raises (lddl_tokenize writes no id past out_cap): the caller
+    grows the buffer and calls again (Packer.tokenize does)."""
     n_sent = sent_off.numel() - 1
     if nbytes is None:
       nbytes = int(data.numel())
@@ -86,7 +98,17 @@ class Tokenizer:
     cap = max(0, out_ids.numel() - 16)
     _lib.check(_lib.lib().lddl_tokenize(self._h, _ptr(data), nbytes, _ptr(sent_off), n_sent, max_tok,
                                         _ptr(out_ids), cap, _ptr(out_ntok), _ptr(out_tok_off), _stream(stream)))
+    if cap < nbytes:
+      total = self.total_tokens(out_tok_off, n_sent, stream)
+      if total > cap:
+        raise CapacityError(total, cap)
     return out_ids, out_ntok, out_tok_off
+
+  @staticmethod
+  def total_tokens(tok_off, n_sent, stream=None):
+    """tok_off[n_sent] read back after the work queued on `stream`"""
+    (stream if stream is not None else torch.cuda.current_stream()).synchronize()
+    return int(tok_off[n_sent].item())
 
   def set_special_flags(self, on=True):
     """following tokenize calls record per-sentence [CLS]/[SEP] flags for a
@@ -124,7 +146,12 @@ class Tokenizer:
   def tokenize(self, text, max_length=512, truncation=True, **kwargs):
     """Same result as BertTokenizerFast.tokenize as called at pretrain.py:79-80
     under transformers 4.16.2 (per-sentence truncation to max_length)."""
-    ids = self.encode_batch([text], max_length if truncation else 65534)[0]
+    cap = max_length if truncation else TOKENS_MAX
+    ids = self.encode_batch([text], cap)[0]
+    if not truncation and len(ids) >= TOKENS_MAX:
+      # the device path counts tokens per sentence in 16 bits: a text this
+      # long cannot be returned whole (BertTokenizerFast would)
+      raise ValueError('lddl_amd: text reaches %d tokens; truncation=False cannot return it whole' % TOKENS_MAX)
     return [self.ids_to_tokens[i] for i in ids]
 
   def convert_tokens_to_ids(self, tokens):

@@ -49,13 +49,20 @@ class OracleTokenizer:
       lib().orc_tok_destroy(self.h)
       self.h = None
 
-  def run(self, data, sent_off, max_tok=512, nthreads=1):
-    """Sparse output like the HIP path: (ids int32[nbytes], ntok int32[n_sent])."""
+  def run(self, data, sent_off, max_tok=512, nthreads=1, out=None):
+    """Sparse output like the HIP path: (ids int32[nbytes], ntok int32[n_sent]).
+    out: preallocated (ids, ntok) of at least those sizes (a timing caller
+    touches them first, so page faults stay out of the timed call)."""
     data = np.ascontiguousarray(data, dtype=np.uint8)
     sent_off = np.ascontiguousarray(sent_off, dtype=np.int64)
     n = len(sent_off) - 1
-    ids = np.zeros(max(1, int(sent_off[-1] - sent_off[0])), dtype=np.int32)
-    ntok = np.zeros(max(1, n), dtype=np.int32)
+    if out is None:
+      ids = np.zeros(max(1, int(sent_off[-1] - sent_off[0])), dtype=np.int32)
+      ntok = np.zeros(max(1, n), dtype=np.int32)
+    else:
+      ids, ntok = out
+      assert ids.dtype == np.int32 and ntok.dtype == np.int32 and ids.flags.c_contiguous
+      assert len(ids) >= int(sent_off[-1] - sent_off[0]) and len(ntok) >= n
     lib().orc_tok_run(self.h, data.ctypes.data, sent_off.ctypes.data, n, max_tok, ids.ctypes.data,
                       ntok.ctypes.data, nthreads)
     return ids, ntok[:n]

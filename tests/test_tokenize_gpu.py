@@ -194,3 +194,41 @@ def test_repeated_calls_reuse_scratch(gpu):
     starts = b.sent_off[:-1] - b.sent_off[0]
     idx = np.repeat(starts, ntok) + (np.arange(ntok.sum()) - np.repeat(np.cumsum(ntok) - ntok, ntok))
     assert np.array_equal(ids[idx].astype(np.int64), oids[idx].astype(np.int64))
+
+
+def test_packer_ids_buffer_grows_past_the_estimate(gpu):
+  """Packer.tokenize sizes ids by Packer.ids_estimate (not the byte count);
+  a corpus with more tokens than that (punctuation: one token per byte) is
+  re-run into a buffer of its exact total, with the same ids as the oracle;
+  a caller buffer that is too small raises CapacityError"""
+  from lddl_amd.pipeline import Packer, ShardSet
+  from lddl_amd.tokenizer import CapacityError
+  sents = [('!' * 400) if k % 5 else 'Hello, world!! a b c.' for k in range(2500)]
+  enc = [s.encode() for s in sents]
+  off = np.zeros(len(enc) + 1, np.int64)
+  np.cumsum([len(b) for b in enc], out=off[1:])
+  data = np.frombuffer(b''.join(enc), np.uint8)
+  pk = Packer(VOCABS['bert'])
+  assert pk.ids_estimate(len(data)) < len(data) // 2
+  d = torch.from_numpy(np.concatenate([data, np.zeros(16, np.uint8)])).cuda()
+  o = torch.from_numpy(off).cuda()
+  sh = ShardSet(d, o, torch.tensor([0, len(enc)], dtype=torch.int64).cuda(),
+                torch.tensor([0, 1], dtype=torch.int64).cuda(), nbytes=len(data))
+  ids, ntok, toff = pk.tokenize(sh)
+  total = int(toff[len(enc)].item())
+  assert total > pk.ids_estimate(len(data)) and ids.numel() >= total + 16
+  oids, ontok = OracleTokenizer(VOCABS['bert']).run(data, off, 512, nthreads=4)
+  assert np.array_equal(ntok.cpu().numpy()[:len(enc)], ontok)
+  got = ids.cpu().numpy().view(np.uint16)[:total].astype(np.int64)
+  assert np.array_equal(got, np.concatenate(compact(oids, ontok, off)).astype(np.int64))
+  small = torch.empty(1000 + 16, dtype=torch.int16, device='cuda')
+  with pytest.raises(CapacityError):
+    pk.tok.tokenize_device(d, o, 512, out_ids=small, nbytes=len(data))
+
+
+def test_tokenize_without_truncation_refuses_what_it_cannot_return(gpu):
+  from lddl_amd.tokenizer import Tokenizer, TOKENS_MAX
+  tok = Tokenizer(VOCABS['bert'])
+  assert len(tok.tokenize('! ' * 600, truncation=False)) == 600
+  with pytest.raises(ValueError):
+    tok.tokenize('!' * (TOKENS_MAX + 10), truncation=False)
