@@ -50,6 +50,10 @@ def parse():
   ap.add_argument('--partition-mb', type=float, default=1.0, help='bytes per partition (--block-size)')
   ap.add_argument('--seed', type=int, default=12345)
   ap.add_argument('--masking', action='store_true', help='static masking (--masking of the reference)')
+  ap.add_argument('--rows', choices=('spans', 'materialize'), default='spans',
+                  help='the step\'s row output: spans of the dense ids (lddl_row_spans, what the writer renders '
+                       'from; with --masking + lddl_masked_lm_spans) or materialised token rows (lddl_materialize '
+                       '[+ lddl_masked_lm])')
   ap.add_argument('--no-cpu-baseline', action='store_true')
   ap.add_argument('--no-sample-check', action='store_true',
                   help='skip the oracle comparison of one full-size partition after the timed steps')
@@ -291,10 +295,25 @@ def sample_partition_check(args, pk, res, base, pdo, reps, seed0):
   bc = res.bin_count.cpu().numpy()
   g0, n = int(bc[:p].sum()), int(bc[p].sum())
   off = res.tok_off[g0:g0 + n + 1].cpu().numpy()
-  tok = res.tokens[int(off[0]):int(off[-1])].cpu().numpy().view(np.uint16).astype(np.int64)
   l0 = res.len0[g0:g0 + n].cpu().numpy().view(np.uint16).astype(np.int64)
   l1 = res.len1[g0:g0 + n].cpu().numpy().view(np.uint16).astype(np.int64)
   fl = res.flags[g0:g0 + n].cpu().numpy()
+  if res.spans:  # the rows rebuilt from the spans over the dense ids
+    s0 = res.src0[g0:g0 + n].cpu().numpy()
+    s1 = res.src1[g0:g0 + n].cpu().numpy()
+    lo, hi = int(min(s0.min(), s1.min())), int(max((s0 + l0).max(), (s1 + l1).max()))
+    ids = res.ids[lo:hi].cpu().numpy().view(np.uint16).astype(np.int64)
+    rws = [np.concatenate([[res.cls_id], ids[s0[g] - lo:s0[g] - lo + l0[g]], [res.sep_id] if fl[g] & 2 else [],
+                           ids[s1[g] - lo:s1[g] - lo + l1[g]], [res.sep_id]]).astype(np.int64) for g in range(n)]
+    if res.mlm_token is not None:  # the masked rows show mlm_token at mlm_pos
+      mo = res.mlm_off[g0:g0 + n + 1].cpu().numpy()
+      mp = res.mlm_pos[int(mo[0]):int(mo[-1])].cpu().numpy().view(np.uint16).astype(np.int64)
+      mt = res.mlm_token[int(mo[0]):int(mo[-1])].cpu().numpy().view(np.uint16).astype(np.int64)
+      for g in range(n):
+        rws[g][mp[mo[g] - mo[0]:mo[g + 1] - mo[0]]] = mt[mo[g] - mo[0]:mo[g + 1] - mo[0]]
+    tok = np.concatenate(rws)
+  else:
+    tok = res.tokens[int(off[0]):int(off[-1])].cpu().numpy().view(np.uint16).astype(np.int64)
   pt = res.part[g0:g0 + n].cpu().numpy()
   if res.mlm_off is not None:
     moff = res.mlm_off[g0:g0 + n + 1].cpu().numpy()
@@ -399,7 +418,8 @@ def frontend_leg(mb):
     raw = os.path.getsize(os.path.join(d, 'wiki', 'en', 'a.txt'))
     a = preprocess.attach_args().parse_args(
         ['--wikipedia', os.path.join(d, 'wiki'), '--sentence-splitter', 'rules', '--sink', os.path.join(d, 'out'),
-         '--target-seq-length', '128', '--block-size', str(1 << 20), '--chunk-mb', '16', '--seed', '7'])
+         '--target-seq-length', '128', '--block-size', str(1 << 20), '--chunk-mb', '4', '--seed', '7',
+         '--split-workers', str(host_cpus()['share'])])
     t0 = time.perf_counter()
     files, t = preprocess.main(a)
     el = time.perf_counter() - t0
@@ -494,7 +514,8 @@ def main():
   pk = Packer(VOCAB_CODEBERT if code else VOCAB_BERT, device=local, masking=args.masking)
   pk.tok.set_timing(True)  # per-kernel HIP events inside the tokenize call (the roofline's kernel time)
   kw = dict(target_seq_length=args.target_seq_length, short_seq_prob=0.1, duplicate_factor=args.duplicate_factor,
-            seed=args.seed + rank * 10_000_000, bin_size=args.bin_size, masking=args.masking, codebert=code)
+            seed=args.seed + rank * 10_000_000, bin_size=args.bin_size, masking=args.masking, codebert=code,
+            spans=args.rows == 'spans')
   tok_ms = []
   gathered = []
 
@@ -589,7 +610,9 @@ def main():
                  'partitions_per_gpu': sh.n_part, 'wordpiece_tokens_per_gpu': n_tok,
                  'pairs_per_gpu': res.n_pairs, 'packed_tokens_per_gpu': res.n_tokens,
                  'masked_positions_per_gpu': res.n_masked,
-                 'parallelism': 'shard%d' % world, 'gathered_partitions': n_gathered},
+                 'parallelism': 'shard%d' % world, 'gathered_partitions': n_gathered,
+                 # the step's row output: spans of the dense ids (what the writer renders from) or materialised rows
+                 'rows': 'spans' if res.spans else 'materialize'},
       'roofline': {'bound': 'hbm', 'kernel': 'lddl::tok5::scan_kernel', 'achieved': achieved, 'peak': HBM_PEAK_GBS,
                    'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS, 'traffic': None,
                    'algorithmic_bytes_per_launch': alg, 'avg_launch_ms': ks['scan_ms'] / nl,

@@ -135,6 +135,22 @@ int lddl_materialize(lddl_ctx *ctx, const uint16_t *d_ids, uint16_t *d_out_token
                      uint16_t *d_out_len0, uint16_t *d_out_len1, uint8_t *d_out_flags, uint8_t *d_out_bin,
                      int64_t *d_out_part, int64_t *d_bin_count, void *stream);
 
+/* The rows of the last pack call as SPANS of the dense ids, in
+ * lddl_materialize's row order, without copying a token: each segment of a
+ * row is one contiguous run of lddl_tokenize's d_out_ids (a document's
+ * sentences are contiguous there and a segment is a window of consecutive
+ * sentences), so row g = [CLS] ids[src0[g], src0[g] + len0[g]) [SEP]
+ * ids[src1[g], src1[g] + len1[g]) [SEP] (CodeBERT: the [SEP] after segment 0
+ * only when flags bit1) -- the same rows as lddl_materialize (binning.py:63-93,
+ * pretrain.py:348-353) for consumers that read the ids through the spans
+ * (lddl_render_strings RENDER_SPAN: the parquet writer's string columns).
+ * len0/len1/flags/bin/part/bin_count as lddl_materialize; d_out_tok_off
+ * (optional, NULL = not written) = the materialised layout's row offsets.
+ * The dense ids must stay live while the spans are read. */
+int lddl_row_spans(lddl_ctx *ctx, int64_t *d_out_src0, int64_t *d_out_src1, int64_t *d_out_tok_off,
+                   uint16_t *d_out_len0, uint16_t *d_out_len1, uint8_t *d_out_flags, uint8_t *d_out_bin,
+                   int64_t *d_out_part, int64_t *d_bin_count, void *stream);
+
 /* After lddl_pack_bert(masking=1) + lddl_materialize: apply the masking to
  * the materialised rows in place (A/B become output_tokens[1:1+len(A)] /
  * [2+len(A):...], pretrain.py:232-233) and write, per row g,
@@ -146,6 +162,19 @@ int lddl_materialize(lddl_ctx *ctx, const uint16_t *d_ids, uint16_t *d_out_token
 int lddl_masked_lm(lddl_ctx *ctx, int64_t *d_out_mlm_off, uint16_t *d_out_mlm_pos, uint16_t *d_out_mlm_label,
                    void *stream);
 
+/* After lddl_pack_bert(masking=1) + lddl_row_spans (no rows materialised):
+ * the static masking of the rows the spans describe.  Per row g,
+ * d_out_mlm_off / _pos / _label exactly as lddl_masked_lm, and
+ * d_out_mlm_token[k] = the token the masked row shows at position
+ * d_out_mlm_pos[k] (the replacement id, or the label when the 10 % "keep"
+ * branch left it, pretrain.py:212-225) -- what lddl_render_masked puts into
+ * the A / B strings.  d_ids = the dense ids; d_src0 / d_src1 / d_len0 /
+ * d_part = that lddl_row_spans call's outputs. */
+int lddl_masked_lm_spans(lddl_ctx *ctx, const uint16_t *d_ids, const int64_t *d_src0, const int64_t *d_src1,
+                         const uint16_t *d_len0, const int64_t *d_part, int64_t *d_out_mlm_off,
+                         uint16_t *d_out_mlm_pos, uint16_t *d_out_mlm_label, uint16_t *d_out_mlm_token,
+                         void *stream);
+
 /* Render one string column of rows [row0, row0 + n_rows) as Arrow string
  * data: d_out_off[0..n_rows] (int64, d_out_off[0] = 0) and the UTF-8 bytes of
  * ' '.join(vocab[t] for t in segment) per row -- the reference's
@@ -154,7 +183,10 @@ int lddl_masked_lm(lddl_ctx *ctx, int64_t *d_out_mlm_off, uint16_t *d_out_mlm_po
  * writes as pa.string() (pretrain.py:457-471).  segment: 0 = first segment
  * (A / doc: row tokens [1, 1 + len0)), 1 = second (B / code, after the [SEP];
  * codebert != 0: a [SEP] follows the doc segment only when flags bit1),
- * 2 = the whole row (d_row_off only; masked_lm labels from lddl_masked_lm).
+ * 2 = the whole row (d_row_off only; masked_lm labels from lddl_masked_lm),
+ * 3 = a span (lddl_row_spans): row r = d_tokens[d_row_off[r], d_row_off[r] +
+ * d_len0[r]) with d_tokens = the dense ids, d_row_off = src0 or src1, d_len0 =
+ * len0 or len1 (d_row_off then has n rows, not n + 1 offsets).
  * Two-phase: *out_nbytes receives the byte count (the stream is synchronised
  * once); with d_out_bytes == NULL that is all (size query), else out_cap
  * must be >= it (LDDL_ECAPACITY) and the bytes are written asynchronously. */
@@ -162,6 +194,18 @@ int lddl_render_strings(lddl_ctx *ctx, const uint16_t *d_tokens, const int64_t *
                         const uint16_t *d_len1, const uint8_t *d_flags, int64_t row0, int64_t n_rows,
                         int32_t segment, int32_t codebert, int64_t *d_out_off, uint8_t *d_out_bytes,
                         int64_t out_cap, int64_t *out_nbytes, void *stream);
+
+/* The masked rows' A (segment 0) or B (segment 1) strings from the spans:
+ * lddl_render_strings' span rendering (d_src / d_len = src0 / len0 or src1 /
+ * len1 of lddl_row_spans over d_ids) where a row position listed in
+ * d_mlm_pos[d_mlm_off[r] .. d_mlm_off[r+1]) shows d_mlm_token instead
+ * (lddl_masked_lm_spans; A's token k sits at row position 1 + k, B's at
+ * len0 + 2 + k): the 'A' / 'B' of pretrain.py:232-233, 348-353 with --masking.
+ * Same two-phase size query / capacity rules as lddl_render_strings. */
+int lddl_render_masked(lddl_ctx *ctx, const uint16_t *d_ids, const int64_t *d_src, const uint16_t *d_len,
+                       const uint16_t *d_len0, int32_t segment, const int64_t *d_mlm_off, const uint16_t *d_mlm_pos,
+                       const uint16_t *d_mlm_token, int64_t row0, int64_t n_rows, int64_t *d_out_off,
+                       uint8_t *d_out_bytes, int64_t out_cap, int64_t *out_nbytes, void *stream);
 
 /* Document index (into the corpus' documents) of every row of the last pack
  * call, in lddl_materialize's row order: the row's own document (seg0's; a

@@ -38,7 +38,13 @@ SIGNATURES = {
                                    ctypes.POINTER(c_int64), c_void_p]),
     'lddl_materialize': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                  c_void_p, c_void_p, c_void_p, c_void_p]),
+    'lddl_row_spans': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                               c_void_p, c_void_p, c_void_p]),
     'lddl_masked_lm': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    'lddl_masked_lm_spans': (c_int, [c_void_p] * 11),
+    'lddl_render_masked': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_void_p,
+                                   c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_int64, ctypes.POINTER(c_int64),
+                                   c_void_p]),
     'lddl_render_strings': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64,
                                     c_int32, c_int32, c_void_p, c_void_p, c_int64, ctypes.POINTER(c_int64),
                                     c_void_p]),

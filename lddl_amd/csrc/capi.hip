@@ -335,6 +335,7 @@ extern "C" int lddl_tokenize(lddl_ctx* c, const uint8_t* d_bytes, int64_t nbytes
   if ((rc = ws_get(c, 19, nt + 1, &tile_sent)) || (rc = ws_get(c, 20, nt, &S.fb_list)) ||
       (rc = ws_get(c, 21, 16, &S.fb_count)) || (rc = ws_get(c, 34, (size_t)seg * 1024 + 4096, &S.ent)) ||
       (rc = ws_get(c, 35, (size_t)slots * 4, &S.rec)) || (rc = ws_get(c, 42, (size_t)slots * 4, &S.pcs)) ||
+      (rc = ws_get(c, 47, (size_t)slots, &S.pch)) ||
       (rc = ws_get(c, 36, (size_t)n_chunks + 16, &S.chunk_fill)) || (rc = ws_get(c, 37, n_sent, &S.smeta)) ||
       (rc = ws_get(c, 43, n_sent, &S.snslot)) || (rc = ws_get(c, 44, (size_t)slots, &S.cnt8)) ||
       (rc = ws_get(c, 45, (size_t)scan_blocks(n_sent) + 1, &S.scan_bsum)))
@@ -360,7 +361,7 @@ extern "C" int lddl_tokenize(lddl_ctx* c, const uint8_t* d_bytes, int64_t nbytes
                                   c->timing ? c->tm : nullptr));
   }
   if (P.dbg) {
-    uint64_t h[20];
+    uint64_t h[24];
     HIP_TRY(hipMemcpyAsync(h, P.dbg, sizeof h, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     const char* nm[12] = {"loop", "setup", "classify", "except", "units", "urec", "prep", "probe", "records",
@@ -369,7 +370,8 @@ extern "C" int lddl_tokenize(lddl_ctx* c, const uint8_t* d_bytes, int64_t nbytes
     for (int k = 0; k < 12; ++k) fprintf(stderr, " %s=%llu", nm[k], (unsigned long long)h[k]);
     const char* wn[6] = {"wp_A", "wp_B", "wp_C", "wp_D", "wp_steps", "wp_lane_steps"};
     for (int k = 0; k < 6; ++k) fprintf(stderr, " %s=%llu", wn[k], (unsigned long long)h[12 + k]);
-    fprintf(stderr, " prep_decode=%llu prep_dirty=%llu", (unsigned long long)h[18], (unsigned long long)h[19]);
+    fprintf(stderr, " prep_decode=%llu prep_dirty=%llu x_list=%llu x_load=%llu x_apply=%llu", (unsigned long long)h[18],
+            (unsigned long long)h[19], (unsigned long long)h[20], (unsigned long long)h[21], (unsigned long long)h[22]);
     fprintf(stderr, "\n");
   }
   return 0;
@@ -618,22 +620,10 @@ extern "C" int lddl_pack_codebert(lddl_ctx* c, const int32_t* d_ntok, const int6
                      n_part, target_seq_length, short_seq_prob, duplicate_factor, seed, bin_size, out_totals, stream);
 }
 
-extern "C" int lddl_materialize(lddl_ctx* c, const uint16_t* d_ids, uint16_t* d_out_tokens, int64_t* d_out_tok_off,
-                                uint16_t* d_out_len0, uint16_t* d_out_len1, uint8_t* d_out_flags, uint8_t* d_out_bin,
-                                int64_t* d_out_part, int64_t* d_bin_count, void* stream) {
-  if (!c) return set_err(LDDL_EINVAL, "null ctx");
-  if (c->last_npairs < 0) return set_err(LDDL_EINVAL, "no successful lddl_pack_* call to materialise");
-  if (!d_ids || !d_out_tokens || !d_out_tok_off || !d_out_len0 || !d_out_len1 || !d_out_flags || !d_out_bin ||
-      !d_out_part)
-    return set_err(LDDL_EINVAL, "null pointer");
-  HIP_TRY(hipSetDevice(c->device));
-  hipStream_t st = (hipStream_t)stream;
+// MatParams of the last pack call (lddl_materialize / lddl_row_spans)
+static MatParams mat_params(lddl_ctx* c) {
   const PackParams& P = c->pp;
   MatParams M{};
-  // LDDL_MAT_ALGO=1: the wave-per-partition materialize kernel (also taken
-  // for unaligned buffers); otherwise the chunked v2 kernel
-  const int mat_algo = getenv("LDDL_MAT_ALGO") ? atoi(getenv("LDDL_MAT_ALGO")) : 2;
-  M.dense = d_ids;
   M.fs_dense = P.fs_dense;
   M.sent_off = P.sent_off;
   M.doc_sent_off = P.doc_sent_off;
@@ -653,6 +643,25 @@ extern "C" int lddl_materialize(lddl_ctx* c, const uint16_t* d_ids, uint16_t* d_
   M.cls_id = c->special[2];
   M.sep_id = c->special[3];
   M.codebert = c->pack_codebert;
+  return M;
+}
+
+extern "C" int lddl_materialize(lddl_ctx* c, const uint16_t* d_ids, uint16_t* d_out_tokens, int64_t* d_out_tok_off,
+                                uint16_t* d_out_len0, uint16_t* d_out_len1, uint8_t* d_out_flags, uint8_t* d_out_bin,
+                                int64_t* d_out_part, int64_t* d_bin_count, void* stream) {
+  if (!c) return set_err(LDDL_EINVAL, "null ctx");
+  if (c->last_npairs < 0) return set_err(LDDL_EINVAL, "no successful lddl_pack_* call to materialise");
+  if (!d_ids || !d_out_tokens || !d_out_tok_off || !d_out_len0 || !d_out_len1 || !d_out_flags || !d_out_bin ||
+      !d_out_part)
+    return set_err(LDDL_EINVAL, "null pointer");
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t st = (hipStream_t)stream;
+  const PackParams& P = c->pp;
+  // LDDL_MAT_ALGO=1: the wave-per-partition materialize kernel (also taken
+  // for unaligned buffers); otherwise the chunked v2 kernel
+  const int mat_algo = getenv("LDDL_MAT_ALGO") ? atoi(getenv("LDDL_MAT_ALGO")) : 2;
+  MatParams M = mat_params(c);
+  M.dense = d_ids;
   M.out_tokens = d_out_tokens;
   M.out_tok_off = d_out_tok_off;
   M.out_len0 = d_out_len0;
@@ -670,6 +679,35 @@ extern "C" int lddl_materialize(lddl_ctx* c, const uint16_t* d_ids, uint16_t* d_
   c->last_tokens = d_out_tokens;
   c->last_tok_off = d_out_tok_off;
   c->last_part = d_out_part;
+  return 0;
+}
+
+extern "C" int lddl_row_spans(lddl_ctx* c, int64_t* d_out_src0, int64_t* d_out_src1, int64_t* d_out_tok_off,
+                              uint16_t* d_out_len0, uint16_t* d_out_len1, uint8_t* d_out_flags, uint8_t* d_out_bin,
+                              int64_t* d_out_part, int64_t* d_bin_count, void* stream) {
+  if (!c) return set_err(LDDL_EINVAL, "null ctx");
+  if (c->last_npairs < 0) return set_err(LDDL_EINVAL, "no successful lddl_pack_* call");
+  if (!d_out_src0 || !d_out_src1 || !d_out_len0 || !d_out_len1 || !d_out_flags || !d_out_bin || !d_out_part)
+    return set_err(LDDL_EINVAL, "null pointer");
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t st = (hipStream_t)stream;
+  const PackParams& P = c->pp;
+  MatParams M = mat_params(c);
+  M.out_src0 = d_out_src0;
+  M.out_src1 = d_out_src1;
+  M.out_tok_off = d_out_tok_off;
+  M.out_len0 = d_out_len0;
+  M.out_len1 = d_out_len1;
+  M.out_flags = d_out_flags;
+  M.out_bin = d_out_bin;
+  M.out_part = d_out_part;
+  if (c->last_npairs == 0) {
+    if (d_out_tok_off) HIP_TRY(hipMemsetAsync(d_out_tok_off, 0, 8, st));
+  } else {
+    HIP_TRY(launch_row_spans(M, c->last_npairs, st));
+  }
+  if (d_bin_count)
+    HIP_TRY(hipMemcpyAsync(d_bin_count, P.bin_count, (size_t)P.n_part * P.nbins * 8, hipMemcpyDeviceToDevice, st));
   return 0;
 }
 
@@ -709,6 +747,47 @@ extern "C" int lddl_masked_lm(lddl_ctx* c, int64_t* d_out_mlm_off, uint16_t* d_o
   return 0;
 }
 
+extern "C" int lddl_masked_lm_spans(lddl_ctx* c, const uint16_t* d_ids, const int64_t* d_src0,
+                                    const int64_t* d_src1, const uint16_t* d_len0, const int64_t* d_part,
+                                    int64_t* d_out_mlm_off, uint16_t* d_out_mlm_pos, uint16_t* d_out_mlm_label,
+                                    uint16_t* d_out_mlm_token, void* stream) {
+  if (!c) return set_err(LDDL_EINVAL, "null ctx");
+  if (c->last_npairs < 0 || c->last_nmask < 0)
+    return set_err(LDDL_EINVAL, "lddl_masked_lm_spans needs lddl_pack_bert(masking=1) then lddl_row_spans");
+  if (!d_out_mlm_off || (c->last_npairs > 0 && (!d_ids || !d_src0 || !d_src1 || !d_len0 || !d_part)) ||
+      (c->last_nmask > 0 && (!d_out_mlm_pos || !d_out_mlm_label || !d_out_mlm_token)))
+    return set_err(LDDL_EINVAL, "null pointer");
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t st = (hipStream_t)stream;
+  const PackParams& P = c->pp;
+  if (c->last_npairs == 0) {
+    HIP_TRY(hipMemsetAsync(d_out_mlm_off, 0, 8, st));
+  } else {
+    MlmParams M{};
+    M.doc_sent_off = P.doc_sent_off;
+    M.part_doc_off = P.part_doc_off;
+    M.pair_base = (const int64_t*)c->ws[15].p;
+    M.binned = P.binned;
+    M.mref = P.mref;
+    M.mloc = P.mloc;
+    M.mask_base = (const int64_t*)c->ws[27].p;
+    M.marena = P.marena;
+    M.n_part = P.n_part;
+    M.dup = P.dup;
+    M.row_part = d_part;
+    M.ids = d_ids;
+    M.src0 = d_src0;
+    M.src1 = d_src1;
+    M.len0 = d_len0;
+    M.out_off = d_out_mlm_off;
+    M.out_pos = d_out_mlm_pos;
+    M.out_label = d_out_mlm_label;
+    M.out_token = d_out_mlm_token;
+    HIP_TRY(launch_masked_lm(M, st));
+  }
+  return 0;
+}
+
 // --------------------------------------------------------------- render --
 extern "C" int lddl_render_strings(lddl_ctx* c, const uint16_t* d_tokens, const int64_t* d_row_off,
                                    const uint16_t* d_len0, const uint16_t* d_len1, const uint8_t* d_flags,
@@ -716,7 +795,7 @@ extern "C" int lddl_render_strings(lddl_ctx* c, const uint16_t* d_tokens, const 
                                    int64_t* d_out_off, uint8_t* d_out_bytes, int64_t out_cap, int64_t* out_nbytes,
                                    void* stream) {
   if (!c) return set_err(LDDL_EINVAL, "null ctx");
-  if (segment < RENDER_SEG0 || segment > RENDER_ROW) return set_err(LDDL_EINVAL, "segment %d not in 0..2", segment);
+  if (segment < RENDER_SEG0 || segment > RENDER_SPAN) return set_err(LDDL_EINVAL, "segment %d not in 0..3", segment);
   if (row0 < 0 || n_rows < 0) return set_err(LDDL_EINVAL, "negative row range");
   if (!d_tokens || !d_row_off || !d_out_off || !out_nbytes) return set_err(LDDL_EINVAL, "null pointer");
   if (segment != RENDER_ROW && (!d_len0 || (segment == RENDER_SEG1 && (!d_len1 || (codebert && !d_flags)))))
@@ -745,6 +824,50 @@ extern "C" int lddl_render_strings(lddl_ctx* c, const uint16_t* d_tokens, const 
   HIP_TRY(hipStreamSynchronize(st));
   *out_nbytes = c->h_tot[6];
   if (!d_out_bytes) return 0;  // size query
+  if (out_cap < c->h_tot[6])
+    return set_err(LDDL_ECAPACITY, "render needs %lld bytes, out_cap %lld", (long long)c->h_tot[6], (long long)out_cap);
+  R.out_off = d_out_off;
+  R.out = d_out_bytes;
+  HIP_TRY(launch_render_bytes(R, c->n_cu, st));
+  return 0;
+}
+
+extern "C" int lddl_render_masked(lddl_ctx* c, const uint16_t* d_ids, const int64_t* d_src, const uint16_t* d_len,
+                                  const uint16_t* d_len0, int32_t segment, const int64_t* d_mlm_off,
+                                  const uint16_t* d_mlm_pos, const uint16_t* d_mlm_token, int64_t row0, int64_t n_rows,
+                                  int64_t* d_out_off, uint8_t* d_out_bytes, int64_t out_cap, int64_t* out_nbytes,
+                                  void* stream) {
+  if (!c) return set_err(LDDL_EINVAL, "null ctx");
+  if (segment != 0 && segment != 1) return set_err(LDDL_EINVAL, "segment %d not 0 / 1", segment);
+  if (row0 < 0 || n_rows < 0) return set_err(LDDL_EINVAL, "negative row range");
+  if (!d_ids || !d_src || !d_len || !d_len0 || !d_mlm_off || !d_mlm_pos || !d_mlm_token || !d_out_off || !out_nbytes)
+    return set_err(LDDL_EINVAL, "null pointer");
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t st = (hipStream_t)stream;
+  RenderParams R{};
+  R.tokens = d_ids;
+  R.row_off = d_src;
+  R.len0 = d_len;
+  R.row0 = row0;
+  R.n_rows = n_rows;
+  R.segment = RENDER_SPAN;
+  R.vinfo = c->d_rinfo;
+  R.vpool = c->d_rpool;
+  R.moff = d_mlm_off;
+  R.mpos = d_mlm_pos;
+  R.mtok = d_mlm_token;
+  R.len0m = d_len0;
+  R.mseg = segment;
+  int64_t* bsum;
+  int rc;
+  if ((rc = ws_get(c, 35, (size_t)n_rows, &R.lens))) return rc;
+  if ((rc = ws_get(c, 36, (size_t)scan_blocks(n_rows) + 1, &bsum))) return rc;
+  HIP_TRY(launch_render_len(R, c->n_cu, st));
+  HIP_TRY(launch_scan_ntok(R.lens, n_rows, d_out_off, bsum, st));
+  HIP_TRY(hipMemcpyAsync(&c->h_tot[6], d_out_off + n_rows, 8, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  *out_nbytes = c->h_tot[6];
+  if (!d_out_bytes) return 0;
   if (out_cap < c->h_tot[6])
     return set_err(LDDL_ECAPACITY, "render needs %lld bytes, out_cap %lld", (long long)c->h_tot[6], (long long)out_cap);
   R.out_off = d_out_off;

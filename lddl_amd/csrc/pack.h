@@ -93,6 +93,12 @@ struct MlmParams {
   int64_t* out_off;             // [n_pairs+1]
   uint16_t* out_pos;            // [n_masked]
   uint16_t* out_label;          // [n_masked]
+  // span mode (tokens == nullptr): the rows as lddl_row_spans described them
+  const uint16_t* ids;          // the dense ids
+  const int64_t* src0;
+  const int64_t* src1;
+  const uint16_t* len0;
+  uint16_t* out_token;          // [n_masked] the token the masked row holds at out_pos
 };
 
 struct MatParams {
@@ -122,6 +128,8 @@ struct MatParams {
   uint8_t* out_flags;           // [n_pairs] bit0 is_random_next, bit1 seg0 present
   uint8_t* out_bin;             // [n_pairs]
   int64_t* out_part;            // [n_pairs] partition id (for ids / file names)
+  int64_t* out_src0;            // lddl_row_spans: [n_pairs] dense-id offset of segment A / doc
+  int64_t* out_src1;            //                 [n_pairs] of segment B / code
 };
 
 hipError_t launch_pack_bert_wave(const PackParams& P, hipStream_t s);
@@ -132,6 +140,8 @@ hipError_t launch_scan_parts(const int64_t* a, const int64_t* b, int64_t n, int6
 // algo 1: wave per partition (u16 copies); otherwise wave per 64 pairs with
 // 16-B stores (needs out_tokens 16-B aligned and dense padded by 16 u16)
 hipError_t launch_materialize(const MatParams& M, int64_t total_pairs, int64_t n_dense, int algo, hipStream_t s);
+// row g's segments as offsets into the dense ids (no token copy); out_tok_off optional
+hipError_t launch_row_spans(const MatParams& M, int64_t total_pairs, hipStream_t s);
 // tokoff[0..n] = exclusive scan of ntok[0..n) (int64); blocksums: scratch of
 // scan_blocks(n) + 1 entries
 __host__ __device__ int64_t scan_blocks(int64_t n);

@@ -359,6 +359,54 @@ __global__ __launch_bounds__(256) void materialize2_kernel(MatParams M, int64_t 
   mat_copy(W, G0, G1, M.dense, n_src, M.out_tokens, M.cls_id, M.sep_id, lane);
 }
 
+// Row spans (lddl_row_spans): the rows of materialize2 without the token
+// copy.  Each segment of a row is ONE contiguous run of the tokenizer's dense
+// ids (a document's sentences are contiguous there and a segment is a window
+// of consecutive sentences), so row g = [CLS] ids[src0, src0 + len0) [SEP]
+// ids[src1, src1 + len1) [SEP] is fully described by two offsets; the string
+// columns (lddl_render_strings, RENDER_SPAN) and the loaders read the ids
+// through them.  Wave per 64 rows, lane per row: the same metadata chain as
+// materialize2 (partition, binned record, pair record, segment starts) and
+// ~38 B written per row instead of the row's 2 B per token.
+__global__ __launch_bounds__(256) void rowspan_kernel(MatParams M, int64_t total) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t gbase = ((int64_t)blockIdx.x * 4 + wv) * 64;
+  if (gbase >= total) return;
+  int64_t plo = 0, phi = M.n_part - 1;
+  while (plo < phi) {
+    const int64_t mid = (plo + phi + 1) >> 1;
+    if (M.pair_base[mid] <= gbase) plo = mid;
+    else phi = mid - 1;
+  }
+  const int64_t g = gbase + lane;
+  if (g >= total) return;
+  int64_t p = plo;
+  while (M.pair_base[p + 1] <= g) ++p;  // partitions of < 64 pairs
+  const int64_t i = g - M.pair_base[p];
+  const int64_t pb = (int64_t)M.dup * M.doc_sent_off[M.part_doc_off[p]];
+  const PairRec r = M.pairs[pb + M.binned[pb + i]];
+  const int32_t l0 = r.hi0 - r.lo0, l1 = r.hi1 - r.lo1;
+  M.out_src0[g] = l0 > 0 ? M.fs_dense[r.fs0] + r.lo0 : 0;
+  M.out_src1[g] = l1 > 0 ? M.fs_dense[r.fs1] + r.lo1 : 0;
+  if (M.out_tok_off) {
+    const int64_t off = M.tok_base[p] + M.tok_local[pb + i];
+    M.out_tok_off[g] = off;
+    if (g == total - 1) M.out_tok_off[total] = off + r.num_tokens;
+  }
+  M.out_len0[g] = (uint16_t)l0;
+  M.out_len1[g] = (uint16_t)l1;
+  M.out_flags[g] = (uint8_t)r.flags;
+  const int32_t b = ((int32_t)r.num_tokens - 1) / M.bin_size;
+  M.out_bin[g] = (uint8_t)(b > M.nbins - 1 ? M.nbins - 1 : b);
+  M.out_part[g] = p;
+}
+
+hipError_t launch_row_spans(const MatParams& M, int64_t total_pairs, hipStream_t s) {
+  const int64_t nblk = (total_pairs + 255) / 256;
+  hipLaunchKernelGGL(rowspan_kernel, dim3((unsigned)nblk), dim3(256), 0, s, M, total_pairs);
+  return hipGetLastError();
+}
+
 // ------------------------------------------------- token offset scans ----
 constexpr int SCAN_ITEMS = 4096;  // ntok entries per scan block (256 x 16)
 
@@ -533,6 +581,41 @@ __global__ __launch_bounds__(256) void masked_lm_kernel(MlmParams M) {
   }
 }
 
+// The same over rows described by spans (lddl_row_spans): no row to mask in
+// place; a masked position's label is read from the dense ids through the
+// row's span (A = positions 1 .. len0, [SEP], B from len0 + 2: candidates
+// never include [CLS] / [SEP], pretrain.py:187-190) and the token the masked
+// row shows there (the replacement, or the label when kept) goes to
+// out_token for the writer (lddl_render_masked).
+__global__ __launch_bounds__(256) void masked_lm_spans_kernel(MlmParams M) {
+  const int sl = threadIdx.x & 15;
+  const int64_t total = M.pair_base[M.n_part];
+  const int64_t ng = (int64_t)gridDim.x * 16;  // row groups of 16 lanes
+  for (int64_t g = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4); g < total; g += ng) {
+    const int64_t p = M.row_part[g];
+    const int64_t i = g - M.pair_base[p];
+    const int64_t pb = (int64_t)M.dup * M.doc_sent_off[M.part_doc_off[p]];
+    const int64_t ref = M.mref[pb + M.binned[pb + i]];
+    const int nm = (int)((uint64_t)ref >> 48);
+    const int64_t aoff = ref & ((int64_t(1) << 48) - 1);
+    const int64_t ooff = M.mask_base[p] + M.mloc[pb + i];
+    const int64_t a = M.src0[g], b = M.src1[g];
+    const int32_t l0 = M.len0[g];
+    if (sl == 0) {
+      M.out_off[g] = ooff;
+      if (g == total - 1) M.out_off[total] = ooff + nm;
+    }
+    for (int k = sl; k < nm; k += 16) {
+      const uint32_t e = M.marena[aoff + k];
+      const uint32_t pos = e & 0xFFFFu, nid = e >> 16;
+      const uint16_t label = M.ids[(int32_t)pos <= l0 ? a + (pos - 1) : b + ((int32_t)pos - l0 - 2)];
+      M.out_pos[ooff + k] = (uint16_t)pos;
+      M.out_label[ooff + k] = label;
+      M.out_token[ooff + k] = nid != MLM_KEEP ? (uint16_t)nid : label;
+    }
+  }
+}
+
 hipError_t launch_sent_special(const uint16_t* ids, const int64_t* tok_off, const int32_t* ntok, int64_t n_sent,
                                uint32_t cls, uint32_t sep, uint8_t* out, hipStream_t s) {
   hipLaunchKernelGGL(sent_special_kernel, dim3(4096), dim3(256), 0, s, ids, tok_off, ntok, n_sent, cls, sep, out);
@@ -540,7 +623,8 @@ hipError_t launch_sent_special(const uint16_t* ids, const int64_t* tok_off, cons
 }
 
 hipError_t launch_masked_lm(const MlmParams& M, hipStream_t s) {
-  hipLaunchKernelGGL(masked_lm_kernel, dim3(2048), dim3(256), 0, s, M);
+  if (M.tokens) hipLaunchKernelGGL(masked_lm_kernel, dim3(2048), dim3(256), 0, s, M);
+  else hipLaunchKernelGGL(masked_lm_spans_kernel, dim3(2048), dim3(256), 0, s, M);
   return hipGetLastError();
 }
 

@@ -7,11 +7,12 @@
 
 namespace lddl {
 
-enum : int32_t { RENDER_SEG0 = 0, RENDER_SEG1 = 1, RENDER_ROW = 2 };
+// RENDER_SPAN: row r = tokens[row_off[r], row_off[r] + len0[r]) (lddl_row_spans' src / len over the dense ids)
+enum : int32_t { RENDER_SEG0 = 0, RENDER_SEG1 = 1, RENDER_ROW = 2, RENDER_SPAN = 3 };
 
 struct RenderParams {
-  const uint16_t* tokens;   // rows (lddl_materialize) or masked_lm labels
-  const int64_t* row_off;   // [rows + 1]
+  const uint16_t* tokens;   // rows (lddl_materialize), masked_lm labels, or the dense ids (RENDER_SPAN)
+  const int64_t* row_off;   // [rows + 1]; RENDER_SPAN: [rows] segment starts
   const uint16_t* len0;     // RENDER_SEG0/1
   const uint16_t* len1;     // RENDER_SEG1
   const uint8_t* flags;     // RENDER_SEG1 with codebert
@@ -22,6 +23,14 @@ struct RenderParams {
   int32_t* lens;            // [n_rows] scratch
   const int64_t* out_off;   // [n_rows + 1] (render_bytes)
   uint8_t* out;
+  // RENDER_SPAN with static masking (lddl_render_masked): row r's positions
+  // mpos[moff[r] .. moff[r+1]) (row coordinates, ascending) show mtok; the
+  // span's token k sits at row position 1 + k (A: mseg 0) or len0m[r] + 2 + k (B: mseg 1)
+  const int64_t* moff;
+  const uint16_t* mpos;
+  const uint16_t* mtok;
+  const uint16_t* len0m;
+  int32_t mseg;
 };
 
 struct RowDocParams {

@@ -26,6 +26,11 @@ namespace lddl {
 
 __device__ __forceinline__ void seg_of(const RenderParams& R, int64_t r, int64_t& start, int32_t& n) {
   const int64_t o = R.row_off[r];
+  if (R.segment == RENDER_SPAN) {
+    start = o;
+    n = R.len0[r];
+    return;
+  }
   if (R.segment == RENDER_ROW) {
     start = o;
     n = (int32_t)(R.row_off[r + 1] - o);
@@ -44,16 +49,50 @@ __device__ __forceinline__ void seg_of(const RenderParams& R, int64_t r, int64_t
   }
 }
 
+__device__ __forceinline__ void rwsync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// token k0 + lane of row r's segment, with row r's masked positions applied
+// (R.moff set): the row's patches falling in this chunk of 64 are scattered
+// into the wave's LDS slots, then each lane reads its own
+__device__ __forceinline__ uint32_t masked_tok(const RenderParams& R, uint32_t* pt, int64_t r, int32_t k0, int32_t n,
+                                               int64_t start, int lane) {
+  const int32_t k = k0 + lane;
+  uint32_t id = k < n ? R.tokens[start + k] : 0u;
+  if (!R.moff) return id;
+  const int64_t m0 = R.moff[r], m1 = R.moff[r + 1];
+  if (m0 == m1) return id;
+  const int32_t base = (R.mseg == 0 ? 1 : (int32_t)R.len0m[r] + 2) + k0;
+  rwsync();
+  pt[lane] = 0u;
+  rwsync();
+  for (int64_t e = m0 + lane; e < m1; e += 64) {
+    const int32_t rel = (int32_t)R.mpos[e] - base;
+    if (rel >= 0 && rel < 64) pt[rel] = 0x10000u | R.mtok[e];
+  }
+  rwsync();
+  const uint32_t v = pt[lane];
+  return v ? (v & 0xFFFFu) : id;
+}
+
 // lens[r] = bytes of ' '.join(vocab[t] for t in segment(r))
 __global__ __launch_bounds__(256) void render_len_kernel(RenderParams R) {
+  __shared__ uint32_t ptch[4][64];
   const int lane = threadIdx.x & 63;
+  uint32_t* const pt = ptch[threadIdx.x >> 6];
   const int64_t nw = (int64_t)gridDim.x * 4;
   for (int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < R.n_rows; i += nw) {
     int64_t start;
     int32_t n;
     seg_of(R, R.row0 + i, start, n);
     uint32_t acc = 0;
-    for (int32_t k = lane; k < n; k += 64) acc += (R.vinfo[R.tokens[start + k]] & 0xFFu) + 1u;
+    for (int32_t k0 = 0; k0 < n; k0 += 64) {
+      const uint32_t t = masked_tok(R, pt, R.row0 + i, k0, n, start, lane);
+      if (k0 + lane < n) acc += (R.vinfo[t] & 0xFFu) + 1u;
+    }
     // wave total: inclusive scan, lane 63 holds the sum
     acc = lane_get(wave_incl_add(acc), 63);
     if (lane == 0) R.lens[i] = n > 0 ? (int32_t)acc - 1 : 0;
@@ -62,7 +101,9 @@ __global__ __launch_bounds__(256) void render_len_kernel(RenderParams R) {
 
 // bytes of row i at out[out_off[i] - out_off[0] ..]
 __global__ __launch_bounds__(256) void render_bytes_kernel(RenderParams R) {
+  __shared__ uint32_t ptch[4][64];
   const int lane = threadIdx.x & 63;
+  uint32_t* const pt = ptch[threadIdx.x >> 6];
   const int64_t nw = (int64_t)gridDim.x * 4;
   const int64_t o0 = R.out_off[0];
   for (int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < R.n_rows; i += nw) {
@@ -73,8 +114,9 @@ __global__ __launch_bounds__(256) void render_bytes_kernel(RenderParams R) {
     for (int32_t k0 = 0; k0 < n; k0 += 64) {
       const int32_t k = k0 + lane;
       uint32_t info = 0, len = 0, w = 0;
+      const uint32_t t = masked_tok(R, pt, R.row0 + i, k0, n, start, lane);
       if (k < n) {
-        info = R.vinfo[R.tokens[start + k]];
+        info = R.vinfo[t];
         len = info & 0xFFu;
         w = len + (k < n - 1 ? 1u : 0u);  // the joining space follows every token but the last
       }

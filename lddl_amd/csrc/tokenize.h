@@ -84,7 +84,9 @@ struct SplitParams {
   const int64_t* tile_off;  // sent_off[tile_sent[t]] (the scan stages a tile's bounds in one round trip)
   uint16_t* ent;
   uint4* rec;              // 4 uint4 per slot
-  uint4* pcs;              // WordPiece output (count + pieces) per slot, apart from the keys
+  uint4* pcs;              // WordPiece pieces 4.. per slot (64 B per slot; the extension slot continues it)
+  uint4* pch;              // WordPiece head per slot: {#pieces, pieces 0-1, pieces 2-3, 0}: dense 16 B, what
+                           // expand reads for nearly every record (one 16-B line share instead of a 64-B stride)
   uint32_t* chunk_fill;
   uint32_t* chunk_ctr;     // [0] chunks handed out
   uint32_t n_chunks;

@@ -284,7 +284,7 @@ __device__ __forceinline__ bool slot_eq(const uint4& a, const uint4& b, const Ke
 // OCC: the waves per SIMD the register allocation is held to (LDS admits 5)
 template <int WAVES, bool DBG, int OCC>
 __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, SplitParams S) {
-  uint64_t acc[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t acc[17] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t tprev = 0;
 #define STAMP(k)                                                                   \
   if (DBG) {                                                                       \
@@ -529,6 +529,7 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
               if (k >= kb && k < kb + XL) xl[k - kb] = (uint16_t)(p0 + __ffs(m) - 1);
           }
           wsync();
+          STAMP(14);
           const uint32_t nl = min(nx - kb, XL);
         for (uint32_t k0 = 0; k0 < nl; k0 += 64) {
           const uint32_t k = k0 + lane;
@@ -547,6 +548,8 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
               e = P.xmap[cp];
             }
           }
+          if (DBG) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          STAMP(15);
           if (brk) {  // [PAD] [UNK] [CLS] [SEP] [MASK] within p's sentence
             const int a = (p + 1) >> 2;
             const uint32_t sh = (uint32_t)((p + 1) & 3);
@@ -602,6 +605,7 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
         CS = mw(3)[lane];
         D = mw(4)[lane];
         if (__any(any_slow)) xslow = slowm[lane];
+        STAMP(16);
       }
       // the full path: exceptions in batches of 4 per lane, the table lookups
       // of a batch (code point -> page -> entry -> multi expansion) together
@@ -1022,7 +1026,7 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
   if (DBG && lane == 0)
     for (int k = 0; k < 12; ++k) atomicAdd((unsigned long long*)&P.dbg[k], (unsigned long long)acc[k]);
   if (DBG && lane == 0)
-    for (int k = 12; k < 14; ++k) atomicAdd((unsigned long long*)&P.dbg[6 + k], (unsigned long long)acc[k]);
+    for (int k = 12; k < 17; ++k) atomicAdd((unsigned long long*)&P.dbg[6 + k], (unsigned long long)acc[k]);
 #undef STAMP
   if (chunk >= 0 && lane == 0) S.chunk_fill[chunk] = cur - cbase;
 }
@@ -1123,7 +1127,7 @@ __global__ __launch_bounds__(64 * WAVES) void wp_kernel(TokParams P, SplitParams
   uint4* const outs = S.pcs;
   auto rec16 = [&]() { return reinterpret_cast<uint16_t*>(outs + (size_t)r * 4); };
   // pieces 0-3 (nearly every word's all) held in two registers and stored
-  // with the count in one 12-B store at the end (what expand loads)
+  // with the count as the slot's dense 16-B head at the end (what expand loads)
   uint32_t pw01 = 0, pw23 = 0;
   auto put_piece = [&](int k, uint32_t id) {
     if (k < 4) {
@@ -1136,8 +1140,7 @@ __global__ __launch_bounds__(64 * WAVES) void wp_kernel(TokParams P, SplitParams
     }
   };
   auto finish = [&]() {
-    typedef uint32_t u32x3s __attribute__((ext_vector_type(3)));
-    *reinterpret_cast<u32x3s*>(reinterpret_cast<uint32_t*>(outs + (size_t)r * 4) + 1) = u32x3s{(uint32_t)np, pw01, pw23};
+    S.pch[r] = make_uint4((uint32_t)np, pw01, pw23, 0u);
     S.cnt8[r] = (uint8_t)np;
     r = -1;
   };
@@ -1385,6 +1388,7 @@ __global__ __launch_bounds__(256) void expand_kernel(TokParams P, SplitParams S)
   const int64_t nwaves = (int64_t)gridDim.x * 4;
   typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
   const uint4* const pcs = S.pcs;
+  const uint4* const pch = S.pch;
   for (int64_t g0 = sA + ((int64_t)blockIdx.x * 4 + wv) * 64; g0 < sB; g0 += nwaves * 64) {
     const int64_t s = g0 + lane;
     uint32_t ne = 0;
@@ -1454,8 +1458,7 @@ __global__ __launch_bounds__(256) void expand_kernel(TokParams P, SplitParams S)
         const bool r = xin[k] && xv[k] >= SPLIT_EDEF && xv[k] != SPLIT_EHOLE;
         xr[k] = u32x3{0u, 0u, 0u};
         if (st0 + 64 * k < T)
-          xr[k] = *reinterpret_cast<const u32x3*>(reinterpret_cast<const uint32_t*>(
-                                                     pcs + (r ? (size_t)(E.sn[xj[k]].qb + (xv[k] & 0xFFFu)) * 4 : 0)) + 1);
+          xr[k] = *reinterpret_cast<const u32x3*>(pch + (r ? (size_t)(E.sn[xj[k]].qb + (xv[k] & 0xFFFu)) : 0));
       }
 #pragma unroll
       for (int k = 0; k < EXP_K; ++k) {

@@ -109,10 +109,45 @@ class PackResult:
   mlm_label: torch.Tensor = None  # int16 view of uint16 label ids
   ntok_host: np.ndarray = None
   part_doc_off: np.ndarray = None
+  mlm_token: torch.Tensor = None  # spans + masking: int16 view of the token each masked position shows
+  src0: torch.Tensor = None       # spans (lddl_row_spans): int64 [n_pairs] dense-id offset of A / doc
+  src1: torch.Tensor = None       # of B / code; tokens is then None (no rows materialised)
+  cls_id: int = 0
+  sep_id: int = 0
+
+  @property
+  def spans(self):
+    return self.src0 is not None
+
+  def host_tokens(self):
+    """the rows back to back on the host (int64), from the materialised
+    rows or rebuilt from the spans over the dense ids"""
+    if not self.spans:
+      return self.tokens[:self.n_tokens].cpu().numpy().view(np.uint16).astype(np.int64)
+    n = self.n_pairs
+    ids = self.ids.cpu().numpy().view(np.uint16).astype(np.int64)
+    s0, s1 = self.src0[:n].cpu().numpy(), self.src1[:n].cpu().numpy()
+    l0 = self.len0[:n].cpu().numpy().view(np.uint16).astype(np.int64)
+    l1 = self.len1[:n].cpu().numpy().view(np.uint16).astype(np.int64)
+    fl = self.flags[:n].cpu().numpy()
+    if self.mlm_token is not None:  # the masked rows show mlm_token at mlm_pos
+      moff = self.mlm_off[:n + 1].cpu().numpy()
+      mpos = self.mlm_pos[:self.n_masked].cpu().numpy().view(np.uint16).astype(np.int64)
+      mtok = self.mlm_token[:self.n_masked].cpu().numpy().view(np.uint16).astype(np.int64)
+    out = []
+    for g in range(n):
+      a = ids[s0[g]:s0[g] + l0[g]]
+      b = ids[s1[g]:s1[g] + l1[g]]
+      sep0 = [self.sep_id] if fl[g] & 2 else []
+      row = np.concatenate([[self.cls_id], a, sep0, b, [self.sep_id]]).astype(np.int64)
+      if self.mlm_token is not None:
+        row[mpos[moff[g]:moff[g + 1]]] = mtok[moff[g]:moff[g + 1]]
+      out.append(row)
+    return np.concatenate(out) if out else np.zeros(0, np.int64)
 
   def rows(self):
     """host copy: list of (partition, A ids, B ids, flags, bin)"""
-    tok = self.tokens[:self.n_tokens].cpu().numpy().view(np.uint16).astype(np.int64)
+    tok = self.host_tokens()
     off = self.tok_off[:self.n_pairs + 1].cpu().numpy()
     l0 = self.len0[:self.n_pairs].cpu().numpy().view(np.uint16).astype(np.int64)
     l1 = self.len1[:self.n_pairs].cpu().numpy().view(np.uint16).astype(np.int64)
@@ -179,10 +214,16 @@ class Packer:
     raise RuntimeError('lddl_amd: tokenize did not fit its exact total')
 
   def pack(self, shards, ids, ntok, tok_off=None, target_seq_length=128, short_seq_prob=0.1, duplicate_factor=5,
-           seed=12345, bin_size=None, codebert=False, masking=False, masked_lm_ratio=0.15, stream=None):
+           seed=12345, bin_size=None, codebert=False, masking=False, masked_lm_ratio=0.15, stream=None,
+           spans=False):
     """ids / ntok / tok_off: tokenize()'s dense CSR result (tok_off None:
     the exclusive scan of ntok, for ids built by hand); ids must hold 16
-    entries of padding past the last id (lddl_materialize's 16-B loads)"""
+    entries of padding past the last id (lddl_materialize's 16-B loads).
+    spans: the rows as spans of the dense ids (lddl_row_spans, no token
+    copy; res.src0 / res.src1) instead of materialised rows -- what the
+    parquet writer renders from; with masking, lddl_masked_lm_spans adds the
+    token each masked position shows (res.mlm_token) in place of rewriting
+    rows."""
     L = _lib.lib()
     if tok_off is None:
       tok_off = torch.zeros(shards.n_sent + 1, dtype=torch.int64, device=self.device)
@@ -209,14 +250,23 @@ class Packer:
     _lib.check(rc)
     n_pairs, n_tokens, nbins = int(tot[0]), int(tot[1]), int(tot[2])
     res = PackResult(n_pairs, n_tokens, nbins,
-                     self._buf('tokens', n_tokens, torch.int16), self._buf('tok_off', n_pairs + 1, torch.int64),
+                     None if spans else self._buf('tokens', n_tokens, torch.int16),
+                     self._buf('tok_off', n_pairs + 1, torch.int64),
                      self._buf('len0', n_pairs, torch.int16), self._buf('len1', n_pairs, torch.int16),
                      self._buf('flags', n_pairs, torch.uint8), self._buf('bins', n_pairs, torch.uint8),
                      self._buf('part', n_pairs, torch.int64),
                      self._buf('bin_count', shards.n_part * nbins, torch.int64))
-    _lib.check(L.lddl_materialize(self.tok.handle, _ptr(ids), _ptr(res.tokens), _ptr(res.tok_off),
+    res.cls_id, res.sep_id = self.tok.cls_id, self.tok.sep_id
+    if spans:
+      res.src0 = self._buf('src0', n_pairs, torch.int64)
+      res.src1 = self._buf('src1', n_pairs, torch.int64)
+      _lib.check(L.lddl_row_spans(self.tok.handle, _ptr(res.src0), _ptr(res.src1), _ptr(res.tok_off),
                                   _ptr(res.len0), _ptr(res.len1), _ptr(res.flags), _ptr(res.bins),
                                   _ptr(res.part), _ptr(res.bin_count), s))
+    else:
+      _lib.check(L.lddl_materialize(self.tok.handle, _ptr(ids), _ptr(res.tokens), _ptr(res.tok_off),
+                                    _ptr(res.len0), _ptr(res.len1), _ptr(res.flags), _ptr(res.bins),
+                                    _ptr(res.part), _ptr(res.bin_count), s))
     res.bin_count = res.bin_count[:shards.n_part * nbins].view(shards.n_part, nbins)
     res.ids, res.ntok, res.ids_off = ids, ntok, tok_off
     if masking and not codebert:
@@ -224,7 +274,13 @@ class Packer:
       res.mlm_off = self._buf('mlm_off', n_pairs + 1, torch.int64)
       res.mlm_pos = self._buf('mlm_pos', res.n_masked, torch.int16)
       res.mlm_label = self._buf('mlm_label', res.n_masked, torch.int16)
-      _lib.check(L.lddl_masked_lm(self.tok.handle, _ptr(res.mlm_off), _ptr(res.mlm_pos), _ptr(res.mlm_label), s))
+      if spans:
+        res.mlm_token = self._buf('mlm_token', res.n_masked, torch.int16)
+        _lib.check(L.lddl_masked_lm_spans(self.tok.handle, _ptr(ids), _ptr(res.src0), _ptr(res.src1),
+                                          _ptr(res.len0), _ptr(res.part), _ptr(res.mlm_off), _ptr(res.mlm_pos),
+                                          _ptr(res.mlm_label), _ptr(res.mlm_token), s))
+      else:
+        _lib.check(L.lddl_masked_lm(self.tok.handle, _ptr(res.mlm_off), _ptr(res.mlm_pos), _ptr(res.mlm_label), s))
     return res
 
   def run(self, shards, **kw):
@@ -233,7 +289,7 @@ class Packer:
 
 def run_bert(corpus, vocab_file=VOCAB_BERT, target_seq_length=128, bin_size=None, n_partitions=1, seed=12345,
              device=None, check_host=False, duplicate_factor=5, short_seq_prob=0.1, part_doc_off=None,
-             codebert=False, masking=False, masked_lm_ratio=0.15):
+             codebert=False, masking=False, masked_lm_ratio=0.15, spans=False):
   device = device or torch.device('cuda', 0)
   if part_doc_off is None:
     part_doc_off = partition_by_bytes(corpus, n_partitions)
@@ -241,7 +297,7 @@ def run_bert(corpus, vocab_file=VOCAB_BERT, target_seq_length=128, bin_size=None
   sh = upload(corpus, part_doc_off, device)
   res = pk.run(sh, target_seq_length=target_seq_length, short_seq_prob=short_seq_prob,
                duplicate_factor=duplicate_factor, seed=seed, bin_size=bin_size, codebert=codebert,
-               masking=masking, masked_lm_ratio=masked_lm_ratio)
+               masking=masking, masked_lm_ratio=masked_lm_ratio, spans=spans)
   torch.cuda.synchronize(device)
   res.part_doc_off = np.asarray(part_doc_off)
   if check_host:

@@ -267,8 +267,10 @@ def attach_args(parser=None, codebert=False):
   p.add_argument('--chunk-mb', type=float, default=64.0,
                  help='raw MB of partitions per pipeline chunk (host split of the next chunks overlaps the GPU and '
                       'the writer on chunk k)')
-  p.add_argument('--split-workers', type=int, default=4,
-                 help='host processes splitting sentences ahead of the GPU (0: split inline)')
+  p.add_argument('--split-workers', type=int, default=None,
+                 help='host processes splitting sentences ahead of the GPU (0: split inline; default: the cores '
+                      'of this process\'s affinity, as the reference\'s --local-n-workers defaults to '
+                      'os.cpu_count(), pretrain.py:678)')
   p.add_argument('--num-shards', type=int, default=None,
                  help='balance the output into this many shard-{k}.parquet[_b] files (balance_dask_output, '
                       'load_balance.py) with counts all-gathered from the packer')
@@ -466,7 +468,13 @@ def main(args, codebert=False):
 
   # split workers: forked here, before anything touches the GPU; they read
   # their records from the index (integers only are inherited)
-  nw = min(max(0, args.split_workers), len(todo)) if len(todo) > 1 else 0
+  sw = args.split_workers
+  if sw is None:
+    try:
+      sw = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+      sw = os.cpu_count() or 1
+  nw = min(max(0, sw), len(todo)) if len(todo) > 1 else 0
   pool = None
   if nw > 0:
     import multiprocessing
@@ -498,6 +506,28 @@ def main(args, codebert=False):
     counts[a - lo:b - lo] = torch.tensor(m['counts'], dtype=torch.int64)
     out += [os.path.join(sink, f) for f in m['files']]
     t['pairs'] += m['n_pairs']
+  # parquet encodes of chunk k run on this pool while chunk k+1 splits,
+  # uploads, tokenizes and packs; a chunk's --resume marker is saved once
+  # all of its files are encoded (in chunk order)
+  import concurrent.futures
+  enc = concurrent.futures.ThreadPoolExecutor(writer.encode_workers()) if args.output_format != 'txt' else None
+  inflight = []  # (a, b, files, futures, counts, n_pairs) per chunk, oldest first
+
+  def settle(keep):
+    """finish the oldest chunks: those whose encodes are done, and while more
+    than `keep` chunks are in flight, the oldest one (waiting for it)"""
+    while inflight:
+      if len(inflight) <= keep and not all(f_.done() for f_ in inflight[0][3]):
+        break
+      a_, b_, files_, futs_, cnt_, np_ = inflight.pop(0)
+      tw_ = time.perf_counter()
+      for f_ in futs_:
+        f_.result()
+      t['write_wait_s'] += time.perf_counter() - tw_
+      if args.resume:
+        save_marker(sink, a_, b_, key, files_, cnt_, np_)
+
+  t['write_wait_s'] = 0.0
   try:
     ahead = max(1, nw)
     futs = {c: submit(c) for c in todo[:ahead]} if pool is not None else {}
@@ -515,24 +545,32 @@ def main(args, codebert=False):
       # partition p packs after random.seed(args.seed + global p)
       res = pk.pack(sh, ids_d, ntok, toff, target_seq_length=args.target_seq_length, short_seq_prob=args.short_seq_prob,
                     duplicate_factor=args.duplicate_factor, seed=args.seed + a, bin_size=args.bin_size,
-                    codebert=codebert, masking=args.masking and not codebert, masked_lm_ratio=args.masked_lm_ratio)
+                    codebert=codebert, masking=args.masking and not codebert, masked_lm_ratio=args.masked_lm_ratio,
+                    spans=True)
       counts[a - lo:b - lo] = res.bin_count.view(b - a, -1).to(torch.int64)
       torch.cuda.synchronize()
       t['gpu_s'] += time.perf_counter() - t0
       t0 = time.perf_counter()
-      wr = writer.write_txt if args.output_format == 'txt' else writer.write_shards
       clear_markers(sink, a, b)
-      wrote = wr(pk, res, sink, bin_size=args.bin_size, codebert=codebert, masking=args.masking and not codebert,
-                 doc_ids=ids, part_base=a)
+      kw = dict(bin_size=args.bin_size, codebert=codebert, masking=args.masking and not codebert, doc_ids=ids,
+                part_base=a)
+      cf = []
+      if enc is None:
+        wrote = writer.write_txt(pk, res, sink, **kw)
+      else:
+        wrote = writer.write_shards(pk, res, sink, executor=enc, pending=cf, **kw)
       out += wrote
-      if args.resume:
-        save_marker(sink, a, b, key, wrote, counts[a - lo:b - lo].tolist(), res.n_pairs)
+      inflight.append((a, b, wrote, cf, counts[a - lo:b - lo].tolist(), res.n_pairs))
+      settle(2)  # at most two chunks' encodes behind the GPU
       t['write_s'] += time.perf_counter() - t0
       t['pairs'] += res.n_pairs
+    settle(0)
   finally:
     if pool is not None:
       pool.terminate()
       pool.join()
+    if enc is not None:
+      enc.shutdown(wait=True)
     index.close()
   if args.num_shards:
     # balance_dask_output's job (load_balance.py:321-369) from the packer's

@@ -33,7 +33,7 @@ import torch
 from . import _lib
 from .tokenizer import _ptr, _stream
 
-SEG0, SEG1, ROW = 0, 1, 2
+SEG0, SEG1, ROW, SPAN = 0, 1, 2, 3
 
 BERT_SCHEMA = [('A', pa.string()), ('B', pa.string()), ('is_random_next', pa.bool_()),
                ('num_tokens', pa.uint16())]
@@ -67,6 +67,36 @@ def render(packer, tokens, row_off, row0, n_rows, segment, len0=None, len1=None,
   data = torch.empty(max(nb.value, 1), dtype=torch.uint8, device=dev)
   _lib.check(L.lddl_render_strings(*args, _ptr(data), nb.value, ctypes.byref(nb), s))
   return off.cpu().numpy(), data[:nb.value].cpu().numpy()
+
+
+def render_masked(packer, res, row0, n_rows, segment, stream=None):
+  """A (segment 0) / B (1) of span rows with the static masking applied
+  (lddl_render_masked): (offsets, bytes) on the host as render()"""
+  L = _lib.lib()
+  off = torch.empty(n_rows + 1, dtype=torch.int64, device=packer.device)
+  nb = ctypes.c_int64(0)
+  s = _stream(stream)
+  src, ln = (res.src0, res.len0) if segment == 0 else (res.src1, res.len1)
+  args = (packer.tok.handle, _ptr(res.ids), _ptr(src), _ptr(ln), _ptr(res.len0), segment, _ptr(res.mlm_off),
+          _ptr(res.mlm_pos), _ptr(res.mlm_token), row0, n_rows, _ptr(off))
+  _lib.check(L.lddl_render_masked(*args, None, 0, ctypes.byref(nb), s))
+  data = torch.empty(max(nb.value, 1), dtype=torch.uint8, device=packer.device)
+  _lib.check(L.lddl_render_masked(*args, _ptr(data), nb.value, ctypes.byref(nb), s))
+  return off.cpu().numpy(), data[:nb.value].cpu().numpy()
+
+
+def seg_columns(packer, res, r0, n, codebert=False, stream=None):
+  """the two segment string columns (A / B, or doc / code) of rows
+  [r0, r0 + n): rendered from the spans over the dense ids (res.spans) or
+  from the materialised rows"""
+  if res.spans and res.mlm_token is not None:
+    return (render_masked(packer, res, r0, n, 0, stream), render_masked(packer, res, r0, n, 1, stream))
+  if res.spans:
+    return (render(packer, res.ids, res.src0, r0, n, SPAN, len0=res.len0, stream=stream),
+            render(packer, res.ids, res.src1, r0, n, SPAN, len0=res.len1, stream=stream))
+  kw = dict(len0=res.len0, len1=res.len1, flags=res.flags, codebert=codebert, stream=stream)
+  return (render(packer, res.tokens, res.tok_off, r0, n, SEG0, **kw),
+          render(packer, res.tokens, res.tok_off, r0, n, SEG1, **kw))
 
 
 def row_docs(packer, n_rows, n_copy=None, stream=None):
@@ -140,13 +170,18 @@ def _arrow(typ, off, data, lo, hi):
 
 
 def write_shards(packer, res, out_dir, bin_size=None, codebert=False, masking=False, doc_ids=None,
-                 part_base=0, compression='snappy', batch_rows=1 << 20, max_parts=None, stream=None):
+                 part_base=0, compression='snappy', batch_rows=1 << 20, max_parts=None, stream=None,
+                 executor=None, pending=None):
   """Write the rows of ``res`` (a pipeline.PackResult) as the reference's
   parquet files under out_dir.  Partition p of this pack call is file
   ``part.{part_base + p}.parquet`` (unbinned) or ``part.{..}.parquet_{b}``
   for every bin b (binned).  doc_ids: CodeBERT 'id' strings (list or Arrow array) per document of
   the packed corpus.  max_parts: only the first max_parts partitions.
-  Returns the list of files written."""
+  executor / pending: the parquet encodes go to the caller's thread pool and
+  their futures to the caller's list, and this call returns once the string
+  columns are rendered and on the host (the device buffers are free again):
+  the encodes run on while the caller's next chunk splits and packs.
+  Returns the list of files (written once the futures are done)."""
   os.makedirs(out_dir, exist_ok=True)
   binned = bin_size is not None
   nbins = res.nbins if binned else 1
@@ -176,9 +211,10 @@ def write_shards(packer, res, out_dir, bin_size=None, codebert=False, masking=Fa
     mpos_all = res.mlm_pos[:int(moff_all[-1])].cpu().numpy().view(np.uint16)
   files = []
   f = 0
-  workers = max(1, min(16, os.cpu_count() or 1))
-  pool = concurrent.futures.ThreadPoolExecutor(workers)
-  pending = []
+  workers = encode_workers()
+  own = executor is None
+  pool = concurrent.futures.ThreadPoolExecutor(workers) if own else executor
+  mine = []
   # render in batches of whole files (>= batch_rows rows, or one big file)
   while f < nfiles:
     g = f + 1
@@ -186,9 +222,7 @@ def write_shards(packer, res, out_dir, bin_size=None, codebert=False, masking=Fa
       g += 1
     r0, r1 = int(file_start[f]), int(file_start[g])
     n = r1 - r0
-    kw = dict(len0=res.len0, len1=res.len1, flags=res.flags, codebert=codebert, stream=stream)
-    c0 = render(packer, res.tokens, res.tok_off, r0, n, SEG0, **kw)
-    c1 = render(packer, res.tokens, res.tok_off, r0, n, SEG1, **kw)
+    c0, c1 = seg_columns(packer, res, r0, n, codebert, stream)
     if masking and not codebert:
       m0 = int(moff_all[r0])
       lab = render(packer, res.mlm_label, res.mlm_off, r0, n, ROW, stream=stream)
@@ -216,17 +250,29 @@ def write_shards(packer, res, out_dir, bin_size=None, codebert=False, masking=Fa
       if binned:
         name += '_%d' % b
       path = os.path.join(out_dir, name)
-      pending.append(pool.submit(pq.write_table, t, path, compression=compression))
+      mine.append(pool.submit(pq.write_table, t, path, compression=compression))
       files.append(path)
     # the parquet encoder releases the GIL: files of a batch encode in
     # parallel on the host cores while the next batch renders on the GPU
-    while len(pending) > 4 * workers:
-      pending.pop(0).result()
+    while len(mine) > 4 * workers:
+      mine.pop(0).result()
     f = g
-  for fu in pending:
-    fu.result()
-  pool.shutdown()
+  if own:
+    for fu in mine:
+      fu.result()
+    pool.shutdown()
+  else:
+    pending.extend(mine)
   return files
+
+
+def encode_workers():
+  """parquet encode threads: this process' cores, at most 16"""
+  try:
+    n = len(os.sched_getaffinity(0))
+  except (AttributeError, OSError):
+    n = os.cpu_count() or 1
+  return max(1, min(16, n))
 
 
 def write_txt(packer, res, out_dir, bin_size=None, codebert=False, masking=False, doc_ids=None, part_base=0,
@@ -275,9 +321,7 @@ def write_txt(packer, res, out_dir, bin_size=None, codebert=False, masking=False
       g += 1
     r0, r1 = int(file_start[f]), int(file_start[g])
     n = r1 - r0
-    kw = dict(len0=res.len0, len1=res.len1, flags=res.flags, codebert=codebert, stream=stream)
-    (o0, d0), (o1, d1) = (render(packer, res.tokens, res.tok_off, r0, n, SEG0, **kw),
-                          render(packer, res.tokens, res.tok_off, r0, n, SEG1, **kw))
+    (o0, d0), (o1, d1) = seg_columns(packer, res, r0, n, codebert, stream)
     if masking and not codebert:
       ol, dl = render(packer, res.mlm_label, res.mlm_off, r0, n, ROW, stream=stream)
     b0, b1 = d0.tobytes(), d1.tobytes()

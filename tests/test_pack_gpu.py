@@ -86,21 +86,24 @@ def test_codebert_golden(cpacker, k):
     assert (a, b, len(tok)) == (e['doc'], e['code'], e['num_tokens'])
 
 
-@pytest.mark.parametrize('caps,mat', [(None, None), ('8192,512,8192', None), ('0,0,256', None), (None, '1')])
+@pytest.mark.parametrize('caps,mat', [(None, None), ('8192,512,8192', None), ('0,0,256', None), (None, '1'),
+                                      (None, 'spans')])
 @pytest.mark.parametrize('seq,bin_size,nparts', [(128, 32, 7), (512, 64, 3), (128, None, 1)])
 def test_bert_end_to_end_vs_oracle(gpu, monkeypatch, seq, bin_size, nparts, caps, mat):
   """caps: the wave packer's per-partition arrays in global memory (default),
   all in LDS, and order/num_tokens in LDS with a capacity some partitions
   exceed (mixed paths in one launch).  mat: the chunked materialize and
-  compaction kernels (default) or the per-partition / per-sentence ones (1)."""
+  compaction kernels (default), the per-partition / per-sentence ones (1),
+  or no materialisation: the rows as spans of the dense ids (lddl_row_spans)."""
   from lddl_amd import synth, pipeline
   if caps:
     monkeypatch.setenv('LDDL_PACK_CAPS', caps)
-  if mat:
+  if mat == '1':
     monkeypatch.setenv('LDDL_MAT_ALGO', mat)
   c = synth.make_wiki(600_000, seed=seq + nparts)
   res = pipeline.run_bert(c, target_seq_length=seq, bin_size=bin_size, n_partitions=nparts, seed=999,
-                          check_host=True)
+                          check_host=True, spans=mat == 'spans')
+  assert res.spans == (mat == 'spans')
   oids, ontok = OracleTokenizer(pipeline.VOCAB_BERT).run(c.data, c.sent_off, 512, nthreads=8)
   assert np.array_equal(res.ntok_host, ontok)
   exp = po.run_bert_shards(c, oids, ontok, res.part_doc_off, seq, 0.1, 5, 999, bin_size)
@@ -131,15 +134,17 @@ def test_wikibooks_seq512_bin64_vs_oracle(gpu, nparts):
     assert np.array_equal(bc[p], np.bincount([po.bin_of(r[3], 64, 8) for r in part], minlength=8))
 
 
-@pytest.mark.parametrize('mat', [None, '1'])
+@pytest.mark.parametrize('mat', [None, '1', 'spans'])
 def test_codebert_end_to_end_vs_oracle(gpu, monkeypatch, mat):
   from lddl_amd import synth, pipeline
-  if mat:
+  if mat == '1':
     monkeypatch.setenv('LDDL_MAT_ALGO', mat)
   c = synth.make_code(400, seed=31)
   pdo = pipeline.partition_by_bytes(c, 3)
   res = pipeline.run_bert(c, vocab_file=pipeline.VOCAB_CODEBERT, target_seq_length=512, bin_size=64,
-                          part_doc_off=pdo, seed=42, duplicate_factor=1, codebert=True, check_host=True)
+                          part_doc_off=pdo, seed=42, duplicate_factor=1, codebert=True, check_host=True,
+                          spans=mat == 'spans')
+  assert res.spans == (mat == 'spans')
   oids, ontok = OracleTokenizer(pipeline.VOCAB_CODEBERT).run(c.data, c.sent_off, 512, nthreads=8)
   assert np.array_equal(res.ntok_host, ontok)
   rows = res.rows()
@@ -191,15 +196,17 @@ def test_many_partitions_and_empty_partitions(packer):
 MASK = (0.15, 30522, 101, 102, 103)  # ratio, |vocab|, [CLS], [SEP], [MASK] of bert-base-uncased
 
 
+@pytest.mark.parametrize('spans', [False, True])
 @pytest.mark.parametrize('k', [i for i, c in enumerate(BERT['cases']) if c['cfg']['masking']])
 @pytest.mark.parametrize('binned', [False, True])
-def test_bert_masked_golden(packer, k, binned):
-  """--masking rows against the reference's create_masked_lm_predictions."""
+def test_bert_masked_golden(packer, k, binned, spans):
+  """--masking rows against the reference's create_masked_lm_predictions
+  (rows materialised and masked in place, or spans + lddl_masked_lm_spans)."""
   case = BERT['cases'][k]
   c = case['cfg']
   sh, ids, ntok = shards_from_docs(case['docs'])
   kw = dict(target_seq_length=c['max_seq'], short_seq_prob=c['ssp'], duplicate_factor=c['dup'],
-            seed=case['seed'], bin_size=case['bin_size'] if binned else None, masking=True)
+            seed=case['seed'], bin_size=case['bin_size'] if binned else None, masking=True, spans=spans)
   if case['error']:
     with pytest.raises(AssertionError):
       packer.pack(sh, ids, ntok, **kw)
@@ -220,12 +227,14 @@ def test_bert_masked_golden(packer, k, binned):
 
 
 # (seq 1024: the MASK = 2 packer instantiation, MaskLds<1024>, 10-bit shuffle draws)
+@pytest.mark.parametrize('spans', [False, True])
 @pytest.mark.parametrize('seq,bin_size,nparts', [(128, 32, 5), (512, 64, 2), (1024, 128, 2)])
-def test_bert_masked_end_to_end_vs_oracle(gpu, seq, bin_size, nparts):
+def test_bert_masked_end_to_end_vs_oracle(gpu, seq, bin_size, nparts, spans):
   from lddl_amd import synth, pipeline
   c = synth.make_wiki(500_000, seed=seq + 3 * nparts)
   res = pipeline.run_bert(c, target_seq_length=seq, bin_size=bin_size, n_partitions=nparts, seed=4242,
-                          check_host=True, masking=True)
+                          check_host=True, masking=True, spans=spans)
+  assert res.spans == spans
   oids, ontok = OracleTokenizer(pipeline.VOCAB_BERT).run(c.data, c.sent_off, 512, nthreads=8)
   assert np.array_equal(res.ntok_host, ontok)
   exp = po.run_bert_shards(c, oids, ontok, res.part_doc_off, seq, 0.1, 5, 4242, bin_size, masking=MASK)
@@ -359,3 +368,29 @@ def test_masked_special_flags_from_tokenizer(gpu):
   a = pk.pack(sh, ids, ntok, toff, **kw).rows()
   b = pk.pack(sh, ids.clone(), ntok, toff, **kw).rows()
   assert len(a) == len(b) and a == b
+
+
+@pytest.mark.parametrize('codebert', [False, True])
+def test_row_spans_equal_materialized_rows(gpu, codebert):
+  """lddl_row_spans describes exactly lddl_materialize's rows: the same
+  row offsets, lengths, flags, bins, partitions and bin counts, and the
+  tokens the spans select from the dense ids equal the materialised rows"""
+  from lddl_amd import synth, pipeline
+  c = synth.make_code(300, seed=8) if codebert else synth.make_wiki(500_000, seed=8)
+  vocab = pipeline.VOCAB_CODEBERT if codebert else pipeline.VOCAB_BERT
+  pdo = pipeline.partition_by_bytes(c, 4)
+  pk = pipeline.Packer(vocab, 0)
+  sh = pipeline.upload(c, pdo, gpu)
+  ids, ntok, toff = pk.tokenize(sh)
+  kw = dict(target_seq_length=256, bin_size=32, seed=5, codebert=codebert, duplicate_factor=1 if codebert else 3)
+  m = pk.pack(sh, ids, ntok, toff, **kw)
+  mt = m.host_tokens()
+  mcopy = {k: getattr(m, k)[:m.n_pairs + (1 if k == 'tok_off' else 0)].cpu().numpy().copy()
+           for k in ('tok_off', 'len0', 'len1', 'flags', 'bins', 'part')}
+  mbc = m.bin_count.cpu().numpy().copy()
+  s = pk.pack(sh, ids, ntok, toff, spans=True, **kw)
+  assert s.spans and s.tokens is None and s.n_pairs == m.n_pairs and s.n_pairs > 0
+  for k, v in mcopy.items():
+    assert np.array_equal(getattr(s, k)[:s.n_pairs + (1 if k == 'tok_off' else 0)].cpu().numpy(), v), k
+  assert np.array_equal(s.bin_count.cpu().numpy(), mbc)
+  assert np.array_equal(s.host_tokens(), mt)

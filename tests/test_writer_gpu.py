@@ -30,9 +30,10 @@ def _read(path):
   return pq.read_table(path).to_pydict()
 
 
+@pytest.mark.parametrize('spans', [False, True])
 @pytest.mark.parametrize('k', [0, 6, 12, 18, 24, 27, 30, 33])
 @pytest.mark.parametrize('binned', [False, True])
-def test_bert_parquet_golden(packer, tmp_path, k, binned):
+def test_bert_parquet_golden(packer, tmp_path, k, binned, spans):
   from lddl_amd import writer
   case = BERT['cases'][k]
   c = case['cfg']
@@ -42,7 +43,8 @@ def test_bert_parquet_golden(packer, tmp_path, k, binned):
   sh, ids, ntok = shards_from_docs(case['docs'])
   bin_size = case['bin_size'] if binned else None
   res = packer.pack(sh, ids, ntok, target_seq_length=c['max_seq'], short_seq_prob=c['ssp'],
-                    duplicate_factor=c['dup'], seed=case['seed'], bin_size=bin_size, masking=masking)
+                    duplicate_factor=c['dup'], seed=case['seed'], bin_size=bin_size, masking=masking, spans=spans)
+  assert res.spans == spans
   files = writer.write_shards(packer, res, str(tmp_path), bin_size=bin_size, masking=masking, part_base=7,
                               batch_rows=97)  # small batches: files split across render batches
   vocab = _vocab(packer.tok.vocab_file)
@@ -73,8 +75,9 @@ def test_bert_parquet_golden(packer, tmp_path, k, binned):
     assert got['masked_lm_labels'] == [_join(vocab, e['masked_lm_labels']) for e in exp]
 
 
+@pytest.mark.parametrize('spans', [False, True])
 @pytest.mark.parametrize('k', range(12))
-def test_codebert_parquet_golden(cpacker, tmp_path, k):
+def test_codebert_parquet_golden(cpacker, tmp_path, k, spans):
   from lddl_amd import writer
   case = CODE['cases'][k]
   c = case['cfg']
@@ -82,7 +85,8 @@ def test_codebert_parquet_golden(cpacker, tmp_path, k):
     pytest.skip('reference raises for this case')
   sh, ids, ntok = shards_from_docs(case['docs'], case['ndoc'])
   res = cpacker.pack(sh, ids, ntok, target_seq_length=c['max_seq'], short_seq_prob=c['ssp'],
-                     duplicate_factor=c['dup'], seed=case['seed'], codebert=True)
+                     duplicate_factor=c['dup'], seed=case['seed'], codebert=True, spans=spans)
+  assert res.spans == spans
   doc_ids = ['py_%d' % d for d in range(len(case['docs']))]
   files = writer.write_shards(cpacker, res, str(tmp_path), codebert=True, doc_ids=doc_ids)
   assert [os.path.basename(f) for f in files] == ['part.0.parquet']
@@ -97,7 +101,8 @@ def test_codebert_parquet_golden(cpacker, tmp_path, k):
   assert got['num_tokens'] == [e['num_tokens'] for e in exp]
 
 
-def test_end_to_end_parquet_vs_oracle(gpu, tmp_path):
+@pytest.mark.parametrize('spans', [False, True])
+def test_end_to_end_parquet_vs_oracle(gpu, tmp_path, spans):
   """synthetic corpus, several partitions (some empty), binned seq 128:
   every file's rows equal the oracle's rendering of its pairs"""
   from lddl_amd import synth, pipeline, writer
@@ -107,7 +112,7 @@ def test_end_to_end_parquet_vs_oracle(gpu, tmp_path):
   pdo = np.concatenate([[0], pdo[:3], pdo[2:]])  # an empty partition (1 -> 2 ... duplicate cut)
   pk = pipeline.Packer(pipeline.VOCAB_BERT, 0)
   sh = pipeline.upload(c, pdo, gpu)
-  res = pk.run(sh, target_seq_length=128, bin_size=32, seed=99)
+  res = pk.run(sh, target_seq_length=128, bin_size=32, seed=99, spans=spans)
   files = writer.write_shards(pk, res, str(tmp_path), bin_size=32, batch_rows=500)
   assert len(files) == (len(pdo) - 1) * 4
   oids, ontok = OracleTokenizer(pipeline.VOCAB_BERT).run(c.data, c.sent_off, 512, nthreads=8)
