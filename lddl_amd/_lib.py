@@ -68,6 +68,8 @@ def lib():
       raise RuntimeError('liblddl_amd.so not built (%s); run python -m lddl_amd.build' % LIB_PATH)
     L = ctypes.CDLL(LIB_PATH)
     for name, (res, args) in SIGNATURES.items():
+      if os.environ.get('LDDL_LIB') and not hasattr(L, name):
+        continue  # an A/B build of an older revision (tools/ab_head.sh) lacks the newer entry points
       f = getattr(L, name)
       f.restype = res
       f.argtypes = args
