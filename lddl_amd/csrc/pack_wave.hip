@@ -456,7 +456,9 @@ __device__ __forceinline__ int range_sum_reg(int dps, int k0, int k1) {
 
 // LDSOK = false: every LDS capacity is 0 (the default), the arrays are in
 // global memory and the LDS/global branches compile away
-template <int MASK, bool LDSOK>
+// DBG: the phase stamps (LDDL_PACK_DEBUG=1) compiled in; the production
+// instantiations carry no per-pair test of P.dbg on the scalar unit
+template <int MASK, bool LDSOK, bool DBG>
 __global__ __launch_bounds__(64, PACK_OCC) void pack_bert_wave_kernel(PackParams P) {
   __shared__ PackWaveLds L;
   __shared__ typename std::conditional<MASK != 0, MaskLds<MASK == 1 ? 512 : MLM_MAX_SEQ>, NoMaskLds>::type ML;
@@ -479,16 +481,16 @@ __global__ __launch_bounds__(64, PACK_OCC) void pack_bert_wave_kernel(PackParams
   // optional phase stamps (wave-uniform branch): filter, LDS fill, seed,
   // pair generation, shuffle, binning; masking: candidates, shuffle draws,
   // pick trace, 80/10/10 choices, sorted writes
-  uint64_t ph[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, tprev = P.dbg ? __builtin_amdgcn_s_memtime() : 0;
+  uint64_t ph[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, tprev = DBG ? __builtin_amdgcn_s_memtime() : 0;
 // generate sub-phases of the unmasked packer reuse the masking slots 6-10
 #define PW_GSTAMP(k)                                    \
-  if (!MASK && P.dbg) {                                 \
+  if (!MASK && DBG) {                                   \
     const uint64_t t_ = __builtin_amdgcn_s_memtime();   \
     ph[k] += t_ - tprev;                                \
     tprev = t_;                                         \
   }
 #define PW_STAMP(k)                                     \
-  if (P.dbg) {                                          \
+  if (DBG) {                                            \
     const uint64_t t_ = __builtin_amdgcn_s_memtime();   \
     ph[k] += t_ - tprev;                                \
     tprev = t_;                                         \
@@ -961,7 +963,7 @@ __global__ __launch_bounds__(64, PACK_OCC) void pack_bert_wave_kernel(PackParams
     if (MASK) P.part_nmask[p] = macc;
   }
   PW_STAMP(5)
-  if (P.dbg && lane == 0) {
+  if (DBG && lane == 0) {
     for (int k = 0; k < 6; ++k) atomicAdd((unsigned long long*)&P.dbg[k], (unsigned long long)ph[k]);
     atomicAdd((unsigned long long*)&P.dbg[6], (unsigned long long)np);
     atomicAdd((unsigned long long*)&P.dbg[7], 1ull);
@@ -975,16 +977,22 @@ hipError_t launch_pack_bert_wave(const PackParams& P, hipStream_t s) {
   const size_t dyn = pack_dyn_bytes(P.cap_lens, P.cap_docs, P.cap_pairs, P.masking != 0);
   const bool lds = P.cap_lens > 0 || P.cap_docs > 0 || P.cap_pairs > 0;
   const dim3 g((unsigned)P.n_part), b(64);
+#define PW_LAUNCH(M, L)                                                                        \
+  do {                                                                                         \
+    if (P.dbg) hipLaunchKernelGGL((pack_bert_wave_kernel<M, L, true>), g, b, dyn, s, P);      \
+    else hipLaunchKernelGGL((pack_bert_wave_kernel<M, L, false>), g, b, dyn, s, P);           \
+  } while (0)
   if (P.masking && P.max_seq <= 512) {
-    if (lds) hipLaunchKernelGGL((pack_bert_wave_kernel<1, true>), g, b, dyn, s, P);
-    else hipLaunchKernelGGL((pack_bert_wave_kernel<1, false>), g, b, dyn, s, P);
+    if (lds) PW_LAUNCH(1, true);
+    else PW_LAUNCH(1, false);
   } else if (P.masking) {
-    if (lds) hipLaunchKernelGGL((pack_bert_wave_kernel<2, true>), g, b, dyn, s, P);
-    else hipLaunchKernelGGL((pack_bert_wave_kernel<2, false>), g, b, dyn, s, P);
+    if (lds) PW_LAUNCH(2, true);
+    else PW_LAUNCH(2, false);
   } else {
-    if (lds) hipLaunchKernelGGL((pack_bert_wave_kernel<0, true>), g, b, dyn, s, P);
-    else hipLaunchKernelGGL((pack_bert_wave_kernel<0, false>), g, b, dyn, s, P);
+    if (lds) PW_LAUNCH(0, true);
+    else PW_LAUNCH(0, false);
   }
+#undef PW_LAUNCH
   return hipGetLastError();
 }
 

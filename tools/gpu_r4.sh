@@ -27,9 +27,14 @@ for S in ${STEPS:-tests tok bench}; do
       timeout -k 10 600 python -u bench.py $BA $X > $OUT/$S.log 2>&1 || { echo "$S failed"; tail -20 $OUT/$S.log; exit 1; }
       tail -1 $OUT/$S.log > $OUT/$S.json
       python3 -c "import json; d=json.load(open('$OUT/$S.json')); print('$S', round(d['ms_per_step'],1), 'ms/step', round(d['value']/1e9,2), 'G tok/s', 'tok', {k: round(v,1) for k,v in d['tokenize_kernels_ms'].items()}, 'writer rows/s', round(d.get('parquet_writer',{}).get('rows_per_s',0)))" ;;
-    kt)
-      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/kt -o kt --output-format csv -- python -u bench.py $BA --parquet-parts 0 --steps 2 --warmup 1 > $OUT/kt.log 2>&1 || { echo "kernel trace failed"; tail -20 $OUT/kt.log; exit 1; }
-      f=$(find $OUT/kt -name '*kernel_stats.csv' | head -1); cp $f $OUT/kernel_stats.csv
-      cut -d, -f1-4 $OUT/kernel_stats.csv | head -14 ;;
+    kt|kthead)
+      # kthead: the same trace with LDDL_LIB=KTLIB (default ab/lib_head.so) and materialised rows
+      X=""; E=""; [ $S = kthead ] && { X="--rows materialize"; E="LDDL_LIB=$PWD/${KTLIB:-ab/lib_head.so}"; }
+      env $E timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/$S -o kt --output-format csv -- python -u bench.py --no-cpu-baseline --frontend-mb 0 $X --parquet-parts 0 --steps 2 --warmup 1 > $OUT/$S.log 2>&1 || { echo "kernel trace failed"; tail -20 $OUT/$S.log; exit 1; }
+      f=$(find $OUT/$S -name '*kernel_stats.csv' | head -1); cp $f $OUT/${S}_stats.csv
+      echo "== $S"; cut -d, -f1-4 $OUT/${S}_stats.csv | head -14 ;;
+    stamps)
+      LDDL_TOK_DEBUG=1 NOCHECK=1 timeout -k 10 200 python tools/tok_check.py 1024 5 > $OUT/stamps.log 2>&1 || { echo "stamps failed"; tail $OUT/stamps.log; exit 1; }
+      grep dbg $OUT/stamps.log | tail -1 ;;
   esac
 done
