@@ -418,7 +418,7 @@ def frontend_leg(mb):
     raw = os.path.getsize(os.path.join(d, 'wiki', 'en', 'a.txt'))
     a = preprocess.attach_args().parse_args(
         ['--wikipedia', os.path.join(d, 'wiki'), '--sentence-splitter', 'rules', '--sink', os.path.join(d, 'out'),
-         '--target-seq-length', '128', '--block-size', str(1 << 20), '--chunk-mb', '4', '--seed', '7',
+         '--target-seq-length', '128', '--block-size', '1M', '--chunk-mb', '4', '--seed', '7',
          '--split-workers', str(host_cpus()['share'])])
     t0 = time.perf_counter()
     files, t = preprocess.main(a)

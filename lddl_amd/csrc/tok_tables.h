@@ -200,15 +200,25 @@ inline int build_vocab_tables(const char* path, VocabTables& V, std::string& err
     const uint64_t key = hash_key(h, vlen[i], vcont[i]);
     V.bloom[(uint32_t)(key >> 40) & (BLOOM_WORDS - 1)] |= (1u << (key & 31)) | (1u << ((key >> 5) & 31));
   }
-  // v4 table: >= 2V buckets of two 32-B slots (load <= 1/4: a key outside
-  // its home bucket costs the WordPiece loop a dependent probe; tools/wp_sim.py),
-  // linear probing over buckets; Bloom filter over the same hashes (common.h vhash)
+  // v4 table: buckets of two 32-B slots, linear probing over buckets; Bloom
+  // filter over the same hashes (common.h vhash)
+  // The scan's whole-word probe reads only slot 0 of a word's home bucket
+  // (tokenize_split.hip): a vocab word displaced from it is not found there
+  // and costs a WordPiece record.  So the buckets are >= 8V (load <= 1/16:
+  // ~5 % of the whole-word keys collide instead of ~17 % at 2V; the table is
+  // read at a few thousand hot lines whatever its size) and every whole-word
+  // key (cont = 0, in vocab order: the frequent words first) is inserted
+  // before the "##" pieces, which the scan never looks up.
   uint32_t nbk = 1;
-  while (nbk < 2 * n) nbk <<= 1;
+  while (nbk < 8 * n) nbk <<= 1;
   V.vt.assign((size_t)nbk * 16, 0u);
   V.vbloom.assign(BLOOM_WORDS, 0u);
-  for (size_t i = 0; i < n; ++i) {
-    if (vlen[i] == 0) continue;
+  std::vector<size_t> order;
+  order.reserve(n);
+  for (int pass = 0; pass < 2; ++pass)
+    for (size_t i = 0; i < n; ++i)
+      if (vlen[i] != 0 && (uint32_t)vcont[i] == (uint32_t)pass) order.push_back(i);
+  for (size_t i : order) {
     uint32_t d[VKEY_DW] = {0, 0, 0, 0, 0, 0};
     memcpy(d, &pool[V.voff[i]], vlen[i] < 24 ? vlen[i] : 24);
     const uint32_t h = vhash(d, vlen[i], vcont[i]), bk = vbkey_of(d, vlen[i], vcont[i]);

@@ -64,9 +64,7 @@ __device__ __forceinline__ uint32_t xm_len(uint32_t e) { return (e >> 24) & 7u; 
 __device__ __forceinline__ uint32_t xm_act(uint32_t e) { return (e >> 27) & 3u; }
 enum : uint32_t { C_W = 1, C_I = 2, C_S = 4, C_D = 8, C_UP = 16, C_X = 32, C_CS = 64 };
 constexpr uint16_t U_EMPTY = 0xFFFEu, U_DEFER = 0xFFFFu;
-#ifndef LDDL_XPRE
-#define LDDL_XPRE 0
-#endif
+
 
 // per lane of the window (LDS, for the unit steps): the first break / dirty
 // byte in a later lane and the sentence starts before the lane
@@ -96,10 +94,6 @@ struct alignas(16) Lds {
   uint8_t xlen[XCAP];          // their number
   int32_t misc[4];             // 0 side-buffer cursor, 1 #markers
   uint32_t sspec[2];           // sentences holding a [CLS] / [SEP] token (P.sent_spec)
-#if LDDL_XPRE
-  uint32_t xpre[64];           // the next tile's first 64 UTF-8 lead bytes: listed positions (u16), then
-                               // their fast exception entries (xmap, LDS-DMA issued during this tile)
-#endif
 };
 
 // SCAN_OCC 4-wave blocks per CU (+ the 256-B class table): SCAN_OCC waves per SIMD
@@ -348,7 +342,6 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
   int64_t n_sa = 0, n_sb = 0, n_A = 0, n_B = 0, n_spos = 0;
   int nst = 0;
   bool dma_pending = false;  // raw-byte DMA issued and not yet waited for
-  bool xpre_next = false, xpre_cur = false;  // (LDDL_XPRE) the next / this tile's lead-byte entries are in L.xpre
   int64_t tn = S.t0 + (int64_t)blockIdx.x * WAVES + wv;
   // (LDS-DMA: lane i of the instruction writes dword i at the LDS base)
   auto dma4 = [&](const void* g, uint32_t* l) {
@@ -399,10 +392,8 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
     stage2();
     const int64_t sa = n_sa, sb = n_sb, A = n_A, B = n_B, spos = n_spos;
     STAMP(0);
-    if (dma_pending) drain();  // this tile's raw bytes (and its prefetched exception entries)
+    if (dma_pending) drain();  // this tile's raw bytes
     dma_pending = false;
-    xpre_cur = xpre_next;
-    xpre_next = false;
     nst = 0;
     tn = t + nwaves;
     stage1();
@@ -550,13 +541,6 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
           const int p = k < nl ? (int)xl[k] : 0;
           uint32_t e = XM_SLOW, n = 0;
           bool brk = false;
-#if LDDL_XPRE
-          // the first 64 listed exceptions' lead bytes in order are the
-          // prefetched ones: entry = xpre[rank among this batch's lead bytes]
-          const bool from_pre = xpre_cur && kb == 0 && k0 == 0;
-          const uint32_t b0 = k < nl ? rawb(L, p) : 0u;
-          const int lrank = lane_rank(__ballot(b0 >= 0xC0u));
-#endif
           if (k < nl) {
             const uint32_t b = rawb(L, p);
             if (b == '[') {
@@ -566,12 +550,7 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
               uint32_t cp = b & (0x3Fu >> (n - 1));
               for (uint32_t q = 1; q < n; ++q) cp = (cp << 6) | (rawb(L, p + (int)q) & 0x3Fu);
               if (cp > 0x10FFFF) cp = 0xFFFD;
-#if LDDL_XPRE
-              if (from_pre) e = L.xpre[lrank];
-              else e = P.xmap[cp];
-#else
               e = P.xmap[cp];
-#endif
             }
           }
           if (DBG) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1020,53 +999,6 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
           cur += need;
           wsync();
           STAMP(8);
-#if LDDL_XPRE
-          if (rb == 0 && r == 0 && dma_pending && !xpre_next) {
-            // the next tile's raw bytes (stage2's DMA, issued before this
-            // step) are in rp: list its UTF-8 lead bytes and fetch their fast
-            // exception entries by LDS-DMA into xpre, so the next tile's
-            // exception pass reads them from LDS instead of a global round trip
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            const int aoff_n = (int)(reinterpret_cast<uintptr_t>(P.bytes + n_A) & 15u);
-            const int nb_n = (int)((n_B - n_A) + aoff_n);
-            const int ln = lane_here(), q0 = ln * 32;
-            uint32_t lead = 0;
-            if (q0 < nb_n) {
-              const uint4 v0 = *reinterpret_cast<const uint4*>(&L.rp[ln * 8]);
-              const uint4 v1 = *reinterpret_cast<const uint4*>(&L.rp[ln * 8 + 4]);
-              const uint32_t wv8[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-#pragma unroll
-              for (int j = 0; j < 8; ++j) {
-                const uint32_t hi = wv8[j] & (wv8[j] << 1) & 0x80808080u;  // bit 7 of bytes >= 0xC0
-                lead |= ((((hi >> 7) * 0x00204081u) >> 21) & 0xFu) << (4 * j);
-              }
-              const int wlo = min(max(aoff_n - q0, 0), 32), whi = min(max(nb_n - q0, 0), 32);
-              lead &= (whi >= 32 ? ~0u : ((1u << whi) - 1u)) & (wlo >= 32 ? 0u : ~((1u << wlo) - 1u));
-            }
-            const uint32_t cl = (uint32_t)__popc(lead);
-            const uint32_t pl = wave_incl_add(cl) - cl;
-            uint16_t* const xpl = reinterpret_cast<uint16_t*>(L.xpre);
-            {
-              uint32_t kk = pl;
-              for (uint32_t m = lead; m && kk < 64; m &= m - 1, ++kk) xpl[kk] = (uint16_t)(q0 + __ffs(m) - 1);
-            }
-            wsync();
-            const uint32_t tot = min(lane_get(pl + cl, 63), 64u);
-            const int pp = ln < (int)tot ? (int)xpl[ln] : 0;
-            uint32_t cp = 0;
-            if (ln < (int)tot) {
-              const uint32_t b = rawb(L, pp);
-              const uint32_t n = (uint32_t)utf8_len(b);
-              cp = b & (0x3Fu >> (n - 1));
-              for (uint32_t q = 1; q < n; ++q) cp = (cp << 6) | (rawb(L, pp + (int)q) & 0x3Fu);
-              if (cp > 0x10FFFF) cp = 0xFFFD;
-            }
-            wsync();  // (every lane has read its position before the entries overwrite them)
-            if (ln < (int)tot)
-              __builtin_amdgcn_global_load_lds(P.xmap + cp, (__attribute__((address_space(3))) uint32_t*)L.xpre, 4, 0, 0);
-            xpre_next = true;
-          }
-#endif
         }
       }
       if (ovf) break;

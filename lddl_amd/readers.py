@@ -113,19 +113,24 @@ def _line_spans(buf, crlf_only):
   n = len(buf)
   if n == 0:
     return np.zeros(0, np.int64), np.zeros(0, np.int64)
+  lf = np.flatnonzero(buf == 10)
   if crlf_only:
-    t = np.flatnonzero((buf[:-1] == 13) & (buf[1:] == 10))
+    t = lf[lf > 0]
+    t = t[buf[t - 1] == 13] - 1  # the CR of each CR LF pair
     tl = np.full(len(t), 2, np.int64)
   else:
-    cr = buf == 13
-    lf = buf == 10
-    lone_lf = lf.copy()
-    lone_lf[1:] &= ~cr[:-1]
-    t = np.flatnonzero(cr | lone_lf)
-    tl = np.ones(len(t), np.int64)
-    if len(t):
-      crlf = cr[t] & np.concatenate([lf[1:], [False]])[t]
-      tl[crlf] = 2
+    # universal newlines: CR LF, lone CR and lone LF each end a line (one
+    # pass for each terminator byte; CRs are rare in practice)
+    cr = np.flatnonzero(buf == 13)
+    if len(cr):
+      lone_lf = lf[~np.isin(lf - 1, cr)]
+      t = np.sort(np.concatenate([cr, lone_lf]))
+      tl = np.ones(len(t), np.int64)
+      nxt = np.minimum(t + 1, n - 1)
+      tl[(buf[t] == 13) & (buf[nxt] == 10) & (t + 1 < n)] = 2
+    else:
+      t = lf
+      tl = np.ones(len(t), np.int64)
   starts = np.concatenate([[0], t + tl]).astype(np.int64)
   ends = np.concatenate([t, [n]]).astype(np.int64)
   if starts[-1] >= n:  # the text ends with a terminator: no final line
@@ -139,13 +144,21 @@ def _strip_spans(buf, starts, ends):
   last non-ASCII-space byte is non-ASCII is decoded to strip Unicode spaces."""
   if len(starts) == 0:
     return np.zeros(0, np.int64), np.zeros(0, np.int64)
-  nz = np.flatnonzero(~_ASCII_WS[buf])
-  i0 = np.searchsorted(nz, starts)
-  i1 = np.searchsorted(nz, ends) - 1
-  keep = i0 <= i1
-  s = np.where(keep, nz[np.minimum(i0, len(nz) - 1)] if len(nz) else 0, 0)
-  e = np.where(keep, nz[np.maximum(i1, 0)] + 1 if len(nz) else 0, 0)
-  off, ln = s[keep].astype(np.int64), (e - s)[keep].astype(np.int64)
+  # ASCII whitespace at the span edges, peeled one byte per round over the
+  # spans that still have some (almost none: no pass over every byte)
+  s, e = starts.astype(np.int64).copy(), ends.astype(np.int64).copy()
+  act = np.flatnonzero(s < e)
+  while len(act):
+    act = act[_ASCII_WS[buf[s[act]]]]
+    s[act] += 1
+    act = act[s[act] < e[act]]
+  act = np.flatnonzero(s < e)
+  while len(act):
+    act = act[_ASCII_WS[buf[e[act] - 1]]]
+    e[act] -= 1
+    act = act[s[act] < e[act]]
+  keep = s < e
+  off, ln = s[keep], (e - s)[keep]
   if len(off):
     # a line may start or end with a Unicode space (str.isspace beyond ASCII:
     # U+0085, U+00A0 lead 0xC2; U+1680, U+2000-U+205F, U+3000 lead 0xE1-0xE3)
