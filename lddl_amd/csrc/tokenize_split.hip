@@ -190,17 +190,24 @@ __device__ int dirty_normalize(Lds& L, const TokParams& P, int p, int q, int* sr
     *src = p;
     return o - p;
   }
+  // (dword reads here too: one LDS round trip per 4 bytes instead of one per
+  // byte; a marker's index byte may sit in the next dword: `skip` carries it)
   int len = 0;
-  for (int i = p; i < q;) {
-    const uint32_t b = nbyte(L.nb, i);
-    if (b == BF) {
-      ++i;
-    } else if (b == BX) {
-      len += L.xlen[nbyte(L.nb, i + 1)];
-      i += 2;
-    } else {
-      ++len;
-      ++i;
+  bool skip = false;
+  for (int a = p & ~3; a < q; a += 4) {
+    const uint32_t v = L.nb[a >> 2];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t b = (v >> (8 * k)) & 0xFFu;
+      if (a + k < p || a + k >= q) continue;
+      if (skip) {
+        len += L.xlen[b];
+        skip = false;
+      } else if (b == BX) {
+        skip = true;
+      } else if (b != BF) {
+        ++len;
+      }
     }
   }
   if (len == 0) return 0;
@@ -208,19 +215,25 @@ __device__ int dirty_normalize(Lds& L, const TokParams& P, int p, int q, int* sr
   if (off + len > DCAP) return -1;
   int o = CAP + off;
   *src = o;
-  for (int i = p; i < q;) {
-    const uint32_t b = nbyte(L.nb, i);
-    if (b == BF) {
-      ++i;
-    } else if (b == BX) {
-      // (the marker's bytes, encoded when the exception pass placed it: no
-      // table load here)
-      const int x = (int)nbyte(L.nb, i + 1), nx = L.xlen[x];
-      for (int t = 0; t < nx; ++t) nput(L.nb, o++, nbyte(L.xrep, 12 * x + t));
-      i += 2;
-    } else {
-      nput(L.nb, o++, b);
-      ++i;
+  // (the side buffer lies past CAP, beyond every span read here)
+  skip = false;
+  for (int a = p & ~3; a < q; a += 4) {
+    const uint32_t v = L.nb[a >> 2];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t b = (v >> (8 * k)) & 0xFFu;
+      if (a + k < p || a + k >= q) continue;
+      if (skip) {
+        // (the marker's bytes, encoded when the exception pass placed it: no
+        // table load here)
+        const int nx = L.xlen[b];
+        for (int t = 0; t < nx; ++t) nput(L.nb, o++, nbyte(L.xrep, 12 * (int)b + t));
+        skip = false;
+      } else if (b == BX) {
+        skip = true;
+      } else if (b != BF) {
+        nput(L.nb, o++, b);
+      }
     }
   }
   return len;

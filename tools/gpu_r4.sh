@@ -30,7 +30,7 @@ for S in ${STEPS:-tests tok bench}; do
     kt|kthead)
       # kthead: the same trace with LDDL_LIB=KTLIB (default ab/lib_head.so) and materialised rows
       X=""; E=""; [ $S = kthead ] && { X="--rows materialize"; E="LDDL_LIB=$PWD/${KTLIB:-ab/lib_head.so}"; }
-      env $E timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/$S -o kt --output-format csv -- python -u bench.py --no-cpu-baseline --frontend-mb 0 $X --parquet-parts 0 --steps 2 --warmup 1 > $OUT/$S.log 2>&1 || { echo "kernel trace failed"; tail -20 $OUT/$S.log; exit 1; }
+      env $E timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/$S -o kt --output-format csv -- python -u bench.py $BA --frontend-mb 0 $X --parquet-parts 0 --steps 2 --warmup 1 > $OUT/$S.log 2>&1 || { echo "kernel trace failed"; tail -20 $OUT/$S.log; exit 1; }
       f=$(find $OUT/$S -name '*kernel_stats.csv' | head -1); cp $f $OUT/${S}_stats.csv
       echo "== $S"; cut -d, -f1-4 $OUT/${S}_stats.csv | head -14 ;;
     stamps)
