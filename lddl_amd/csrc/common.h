@@ -74,32 +74,17 @@ LDDL_HD uint32_t vfinal(uint32_t h, uint32_t len, uint32_t cont) {
   h ^= h >> 15;
   return h;
 }
-#ifndef LDDL_VH3
-#define LDDL_VH3 0
-#endif
-#if LDDL_VH3
-// Bucket index over the first 12 bytes (three dwords, zero past the key),
-// the byte length and the "##" flag: always three mixes, so the scan's
-// whole-word probe hashes a key without selecting among prefix mixes (no
-// two keys of either vocab share their first 12 bytes, length and flag:
-// the probe sequences stay as short as over 24 bytes).
+// Bucket index of a candidate piece: its first 12 bytes (three dwords, zero
+// past the key), its byte length and the "##" flag -- always three mixes, so
+// the scan's whole-word probe hashes a key without selecting among prefix
+// mixes (no two keys of either vocab share their first 12 bytes, length and
+// flag).  The WordPiece loop re-hashes a shorter candidate from the same
+// three dwords (its prefix mix H3 for >= 12 bytes).
 LDDL_HD uint32_t vmask_rem(uint32_t d, int rem) { return rem >= 4 ? d : rem <= 0 ? 0u : d & ((1u << (8 * rem)) - 1u); }
 LDDL_HD uint32_t vhash(const uint32_t* d, uint32_t len, uint32_t cont) {
   const int l = (int)len;
   return vfinal(vmix(vmix(vmix(VSEED, vmask_rem(d[0], l)), vmask_rem(d[1], l - 4)), vmask_rem(d[2], l - 8)), len, cont);
 }
-#else
-// Prefix-structured, so a kernel holding the mixes of the first k dwords of
-// a candidate re-hashes any shorter candidate with one mix: full dwords, then
-// the masked tail dword (only if len % 4), over the first 24 bytes.
-LDDL_HD uint32_t vhash(const uint32_t* d, uint32_t len, uint32_t cont) {
-  const uint32_t l = len < 24u ? len : 24u, q = l >> 2, r = l & 3u;
-  uint32_t h = VSEED;
-  for (uint32_t k = 0; k < q; ++k) h = vmix(h, d[k]);
-  if (r) h = vmix(h, d[q] & ((1u << (8 * r)) - 1u));
-  return vfinal(h, len, cont);
-}
-#endif
 // low 32 bits of the product of the low 24 bits of a and b (v_mul_u32_u24,
 // full rate; a 32-bit v_mul_lo_u32 is quarter rate)
 LDDL_HD uint32_t mul24(uint32_t a, uint32_t b) {

@@ -277,18 +277,7 @@ __device__ __forceinline__ uint32_t opq(uint32_t x) {
 // == vhash (common.h) of a loaded key; branch-free: the six mixes, then the
 // one of the key's length selected (a branch per dword diverges across lanes)
 __device__ __forceinline__ uint32_t key_hash(const Key6& k, int len, uint32_t cont) {
-#if LDDL_VH3
   return vfinal(vmix(vmix(vmix(VSEED, k.d0), k.d1), k.d2), (uint32_t)len, cont);  // (key dwords zero past len)
-#else
-  const int lc = min(len, 24);
-  // (opaque: LLVM otherwise sinks each mix into a branch on lc, divergent
-  // across the step's lanes: scan 3.49 -> 3.46 ms per GiB)
-  const uint32_t h1 = opq(vmix(VSEED, k.d0)), h2 = opq(vmix(h1, k.d1)), h3 = opq(vmix(h2, k.d2)),
-                 h4 = opq(vmix(h3, k.d3)), h5 = opq(vmix(h4, k.d4)), h6 = opq(vmix(h5, k.d5));
-  uint32_t h = lc > 20 ? h6 : lc > 16 ? h5 : lc > 12 ? h4 : lc > 8 ? h3 : lc > 4 ? h2 : h1;
-  if (lc <= 0) h = VSEED;
-  return vfinal(h, (uint32_t)len, cont);
-#endif
 }
 // branch-free (an && chain lets the compiler sink the slot's other loads
 // behind the first compare: a second dependent round trip on every hit)
@@ -1115,15 +1104,8 @@ __global__ __launch_bounds__(64 * WAVES) void wp_kernel(TokParams P, SplitParams
   auto selH = [&](int q) { return q <= 0 ? H0 : q == 1 ? H1 : q == 2 ? H2 : q == 3 ? H3 : q == 4 ? H4 : q == 5 ? H5 : H6; };
   auto selD = [&](int q) { return q <= 0 ? c0 : q == 1 ? c1 : q == 2 ? c2 : q == 3 ? c3 : q == 4 ? c4 : c5; };
   auto hash_len = [&](int l) {  // == vhash of the candidate [s, s+l)
-#if LDDL_VH3
     const uint32_t h = l >= 12 ? H3 : vmix(vmix(vmix(VSEED, vmask_rem(c0, l)), vmask_rem(c1, l - 4)), vmask_rem(c2, l - 8));
     return vfinal(h, (uint32_t)l, cont);
-#else
-    const int lc = min(l, 24), q = lc >> 2, rr = lc & 3;
-    uint32_t h = selH(q);
-    if (rr) h = vmix(h, selD(q) & ((1u << (8 * rr)) - 1u));
-    return vfinal(h, (uint32_t)l, cont);
-#endif
   };
   auto bkey_len = [&](int l) {  // == vbkey of the candidate [s, s+l)
     const int lc = min(l, 24), q = lc >> 2, rr = lc & 3;
