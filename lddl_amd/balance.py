@@ -243,7 +243,9 @@ def write_shards(shards, outdir, rank=0, world=1, compression='snappy'):
       raise ValueError('shard %s has no rows' % name)
     assert t.num_rows == n, (name, t.num_rows, n)
     path = os.path.join(outdir, name)
-    pq.write_table(t, path, compression=compression)
+    from .writer import DENSE_COLS
+    pq.write_table(t, path, compression=compression,
+                   use_dictionary=[c for c in t.schema.names if c not in DENSE_COLS])
     written.append(path)
   return written
 

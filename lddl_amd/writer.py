@@ -34,6 +34,7 @@ from . import _lib
 from .tokenizer import _ptr, _stream
 
 SEG0, SEG1, ROW, SPAN = 0, 1, 2, 3
+DENSE_COLS = ('A', 'B', 'doc', 'code', 'masked_lm_positions', 'masked_lm_labels')
 
 BERT_SCHEMA = [('A', pa.string()), ('B', pa.string()), ('is_random_next', pa.bool_()),
                ('num_tokens', pa.uint16())]
@@ -194,6 +195,10 @@ def write_shards(packer, res, out_dir, bin_size=None, codebert=False, masking=Fa
   np.cumsum(file_rows, out=file_start[1:])
   assert file_start[-1] == res.n_pairs, (file_start[-1], res.n_pairs)
   sch = schema(codebert, masking and not codebert, binned)
+  # dictionary pages only where values repeat (flags, lengths, bins, the
+  # CodeBERT id of a document's rows): the segment / label strings are unique
+  # per row and the encoder would build and then discard a dictionary for them
+  dict_cols = [n_ for n_ in sch.names if n_ not in DENSE_COLS]
   nfiles = len(file_rows) if max_parts is None else min(len(file_rows), max_parts * nbins)
   n_rows = int(file_start[nfiles])  # rows of the files written
   num_tokens = np.diff(res.tok_off[:n_rows + 1].cpu().numpy()).astype(np.uint16)
@@ -250,7 +255,7 @@ def write_shards(packer, res, out_dir, bin_size=None, codebert=False, masking=Fa
       if binned:
         name += '_%d' % b
       path = os.path.join(out_dir, name)
-      mine.append(pool.submit(pq.write_table, t, path, compression=compression))
+      mine.append(pool.submit(pq.write_table, t, path, compression=compression, use_dictionary=dict_cols))
       files.append(path)
     # the parquet encoder releases the GIL: files of a batch encode in
     # parallel on the host cores while the next batch renders on the GPU
