@@ -395,7 +395,7 @@ def parquet_sample(args, pk, res, sh):
     shutil.rmtree(d, ignore_errors=True)
 
 
-def frontend_leg(mb):
+def frontend_leg(mb, chunk_mb=32.0):
   """The preprocessor CLI end to end (lddl_amd.preprocess.main, the
   reference's preprocess_bert_pretrain) on BASELINE.json configs[0]: mb MB of
   synthetic Wikipedia-style raw input (one ``wiki-<id> <text>`` document per
@@ -418,7 +418,7 @@ def frontend_leg(mb):
     raw = os.path.getsize(os.path.join(d, 'wiki', 'en', 'a.txt'))
     a = preprocess.attach_args().parse_args(
         ['--wikipedia', os.path.join(d, 'wiki'), '--sentence-splitter', 'rules', '--sink', os.path.join(d, 'out'),
-         '--target-seq-length', '128', '--block-size', '1M', '--chunk-mb', '4', '--seed', '7',
+         '--target-seq-length', '128', '--block-size', '1M', '--chunk-mb', str(chunk_mb), '--seed', '7',
          '--split-workers', str(host_cpus()['share'])])
     t0 = time.perf_counter()
     files, t = preprocess.main(a)

@@ -111,6 +111,44 @@ __device__ __attribute__((noinline)) void pack_mt_refill(lds_u32* mt, int lane) 
 }
 
 // ---- CPython MT19937 with the state in LDS -----------------------------
+// init_by_array starts from init_genrand(19650218) whatever the seed: that
+// state is a compile-time table
+struct MtTable {
+  uint32_t v[MT_N];
+};
+constexpr MtTable mt_genrand_table(uint32_t s) {
+  MtTable t{};
+  t.v[0] = s;
+  for (int i = 1; i < MT_N; ++i) t.v[i] = 1812433253u * (t.v[i - 1] ^ (t.v[i - 1] >> 30)) + (uint32_t)i;
+  return t;
+}
+__constant__ MtTable kMtGenrand = mt_genrand_table(19650218u);
+
+// init_by_array's chain over positions [base + l0, base + l1) (l0 even,
+// l1 - l0 even): the positions' old words one per lane (src), the chain's
+// carried word mt[i-1] in `prev`, the new words written back lane-wise (no
+// LDS round trip per step).  PASS 1: mt[i] = (mt[i] ^ f(mt[i-1]) * 1664525)
+// + key[j] + j, j = (i - 1) % klen (klen <= 2; base is even, so position
+// base + l adds kb for even l, ka for odd l); PASS 2: mt[i] = (mt[i] ^
+// f(mt[i-1]) * 1566083941) - i.
+template <int PASS>
+__device__ __forceinline__ uint32_t mt_seed_run(uint32_t src, int base, int l0, int l1, uint32_t& prev, uint32_t ka,
+                                                uint32_t kb, int lane) {
+  uint32_t out = src;
+  auto step = [&](int l, uint32_t add) {
+    const uint32_t old = (uint32_t)__builtin_amdgcn_readlane((int)src, l);
+    const uint32_t f = prev ^ (prev >> 30);
+    prev = PASS == 1 ? (old ^ (f * 1664525u)) + add : (old ^ (f * 1566083941u)) - (uint32_t)(base + l);
+    out = lane == l ? prev : out;
+  };
+#pragma unroll 2
+  for (int l = l0; l < l1; l += 2) {
+    step(l, kb);
+    step(l + 1, ka);
+  }
+  return out;
+}
+
 struct WaveRng {
   PackWaveLds& L;
   int lane;
@@ -119,26 +157,47 @@ struct WaveRng {
   int wend = 0;       // min(wbase + 64, MT_N): draws below it come from `win`
   uint32_t win = 0;
 
+  // random.seed(n) for 0 <= n < 2^64: init_by_array(key = n's 32-bit words,
+  // klen <= 2).  Its first loop visits positions 1..623 then 1 again (MT_N
+  // steps), its second 2..623 then 1 (MT_N - 1 steps); mt[i-1] of position 1
+  // is mt[0] = the new mt[623], i.e. the chain's carried word; mt[0] ends as
+  // 0x80000000.
   __device__ __forceinline__ void seed(uint64_t n) {
-    if (lane == 0) {
-      uint32_t* mt = L.mt;
-      uint32_t key[2] = {(uint32_t)n, (uint32_t)(n >> 32)};
-      const int klen = (n >> 32) ? 2 : 1;
-      mt[0] = 19650218u;
-      for (int i = 1; i < MT_N; ++i) mt[i] = 1812433253u * (mt[i - 1] ^ (mt[i - 1] >> 30)) + (uint32_t)i;
-      int i = 1, j = 0;
-      for (int k = MT_N > klen ? MT_N : klen; k; --k) {
-        mt[i] = (mt[i] ^ ((mt[i - 1] ^ (mt[i - 1] >> 30)) * 1664525u)) + key[j] + (uint32_t)j;
-        ++i; ++j;
-        if (i >= MT_N) { mt[0] = mt[MT_N - 1]; i = 1; }
-        if (j >= klen) j = 0;
-      }
-      for (int k = MT_N - 1; k; --k) {
-        mt[i] = (mt[i] ^ ((mt[i - 1] ^ (mt[i - 1] >> 30)) * 1566083941u)) - (uint32_t)i;
-        ++i;
-        if (i >= MT_N) { mt[0] = mt[MT_N - 1]; i = 1; }
-      }
-      mt[0] = 0x80000000u;
+    const uint32_t ka = (uint32_t)n;                                // j = 0: key[0] + 0
+    const uint32_t kb = (n >> 32) ? (uint32_t)(n >> 32) + 1u : ka;  // j = 1 (klen 2): key[1] + 1
+    uint32_t* mt = L.mt;
+    constexpr int NC = (MT_N + 63) / 64;
+    // first loop: position 1 (j = 0), then 2..623, then 1 again
+    uint32_t prev;
+    {
+      const uint32_t f = 19650218u ^ (19650218u >> 30);  // init_genrand's mt[0]
+      prev = (kMtGenrand.v[1] ^ (f * 1664525u)) + ka;
+    }
+    const uint32_t m1a = prev;
+    for (int c = 0; c < NC; ++c) {
+      const int i = 64 * c + lane;
+      uint32_t w = kMtGenrand.v[min(i, MT_N - 1)];
+      w = mt_seed_run<1>(w, 64 * c, c == 0 ? 2 : 0, min(64, MT_N - 64 * c), prev, ka, kb, lane);
+      if (i < MT_N) mt[i] = w;
+    }
+    uint32_t m1;
+    {  // step MT_N: position 1 again, j = (MT_N - 1) % klen -> kb
+      const uint32_t f = prev ^ (prev >> 30);
+      m1 = (m1a ^ (f * 1664525u)) + kb;
+      prev = m1;
+    }
+    // second loop: positions 2..623, then 1 (each lane re-reads only what it wrote)
+    for (int c = 0; c < NC; ++c) {
+      const int i = 64 * c + lane;
+      uint32_t w = mt[min(i, MT_N - 1)];
+      w = mt_seed_run<2>(w, 64 * c, c == 0 ? 2 : 0, min(64, MT_N - 64 * c), prev, ka, kb, lane);
+      if (i < MT_N) mt[i] = w;
+    }
+    {
+      const uint32_t f = prev ^ (prev >> 30);
+      const uint32_t p1 = (m1 ^ (f * 1566083941u)) - 1u;
+      if (lane == 0) mt[0] = 0x80000000u;
+      if (lane == 1) mt[1] = p1;
     }
     wsync();
     idx = MT_N;
@@ -622,6 +681,25 @@ __global__ __launch_bounds__(64, PACK_OCC) void pack_bert_wave_kernel(PackParams
     return n <= 64 && lane < n ? len_at(f + lane) : 0;
   };
   int dl_next = nd > 0 ? doc_lens(0) : 0;
+  // the records of the current 64 pairs, one per lane (lane k = pair
+  // (np & ~63) + k), written by one coalesced flush per 64 pairs: each pair's
+  // fields are selected into these columns by the vector unit instead of
+  // being packed, addressed and stored by lane 0 from scalar registers
+  int c_fs0 = 0, c_fs1 = 0, c_lo0 = 0, c_hi0 = 0, c_lo1 = 0, c_hi1 = 0, c_n0 = 0, c_n1 = 0, c_rn = 0;
+  auto flush = [&](int b, int cnt) {
+    if (lane < cnt) {
+      PairRec q;
+      q.fs0 = s0 + c_fs0;
+      q.fs1 = s0 + c_fs1;
+      q.lo0 = (uint16_t)c_lo0; q.hi0 = (uint16_t)c_hi0;
+      q.lo1 = (uint16_t)c_lo1; q.hi1 = (uint16_t)c_hi1;
+      q.n0 = (uint16_t)c_n0; q.n1 = (uint16_t)c_n1;
+      q.flags = (uint16_t)(c_rn | 2);
+      q.num_tokens = (uint16_t)((c_hi0 - c_lo0) + (c_hi1 - c_lo1) + 3);
+      out[b + lane] = q;
+      if (b + lane < pcap) D.ntk[b + lane] = q.num_tokens;
+    }
+  };
   for (int dup = 0; dup < P.dup && !err; ++dup) {
     for (int di = 0; di < nd && !err; ++di) {
       const int first = doc_first(di), len = doc_n(di);
@@ -696,11 +774,13 @@ __global__ __launch_bounds__(64, PACK_OCC) void pack_bert_wave_kernel(PackParams
           const int t = t0 + lane;
           bool sideA = d0l > 0 ? (t < d0l ? true : ((t - d0l) & 1) != 0) : (t < nb0 ? false : ((t - nb0) & 1) == 0);
           const bool front = lane < n ? (WaveRng::temper(L.mt[rng.idx + 2 * lane]) >> 31) == 0 : false;
-          const bool act = lane < n;
-          alo += __popcll(__ballot(act && sideA && front));
-          ahi -= __popcll(__ballot(act && sideA && !front));
-          blo += __popcll(__ballot(act && !sideA && front));
-          bhi -= __popcll(__ballot(act && !sideA && !front));
+          // two ballots: the n steps' A side (SA) and front (F) masks
+          const uint64_t SA = __ballot(lane < n && sideA), F = __ballot(front);
+          const int x = __popcll(SA & F), a = __popcll(SA), f = __popcll(F);
+          alo += x;
+          ahi -= a - x;
+          blo += f - x;
+          bhi -= n - a - f + x;
           rng.idx += 2 * n;
           t0 += n;
           E -= n;
@@ -874,17 +954,27 @@ __global__ __launch_bounds__(64, PACK_OCC) void pack_bert_wave_kernel(PackParams
           wsync();
           PW_STAMP(10)
         }
-        if (lane == 0) {
-          out[np] = r;
-          if (np < pcap) D.ntk[np] = r.num_tokens;
-          if (MASK) P.mref[pb + np] = mref;
+        {
+          const bool me = lane == (np & 63);
+          c_fs0 = me ? (int)(r.fs0 - s0) : c_fs0;
+          c_fs1 = me ? (int)(r.fs1 - s0) : c_fs1;
+          c_lo0 = me ? alo : c_lo0;
+          c_hi0 = me ? ahi : c_hi0;
+          c_lo1 = me ? blo : c_lo1;
+          c_hi1 = me ? bhi : c_hi1;
+          c_n0 = me ? (int)r.n0 : c_n0;
+          c_n1 = me ? (int)r.n1 : c_n1;
+          c_rn = me ? (rn ? 1 : 0) : c_rn;
         }
+        if (MASK && lane == 0) P.mref[pb + np] = mref;
         ++np;
+        if ((np & 63) == 0) flush(np - 64, 64);
         i = i_next;
         PW_GSTAMP(10)
       }
     }
   }
+  if (!err && (np & 63)) flush(np & ~63, np & 63);
   PW_STAMP(3)
   if (lane == 0) P.part_err[p] = err;
   if (err) {
@@ -1039,8 +1129,9 @@ __device__ __forceinline__ void trunc_seq_wave(WaveRng& rng, PackWaveLds& L, int
     const int n = min(min(E, 64), avail);
     const bool act = lane < n;
     const bool front = act ? (WaveRng::temper(L.mt[rng.idx + 2 * lane]) >> 31) == 0 : false;
-    lo += __popcll(__ballot(act && front));
-    hi -= __popcll(__ballot(act && !front));
+    const int f = __popcll(__ballot(front));  // (front is false past the n steps)
+    lo += f;
+    hi -= n - f;
     rng.idx += 2 * n;
     E -= n;
   }

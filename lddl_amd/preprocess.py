@@ -363,9 +363,47 @@ def _split_worker(a, b):
   recs = _FE['index'].texts(_FE['order'][a:b])
   corpus, ids = split_records(recs, _FE['codebert'], _FE['split'])
   if _FE['codebert']:  # the writer's id column, built here in the worker, off the writer's path
-    import pyarrow as pa
-    ids = pa.array(ids, type=pa.string())
+    from .writer import str_array
+    ids = str_array(ids)
   return corpus, ids, time.perf_counter() - ts
+
+
+def chunk_pieces(part_end, lo, a, b, n):
+  """partitions [a, b) cut into about n runs of ~equal bytes (whole
+  partitions); part_end[p - lo] = bytes up to the end of partition p"""
+  start = lambda q: int(part_end[q - 1 - lo]) if q > lo else 0
+  if n <= 1 or b - a < 2:
+    return [(a, b)]
+  want = max(1, -(-(int(part_end[b - 1 - lo]) - start(a)) // n))
+  out, s = [], a
+  for q in range(a, b):
+    if q + 1 == b or int(part_end[q - lo]) - start(s) >= want:
+      out.append((s, q + 1))
+      s = q + 1
+  return out
+
+
+def concat_corpora(corpora, ids):
+  """one synth.Corpus and doc-id list / Arrow array of consecutive pieces"""
+  if len(corpora) == 1:
+    return corpora[0], ids[0]
+  data = np.concatenate([c.data[c.sent_off[0]:c.sent_off[-1]] for c in corpora])
+  so, dso = [np.zeros(1, np.int64)], [np.zeros(1, np.int64)]
+  nb = ns = 0
+  for c in corpora:
+    so.append(c.sent_off[1:] - c.sent_off[0] + nb)
+    dso.append(c.doc_sent_off[1:] - c.doc_sent_off[0] + ns)
+    nb += c.nbytes
+    ns += c.n_sent
+  nseg = None
+  if corpora[0].doc_nseg_doc is not None:
+    nseg = np.concatenate([c.doc_nseg_doc for c in corpora])
+  if isinstance(ids[0], list):
+    all_ids = [x for i in ids for x in i]
+  else:
+    import pyarrow as pa
+    all_ids = pa.concat_arrays(ids)
+  return synth.Corpus(data, np.concatenate(so), np.concatenate(dso), nseg), all_ids
 
 
 def input_files(args, codebert=False):
@@ -474,7 +512,9 @@ def main(args, codebert=False):
       sw = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
       sw = os.cpu_count() or 1
-  nw = min(max(0, sw), len(todo)) if len(todo) > 1 else 0
+  # (a chunk's pieces are whole partitions: no more workers than partitions to split)
+  n_todo = sum(chunks[c][1] - chunks[c][0] for c in todo)
+  nw = min(max(0, sw), n_todo) if n_todo > 1 else 0
   pool = None
   if nw > 0:
     import multiprocessing
@@ -482,17 +522,30 @@ def main(args, codebert=False):
     pool = multiprocessing.get_context('fork').Pool(nw)
     _FE.clear()
 
+  # a chunk is split as pieces of ~1/(2 nw) of it (whole partitions) on all
+  # the workers at once: the GPU packs a chunk's partitions in parallel, one
+  # wave each, so a chunk costs about one partition's latency and wants many
+  # partitions, while its split should not wait on one worker
+  def pieces(c):
+    a, b = chunks[c]
+    return chunk_pieces(part_end, lo, a, b, 2 * nw if pool is not None else 1)
+
   def submit(c):
-    a, b = int(pro[chunks[c][0]]), int(pro[chunks[c][1]])
     if pool is not None:
-      return pool.apply_async(_split_worker, (a, b))
+      return [pool.apply_async(_split_worker, (int(pro[a]), int(pro[b]))) for a, b in pieces(c)]
     ts = time.perf_counter()
-    corpus, ids = split_records(index.texts(order[a:b]), codebert, split)
+    a, b = chunks[c]
+    corpus, ids = split_records(index.texts(order[int(pro[a]):int(pro[b])]), codebert, split)
 
     class Done:
       def get(self):
         return corpus, ids, time.perf_counter() - ts
-    return Done()
+    return [Done()]
+
+  def gather(fs):
+    """the pieces of a chunk, in order, as one corpus (+ ids, split seconds)"""
+    got = [f_.get() for f_ in fs]
+    return concat_corpora([g[0] for g in got], [g[1] for g in got]) + (sum(g[2] for g in got),)
 
   device = torch.device('cuda', local)
   torch.cuda.set_device(device)
@@ -529,12 +582,12 @@ def main(args, codebert=False):
 
   t['write_wait_s'] = 0.0
   try:
-    ahead = max(1, nw)
+    ahead = 2  # chunks split ahead of the GPU
     futs = {c: submit(c) for c in todo[:ahead]} if pool is not None else {}
     for i, c in enumerate(todo):
       a, b = chunks[c]
       tw = time.perf_counter()
-      corpus, ids, ts = (futs.pop(c) if c in futs else submit(c)).get()
+      corpus, ids, ts = gather(futs.pop(c) if c in futs else submit(c))
       t['split_wait_s'] += time.perf_counter() - tw
       t['host_split_s'] += ts
       if pool is not None and i + ahead < len(todo):

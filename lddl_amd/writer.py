@@ -160,6 +160,28 @@ def _npy_positions_u16(k, inv, hdr, mlm_pos):
   return off16 * 2, data.view(np.uint8)
 
 
+# Arrow arrays straight from buffers: pa.array() on numpy arrays or Python
+# lists imports pandas on its first call (~0.4-0.5 s per process)
+_NP_TYPES = {np.dtype(np.uint16): pa.uint16(), np.dtype(np.int64): pa.int64(), np.dtype(np.int32): pa.int32()}
+
+
+def np_array(x):
+  """Arrow array of a 1-D numpy array (bool, uint16, int32 or int64), no copy
+  except bools (bit-packed)"""
+  x = np.ascontiguousarray(x)
+  if x.dtype == np.bool_:
+    return pa.Array.from_buffers(pa.bool_(), len(x), [None, pa.py_buffer(np.packbits(x, bitorder='little'))])
+  return pa.Array.from_buffers(_NP_TYPES[x.dtype], len(x), [None, pa.py_buffer(x)])
+
+
+def str_array(strs):
+  """Arrow string array of a list of str"""
+  b = [s.encode('utf-8') for s in strs]
+  off = np.zeros(len(b) + 1, dtype=np.int64)
+  np.cumsum(np.fromiter(map(len, b), dtype=np.int64, count=len(b)), out=off[1:])
+  return _arrow(pa.string(), off, np.frombuffer(b''.join(b), dtype=np.uint8), 0, len(b))
+
+
 def _arrow(typ, off, data, lo, hi):
   """rows [lo, hi) of a (int64 offsets, bytes) column as an Arrow array"""
   o = off[lo:hi + 1] - off[lo]
@@ -208,9 +230,9 @@ def write_shards(packer, res, out_dir, bin_size=None, codebert=False, masking=Fa
   if codebert:
     if doc_ids is None:
       raise ValueError('CodeBERT shards need doc_ids (the id column)')
-    docs = pa.array(row_docs(packer, res.n_pairs, n_rows, stream))
-    ids_arr = doc_ids if isinstance(doc_ids, pa.Array) else pa.array(doc_ids, type=pa.string())
-    ids_col = ids_arr.take(docs) if n_rows else pa.array([], pa.string())
+    docs = np_array(row_docs(packer, res.n_pairs, n_rows, stream))
+    ids_arr = doc_ids if isinstance(doc_ids, pa.Array) else str_array(doc_ids)
+    ids_col = ids_arr.take(docs) if n_rows else str_array([])
   if masking and not codebert:
     moff_all = res.mlm_off[:n_rows + 1].cpu().numpy()
     mpos_all = res.mlm_pos[:int(moff_all[-1])].cpu().numpy().view(np.uint16)
@@ -243,13 +265,13 @@ def write_shards(packer, res, out_dir, bin_size=None, codebert=False, masking=Fa
       else:
         cols['A'] = _arrow(pa.string(), *c0, lo, hi)
         cols['B'] = _arrow(pa.string(), *c1, lo, hi)
-        cols['is_random_next'] = pa.array((flags[r0 + lo:r0 + hi] & 1).astype(bool))
-      cols['num_tokens'] = pa.array(num_tokens[r0 + lo:r0 + hi])
+        cols['is_random_next'] = np_array((flags[r0 + lo:r0 + hi] & 1).astype(bool))
+      cols['num_tokens'] = np_array(num_tokens[r0 + lo:r0 + hi])
       if masking and not codebert:
         cols['masked_lm_positions'] = _arrow(pa.binary(), *pos, lo, hi)
         cols['masked_lm_labels'] = _arrow(pa.string(), *lab, lo, hi)
       if binned:
-        cols['bin_id'] = pa.array(bins[r0 + lo:r0 + hi])
+        cols['bin_id'] = np_array(bins[r0 + lo:r0 + hi])
       t = pa.Table.from_arrays([cols[name] for name in sch.names], schema=sch)
       name = 'part.%d.parquet' % (part_base + p)
       if binned:

@@ -116,6 +116,18 @@ def test_bert_end_to_end_vs_oracle(gpu, monkeypatch, seq, bin_size, nparts, caps
     assert np.array_equal(bc[p], cnt)
 
 
+@pytest.mark.parametrize('seed', [0, 2**32 - 2, 2**40 + 3])
+def test_bert_partition_seeds_vs_oracle(gpu, seed):
+  """random.seed(seed + p) for seeds of one and two 32-bit key words
+  (init_by_array's klen 1 / 2; 2**32 - 2 + p crosses the boundary) and 0"""
+  from lddl_amd import synth, pipeline
+  c = synth.make_wiki(300_000, seed=17)
+  res = pipeline.run_bert(c, target_seq_length=128, bin_size=32, n_partitions=4, seed=seed, check_host=True)
+  oids, ontok = OracleTokenizer(pipeline.VOCAB_BERT).run(c.data, c.sent_off, 512, nthreads=8)
+  exp = po.run_bert_shards(c, oids, ontok, res.part_doc_off, 128, 0.1, 5, seed, 32)
+  pipeline.assert_same_pairs(res, exp)
+
+
 @pytest.mark.parametrize('nparts', [2, 5])
 def test_wikibooks_seq512_bin64_vs_oracle(gpu, nparts):
   """BASELINE config C5 at a size the oracle finishes quickly: a Wikipedia +

@@ -292,3 +292,57 @@ def test_clear_markers_removes_overlapping_chunks(tmp_path):
   assert left == ['chunk_0_4.json', 'chunk_8_12.json']
   assert preprocess.load_marker(sink, 0, 4, 'k') is not None
   preprocess.clear_markers(str(tmp_path / 'nothing'), 0, 1)  # no marker dir: no error
+
+
+@pytest.mark.parametrize('codebert', [False, True])
+def test_concat_corpora_equals_one_split(codebert):
+  """a chunk split as pieces on several workers and concatenated is the
+  chunk split at once"""
+  from lddl_amd import synth, writer
+  if codebert:
+    recs = synth.make_code_lines(23, seed=3)
+    split = None
+  else:
+    recs = ['wiki-%d %s' % (i, ' '.join(d)) for i, d in enumerate(synth.make_wiki(1 << 14, seed=5).documents())]
+    split = preprocess.sentence_splitter('rules')[0]
+  whole, ids = preprocess.split_records(recs, codebert, split)
+  cuts = [0, 1, 1, len(recs) // 3, len(recs) - 1, len(recs)]
+  parts = [preprocess.split_records(recs[a:b], codebert, split) for a, b in zip(cuts[:-1], cuts[1:])]
+  pid = [writer.str_array(p[1]) for p in parts] if codebert else [p[1] for p in parts]
+  got, gids = preprocess.concat_corpora([p[0] for p in parts], pid)
+  assert bytes(got.data) == bytes(whole.data[:whole.nbytes])
+  np.testing.assert_array_equal(got.sent_off, whole.sent_off)
+  np.testing.assert_array_equal(got.doc_sent_off, whole.doc_sent_off)
+  if codebert:
+    np.testing.assert_array_equal(got.doc_nseg_doc, whole.doc_nseg_doc)
+    assert gids.to_pylist() == ids
+  else:
+    assert got.doc_nseg_doc is None and gids == ids
+
+
+def test_arrow_columns_without_pandas():
+  """the writer's Arrow columns come from buffers (pa.array() imports pandas,
+  ~0.5 s on the first call of a process)"""
+  from lddl_amd import writer
+  x = np.array([True, False, True, True, False, False, True, False, True])
+  assert writer.np_array(x).to_pylist() == x.tolist()
+  assert writer.np_array(x).slice(3, 5).to_pylist() == x[3:8].tolist()
+  u = np.array([0, 7, 65535], np.uint16)
+  assert writer.np_array(u).to_pylist() == u.tolist()
+  assert writer.np_array(np.array([-3, 2**40], np.int64)).to_pylist() == [-3, 2**40]
+  assert writer.str_array(['a', '', 'é☃']).to_pylist() == ['a', '', 'é☃']
+  assert writer.str_array([]).to_pylist() == []
+
+
+def test_chunk_pieces_cover_the_chunk():
+  rng = np.random.default_rng(1)
+  sizes = rng.integers(1, 1000, 40)
+  part_end = np.cumsum(sizes)
+  for lo, a, b, n in [(0, 0, 40, 8), (0, 5, 6, 8), (0, 3, 17, 1), (0, 0, 40, 100), (0, 10, 40, 3)]:
+    pcs = preprocess.chunk_pieces(part_end[lo:], lo, a, b, n)
+    assert pcs[0][0] == a and pcs[-1][1] == b
+    assert all(x[1] == y[0] and x[0] < x[1] for x, y in zip(pcs, pcs[1:] + [(b, b + 1)]))
+    assert len(pcs) <= max(1, n) + 1
+  assert len(preprocess.chunk_pieces(np.full(32, 10).cumsum(), 0, 0, 32, 8)) == 8
+  # a rank's range starting at lo > 0
+  assert preprocess.chunk_pieces(np.full(10, 5).cumsum(), 7, 9, 17, 4) == [(9, 11), (11, 13), (13, 15), (15, 17)]

@@ -176,11 +176,19 @@ def test_cli_bert_end_to_end(gpu, tmp_path):
                      text=True, timeout=300)
   assert r.returncode == 0, r.stderr[-2000:]
   assert "'split_workers': 2" in r.stdout and ("'chunks': %d" % n_part) in r.stdout, r.stdout
+  # one chunk of every partition, split as pieces on the two workers at once
+  sink4 = tmp_path / 'out4'
+  r4 = subprocess.run([sys.executable, '-m', 'lddl_amd.preprocess', '--sink', str(sink4), '--split-workers', '2'] +
+                      common[:-1] + ['100'], cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                      capture_output=True, text=True, timeout=300)
+  assert r4.returncode == 0, r4.stderr[-2000:]
+  assert "'split_workers': 2" in r4.stdout and "'chunks': 1," in r4.stdout, r4.stdout
   files3, t3 = preprocess.main(preprocess.attach_args().parse_args(['--sink', str(sink3), '--split-workers', '0'] +
                                                                      common))
   assert t3['chunks'] > 1 and t['chunks'] == 1
   for f in files:
-    assert _read(f) == _read(str(sink2 / os.path.basename(f))) == _read(str(sink3 / os.path.basename(f)))
+    assert _read(f) == _read(str(sink2 / os.path.basename(f))) == _read(str(sink3 / os.path.basename(f))) == \
+        _read(str(sink4 / os.path.basename(f)))
   corpus, ids = preprocess.split_records(recs, splitter=preprocess._rule_split)
   oids, ontok = OracleTokenizer(pipeline.VOCAB_BERT).run(corpus.data, corpus.sent_off, 512, nthreads=8)
   exp = po.run_bert_shards(corpus, oids, ontok, pdo, 128, 0.1, 5, 5, 32)
