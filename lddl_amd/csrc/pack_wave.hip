@@ -153,8 +153,8 @@ struct WaveRng {
   PackWaveLds& L;
   int lane;
   int idx;            // wave-uniform
-  int wbase = -1024;  // tw[wbase + lane] is held in `win` (one LDS read per 64 draws)
-  int wend = 0;       // min(wbase + 64, MT_N): draws below it come from `win`
+  int wend = 0;       // tempered words [wend - 64, wend) (64-aligned) held in `win`, one per lane
+                      // (one LDS read per 64 draws); draws below wend come from it
   uint32_t win = 0;
 
   // random.seed(n) for 0 <= n < 2^64: init_by_array(key = n's 32-bit words,
@@ -174,6 +174,7 @@ struct WaveRng {
       prev = (kMtGenrand.v[1] ^ (f * 1664525u)) + ka;
     }
     const uint32_t m1a = prev;
+#pragma unroll 1
     for (int c = 0; c < NC; ++c) {
       const int i = 64 * c + lane;
       uint32_t w = kMtGenrand.v[min(i, MT_N - 1)];
@@ -187,6 +188,7 @@ struct WaveRng {
       prev = m1;
     }
     // second loop: positions 2..623, then 1 (each lane re-reads only what it wrote)
+#pragma unroll 1
     for (int c = 0; c < NC; ++c) {
       const int i = 64 * c + lane;
       uint32_t w = mt[min(i, MT_N - 1)];
@@ -215,7 +217,6 @@ struct WaveRng {
   __device__ __forceinline__ void refill() {
     pack_mt_refill((lds_u32*)L.mt, lane);
     idx = 0;
-    wbase = -1024;
     wend = 0;
   }
 
@@ -224,20 +225,37 @@ struct WaveRng {
   __device__ __forceinline__ uint32_t next() {
     if (idx >= wend) {
       if (idx >= MT_N) refill();
-      wbase = idx;
-      wend = min(idx + 64, MT_N);
-      win = temper(L.mt[idx + lane < MT_N ? idx + lane : MT_N - 1]);
+      const int wb = idx & ~63;  // windows start at multiples of 64
+      wend = min(wb + 64, MT_N);
+      win = temper(L.mt[min(wb + lane, MT_N - 1)]);
     }
-    const int o = idx - wbase;
-    ++idx;
-    return (uint32_t)__builtin_amdgcn_readlane((int)win, o);
+    // v_readlane's lane select is its SGPR operand's bits [5:0]: with
+    // 64-aligned windows the word at idx is lane idx & 63 (no offset math)
+    return (uint32_t)__builtin_amdgcn_readlane((int)win, idx++);
+  }
+  // two consecutive words with one window test when both are in the window
+  __device__ __forceinline__ void next2(uint32_t& a, uint32_t& b) {
+    if (idx + 1 < wend) {
+      a = (uint32_t)__builtin_amdgcn_readlane((int)win, idx);
+      b = (uint32_t)__builtin_amdgcn_readlane((int)win, idx + 1);
+      idx += 2;
+    } else {
+      a = next();
+      b = next();
+    }
   }
   __device__ __forceinline__ double random() {
-    const uint32_t a = next() >> 5, b = next() >> 6;
-    return ((double)a * 67108864.0 + (double)b) * (1.0 / 9007199254740992.0);
+    uint32_t a, b;
+    next2(a, b);
+    return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) * (1.0 / 9007199254740992.0);
   }
   // random() < 0.5  <=>  MSB of the first word is 0 (second word consumed)
   __device__ __forceinline__ bool coin_lt_half() {
+    if (idx + 1 < wend) {
+      const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)win, idx);
+      idx += 2;
+      return (a >> 31) == 0;
+    }
     const uint32_t a = next();
     next();
     return (a >> 31) == 0;
@@ -469,18 +487,20 @@ __device__ __forceinline__ void pack_order_nt(int32_t* order, const PairRec* out
 }
 
 // smallest k in [k0, n) with (k == n-1) or (sum lens[k0..k] >= target);
-// returns k and the sum.  lens via GET (LDS or global).
+// returns k and the sum.  lens via GET (LDS or global).  Positions past n
+// read a length no target stops short of, so the first lane whose sum
+// reaches the target, clamped to n - 1, is the answer (one compare per lane,
+// no end-of-range masks on the scalar unit).
 template <class GET>
 __device__ __forceinline__ int find_fill(const GET& len_at, int k0, int n, int target, int lane, int* sum_out) {
   int base = 0;
   for (int k = k0; k < n; k += 64) {
     const int kk = k + lane;
-    const int l = kk < n ? len_at(kk) : 0;
+    const int l = kk < n ? len_at(kk) : (1 << 20);
     const int ps = base + wscan_incl(l, lane);
-    const bool cond = kk < n && (kk == n - 1 || ps >= target);
-    const uint64_t m = __ballot(cond);
+    const uint64_t m = __ballot(ps >= target);
     if (m) {
-      const int j = __ffsll((unsigned long long)m) - 1;
+      const int j = min((int)__builtin_ctzll(m), n - 1 - k);
       *sum_out = lane_get(ps, j);
       return k + j;
     }
@@ -497,20 +517,21 @@ __device__ __forceinline__ int range_sum(const GET& len_at, int k0, int k1, int 
   return wsum(s);
 }
 
-// find_fill / range_sum over a document of <= 64 sentences whose lengths'
-// inclusive prefix sums are held one per lane in dps (lane k = sentence k,
-// flat beyond; one wave scan per document visit): a chunk is a ballot and two
-// lane reads, no scan per chunk
-__device__ __forceinline__ int find_fill_reg(int dps, int k0, int n, int target, int lane, int* sum_out) {
-  const int base = k0 > 0 ? __builtin_amdgcn_readlane(dps, k0 - 1) : 0;
-  const bool in = lane >= k0 && lane < n;
-  const uint64_t m = __ballot(in && (lane == n - 1 || dps - base >= target));  // lane n-1 always qualifies
-  const int j = __ffsll((unsigned long long)m) - 1;
+// find_fill over a document of <= 64 sentences whose lengths' inclusive
+// prefix sums are held one per lane in dps (lane k = sentence k, flat at the
+// document total `tot` beyond it; one wave scan per document visit), dex the
+// exclusive sums.  Lengths are >= 1 (kept sentences), so the sums rise
+// strictly: the answer is the first lane whose sum reaches base + min(target,
+// tot - base) (lane n - 1 when the target is out of reach), and lanes below
+// k0 never do (the goal is >= base + 1).  One compare + one ballot, base
+// returned for the A length (range_sum = dps[k1 - 1] - base).
+__device__ __forceinline__ int find_fill_reg(int dps, int dex, int tot, int k0, int target, int* sum_out, int* base_out) {
+  const int base = __builtin_amdgcn_readlane(dex, k0);
+  const int goal = base + max(1, min(target, tot - base));
+  const int j = (int)__builtin_ctzll(__ballot(dps >= goal));
   *sum_out = __builtin_amdgcn_readlane(dps, j) - base;
+  *base_out = base;
   return j;
-}
-__device__ __forceinline__ int range_sum_reg(int dps, int k0, int k1) {
-  return __builtin_amdgcn_readlane(dps, k1 - 1) - (k0 > 0 ? __builtin_amdgcn_readlane(dps, k0 - 1) : 0);
 }
 
 // LDSOK = false: every LDS capacity is 0 (the default), the arrays are in
@@ -706,6 +727,8 @@ __global__ __launch_bounds__(64, PACK_OCC) void pack_bert_wave_kernel(PackParams
       const bool dreg = len <= 64;
       const int dl = dl_next;
       const int dps = dreg ? wave_incl_add(dl) : 0;  // (dl is 0 past the document)
+      const int dex = dps - dl;
+      const int dtot = dreg ? __builtin_amdgcn_readlane(dps, 63) : 0;  // (flat past the document)
       if (di + 1 < nd) dl_next = doc_lens(di + 1);
       else if (dup + 1 < P.dup) dl_next = doc_lens(0);
       int target = max_num;
@@ -715,13 +738,14 @@ __global__ __launch_bounds__(64, PACK_OCC) void pack_bert_wave_kernel(PackParams
       while (i < len) {
         const int cs = i;
         int cur;
-        const int j = dreg ? find_fill_reg(dps, cs, len, target, lane, &cur)
+        int fbase = 0;
+        const int j = dreg ? find_fill_reg(dps, dex, dtot, cs, target, &cur, &fbase)
                            : find_fill([&](int k) { return len_at(first + k); }, cs, len, target, lane, &cur);
         const int nchunk = j - cs + 1;
         int a_end = 1;
         if (nchunk >= 2) a_end = (int)rng.randint(1, nchunk - 1);
         const int la = a_end == nchunk ? cur
-                       : dreg ? range_sum_reg(dps, cs, cs + a_end)
+                       : dreg ? __builtin_amdgcn_readlane(dps, cs + a_end - 1) - fbase
                               : range_sum([&](int k) { return len_at(first + k); }, cs, cs + a_end, lane);
         PW_GSTAMP(7)
         PairRec r;
@@ -733,12 +757,12 @@ __global__ __launch_bounds__(64, PACK_OCC) void pack_bert_wave_kernel(PackParams
         if (nchunk == 1 || rng.coin_lt_half()) {
           rn = true;
           const int tb = target - la;
-          int rdi = 0;
-          for (int t = 0; t < 10; ++t) {
-            rdi = (int)rng.randint(0, nd - 1);
-            if (rdi != di) break;
+          // up to 10 draws for a document other than di (the first one almost always)
+          int rdi = (int)rng.randbelow((uint32_t)nd);
+          if (rdi == di) {
+            for (int t = 1; t < 10 && rdi == di; ++t) rdi = (int)rng.randbelow((uint32_t)nd);
+            if (rdi == di) rn = false;
           }
-          if (rdi == di) rn = false;
           const int rfirst = doc_first(rdi), rlen = doc_n(rdi);
           const int rstart = (int)rng.randint(0, rlen - 1);
           const int k = find_fill([&](int q) { return len_at(rfirst + q); }, rstart, rlen, tb, lane, &lb);
@@ -753,29 +777,22 @@ __global__ __launch_bounds__(64, PACK_OCC) void pack_bert_wave_kernel(PackParams
           i_next = j + 1;
         }
         PW_GSTAMP(8)
-        // _truncate_seq_pair, 64 steps per round
+        // _truncate_seq_pair, 64 steps per round.  Step t trims A while
+        // t < th when A starts longer (pos), B while t < th otherwise, then
+        // the sides alternate: side_a(t) = t < th ? pos : odd(t - th) == pos
         int alo = 0, ahi = la, blo = 0, bhi = lb;
         int E = la + lb - max_num;
         int t0 = 0;
         const int d0l = la - lb;
-        const int nb0 = 1 - d0l;  // initial B steps when d0 <= 0
-        while (E > 0) {
-          int avail = (MT_N - rng.idx) >> 1;
-          if (avail == 0) {  // a step straddles the twist: one serial step
-            const int t = t0;
-            bool sideA = d0l > 0 ? (t < d0l ? true : ((t - d0l) & 1) != 0) : (t < nb0 ? false : ((t - nb0) & 1) == 0);
-            const bool front = rng.coin_lt_half();
-            if (sideA) { if (front) ++alo; else --ahi; } else { if (front) ++blo; else --bhi; }
-            ++t0;
-            --E;
-            continue;
-          }
-          const int n = min(min(E, 64), avail);
-          const int t = t0 + lane;
-          bool sideA = d0l > 0 ? (t < d0l ? true : ((t - d0l) & 1) != 0) : (t < nb0 ? false : ((t - nb0) & 1) == 0);
-          const bool front = lane < n ? (WaveRng::temper(L.mt[rng.idx + 2 * lane]) >> 31) == 0 : false;
-          // two ballots: the n steps' A side (SA) and front (F) masks
-          const uint64_t SA = __ballot(lane < n && sideA), F = __ballot(front);
+        const bool pos = d0l > 0;
+        const int th = pos ? d0l : 1 - d0l;
+        auto side_a = [&](int t) -> bool { return t < th ? pos : (((t - th) & 1) != 0) == pos; };
+        // n steps t0 .. t0 + n - 1 from the next 2n words (n <= 64, before the twist)
+        auto trunc_round = [&](int n) {
+          const bool act = lane < n;
+          const bool sa = act && side_a(t0 + lane);
+          const bool front = act && (WaveRng::temper(L.mt[min(rng.idx + 2 * lane, MT_N - 1)]) >> 31) == 0;
+          const uint64_t SA = __ballot(sa), F = __ballot(front);
           const int x = __popcll(SA & F), a = __popcll(SA), f = __popcll(F);
           alo += x;
           ahi -= a - x;
@@ -784,6 +801,22 @@ __global__ __launch_bounds__(64, PACK_OCC) void pack_bert_wave_kernel(PackParams
           rng.idx += 2 * n;
           t0 += n;
           E -= n;
+        };
+        if (E > 0 && E <= 64 && 2 * E <= MT_N - rng.idx) {
+          trunc_round(E);  // (the common case: one round, no loop)
+        } else {
+          while (E > 0) {
+            const int avail = (MT_N - rng.idx) >> 1;
+            if (avail == 0) {  // a step straddles the twist: one serial step
+              const bool sideA = side_a(t0);
+              const bool front = rng.coin_lt_half();
+              if (sideA) { if (front) ++alo; else --ahi; } else { if (front) ++blo; else --bhi; }
+              ++t0;
+              --E;
+              continue;
+            }
+            trunc_round(min(min(E, 64), avail));
+          }
         }
         PW_GSTAMP(9)
         if (ahi - alo < 1 || bhi - blo < 1) { err = PACK_EASSERT; break; }

@@ -264,7 +264,7 @@ def attach_args(parser=None, codebert=False):
   attach_bool_arg(p, 'masking', default=False, help_str='static masking (pretrain.py:859-866)')
   p.add_argument('--masked-lm-ratio', type=float, default=0.15)
   p.add_argument('--sentence-splitter', type=str, default='auto', choices=['auto', 'punkt', 'rules'])
-  p.add_argument('--chunk-mb', type=float, default=64.0,
+  p.add_argument('--chunk-mb', type=float, default=32.0,
                  help='raw MB of partitions per pipeline chunk (host split of the next chunks overlaps the GPU and '
                       'the writer on chunk k)')
   p.add_argument('--split-workers', type=int, default=None,
@@ -519,7 +519,9 @@ def main(args, codebert=False):
   if nw > 0:
     import multiprocessing
     _FE.update(index=index, order=order, codebert=codebert, split=split)
+    t0 = time.perf_counter()
     pool = multiprocessing.get_context('fork').Pool(nw)
+    t['pool_start_s'] = time.perf_counter() - t0
     _FE.clear()
 
   # a chunk is split as pieces of ~1/(2 nw) of it (whole partitions) on all
@@ -547,9 +549,21 @@ def main(args, codebert=False):
     got = [f_.get() for f_ in fs]
     return concat_corpora([g[0] for g in got], [g[1] for g in got]) + (sum(g[2] for g in got),)
 
+  # the first chunks split while this process brings up the GPU context and
+  # the device tables
+  ahead = 2  # chunks split ahead of the GPU
+  futs = {c: submit(c) for c in todo[:ahead]} if pool is not None else {}
+  t0 = time.perf_counter()
   device = torch.device('cuda', local)
-  torch.cuda.set_device(device)
-  pk = pipeline.Packer(vocab, local, masking=args.masking and not codebert)
+  try:
+    torch.cuda.set_device(device)
+    pk = pipeline.Packer(vocab, local, masking=args.masking and not codebert)
+  except BaseException:
+    if pool is not None:
+      pool.terminate()
+      pool.join()
+    raise
+  t['gpu_init_s'] = time.perf_counter() - t0
   out = []
   counts = torch.zeros(hi - lo, nbins, dtype=torch.int64, device=device)  # rows per (partition, bin)
   t.update(host_split_s=0.0, split_wait_s=0.0, gpu_s=0.0, write_s=0.0, pairs=0, split_workers=nw,
@@ -582,8 +596,6 @@ def main(args, codebert=False):
 
   t['write_wait_s'] = 0.0
   try:
-    ahead = 2  # chunks split ahead of the GPU
-    futs = {c: submit(c) for c in todo[:ahead]} if pool is not None else {}
     for i, c in enumerate(todo):
       a, b = chunks[c]
       tw = time.perf_counter()
@@ -617,14 +629,18 @@ def main(args, codebert=False):
       settle(2)  # at most two chunks' encodes behind the GPU
       t['write_s'] += time.perf_counter() - t0
       t['pairs'] += res.n_pairs
+    t0 = time.perf_counter()
     settle(0)
+    t['drain_s'] = time.perf_counter() - t0  # the last chunks' encodes
   finally:
+    t0 = time.perf_counter()
     if pool is not None:
       pool.terminate()
       pool.join()
     if enc is not None:
       enc.shutdown(wait=True)
     index.close()
+    t['teardown_s'] = time.perf_counter() - t0
   if args.num_shards:
     # balance_dask_output's job (load_balance.py:321-369) from the packer's
     # counts: one all-gather (RCCL) instead of its per-file count pass + MPI

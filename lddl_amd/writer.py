@@ -182,6 +182,18 @@ def str_array(strs):
   return _arrow(pa.string(), off, np.frombuffer(b''.join(b), dtype=np.uint8), 0, len(b))
 
 
+OFF32_LIMIT = 2**31
+
+
+def _arrow_rows(typ, off, data, n):
+  """all n rows of a (int64 offsets from 0, bytes) column: 32-bit offsets, or
+  the large type when the bytes pass 2 GiB (files slice and cast it)"""
+  if off[n] < OFF32_LIMIT:
+    return pa.Array.from_buffers(typ, n, [None, pa.py_buffer(off[:n + 1].astype(np.int32)), pa.py_buffer(data)])
+  big = pa.large_string() if typ == pa.string() else pa.large_binary()
+  return pa.Array.from_buffers(big, n, [None, pa.py_buffer(np.ascontiguousarray(off[:n + 1])), pa.py_buffer(data)])
+
+
 def _arrow(typ, off, data, lo, hi):
   """rows [lo, hi) of a (int64 offsets, bytes) column as an Arrow array"""
   o = off[lo:hi + 1] - off[lo]
@@ -254,25 +266,31 @@ def write_shards(packer, res, out_dir, bin_size=None, codebert=False, masking=Fa
       m0 = int(moff_all[r0])
       lab = render(packer, res.mlm_label, res.mlm_off, r0, n, ROW, stream=stream)
       pos = npy_positions(moff_all[r0:r1 + 1] - m0, mpos_all[m0:int(moff_all[r1])])
+    # one table over the batch's rows; a file is a zero-copy slice of it
+    cols = {}
+    if codebert:
+      cols['id'] = ids_col.slice(r0, n)
+      cols['doc'] = _arrow_rows(pa.string(), *c0, n)
+      cols['code'] = _arrow_rows(pa.string(), *c1, n)
+    else:
+      cols['A'] = _arrow_rows(pa.string(), *c0, n)
+      cols['B'] = _arrow_rows(pa.string(), *c1, n)
+      cols['is_random_next'] = np_array((flags[r0:r1] & 1).astype(bool))
+    cols['num_tokens'] = np_array(num_tokens[r0:r1])
+    if masking and not codebert:
+      cols['masked_lm_positions'] = _arrow_rows(pa.binary(), *pos, n)
+      cols['masked_lm_labels'] = _arrow_rows(pa.string(), *lab, n)
+    if binned:
+      cols['bin_id'] = np_array(bins[r0:r1])
+    arrs = [cols[name] for name in sch.names]
+    large = any(a.type != fd.type for a, fd in zip(arrs, sch))
+    tb = pa.Table.from_arrays(arrs, names=sch.names)
     for fi in range(f, g):
       lo, hi = int(file_start[fi] - r0), int(file_start[fi + 1] - r0)
       p, b = divmod(fi, nbins)
-      cols = {}
-      if codebert:
-        cols['id'] = ids_col.slice(r0 + lo, hi - lo)
-        cols['doc'] = _arrow(pa.string(), *c0, lo, hi)
-        cols['code'] = _arrow(pa.string(), *c1, lo, hi)
-      else:
-        cols['A'] = _arrow(pa.string(), *c0, lo, hi)
-        cols['B'] = _arrow(pa.string(), *c1, lo, hi)
-        cols['is_random_next'] = np_array((flags[r0 + lo:r0 + hi] & 1).astype(bool))
-      cols['num_tokens'] = np_array(num_tokens[r0 + lo:r0 + hi])
-      if masking and not codebert:
-        cols['masked_lm_positions'] = _arrow(pa.binary(), *pos, lo, hi)
-        cols['masked_lm_labels'] = _arrow(pa.string(), *lab, lo, hi)
-      if binned:
-        cols['bin_id'] = np_array(bins[r0 + lo:r0 + hi])
-      t = pa.Table.from_arrays([cols[name] for name in sch.names], schema=sch)
+      t = tb.slice(lo, hi - lo)
+      if large:  # (a file's own bytes fit 32-bit offsets)
+        t = t.cast(sch)
       name = 'part.%d.parquet' % (part_base + p)
       if binned:
         name += '_%d' % b

@@ -346,3 +346,19 @@ def test_chunk_pieces_cover_the_chunk():
   assert len(preprocess.chunk_pieces(np.full(32, 10).cumsum(), 0, 0, 32, 8)) == 8
   # a rank's range starting at lo > 0
   assert preprocess.chunk_pieces(np.full(10, 5).cumsum(), 7, 9, 17, 4) == [(9, 11), (11, 13), (13, 15), (15, 17)]
+
+
+def test_batch_columns_past_32bit_offsets(monkeypatch):
+  """a writer batch whose string bytes pass the 32-bit offset range is built
+  with the large type and each file's slice cast back to the schema's"""
+  import pyarrow as pa
+  from lddl_amd import writer
+  off = np.array([0, 3, 3, 7, 9], np.int64)
+  data = np.frombuffer(b'abcdefghi', np.uint8)
+  monkeypatch.setattr(writer, 'OFF32_LIMIT', 4)
+  a = writer._arrow_rows(pa.string(), off, data, 4)
+  assert a.type == pa.large_string()
+  t = pa.Table.from_arrays([a], names=['A']).slice(1, 2).cast(pa.schema([('A', pa.string())]))
+  assert t.schema.field('A').type == pa.string() and t.column('A').to_pylist() == ['', 'defg']
+  monkeypatch.setattr(writer, 'OFF32_LIMIT', 2**31)
+  assert writer._arrow_rows(pa.binary(), off, data, 4).type == pa.binary()
