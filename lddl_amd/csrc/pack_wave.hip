@@ -787,12 +787,16 @@ __global__ __launch_bounds__(64, PACK_OCC) void pack_bert_wave_kernel(PackParams
         const bool pos = d0l > 0;
         const int th = pos ? d0l : 1 - d0l;
         auto side_a = [&](int t) -> bool { return t < th ? pos : (((t - th) & 1) != 0) == pos; };
-        // n steps t0 .. t0 + n - 1 from the next 2n words (n <= 64, before the twist)
+        // n steps t0 .. t0 + n - 1 from the next 2n words (n <= 64, before the
+        // twist): every lane reads and compares unconditionally (no exec-mask
+        // branches); the lane mask of the n steps is applied to the ballots
+        const int posi = pos ? 1 : 0;
         auto trunc_round = [&](int n) {
-          const bool act = lane < n;
-          const bool sa = act && side_a(t0 + lane);
-          const bool front = act && (WaveRng::temper(L.mt[min(rng.idx + 2 * lane, MT_N - 1)]) >> 31) == 0;
-          const uint64_t SA = __ballot(sa), F = __ballot(front);
+          const uint64_t act = __ballot(lane < n);
+          const int t = t0 + lane;
+          const int sbit = t < th ? posi : (((t - th) & 1) ^ posi ^ 1);  // 1: this step trims A
+          const int w = (int)WaveRng::temper(L.mt[min(rng.idx + 2 * lane, MT_N - 1)]);
+          const uint64_t SA = __ballot(sbit != 0) & act, F = __ballot(w >= 0) & act;  // front: MSB 0
           const int x = __popcll(SA & F), a = __popcll(SA), f = __popcll(F);
           alo += x;
           ahi -= a - x;

@@ -10,6 +10,7 @@ mkdir -p $O
 export TMPDIR=/tmp
 TESTS="tests/test_pack_gpu.py tests/test_writer_gpu.py tests/test_preprocess.py"
 [ -n "$SKIP_PACK" ] && TESTS="tests/test_writer_gpu.py tests/test_preprocess.py"
+[ -n "$SKIP_FE" ] && TESTS="tests/test_pack_gpu.py"
 timeout -k 10 600 python -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu $TESTS > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
 tail -1 $O/pytest.log
 if [ -n "$CODE_WRITER" ]; then
@@ -23,6 +24,7 @@ f=$(find $O/kt -name '*kernel_stats.csv' | head -1); cp $f $O/kernel_stats.csv
 grep -E "pack_bert_wave|scan_kernel" $O/kernel_stats.csv | cut -c1-160
 timeout -s KILL 200 rocprofv3 --pmc SQ_INSTS_SALU SQ_INSTS_VALU SQ_WAVES -d $O/p1 -o pmc --output-format csv -- python -u $B --steps 1 --warmup 0 > $O/p1.log 2>&1 || { tail -5 $O/p1.log; exit 1; }
 python tools/pmc_summary.py $O > $O/pmc_summary.txt; grep -A3 'pack_bert_wave' $O/pmc_summary.txt | head -4; }
+[ -n "$SKIP_FE" ] && exit 0
 for c in ${CHUNKS:-8 16 32 64}; do
   timeout -k 10 200 python -u -c "import bench, json; print(json.dumps(bench.frontend_leg(100, $c)))" \
     > $O/fe_$c.json 2> $O/fe_$c.err || { tail -5 $O/fe_$c.err; exit 1; }
