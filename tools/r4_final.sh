@@ -28,6 +28,9 @@ if [ -z "$SKIP_CONFIGS" ]; then
   done
 fi
 B="bench.py --no-cpu-baseline --parquet-parts 0 --frontend-mb 0"
+# packer phase stamps (the diagnostic instantiation; s_memtime ticks summed over the waves)
+LDDL_PACK_DEBUG=1 timeout -k 10 300 python -u $B --steps 1 --warmup 0 --no-sample-check > $OUT/stamps.log 2>&1 || { echo "stamps failed"; tail -5 $OUT/stamps.log; exit 1; }
+grep "pack dbg" $OUT/stamps.log | head -1
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/kt -o kt --output-format csv -- python -u $B --steps 2 --warmup 1 > $OUT/kt.log 2>&1 || { echo "kernel trace failed"; tail -20 $OUT/kt.log; exit 1; }
 f=$(find $OUT/kt -name '*kernel_stats.csv' | head -1); cp $f $OUT/kernel_stats.csv
 [ -n "$SKIP_PMC" ] && exit 0
