@@ -697,9 +697,12 @@ __global__ __launch_bounds__(64, PACK_OCC) void pack_bert_wave_kernel(PackParams
   };
   // a document of <= 64 sentences keeps its lengths in a register, loaded
   // one document visit ahead (the load flies while this visit's pairs run)
+  // (with the document's first slot and length, carried to its visit)
+  int df_next = 0, dn_next = 0;
   auto doc_lens = [&](int d) -> int {
-    const int f = doc_first(d), n = doc_n(d);
-    return n <= 64 && lane < n ? len_at(f + lane) : 0;
+    df_next = doc_first(d);
+    dn_next = doc_n(d);
+    return dn_next <= 64 && lane < dn_next ? len_at(df_next + lane) : 0;
   };
   int dl_next = nd > 0 ? doc_lens(0) : 0;
   // the records of the current 64 pairs, one per lane (lane k = pair
@@ -723,7 +726,7 @@ __global__ __launch_bounds__(64, PACK_OCC) void pack_bert_wave_kernel(PackParams
   };
   for (int dup = 0; dup < P.dup && !err; ++dup) {
     for (int di = 0; di < nd && !err; ++di) {
-      const int first = doc_first(di), len = doc_n(di);
+      const int first = df_next, len = dn_next;  // doc_first(di), doc_n(di) from the prefetch
       const bool dreg = len <= 64;
       const int dl = dl_next;
       const int dps = dreg ? wave_incl_add(dl) : 0;  // (dl is 0 past the document)
