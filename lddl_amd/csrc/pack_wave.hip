@@ -766,7 +766,19 @@ __global__ __launch_bounds__(64, PACK_OCC) void pack_bert_wave_kernel(PackParams
             for (int t = 1; t < 10 && rdi == di; ++t) rdi = (int)rng.randbelow((uint32_t)nd);
             if (rdi == di) rn = false;
           }
-          const int rfirst = doc_first(rdi), rlen = doc_n(rdi);
+          int rfirst, rlen;  // (one branch on the table's residence for both fields)
+          bool rdone = false;
+          if constexpr (!MASK) {
+            if (dres) {
+              rfirst = (int)DL.dfirst[rdi];
+              rlen = (int)DL.dn[rdi];
+              rdone = true;
+            }
+          }
+          if (!rdone) {
+            rfirst = doc_first(rdi);
+            rlen = doc_n(rdi);
+          }
           const int rstart = (int)rng.randint(0, rlen - 1);
           const int k = find_fill([&](int q) { return len_at(rfirst + q); }, rstart, rlen, tb, lane, &lb);
           r.fs1 = s0 + rfirst + rstart;
