@@ -700,8 +700,18 @@ __global__ __launch_bounds__(64, PACK_OCC) void pack_bert_wave_kernel(PackParams
   // (with the document's first slot and length, carried to its visit)
   int df_next = 0, dn_next = 0;
   auto doc_lens = [&](int d) -> int {
-    df_next = doc_first(d);
-    dn_next = doc_n(d);
+    bool got = false;
+    if constexpr (!MASK) {
+      if (dres) {  // (one residence branch for both fields)
+        df_next = (int)DL.dfirst[d];
+        dn_next = (int)DL.dn[d];
+        got = true;
+      }
+    }
+    if (!got) {
+      df_next = doc_first(d);
+      dn_next = doc_n(d);
+    }
     return dn_next <= 64 && lane < dn_next ? len_at(df_next + lane) : 0;
   };
   int dl_next = nd > 0 ? doc_lens(0) : 0;
