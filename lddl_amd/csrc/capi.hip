@@ -82,7 +82,7 @@ struct lddl_ctx {
     void* p = nullptr;
     size_t cap = 0;
   };
-  Buf ws[48];
+  Buf ws[50];
   PackParams pp{};
   int64_t last_npairs = -1, last_ntok = -1;
   int64_t* h_tot = nullptr;  // pinned [8]
@@ -704,6 +704,15 @@ extern "C" int lddl_row_spans(lddl_ctx* c, int64_t* d_out_src0, int64_t* d_out_s
   if (c->last_npairs == 0) {
     if (d_out_tok_off) HIP_TRY(hipMemsetAsync(d_out_tok_off, 0, 8, st));
   } else {
+    int32_t* chunk_part = nullptr;
+    int64_t* part_pb = nullptr;
+    int rc;
+    if ((rc = ws_get(c, 48, (size_t)((c->last_npairs + 63) >> 6), &chunk_part)) ||
+        (rc = ws_get(c, 49, (size_t)P.n_part, &part_pb)))
+      return rc;
+    HIP_TRY(launch_chunk_parts(M.pair_base, P.doc_sent_off, P.part_doc_off, P.dup, P.n_part, chunk_part, part_pb, st));
+    M.chunk_part = chunk_part;
+    M.part_pb = part_pb;
     HIP_TRY(launch_row_spans(M, c->last_npairs, st));
   }
   if (d_bin_count)

@@ -115,6 +115,8 @@ struct MatParams {
   const int64_t* part_npairs;
   const int64_t* pair_base;     // [n_part+1] exclusive scan of part_npairs
   const int64_t* tok_base;      // [n_part+1] exclusive scan of part_ntok
+  const int32_t* chunk_part;    // row spans: partition of row 64c, per 64-row chunk c (chunk_parts_kernel)
+  const int64_t* part_pb;       // row spans: dup * first sentence of partition p (its pair arrays' base)
   int64_t n_part;
   int32_t dup;
   int32_t bin_size, nbins;
@@ -142,6 +144,8 @@ hipError_t launch_scan_parts(const int64_t* a, const int64_t* b, int64_t n, int6
 hipError_t launch_materialize(const MatParams& M, int64_t total_pairs, int64_t n_dense, int algo, hipStream_t s);
 // row g's segments as offsets into the dense ids (no token copy); out_tok_off optional
 hipError_t launch_row_spans(const MatParams& M, int64_t total_pairs, hipStream_t s);
+hipError_t launch_chunk_parts(const int64_t* pair_base, const int64_t* doc_sent_off, const int64_t* part_doc_off,
+                              int32_t dup, int64_t n_part, int32_t* chunk_part, int64_t* part_pb, hipStream_t s);
 // tokoff[0..n] = exclusive scan of ntok[0..n) (int64); blocksums: scratch of
 // scan_blocks(n) + 1 entries
 __host__ __device__ int64_t scan_blocks(int64_t n);

@@ -16,8 +16,11 @@
 // holds the partition scans, materialisation (the bulk byte work: gathering
 // token ids into [CLS] A [SEP] B [SEP] rows, wave-parallel per 64 rows), the
 // token offset scans and the static-masking kernels.
+#include <algorithm>
+
 #include "common.h"
 #include "pack.h"
+#include "wave.h"
 
 namespace lddl {
 
@@ -368,22 +371,37 @@ __global__ __launch_bounds__(256) void materialize2_kernel(MatParams M, int64_t 
 // through them.  Wave per 64 rows, lane per row: the same metadata chain as
 // materialize2 (partition, binned record, pair record, segment starts) and
 // ~38 B written per row instead of the row's 2 B per token.
+// Per partition p: part_pb[p] and the 64-row chunks whose first row is p's
+// (chunk_part), so a row-spans wave finds its partition with one load instead
+// of a binary search over pair_base (15 dependent loads per wave).
+__global__ __launch_bounds__(256) void chunk_parts_kernel(const int64_t* pair_base, const int64_t* doc_sent_off,
+                                                          const int64_t* part_doc_off, int32_t dup, int64_t n_part,
+                                                          int32_t* chunk_part, int64_t* part_pb) {
+  for (int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x; p < n_part; p += (int64_t)gridDim.x * 256) {
+    part_pb[p] = (int64_t)dup * doc_sent_off[part_doc_off[p]];
+    const int64_t c0 = (pair_base[p] + 63) >> 6, c1 = (pair_base[p + 1] + 63) >> 6;
+    for (int64_t c = c0; c < c1; ++c) chunk_part[c] = (int32_t)p;
+  }
+}
+
+hipError_t launch_chunk_parts(const int64_t* pair_base, const int64_t* doc_sent_off, const int64_t* part_doc_off,
+                              int32_t dup, int64_t n_part, int32_t* chunk_part, int64_t* part_pb, hipStream_t s) {
+  const int64_t nblk = std::max<int64_t>(1, std::min<int64_t>((n_part + 255) / 256, 1024));
+  hipLaunchKernelGGL(chunk_parts_kernel, dim3((unsigned)nblk), dim3(256), 0, s, pair_base, doc_sent_off, part_doc_off,
+                     dup, n_part, chunk_part, part_pb);
+  return hipGetLastError();
+}
+
 __global__ __launch_bounds__(256) void rowspan_kernel(MatParams M, int64_t total) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t gbase = ((int64_t)blockIdx.x * 4 + wv) * 64;
   if (gbase >= total) return;
-  int64_t plo = 0, phi = M.n_part - 1;
-  while (plo < phi) {
-    const int64_t mid = (plo + phi + 1) >> 1;
-    if (M.pair_base[mid] <= gbase) plo = mid;
-    else phi = mid - 1;
-  }
   const int64_t g = gbase + lane;
   if (g >= total) return;
-  int64_t p = plo;
+  int64_t p = M.chunk_part[gbase >> 6];
   while (M.pair_base[p + 1] <= g) ++p;  // partitions of < 64 pairs
   const int64_t i = g - M.pair_base[p];
-  const int64_t pb = (int64_t)M.dup * M.doc_sent_off[M.part_doc_off[p]];
+  const int64_t pb = M.part_pb[p];
   const PairRec r = M.pairs[pb + M.binned[pb + i]];
   const int32_t l0 = r.hi0 - r.lo0, l1 = r.hi1 - r.lo1;
   M.out_src0[g] = l0 > 0 ? M.fs_dense[r.fs0] + r.lo0 : 0;
@@ -587,32 +605,91 @@ __global__ __launch_bounds__(256) void masked_lm_kernel(MlmParams M) {
 // never include [CLS] / [SEP], pretrain.py:187-190) and the token the masked
 // row shows there (the replacement, or the label when kept) goes to
 // out_token for the writer (lddl_render_masked).
+constexpr int MLM_SPAN_UNROLL = 4;  // masked positions per lane with loads in flight together
+
 __global__ __launch_bounds__(256) void masked_lm_spans_kernel(MlmParams M) {
-  const int sl = threadIdx.x & 15;
+  // A wave per 64 rows.  First every lane resolves one row (partition, its
+  // pair's arena reference, output offset, span starts): the rows' dependent
+  // lookups are all in flight together instead of one row per 16 lanes at a
+  // time.  Then the 64 rows' masked positions are walked as one flat list,
+  // MLM_SPAN_UNROLL positions per lane at a time (their arena and id loads in
+  // flight together); a position's row is found by advancing a per-lane row
+  // cursor over the rows' exclusive position counts in LDS, and the outputs
+  // of consecutive positions are adjacent (coalesced stores).
+  struct RowLds {
+    int64_t aoff[64], ooff[64], a[64], b[64];
+    int32_t l0[64], pre[65];
+  };
+  __shared__ RowLds R[4];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  RowLds& L = R[wv];
   const int64_t total = M.pair_base[M.n_part];
-  const int64_t ng = (int64_t)gridDim.x * 16;  // row groups of 16 lanes
-  for (int64_t g = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4); g < total; g += ng) {
-    const int64_t p = M.row_part[g];
-    const int64_t i = g - M.pair_base[p];
-    const int64_t pb = (int64_t)M.dup * M.doc_sent_off[M.part_doc_off[p]];
-    const int64_t ref = M.mref[pb + M.binned[pb + i]];
-    const int nm = (int)((uint64_t)ref >> 48);
-    const int64_t aoff = ref & ((int64_t(1) << 48) - 1);
-    const int64_t ooff = M.mask_base[p] + M.mloc[pb + i];
-    const int64_t a = M.src0[g], b = M.src1[g];
-    const int32_t l0 = M.len0[g];
-    if (sl == 0) {
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t g0 = ((int64_t)blockIdx.x * 4 + wv) * 64; g0 < total; g0 += nw * 64) {
+    const int64_t g = g0 + lane;
+    int nm = 0;
+    if (g < total) {
+      const int64_t p = M.row_part[g];
+      const int64_t i = g - M.pair_base[p];
+      const int64_t pb = (int64_t)M.dup * M.doc_sent_off[M.part_doc_off[p]];
+      const int64_t ref = M.mref[pb + M.binned[pb + i]];
+      nm = (int)((uint64_t)ref >> 48);
+      const int64_t ooff = M.mask_base[p] + M.mloc[pb + i];
+      L.aoff[lane] = ref & ((int64_t(1) << 48) - 1);
+      L.ooff[lane] = ooff;
+      L.a[lane] = M.src0[g];
+      L.b[lane] = M.src1[g];
+      L.l0[lane] = M.len0[g];
       M.out_off[g] = ooff;
       if (g == total - 1) M.out_off[total] = ooff + nm;
     }
-    for (int k = sl; k < nm; k += 16) {
-      const uint32_t e = M.marena[aoff + k];
-      const uint32_t pos = e & 0xFFFFu, nid = e >> 16;
-      const uint16_t label = M.ids[(int32_t)pos <= l0 ? a + (pos - 1) : b + ((int32_t)pos - l0 - 2)];
-      M.out_pos[ooff + k] = (uint16_t)pos;
-      M.out_label[ooff + k] = label;
-      M.out_token[ooff + k] = nid != MLM_KEEP ? (uint16_t)nid : label;
+    const int incl = wave_incl_add(nm);
+    L.pre[lane] = incl - nm;
+    if (lane == 63) L.pre[64] = incl;
+    const int T = lane_get(incl, 63);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    int r = 0;  // this lane's row cursor (positions rise with t)
+    constexpr int U = MLM_SPAN_UNROLL;
+    for (int t0 = 0; t0 < T; t0 += 64 * U) {
+      int rr[U], kk[U];
+      uint32_t e[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int t = t0 + 64 * u + lane;
+        rr[u] = -1;
+        if (t < T) {
+          while (L.pre[r + 1] <= t) ++r;
+          rr[u] = r;
+          kk[u] = t - L.pre[r];
+          e[u] = M.marena[L.aoff[r] + kk[u]];
+        }
+      }
+      uint16_t lab[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (rr[u] >= 0) {
+          const int q = rr[u];
+          const int32_t pos = (int32_t)(e[u] & 0xFFFFu);
+          lab[u] = M.ids[pos <= L.l0[q] ? L.a[q] + (pos - 1) : L.b[q] + (pos - L.l0[q] - 2)];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (rr[u] >= 0) {
+          const int q = rr[u];
+          const int64_t o = L.ooff[q] + kk[u];
+          const uint32_t nid = e[u] >> 16;
+          M.out_pos[o] = (uint16_t)(e[u] & 0xFFFFu);
+          M.out_label[o] = lab[u];
+          M.out_token[o] = nid != MLM_KEEP ? (uint16_t)nid : lab[u];
+        }
+      }
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
 }
 
@@ -624,7 +701,7 @@ hipError_t launch_sent_special(const uint16_t* ids, const int64_t* tok_off, cons
 
 hipError_t launch_masked_lm(const MlmParams& M, hipStream_t s) {
   if (M.tokens) hipLaunchKernelGGL(masked_lm_kernel, dim3(2048), dim3(256), 0, s, M);
-  else hipLaunchKernelGGL(masked_lm_spans_kernel, dim3(2048), dim3(256), 0, s, M);
+  else hipLaunchKernelGGL(masked_lm_spans_kernel, dim3(4096), dim3(256), 0, s, M);
   return hipGetLastError();
 }
 

@@ -186,12 +186,15 @@ def test_codebert_end_to_end_vs_oracle(gpu, monkeypatch, mat):
   assert g == len(rows)
 
 
-def test_many_partitions_and_empty_partitions(packer):
-  # partitions with zero docs and docs with empty sentences
+@pytest.mark.parametrize('spans', [False, True])
+def test_many_partitions_and_empty_partitions(packer, spans):
+  # partitions with zero docs and docs with empty sentences; as span rows,
+  # partitions of fewer than 64 rows share a row-spans wave
   docs = [[[5, 6, 7], [], [8, 9]], [[]], [[10] * 40, [11] * 30, [12] * 50], [[13] * 3]] * 20
   pdo = [0, 0, 5, 5, 17, 40, 80, 80]
   sh, ids, ntok = shards_from_docs(docs, part_doc_off=pdo)
-  res = packer.pack(sh, ids, ntok, target_seq_length=64, duplicate_factor=2, seed=7, bin_size=16)
+  res = packer.pack(sh, ids, ntok, target_seq_length=64, duplicate_factor=2, seed=7, bin_size=16, spans=spans)
+  assert res.spans == spans
   rows = res.rows()
   fdocs = [[s for s in d if s] for d in docs]
   exp = []
