@@ -88,6 +88,16 @@ __device__ __forceinline__ int wscan_incl(int v, int lane) {
 
 __device__ __forceinline__ int wsum(int v) { return lane_get(wave_incl_add(v), 63); }
 
+// popcount of a wave mask on the vector unit (two v_bcnt_u32_b32): the result
+// is a VGPR value the scalar unit does not touch
+__device__ __forceinline__ int vpopc64(uint64_t m) {
+  int r;
+  asm volatile("v_bcnt_u32_b32 %0, %1, 0\n\tv_bcnt_u32_b32 %0, %2, %0"
+               : "=&v"(r)
+               : "s"((uint32_t)m), "s"((uint32_t)(m >> 32)));
+  return r;
+}
+
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 
 // MT19937 twist (64-word chunks, ascending: the in-place dependences of the
@@ -822,7 +832,10 @@ __global__ __launch_bounds__(64, PACK_OCC) void pack_bert_wave_kernel(PackParams
           const int sbit = t < th ? posi : (((t - th) & 1) ^ posi ^ 1);  // 1: this step trims A
           const int w = (int)WaveRng::temper(L.mt[min(rng.idx + 2 * lane, MT_N - 1)]);
           const uint64_t SA = __ballot(sbit != 0) & act, F = __ballot(w >= 0) & act;  // front: MSB 0
-          const int x = __popcll(SA & F), a = __popcll(SA), f = __popcll(F);
+          // (the counts on the vector unit: the segment bounds then live in
+          // VGPRs, where the record columns take them; the CU's one scalar
+          // unit is the packer's bound)
+          const int x = vpopc64(SA & F), a = vpopc64(SA), f = vpopc64(F);
           alo += x;
           ahi -= a - x;
           blo += f - x;
@@ -848,7 +861,13 @@ __global__ __launch_bounds__(64, PACK_OCC) void pack_bert_wave_kernel(PackParams
           }
         }
         PW_GSTAMP(9)
-        if (ahi - alo < 1 || bhi - blo < 1) { err = PACK_EASSERT; break; }
+        if (__builtin_amdgcn_readfirstlane((ahi - alo < 1 || bhi - blo < 1) ? 1 : 0)) { err = PACK_EASSERT; break; }
+        if constexpr (MASK != 0) {  // (the masking code wants them uniform)
+          alo = __builtin_amdgcn_readfirstlane(alo);
+          ahi = __builtin_amdgcn_readfirstlane(ahi);
+          blo = __builtin_amdgcn_readfirstlane(blo);
+          bhi = __builtin_amdgcn_readfirstlane(bhi);
+        }
         r.lo0 = (uint16_t)alo; r.hi0 = (uint16_t)ahi;
         r.lo1 = (uint16_t)blo; r.hi1 = (uint16_t)bhi;
         r.flags = (uint16_t)((rn ? 1 : 0) | 2);
