@@ -88,6 +88,14 @@ __device__ __forceinline__ int wscan_incl(int v, int lane) {
 
 __device__ __forceinline__ int wsum(int v) { return lane_get(wave_incl_add(v), 63); }
 
+// a wave-uniform value copied into a VGPR (v_mov): arithmetic on it runs on
+// the vector unit -- for values only per-lane tests read
+__device__ __forceinline__ int vgpr(int x) {
+  int v;
+  asm("v_mov_b32 %0, %1" : "=v"(v) : "s"(x));
+  return v;
+}
+
 // popcount of a wave mask on the vector unit (two v_bcnt_u32_b32): the result
 // is a VGPR value the scalar unit does not touch
 __device__ __forceinline__ int vpopc64(uint64_t m) {
@@ -818,14 +826,11 @@ __global__ __launch_bounds__(64, PACK_OCC) void pack_bert_wave_kernel(PackParams
         int alo = 0, ahi = la, blo = 0, bhi = lb;
         int E = la + lb - max_num;
         int t0 = 0;
-        const int d0l = la - lb;
-        const bool pos = d0l > 0;
-        const int th = pos ? d0l : 1 - d0l;
-        auto side_a = [&](int t) -> bool { return t < th ? pos : (((t - th) & 1) != 0) == pos; };
-        // n steps t0 .. t0 + n - 1 from the next 2n words (n <= 64, before the
-        // twist): every lane reads and compares unconditionally (no exec-mask
-        // branches); the lane mask of the n steps is applied to the ballots
-        const int posi = pos ? 1 : 0;
+        // (th / pos on the vector unit: only the per-lane side test reads them)
+        const int d0l = vgpr(la) - lb;
+        const int posi = d0l > 0 ? 1 : 0;
+        const int th = posi ? d0l : 1 - d0l;
+        auto side_a = [&](int t) -> bool { return (t < th ? posi : (((t - th) & 1) ^ posi ^ 1)) != 0; };
         auto trunc_round = [&](int n) {
           const uint64_t act = __ballot(lane < n);
           const int t = t0 + lane;
