@@ -6,6 +6,10 @@ set -o pipefail
 O=gpurun_out/${TAG:-r4_ab}
 mkdir -p $O
 export TMPDIR=/tmp
+if [ -n "$TESTS" ]; then  # the tree's pack GPU tests first
+  timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu $TESTS > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
+  tail -1 $O/pytest.log
+fi
 B="bench.py --no-cpu-baseline --parquet-parts 0 --frontend-mb 0 --no-sample-check"
 for LIB in tree $LIBS; do
   N=$(basename $LIB .so)
@@ -24,3 +28,9 @@ for f in glob.glob(sys.argv[1] + '/**/*counter_collection.csv', recursive=True):
 print({k: '%.4g' % v for k, v in agg.items()})
 PY
 done
+if [ -n "$MASK_STAMPS" ]; then  # masked packer phase stamps of the tree
+  unset LDDL_LIB
+  LDDL_PACK_DEBUG=1 timeout -k 10 300 python -u bench.py --masking --steps 1 --warmup 0 --no-cpu-baseline --frontend-mb 0 \
+    --parquet-parts 0 --no-sample-check > $O/mask_stamps.log 2>&1 || { tail -5 $O/mask_stamps.log; exit 1; }
+  grep "pack dbg" $O/mask_stamps.log | head -1
+fi
