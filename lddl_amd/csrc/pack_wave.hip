@@ -545,7 +545,8 @@ __device__ __forceinline__ int range_sum(const GET& len_at, int k0, int k1, int 
 // returned for the A length (range_sum = dps[k1 - 1] - base).
 __device__ __forceinline__ int find_fill_reg(int dps, int dex, int tot, int k0, int target, int* sum_out, int* base_out) {
   const int base = __builtin_amdgcn_readlane(dex, k0);
-  const int goal = base + max(1, min(target, tot - base));
+  const int vb = vgpr(base);  // (the goal on the vector unit: only the per-lane compare reads it)
+  const int goal = vb + max(1, min(target, tot - vb));
   const int j = (int)__builtin_ctzll(__ballot(dps >= goal));
   *sum_out = __builtin_amdgcn_readlane(dps, j) - base;
   *base_out = base;
@@ -807,8 +808,22 @@ __global__ __launch_bounds__(64, PACK_OCC) void pack_bert_wave_kernel(PackParams
             rfirst = doc_first(rdi);
             rlen = doc_n(rdi);
           }
+          // a document of <= 64 sentences: its lengths are loaded before
+          // rstart is drawn (the load flies during the draw), then the fill
+          // from rstart is one scan + one compare per lane (lengths >= 1:
+          // the sums from rstart rise strictly, lanes below rstart hold 0)
+          const bool rreg = rlen <= 64;
+          const int rl = rreg && lane < rlen ? len_at(rfirst + lane) : 0;
           const int rstart = (int)rng.randint(0, rlen - 1);
-          const int k = find_fill([&](int q) { return len_at(rfirst + q); }, rstart, rlen, tb, lane, &lb);
+          int k;
+          if (rreg) {
+            const int ps = wave_incl_add(lane >= rstart ? rl : 0);
+            const int vt = vgpr(lane_get(ps, 63));
+            k = (int)__builtin_ctzll(__ballot(ps >= max(1, min(tb, vt))));
+            lb = lane_get(ps, k);
+          } else {
+            k = find_fill([&](int q) { return len_at(rfirst + q); }, rstart, rlen, tb, lane, &lb);
+          }
           r.fs1 = s0 + rfirst + rstart;
           r.n1 = (uint16_t)(k - rstart + 1);
           i_next = j - (nchunk - a_end) + 1;
