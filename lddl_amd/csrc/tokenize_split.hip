@@ -1616,7 +1616,15 @@ hipError_t finish_segment(TokParams P, const SplitParams& S, int n_cu, int fb_gr
   if ((e = launch_scan_ntok_range(P.out_ntok, S.tile_sent + S.t0, S.tile_sent + S.t1, S.seg_sent_cap, P.out_tok_off,
                                   S.scan_bsum, s)) != hipSuccess)
     return e;
-  hipLaunchKernelGGL(tok5::expand_kernel, dim3((unsigned)std::max(1, n_cu * 8)), dim3(256), 0, s, P, S);
+  // blocks per CU of the grid-stride expand (4 waves each; more than fit at once: the later ones
+  // balance the tail): LDDL_EXP_BLOCKS (A/B), default 16 (finish 1.75 -> 1.65 ms per 2 GiB,
+  // profiles/r4_exp.txt)
+  static const int exp_blocks = [] {
+    const char* v = getenv("LDDL_EXP_BLOCKS");
+    const int b = v ? atoi(v) : 0;
+    return b > 0 && b <= 32 ? b : 16;
+  }();
+  hipLaunchKernelGGL(tok5::expand_kernel, dim3((unsigned)std::max(1, n_cu * exp_blocks)), dim3(256), 0, s, P, S);
   return hipGetLastError();
 }
 
