@@ -87,6 +87,45 @@ def upload(corpus, part_doc_off, device):
                   corpus.nbytes)
 
 
+def upload_pieces(corpora, part_doc_off, device):
+  """upload() of consecutive corpus pieces (a chunk split on several host
+  workers) without concatenating them on the host first: each piece is
+  copied once, straight into the pinned staging buffers of the H2D copies."""
+  if len(corpora) == 1:
+    return upload(corpora[0], part_doc_off, device)
+  part_doc_off = np.asarray(part_doc_off, dtype=np.int64)
+  NB = sum(c.nbytes for c in corpora)
+  NS = sum(c.n_sent for c in corpora)
+  ND = sum(c.n_doc for c in corpora)
+  if part_doc_off[0] != 0 or part_doc_off[-1] != ND or np.any(np.diff(part_doc_off) < 0):
+    raise ValueError('part_doc_off must be a non-decreasing cover of [0, n_doc]')
+  data_h = torch.empty(max(NB, 1), dtype=torch.uint8, pin_memory=True)
+  so_h = torch.empty(NS + 1, dtype=torch.int64, pin_memory=True)
+  dso_h = torch.empty(ND + 1, dtype=torch.int64, pin_memory=True)
+  dv, sv, dsv = data_h.numpy(), so_h.numpy(), dso_h.numpy()
+  sv[0] = dsv[0] = 0
+  b = ns = nd = 0
+  for c in corpora:
+    if np.any(np.diff(c.doc_sent_off) < 0) or np.any(np.diff(c.sent_off) < 0):
+      raise ValueError('offsets must be non-decreasing')
+    s0 = int(c.sent_off[0])
+    dv[b:b + c.nbytes] = c.data[s0:s0 + c.nbytes]
+    np.add(c.sent_off[1:], b - s0, out=sv[ns + 1:ns + 1 + c.n_sent])
+    np.add(c.doc_sent_off[1:], ns - int(c.doc_sent_off[0]), out=dsv[nd + 1:nd + 1 + c.n_doc])
+    b += c.nbytes
+    ns += c.n_sent
+    nd += c.n_doc
+  data = torch.empty(NB + 16, dtype=torch.uint8, device=device)
+  data[:NB].copy_(data_h[:NB], non_blocking=True)
+  data[NB:].zero_()
+  nseg = None
+  if corpora[0].doc_nseg_doc is not None:
+    nseg = torch.from_numpy(np.concatenate([c.doc_nseg_doc for c in corpora]).astype(np.int32)).pin_memory().to(
+        device, non_blocking=True)
+  h2d = lambda t: t.to(device, non_blocking=True)  # noqa: E731
+  return ShardSet(data, h2d(so_h), h2d(dso_h), h2d(torch.from_numpy(part_doc_off).pin_memory()), nseg, NB)
+
+
 @dataclasses.dataclass
 class PackResult:
   n_pairs: int

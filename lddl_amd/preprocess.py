@@ -398,12 +398,17 @@ def concat_corpora(corpora, ids):
   nseg = None
   if corpora[0].doc_nseg_doc is not None:
     nseg = np.concatenate([c.doc_nseg_doc for c in corpora])
+  return synth.Corpus(data, np.concatenate(so), np.concatenate(dso), nseg), concat_ids(ids)
+
+
+def concat_ids(ids):
+  """the doc ids of consecutive pieces: lists (BERT) or Arrow arrays (CodeBERT)"""
+  if len(ids) == 1:
+    return ids[0]
   if isinstance(ids[0], list):
-    all_ids = [x for i in ids for x in i]
-  else:
-    import pyarrow as pa
-    all_ids = pa.concat_arrays(ids)
-  return synth.Corpus(data, np.concatenate(so), np.concatenate(dso), nseg), all_ids
+    return [x for i in ids for x in i]
+  import pyarrow as pa
+  return pa.concat_arrays(ids)
 
 
 def input_files(args, codebert=False):
@@ -545,9 +550,10 @@ def main(args, codebert=False):
     return [Done()]
 
   def gather(fs):
-    """the pieces of a chunk, in order, as one corpus (+ ids, split seconds)"""
+    """the pieces of a chunk, in order: (corpora, doc ids, split seconds);
+    pipeline.upload_pieces stages them for the GPU without a host concat"""
     got = [f_.get() for f_ in fs]
-    return concat_corpora([g[0] for g in got], [g[1] for g in got]) + (sum(g[2] for g in got),)
+    return [g[0] for g in got], concat_ids([g[1] for g in got]), sum(g[2] for g in got)
 
   # the first chunks split while this process brings up the GPU context and
   # the device tables
@@ -605,7 +611,7 @@ def main(args, codebert=False):
       if pool is not None and i + ahead < len(todo):
         futs[todo[i + ahead]] = submit(todo[i + ahead])  # overlaps this chunk's GPU work and parquet writes
       t0 = time.perf_counter()
-      sh = pipeline.upload(corpus, pro[a:b + 1] - pro[a], device)
+      sh = pipeline.upload_pieces(corpus, pro[a:b + 1] - pro[a], device)
       ids_d, ntok, toff = pk.tokenize(sh)
       # partition p packs after random.seed(args.seed + global p)
       res = pk.pack(sh, ids_d, ntok, toff, target_seq_length=args.target_seq_length, short_seq_prob=args.short_seq_prob,

@@ -409,3 +409,32 @@ def test_row_spans_equal_materialized_rows(gpu, codebert):
     assert np.array_equal(getattr(s, k)[:s.n_pairs + (1 if k == 'tok_off' else 0)].cpu().numpy(), v), k
   assert np.array_equal(s.bin_count.cpu().numpy(), mbc)
   assert np.array_equal(s.host_tokens(), mt)
+
+
+@pytest.mark.parametrize('codebert', [False, True])
+def test_upload_pieces_equals_upload_of_concat(gpu, codebert):
+  """a chunk's pieces staged straight into the pinned H2D buffers equal the
+  upload of their host concatenation"""
+  import torch
+  from lddl_amd import synth, pipeline, preprocess, writer
+  if codebert:
+    recs = synth.make_code_lines(31, seed=4)
+    split = None
+  else:
+    recs = ['wiki-%d %s' % (i, ' '.join(d)) for i, d in enumerate(synth.make_wiki(1 << 15, seed=6).documents())]
+    split = preprocess.sentence_splitter('rules')[0]
+  cuts = [0, 2, 2, len(recs) // 2, len(recs)]
+  parts = [preprocess.split_records(recs[a:b], codebert, split) for a, b in zip(cuts[:-1], cuts[1:])]
+  ids = [writer.str_array(p[1]) for p in parts] if codebert else [p[1] for p in parts]
+  whole, _ = preprocess.concat_corpora([p[0] for p in parts], ids)
+  pdo = np.array([0, 1, whole.n_doc // 2, whole.n_doc], np.int64)
+  dev = torch.device('cuda', 0)
+  a = pipeline.upload(whole, pdo, dev)
+  b = pipeline.upload_pieces([p[0] for p in parts], pdo, dev)
+  torch.cuda.synchronize()
+  assert a.nbytes == b.nbytes
+  for f in ('data', 'sent_off', 'doc_sent_off', 'part_doc_off'):
+    assert torch.equal(getattr(a, f), getattr(b, f)), f
+  assert (a.doc_nseg_doc is None) == (b.doc_nseg_doc is None)
+  if codebert:
+    assert torch.equal(a.doc_nseg_doc, b.doc_nseg_doc)
