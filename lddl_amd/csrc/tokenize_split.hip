@@ -1061,14 +1061,26 @@ __global__ __launch_bounds__(64 * WAVES) void wp_kernel(TokParams P, SplitParams
   const uint32_t nwaves = gridDim.x * WAVES;
   const int mb0 = (int)P.maxb[0], mb1 = (int)P.maxb[1];
   const uint32_t vmask = P.vt_mask;
-  // the wave's slot stream: chunks gw, gw + nwaves, ...
+  // the wave's slot stream: chunk gw first, then chunks handed out by a
+  // counter (chunks hold different work: dynamic hand-out balances the
+  // launch's tail); the next chunk is fetched one chunk ahead, so the
+  // atomic's round trip flies with the current chunk's loads
+  uint32_t* const wctr = S.chunk_ctr + 1;  // zeroed with chunk_ctr per segment
   uint32_t c = blockIdx.x * WAVES + wv, off = 0, fill = 0;
-  if (c < nch) fill = __builtin_amdgcn_readfirstlane(S.chunk_fill[c]);
+  uint32_t cn = 0;  // (lane 0) the next chunk
+  if (c < nch) {
+    fill = __builtin_amdgcn_readfirstlane(S.chunk_fill[c]);
+    if (lane == 0) cn = nwaves + atomicAdd(wctr, 1u);
+  }
   auto advance = [&]() {
     while (off >= fill && c < nch) {
-      c += nwaves;
+      c = (uint32_t)__builtin_amdgcn_readlane((int)cn, 0);
       off = 0;
-      fill = c < nch ? __builtin_amdgcn_readfirstlane(S.chunk_fill[c]) : 0u;
+      fill = 0u;
+      if (c < nch) {
+        fill = __builtin_amdgcn_readfirstlane(S.chunk_fill[c]);
+        if (lane == 0) cn = nwaves + atomicAdd(wctr, 1u);
+      }
     }
   };
   advance();
@@ -1589,7 +1601,7 @@ hipError_t launch_tokenize_split(const TokParams& P, int64_t nbytes, int64_t* ti
   for (int64_t t0 = 0; t0 < n_tiles; t0 += seg) {
     S.t0 = t0;
     S.t1 = std::min(n_tiles, t0 + seg);
-    if ((e = hipMemsetAsync(S.chunk_ctr, 0, 4, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(S.chunk_ctr, 0, 8, s)) != hipSuccess) return e;  // scan's and wp's chunk counters
     if ((e = hipMemsetAsync(S.fb_count, 0, 4, s)) != hipSuccess) return e;
     if ((e = mark(0, 0)) != hipSuccess) return e;
     if (P.dbg) e = tok5::launch_scan<SCAN_WAVES, true, tok5::SCAN_OCC>(P, S, n_cu, s);
