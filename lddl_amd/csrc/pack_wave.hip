@@ -22,6 +22,7 @@
 #include "pack.h"
 #include "wave.h"
 
+#include <cstdlib>
 #include <type_traits>
 
 namespace lddl {
@@ -1164,14 +1165,30 @@ __global__ __launch_bounds__(64, PACK_OCC) void pack_bert_wave_kernel(PackParams
 #undef PW_GSTAMP
 }
 
+// LDDL_PACK_WAVES_CU=w (occupancy experiments): dynamic LDS padded so that at
+// most w of the kernel's one-wave blocks fit on a CU (160 KiB LDS)
+static size_t occupancy_pad(const void* fn, size_t dyn) {
+  const char* e = getenv("LDDL_PACK_WAVES_CU");
+  const int w = e ? atoi(e) : 0;
+  hipFuncAttributes a;
+  if (w <= 0 || hipFuncGetAttributes(&a, fn) != hipSuccess) return dyn;
+  const size_t per = (size_t)160 * 1024 / (size_t)(w + 1) + 512;  // > 1/(w+1) of the LDS per block
+  return per > a.sharedSizeBytes + dyn ? per - a.sharedSizeBytes : dyn;
+}
+
 hipError_t launch_pack_bert_wave(const PackParams& P, hipStream_t s) {
-  const size_t dyn = pack_dyn_bytes(P.cap_lens, P.cap_docs, P.cap_pairs, P.masking != 0);
+  const size_t dyn0 = pack_dyn_bytes(P.cap_lens, P.cap_docs, P.cap_pairs, P.masking != 0);
   const bool lds = P.cap_lens > 0 || P.cap_docs > 0 || P.cap_pairs > 0;
   const dim3 g((unsigned)P.n_part), b(64);
-#define PW_LAUNCH(M, L)                                                                        \
-  do {                                                                                         \
-    if (P.dbg) hipLaunchKernelGGL((pack_bert_wave_kernel<M, L, true>), g, b, dyn, s, P);      \
-    else hipLaunchKernelGGL((pack_bert_wave_kernel<M, L, false>), g, b, dyn, s, P);           \
+#define PW_LAUNCH(M, L)                                                                                  \
+  do {                                                                                                   \
+    if (P.dbg) {                                                                                         \
+      const size_t dyn = occupancy_pad((const void*)pack_bert_wave_kernel<M, L, true>, dyn0);           \
+      hipLaunchKernelGGL((pack_bert_wave_kernel<M, L, true>), g, b, dyn, s, P);                         \
+    } else {                                                                                             \
+      const size_t dyn = occupancy_pad((const void*)pack_bert_wave_kernel<M, L, false>, dyn0);          \
+      hipLaunchKernelGGL((pack_bert_wave_kernel<M, L, false>), g, b, dyn, s, P);                        \
+    }                                                                                                    \
   } while (0)
   if (P.masking && P.max_seq <= 512) {
     if (lds) PW_LAUNCH(1, true);
