@@ -22,6 +22,8 @@
 #include "pack.h"
 #include "wave.h"
 
+#include <cmath>
+#include <cstddef>
 #include <cstdlib>
 #include <type_traits>
 
@@ -55,13 +57,15 @@ struct PackDyn {                // views into the dynamic LDS region
 extern __shared__ __attribute__((aligned(16))) uint8_t pw_dyn[];
 
 // static masking lists (MASK instantiations only), sized for target_seq_length
-// <= 512 (MASK = 1) or <= MLM_MAX_SEQ (MASK = 2): the half-size lists leave
-// LDS for more resident waves
-template <int CAP>
+// <= 512 with <= MLM_PICKS_1 picks per pair (MASK = 1) or <= MLM_MAX_SEQ
+// (MASK = 2): the smaller lists leave LDS for more resident waves (MASK = 1:
+// 4.5 KB with the MT state, 32 one-wave blocks per CU)
+constexpr int MLM_PICKS_1 = 256;
+template <int CAP, int PCAP>
 struct MaskLds {
   alignas(16) uint16_t jb[CAP + 8];  // shuffle draws: swap x[i] <-> x[jb[i]]
-  uint16_t mpos[CAP];           // picked positions in pick order
-  uint16_t mid[CAP];            // their replacement ids (MLM_KEEP = unchanged)
+  uint16_t mpos[PCAP];          // picked positions in pick order
+  uint16_t mid[PCAP];           // their replacement ids (MLM_KEEP = unchanged)
 };
 struct NoMaskLds {};
 
@@ -561,7 +565,7 @@ __device__ __forceinline__ int find_fill_reg(int dps, int dex, int tot, int k0, 
 template <int MASK, bool LDSOK, bool DBG>
 __global__ __launch_bounds__(64, PACK_OCC) void pack_bert_wave_kernel(PackParams P) {
   __shared__ PackWaveLds L;
-  __shared__ typename std::conditional<MASK != 0, MaskLds<MASK == 1 ? 512 : MLM_MAX_SEQ>, NoMaskLds>::type ML;
+  __shared__ typename std::conditional<MASK != 0, MaskLds<MASK == 1 ? 512 : MLM_MAX_SEQ, MASK == 1 ? MLM_PICKS_1 : MLM_MAX_SEQ>, NoMaskLds>::type ML;
   __shared__ typename std::conditional<MASK != 0, NoMaskLds, PackDocLds>::type DL;
   PackDyn D;
   D.lens = reinterpret_cast<uint16_t*>(pw_dyn);
@@ -951,26 +955,41 @@ __global__ __launch_bounds__(64, PACK_OCC) void pack_bert_wave_kernel(PackParams
           // at v < nm after them is found by successor chains -- F[v] = the
           // smallest q >= nm with j_q = v (the last early swap writing v), then
           // F[q] = the smallest q' > q with j_q' = q, ... until no swap wrote
-          // the position (its original element).  One atomicMin pass builds F
-          // (u32 over the mpos + mid lists, unused until the picks are known).
+          // the position (its original element).  F is u16 over the mpos + mid
+          // lists (unused until the picks are known), built in chunks of 64
+          // swaps from the last down: a later chunk's smaller q overwrite, and
+          // lanes of one chunk on the same j store again until the smallest
+          // stands (LDS has no 16-bit min; collisions are rare).
           constexpr int MCAP = MASK == 1 ? 512 : MLM_MAX_SEQ;
           const int nm8 = (nm + 7) & ~7;
           const bool split = nm < m && nm8 + nm <= MCAP;
           const int tr8 = split ? nm8 : (m + 7) & ~7;  // the traced swaps: [1, tr8)
           if (split) {
-            uint32_t* F = reinterpret_cast<uint32_t*>(ML.mpos);
-            static_assert(sizeof(ML.mpos) + sizeof(ML.mid) >= 4 * MCAP, "F spans mpos + mid");
-            for (int k = lane; k < m; k += 64) F[k] = 0xFFFFFFFFu;
+            uint16_t* F = ML.mpos;
+            using MLT = std::remove_reference_t<decltype(ML)>;
+            static_assert(offsetof(MLT, mid) == offsetof(MLT, mpos) + sizeof(ML.mpos), "mid follows mpos");
+            static_assert(sizeof(ML.mpos) + sizeof(ML.mid) >= 2 * MCAP, "F spans mpos + mid");
+            for (int k = lane; k < m; k += 64) F[k] = 0xFFFFu;
             wsync();
-            for (int q = nm + lane; q < m; q += 64) {
-              const uint32_t j = (uint32_t)((int)(int16_t)ML.jb[q] + (q & ~7));
-              if ((uint32_t)q > j) atomicMin(&F[j], (uint32_t)q);
+            for (int qb = nm + ((m - nm - 1) & ~63); qb >= nm; qb -= 64) {
+              const int q = qb + lane;
+              uint32_t j = 0;
+              bool pend = false;
+              if (q < m) {
+                j = (uint32_t)((int)(int16_t)ML.jb[q] + (q & ~7));
+                pend = (uint32_t)q > j;
+              }
+              while (__ballot(pend) != 0) {
+                if (pend) F[j] = (uint16_t)q;
+                wsync();
+                if (pend) pend = (uint32_t)F[j] > (uint32_t)q;
+                wsync();
+              }
             }
-            wsync();
             // element at v after the early swaps -> jb[nm8 + v]
             for (int v = lane; v < nm; v += 64) {
               uint32_t val = (uint32_t)v, t = F[v];
-              while (t != 0xFFFFFFFFu) {
+              while (t != 0xFFFFu) {
                 val = t;
                 t = F[t];
               }
@@ -1190,7 +1209,8 @@ hipError_t launch_pack_bert_wave(const PackParams& P, hipStream_t s) {
       hipLaunchKernelGGL((pack_bert_wave_kernel<M, L, false>), g, b, dyn, s, P);                        \
     }                                                                                                    \
   } while (0)
-  if (P.masking && P.max_seq <= 512) {
+  // (every pair's picks: max(1, rint(num_tokens * ratio)), num_tokens <= max_seq)
+  if (P.masking && P.max_seq <= 512 && std::max(1, (int)rint((double)P.max_seq * P.mlm_ratio)) <= MLM_PICKS_1) {
     if (lds) PW_LAUNCH(1, true);
     else PW_LAUNCH(1, false);
   } else if (P.masking) {
