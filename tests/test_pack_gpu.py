@@ -261,6 +261,21 @@ def test_bert_masked_end_to_end_vs_oracle(gpu, seq, bin_size, nparts, spans):
   assert 0.75 < n_mask / n < 0.85
 
 
+# seq 512 at a high masking ratio: 0.5 puts up to 256 picks per pair in the
+# MASK = 1 lists (their capacity, MLM_PICKS_1), 0.6 up to 307 picks, which
+# the launch sends to the MASK = 2 instantiation
+@pytest.mark.parametrize('ratio', [0.5, 0.6])
+def test_bert_masked_high_ratio_vs_oracle(gpu, ratio):
+  from lddl_amd import synth, pipeline
+  c = synth.make_wiki(300_000, seed=77)
+  res = pipeline.run_bert(c, target_seq_length=512, bin_size=64, n_partitions=2, seed=99, check_host=True,
+                          masking=True, masked_lm_ratio=ratio, spans=True)
+  oids, ontok = OracleTokenizer(pipeline.VOCAB_BERT).run(c.data, c.sent_off, 512, nthreads=8)
+  exp = po.run_bert_shards(c, oids, ontok, res.part_doc_off, 512, 0.1, 5, 99, 64, masking=(ratio,) + MASK[1:])
+  pipeline.assert_same_pairs(res, exp)
+  assert max(len(r[6]) for r in res.rows()) > 200
+
+
 def test_bert_masked_special_tokens_and_arena_regrow(gpu, monkeypatch):
   """Sentences holding literal [CLS]/[SEP] tokens take the explicit candidate
   list (pretrain.py:187-190); a tiny initial arena forces the regrow path."""
