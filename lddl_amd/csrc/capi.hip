@@ -65,6 +65,12 @@ struct lddl_ctx {
   uint32_t vt_mask = 0;
   uint32_t* d_vbloom = nullptr;  // its Bloom filter
   bool scan_ok = false;          // the ASCII page fits the split scan's per-byte class table
+  // lane tokenizer (tokenize_lane.hip): the vocab trie, its roots, the byte classes
+  uint2* d_trie = nullptr;
+  uint32_t trie_base[2] = {0, 0};
+  uint16_t* d_lane_ctab = nullptr;
+  bool lane_ok = false;
+  uint64_t* d_lane_stats = nullptr;
   // per-kernel timing of the split tokenizer (lddl_set_timing)
   bool timing = false;
   SplitTiming* tm = nullptr;
@@ -95,7 +101,7 @@ struct lddl_ctx {
   int pack_codebert = 0;
   // scratch
   int tok_grid = 0;
-  int tok_algo = 5;  // 5 = split tokenizer, 0 = every tile through the exact serial path
+  int tok_algo = 6;  // 6 = lane tokenizer, 5 = split tokenizer, 0 = every tile through the exact serial path
   uint8_t* d_ovf = nullptr;
   uint32_t* d_counter = nullptr;
   // collate: whole-token vocab table (built on first use)
@@ -141,6 +147,9 @@ static void free_ctx(lddl_ctx* c) {
   (void)hipFree(c->d_counter);
   (void)hipFree(c->d_ctab);
   (void)hipFree(c->d_nrec);
+  (void)hipFree(c->d_trie);
+  (void)hipFree(c->d_lane_ctab);
+  (void)hipFree(c->d_lane_stats);
   if (c->tm) {
     for (int k = 0; k < 3; ++k)
       for (int j = 0; j < 2; ++j)
@@ -170,6 +179,8 @@ static int load_table(lddl_ctx* c, const char* path) {
   int rc = build_uni_tables(path, T, err);
   if (rc) return set_err(rc, "%s", err.c_str());
   c->scan_ok = T.scan_ok;
+  c->lane_ok = T.lane_ok;
+  if ((rc = upload(&c->d_lane_ctab, T.lane_ctab.data(), T.lane_ctab.size() * 2))) return rc;
   if ((rc = upload(&c->d_top, T.top.data(), T.top.size() * 2))) return rc;
   if ((rc = upload(&c->d_pages, T.pages.data(), T.pages.size() * 4))) return rc;
   if ((rc = upload(&c->d_multi, T.multi.data(), T.multi.size() * 4))) return rc;
@@ -197,6 +208,13 @@ static int load_vocab(lddl_ctx* c, const char* path) {
   if ((rc = upload(&c->d_voff, V.voff.data(), V.voff.size() * 4))) return rc;
   if ((rc = upload(&c->d_rpool, V.rpool.data(), V.rpool.size()))) return rc;
   if ((rc = upload(&c->d_rinfo, V.rinfo.data(), V.rinfo.size() * 4))) return rc;
+  if (V.trie.empty()) {
+    c->lane_ok = false;
+  } else {
+    if ((rc = upload(&c->d_trie, V.trie.data(), V.trie.size() * sizeof(uint2)))) return rc;
+    c->trie_base[0] = V.trie_base[0];
+    c->trie_base[1] = V.trie_base[1];
+  }
   c->vocab = std::move(V.vocab);
   return 0;
 }
@@ -215,12 +233,16 @@ extern "C" int lddl_create(const char* vocab_path, const char* table_path, int d
   if (hipGetDeviceProperties(&prop, device) != hipSuccess) { free_ctx(c); return set_err(LDDL_EHIP, "hipGetDeviceProperties"); }
   c->n_cu = prop.multiProcessorCount;
   if ((rc = load_table(c, table_path)) || (rc = load_vocab(c, vocab_path))) { free_ctx(c); return rc; }
-  // 5: the split tokenizer (default); 0: every tile through the exact serial
-  // path -- forced by LDDL_TOKENIZE_ALGO=0 (tests), or taken when the split
-  // tokenizer does not model the tables (its entries keep ids below
-  // SPLIT_EDEF; it derives a byte-class table from the ASCII page)
+  // 6: the lane tokenizer (default); 5: the split tokenizer of rounds 2-4
+  // (A/B); 0: every tile through the exact serial path -- LDDL_TOKENIZE_ALGO
+  // selects (tests); an algorithm that does not model the tables falls back
+  // to the serial one (the lane tokenizer needs the trie and a table in which
+  // no code point normalises to more chars than its UTF-8 bytes; the split
+  // one keeps ids below SPLIT_EDEF and derives its byte classes from the
+  // ASCII page)
   const char* algo = getenv("LDDL_TOKENIZE_ALGO");
-  c->tok_algo = (algo && algo[0] == '0') ? 0 : 5;
+  c->tok_algo = !algo ? 6 : algo[0] == '0' ? 0 : algo[0] == '5' ? 5 : 6;
+  if (c->tok_algo == 6 && !c->lane_ok) c->tok_algo = 0;
   if (c->tok_algo == 5 && (!c->scan_ok || c->vocab_size > (int)SPLIT_EDEF)) c->tok_algo = 0;
   const char* mcap = getenv("LDDL_MLM_CAP");  // initial masking arena (tests force the regrow path)
   c->mlm_cap = mcap ? (uint64_t)atoll(mcap) : 0;
@@ -326,20 +348,26 @@ extern "C" int lddl_tokenize(lddl_ctx* c, const uint8_t* d_bytes, int64_t nbytes
   const char* ech = getenv("LDDL_SPLIT_CHUNKS");
   const int64_t seg_max = c->tok_algo == 0 ? nt : eseg && atoll(eseg) > 0 ? atoll(eseg) : SPLIT_SEG_TILES;
   const int64_t seg = nt < seg_max ? nt : seg_max;
-  int64_t n_chunks = c->tok_algo == 0 ? 1 : split_seg_slots(seg, c->n_cu) / SPLIT_CHUNK;
-  if (ech && atoll(ech) > 0 && c->tok_algo != 0) n_chunks = atoll(ech);
+  const bool split = c->tok_algo == 5;
+  int64_t n_chunks = !split ? 1 : split_seg_slots(seg, c->n_cu) / SPLIT_CHUNK;
+  if (ech && atoll(ech) > 0 && split) n_chunks = atoll(ech);
   const int64_t slots = n_chunks * SPLIT_CHUNK;
   int64_t* tile_sent;
   SplitParams S{};
   int rc;
+  // (the entry / staging buffer: u16 per byte of a segment + the last
+  // sentence's ids past its end)
   if ((rc = ws_get(c, 19, nt + 1, &tile_sent)) || (rc = ws_get(c, 20, nt, &S.fb_list)) ||
-      (rc = ws_get(c, 21, 16, &S.fb_count)) || (rc = ws_get(c, 34, (size_t)seg * 1024 + 4096, &S.ent)) ||
-      (rc = ws_get(c, 35, (size_t)slots * 4, &S.rec)) || (rc = ws_get(c, 42, (size_t)slots * 4, &S.pcs)) ||
-      (rc = ws_get(c, 47, (size_t)slots, &S.pch)) ||
-      (rc = ws_get(c, 36, (size_t)n_chunks + 16, &S.chunk_fill)) || (rc = ws_get(c, 37, n_sent, &S.smeta)) ||
-      (rc = ws_get(c, 43, n_sent, &S.snslot)) || (rc = ws_get(c, 44, (size_t)slots, &S.cnt8)) ||
+      (rc = ws_get(c, 21, 16, &S.fb_count)) ||
+      (rc = ws_get(c, 34, (size_t)seg * 1024 + (size_t)max_tok + 4096, &S.ent)) ||
+      (rc = ws_get(c, 36, (size_t)n_chunks + 16, &S.chunk_fill)) ||
       (rc = ws_get(c, 45, (size_t)scan_blocks(n_sent) + 1, &S.scan_bsum)))
     return rc;
+  if (split && ((rc = ws_get(c, 35, (size_t)slots * 4, &S.rec)) || (rc = ws_get(c, 42, (size_t)slots * 4, &S.pcs)) ||
+                (rc = ws_get(c, 47, (size_t)slots, &S.pch)) || (rc = ws_get(c, 37, n_sent, &S.smeta)) ||
+                (rc = ws_get(c, 43, n_sent, &S.snslot)) || (rc = ws_get(c, 44, (size_t)slots, &S.cnt8))))
+    return rc;
+  if (c->tok_algo == 0 && (rc = ws_get(c, 37, n_sent, &S.smeta))) return rc;
   int64_t* tile_off = nullptr;
   if (c->tok_algo != 0 && (rc = ws_get(c, 46, nt + 1, &tile_off))) return rc;
   S.tile_off = tile_off;
@@ -356,6 +384,25 @@ extern "C" int lddl_tokenize(lddl_ctx* c, const uint8_t* d_bytes, int64_t nbytes
   c->last_tok_sent = n_sent;
   if (c->tok_algo == 0) {
     HIP_TRY(launch_tokenize_serial_dense(P, nbytes, tile_sent, S, c->n_cu, c->tok_grid, st));
+  } else if (c->tok_algo == 6) {
+    tok6::LaneParams Q{};
+    Q.trie = c->d_trie;
+    Q.rbase[0] = c->trie_base[0];
+    Q.rbase[1] = c->trie_base[1];
+    if (getenv("LDDL_LANE_STATS")) {
+      if (!c->d_lane_stats) HIP_TRY(hipMalloc((void**)&c->d_lane_stats, 64));
+      HIP_TRY(hipMemsetAsync(c->d_lane_stats, 0, 64, st));
+      Q.stats = c->d_lane_stats;
+    }
+    HIP_TRY(launch_tokenize_lane(P, nbytes, tile_sent, S, Q, c->d_lane_ctab, c->n_cu, c->tok_grid, st,
+                                 c->timing ? c->tm : nullptr));
+    if (Q.stats) {
+      uint64_t h[3];
+      HIP_TRY(hipMemcpyAsync(h, Q.stats, sizeof h, hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipStreamSynchronize(st));
+      fprintf(stderr, "[lddl tok6] lane-iterations %llu busy %.4f slow passes %llu\n", (unsigned long long)h[0],
+              h[0] ? (double)h[1] / (double)h[0] : 0.0, (unsigned long long)h[2]);
+    }
   } else {
     HIP_TRY(launch_tokenize_split(P, nbytes, tile_sent, S, c->n_cu, c->tok_grid, st,
                                   c->timing ? c->tm : nullptr));

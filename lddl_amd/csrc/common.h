@@ -119,6 +119,23 @@ LDDL_HD uint32_t vbkey_ext(uint32_t hq, uint32_t plen, uint32_t cont) { return v
 LDDL_HD uint32_t vbloom_word(uint32_t x) { return x >> 19; }
 LDDL_HD uint32_t vbloom_bits(uint32_t x) { return (1u << ((x >> 9) & 31u)) | (1u << ((x >> 14) & 31u)); }
 
+// ---- double-array trie of the vocab keys (tok_tables.h build_trie, tokenize_lane.h)
+// Node i's child on byte c sits at base(i) + c and is valid iff its check is
+// i; node 0 is the whole-word root, node 1 the "##" root (keys without the
+// "##").  One 8-B entry per node, so one load per byte of a greedy
+// longest-match walk:
+//   x = check (bits 0-19; TRIE_EMPTY for a free slot) | id bits 0-11 << 20
+//   y = base (bits 0-19) | id bits 12-15 << 20 | accept << 31
+constexpr uint32_t TRIE_EMPTY = 0xFFFFFu;
+LDDL_HD uint32_t trie_check(uint2 e) { return e.x & 0xFFFFFu; }
+LDDL_HD uint32_t trie_base(uint2 e) { return e.y & 0xFFFFFu; }
+LDDL_HD uint32_t trie_id(uint2 e) { return (e.x >> 20) | ((e.y >> 8) & 0xF000u); }
+LDDL_HD bool trie_accept(uint2 e) { return (e.y >> 31) != 0u; }
+
+// lane tokenizer byte classes (tok_tables.h lane_ctab, tokenize_lane.h): an
+// ASCII word char, isolate, space, dropped control, '[', else the slow path
+enum : uint32_t { LANE_CW = 1, LANE_CI = 2, LANE_CSP = 3, LANE_CDR = 4, LANE_CLB = 5, LANE_CNA = 6 };
+
 // ---- MT19937 (CPython random) ----------------------------------------------
 constexpr int MT_N = 624;
 constexpr int MT_M = 397;

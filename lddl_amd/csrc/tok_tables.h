@@ -5,6 +5,7 @@
 // AddressSanitizer.  Reference: the vocab / BertNormalizer of the tokenizer
 // that lddl/dask/bert/pretrain.py:79-80 calls.
 #pragma once
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -23,7 +24,14 @@ struct UniTables {
   std::vector<uint32_t> bmp;     // [0x10000] flattened BMP entries
   std::vector<uint32_t> xmap;    // [0x110000] the split scan's fast exception entries
   bool scan_ok = false;          // the ASCII page fits the split scan's per-byte class table
+  // lane tokenizer (tokenize_lane.hip): per byte, its normalised byte | class << 8 (LANE_C*);
+  // lane_ok: no code point normalises to more chars than its UTF-8 bytes, so a
+  // sentence never has more tokens than bytes (its ids are staged at its byte offset)
+  std::vector<uint16_t> lane_ctab;
+  bool lane_ok = false;
 };
+
+
 
 struct VocabTables {
   std::vector<std::string> vocab;
@@ -39,7 +47,86 @@ struct VocabTables {
   std::vector<uint32_t> vbloom;           // [BLOOM_WORDS] over the v4 keys + extension keys
   std::vector<uint8_t> rpool;             // vocab entries verbatim, 4-aligned (rendering)
   std::vector<uint32_t> rinfo;            // [V] offset << 8 | length into rpool
+  std::vector<uint2> trie;                // lane tokenizer's double-array trie (trie_* below)
+  uint32_t trie_base[2] = {0, 0};         // children offsets of the two roots (whole word, "##")
 };
+
+// ---- double-array trie of the vocab keys (layout: common.h trie_*) -------
+// keys[i] = (cont, bytes) of vocab id i (empty: none); the last duplicate wins.
+// Returns false when the array would pass 2^20 entries.
+inline bool build_trie(const std::vector<std::string>& vocab, std::vector<uint2>& da, uint32_t base_out[2]) {
+  struct Node {
+    std::vector<std::pair<uint8_t, uint32_t>> kids;  // byte -> node
+    int32_t id = -1;
+  };
+  std::vector<Node> nodes(2);
+  for (size_t i = 0; i < vocab.size(); ++i) {
+    const std::string& w = vocab[i];
+    const uint32_t cont = (w.size() >= 2 && w[0] == '#' && w[1] == '#') ? 1u : 0u;
+    if (w.size() == 2 * cont) continue;  // "" / "##": no key
+    uint32_t n = cont;
+    for (size_t k = 2 * cont; k < w.size(); ++k) {
+      const uint8_t c = (uint8_t)w[k];
+      uint32_t nx = 0;
+      for (auto& kc : nodes[n].kids)
+        if (kc.first == c) nx = kc.second;
+      if (!nx) {
+        nx = (uint32_t)nodes.size();
+        nodes[n].kids.push_back({c, nx});
+        nodes.emplace_back();
+      }
+      n = nx;
+    }
+    nodes[n].id = (int32_t)i;
+  }
+  // place breadth-first: slot[node], base[node]; first fit over a used map
+  std::vector<uint32_t> slot(nodes.size(), 0), base(nodes.size(), 0);
+  std::vector<uint8_t> used(1u << 20, 0);
+  used[0] = used[1] = 1;
+  slot[0] = 0;
+  slot[1] = 1;
+  std::vector<uint32_t> order = {0, 1};
+  uint32_t first_free = 2, top = 2;
+  for (size_t qi = 0; qi < order.size(); ++qi) {
+    Node& nd = nodes[order[qi]];
+    if (nd.kids.empty()) continue;
+    std::sort(nd.kids.begin(), nd.kids.end());
+    const uint32_t c0 = nd.kids[0].first;
+    uint32_t b = first_free > c0 ? first_free - c0 : 0;
+    for (;; ++b) {
+      if (b + 256 >= used.size()) return false;
+      bool fit = true;
+      for (auto& kc : nd.kids)
+        if (used[b + kc.first]) { fit = false; break; }
+      if (fit) break;
+    }
+    base[order[qi]] = b;
+    for (auto& kc : nd.kids) {
+      used[b + kc.first] = 1;
+      slot[kc.second] = b + kc.first;
+      order.push_back(kc.second);
+      if (b + kc.first + 1 > top) top = b + kc.first + 1;
+    }
+    while (used[first_free]) ++first_free;
+  }
+  uint32_t maxb = 0;
+  for (uint32_t b : base) maxb = b > maxb ? b : maxb;
+  const size_t size = std::max<size_t>(top, (size_t)maxb + 256) + 1;
+  if (size >= TRIE_EMPTY) return false;
+  da.assign(size, make_uint2(TRIE_EMPTY, 0u));
+  for (size_t i = 0; i < nodes.size(); ++i) {
+    const int32_t id = nodes[i].id < 0 ? 0 : nodes[i].id;
+    uint2 e;
+    e.x = TRIE_EMPTY | ((uint32_t)id & 0xFFFu) << 20;
+    e.y = base[i] | (((uint32_t)id >> 12) & 0xFu) << 20 | (nodes[i].id >= 0 ? 0x80000000u : 0u);
+    da[slot[i]] = e;
+  }
+  for (size_t i = 0; i < nodes.size(); ++i)
+    for (auto& kc : nodes[i].kids) da[slot[kc.second]].x = (da[slot[kc.second]].x & ~0xFFFFFu) | slot[i];
+  base_out[0] = base[0];
+  base_out[1] = base[1];
+  return true;
+}
 
 // Returns 0, or an LDDL_E* code with the reason in err.
 inline int build_uni_tables(const char* path, UniTables& T, std::string& err) {
@@ -83,6 +170,28 @@ inline int build_uni_tables(const char* path, UniTables& T, std::string& err) {
     if (kind == KIND_MAP && cls == CLS_OTHER && !(b >= 'A' && b <= 'Z' && ent_payload(e) == b + 32)) T.scan_ok = false;
   }
   if (ent_cls(T.pages[(size_t)T.top[0] * 256 + '[']) != CLS_ISOLATE) T.scan_ok = false;
+  // the lane tokenizer's byte classes: an ASCII word char (normalised byte
+  // below 0x80), an ASCII isolate, space, drop, '[', else the slow path
+  T.lane_ctab.assign(256, (uint16_t)(LANE_CNA << 8));
+  T.lane_ok = true;
+  for (uint32_t b = 0; b < 128; ++b) {
+    const uint32_t e = T.pages[(size_t)T.top[0] * 256 + b];
+    const uint32_t kind = ent_kind(e), cls = ent_cls(e), out = kind == KIND_IDENT ? b : ent_payload(e);
+    uint32_t c = LANE_CNA;
+    if (ent_rank(e) != 0 || kind == KIND_MULTI) c = LANE_CNA;
+    else if (kind == KIND_DROP_T || kind == KIND_DROP_D) c = LANE_CDR;
+    else if (cls == CLS_SPACE) c = LANE_CSP;
+    else if (out >= 0x80) c = LANE_CNA;
+    else if (cls == CLS_ISOLATE) c = b == '[' ? (out == '[' ? LANE_CLB : LANE_CNA) : LANE_CI;
+    else c = LANE_CW;
+    if (b == '[' && c != LANE_CLB) c = LANE_CNA;  // (specials are matched on the raw byte)
+    T.lane_ctab[b] = (uint16_t)((c << 8) | (out < 0x80 ? out : 0u));
+  }
+  for (uint32_t cp = 0x80; cp < 0x110000; ++cp) {
+    const uint32_t e = T.pages[(size_t)T.top[cp >> 8] * 256 + (cp & 255)];
+    if (ent_kind(e) == KIND_MULTI && T.multi[(size_t)ent_payload(e) * 4] > (cp < 0x800 ? 2u : cp < 0x10000 ? 3u : 4u))
+      T.lane_ok = false;
+  }
   // the BMP flattened (256 KiB, L2-resident): one load per code point < U+10000
   T.bmp.assign(0x10000, 0);
   for (uint32_t cp = 0; cp < 0x10000; ++cp) T.bmp[cp] = T.pages[(size_t)T.top[cp >> 8] * 256 + (cp & 255)];
@@ -256,6 +365,7 @@ inline int build_vocab_tables(const char* path, VocabTables& V, std::string& err
     V.rpool.resize((V.rpool.size() + 3) & ~(size_t)3, 0);
   }
   V.rpool.resize(V.rpool.size() + 16, 0);
+  if (!build_trie(V.vocab, V.trie, V.trie_base)) V.trie.clear();  // (the lane tokenizer then stays off)
   return 0;
 }
 

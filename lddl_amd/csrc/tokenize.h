@@ -116,4 +116,27 @@ hipError_t launch_tokenize_serial_dense(const TokParams& P, int64_t nbytes, int6
 // scanning wave of the scan's real grid on n_cu CUs
 int64_t split_seg_slots(int64_t seg_tiles, int n_cu);
 
+// lane tokenizer (tokenize_lane.hip, tokenize_lane.h)
+namespace tok6 {
+struct LaneParams {
+  const uint2* trie;
+  uint32_t rbase[2];      // children bases of the two roots
+  uint16_t* stage;        // ids at (sentence byte offset - segb)
+  int64_t segb;           // absolute byte offset of staging index 0 (the host passes t0 << 10;
+                          // the kernels add sent_off[0])
+  int64_t bytes_end;      // absolute end of the corpus (set on the device; ring loads start below it)
+  const int64_t* tile_sent;
+  const int64_t* tile_off;
+  int64_t t0, t1;         // the segment's tiles
+  uint32_t* ctr;          // [0] tile batches handed out
+  int32_t* fb_list;
+  int32_t* fb_count;
+  uint32_t* n_fallback;
+  uint64_t* stats;        // optional: [0] iterations x 64, [1] lane-iterations busy, [2] slow passes
+};
+}  // namespace tok6
+hipError_t launch_tokenize_lane(const TokParams& P, int64_t nbytes, int64_t* tile_sent, SplitParams S,
+                                tok6::LaneParams Q, const uint16_t* d_ctab, int n_cu, int fb_grid, hipStream_t s,
+                                SplitTiming* tm);
+
 }  // namespace lddl

@@ -123,7 +123,7 @@ def adversarial_sentences(rng, n):
   return out
 
 
-@pytest.mark.parametrize('algo', ['0', '5'])
+@pytest.mark.parametrize('algo', ['0', '5', '6'])
 @pytest.mark.parametrize('name', ['bert', 'codebert'])
 def test_hip_tokenize_adversarial_vs_oracle(gpu, monkeypatch, algo, name):
   from lddl_amd.synth import corpus_from_sentences
@@ -142,7 +142,7 @@ def test_hip_tokenize_adversarial_vs_oracle(gpu, monkeypatch, algo, name):
       assert np.array_equal(a.astype(np.int64), b.astype(np.int64)), (i, repr(sents[i][:80]))
 
 
-@pytest.mark.parametrize('algo', ['0', '5'])
+@pytest.mark.parametrize('algo', ['0', '5', '6'])
 def test_hip_tokenize_algos_agree_on_wiki(gpu, monkeypatch, algo):
   from lddl_amd import synth
   from lddl_amd.tokenizer import Tokenizer
@@ -168,6 +168,24 @@ def test_hip_tokenize_split_segments_and_capacity(gpu, monkeypatch, env, name):
   for k, v in env.items():
     monkeypatch.setenv(k, v)
   c = synth.make_wiki(2_000_000, seed=29) if name == 'bert' else synth.make_code(1500, seed=31)
+  for max_tok in (512, 5):
+    ids, ntok = run_hip(Tokenizer(VOCABS[name]), c.data, c.sent_off, max_tok)
+    oids, ontok = OracleTokenizer(VOCABS[name]).run(c.data, c.sent_off, max_tok, nthreads=8)
+    assert np.array_equal(ntok, ontok)
+    for a, b in zip(compact(ids, ntok, c.sent_off), compact(oids, ontok, c.sent_off)):
+      assert np.array_equal(a.astype(np.int64), b.astype(np.int64))
+
+
+@pytest.mark.parametrize('seg', ['1', '97'])
+@pytest.mark.parametrize('name', ['bert', 'codebert'])
+def test_hip_tokenize_lane_segments(gpu, monkeypatch, seg, name):
+  """The lane tokenizer (v6) over many small segments: staging, offset scan
+  and compaction continue across segment seams; max_tok 512 and 5."""
+  from lddl_amd import synth
+  from lddl_amd.tokenizer import Tokenizer
+  monkeypatch.setenv('LDDL_TOKENIZE_ALGO', '6')
+  monkeypatch.setenv('LDDL_SPLIT_SEG', seg)
+  c = synth.make_wiki(600_000, seed=33) if name == 'bert' else synth.make_code(600, seed=35)
   for max_tok in (512, 5):
     ids, ntok = run_hip(Tokenizer(VOCABS[name]), c.data, c.sent_off, max_tok)
     oids, ontok = OracleTokenizer(VOCABS[name]).run(c.data, c.sent_off, max_tok, nthreads=8)

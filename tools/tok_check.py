@@ -1,6 +1,6 @@
 """GPU tokenizer check + timing for the kernel variants (GPU box tool).
 
-    python tools/tok_check.py [MB] [algo ...]   (algo 5: split tokenizer, 0: serial path)
+    python tools/tok_check.py [MB] [algo ...]   (algo 6: lane tokenizer, 5: split tokenizer, 0: serial path)
 
 Tokenizes a synthetic Wikipedia-style corpus of MB megabytes with each
 variant, compares ids / counts with the oracle (first MB only, for speed)
@@ -59,7 +59,7 @@ def main():
     ok = len(bad) == 0 and nbad_ids == 0
     ntoks = int(h_ntok.sum())
     times, ks = [], []
-    if algo == '5':
+    if algo in ('5', '6'):
       tok.set_timing(True)
     for _ in range(3):
       s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -68,7 +68,7 @@ def main():
       e.record()
       torch.cuda.synchronize()
       times.append(s.elapsed_time(e))
-      if algo == '5':
+      if algo in ('5', '6'):
         ks.append(tok.stats())
     ms = min(times)
     if ks:
