@@ -363,11 +363,13 @@ extern "C" int lddl_tokenize(lddl_ctx* c, const uint8_t* d_bytes, int64_t nbytes
       (rc = ws_get(c, 36, (size_t)n_chunks + 16, &S.chunk_fill)) ||
       (rc = ws_get(c, 45, (size_t)scan_blocks(n_sent) + 1, &S.scan_bsum)))
     return rc;
-  if (split && ((rc = ws_get(c, 35, (size_t)slots * 4, &S.rec)) || (rc = ws_get(c, 42, (size_t)slots * 4, &S.pcs)) ||
-                (rc = ws_get(c, 47, (size_t)slots, &S.pch)) || (rc = ws_get(c, 37, n_sent, &S.smeta)) ||
-                (rc = ws_get(c, 43, n_sent, &S.snslot)) || (rc = ws_get(c, 44, (size_t)slots, &S.cnt8))))
+  // (the serial path (0) runs the split path's finish: count / expand read
+  // smeta, snslot, cnt8 and, unconditionally, pch[0] -- one chunk of them)
+  if (c->tok_algo != 6 &&
+      ((rc = ws_get(c, 35, (size_t)slots * 4, &S.rec)) || (rc = ws_get(c, 42, (size_t)slots * 4, &S.pcs)) ||
+       (rc = ws_get(c, 47, (size_t)slots, &S.pch)) || (rc = ws_get(c, 37, n_sent, &S.smeta)) ||
+       (rc = ws_get(c, 43, n_sent, &S.snslot)) || (rc = ws_get(c, 44, (size_t)slots, &S.cnt8))))
     return rc;
-  if (c->tok_algo == 0 && (rc = ws_get(c, 37, n_sent, &S.smeta))) return rc;
   int64_t* tile_off = nullptr;
   if (c->tok_algo != 0 && (rc = ws_get(c, 46, nt + 1, &tile_off))) return rc;
   S.tile_off = tile_off;
@@ -397,11 +399,13 @@ extern "C" int lddl_tokenize(lddl_ctx* c, const uint8_t* d_bytes, int64_t nbytes
     HIP_TRY(launch_tokenize_lane(P, nbytes, tile_sent, S, Q, c->d_lane_ctab, c->n_cu, c->tok_grid, st,
                                  c->timing ? c->tm : nullptr));
     if (Q.stats) {
-      uint64_t h[3];
+      uint64_t h[7];
       HIP_TRY(hipMemcpyAsync(h, Q.stats, sizeof h, hipMemcpyDeviceToHost, st));
       HIP_TRY(hipStreamSynchronize(st));
-      fprintf(stderr, "[lddl tok6] lane-iterations %llu busy %.4f slow passes %llu\n", (unsigned long long)h[0],
-              h[0] ? (double)h[1] / (double)h[0] : 0.0, (unsigned long long)h[2]);
+      fprintf(stderr, "[lddl tok6] lane-iterations %llu busy %.4f slow passes %llu ticks handout %llu refill %llu "
+              "slow %llu step %llu\n", (unsigned long long)h[0], h[0] ? (double)h[1] / (double)h[0] : 0.0,
+              (unsigned long long)h[2], (unsigned long long)h[3], (unsigned long long)h[4], (unsigned long long)h[5],
+              (unsigned long long)h[6]);
     }
   } else {
     HIP_TRY(launch_tokenize_split(P, nbytes, tile_sent, S, c->n_cu, c->tok_grid, st,

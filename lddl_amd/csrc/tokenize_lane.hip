@@ -64,8 +64,18 @@ struct DevEnv {
   }
 };
 
-template <int WAVES>
+// DBG: phase stamps (s_memtime, wave-summed) into Q.stats[3..]: hand-out,
+// refill (with its wait), slow pass, step
+template <int WAVES, bool DBG>
 __global__ __launch_bounds__(64 * WAVES) void lane_kernel(TokParams P, LaneParams Q0, const uint16_t* g_ctab) {
+  uint64_t acc[4] = {0, 0, 0, 0}, tprev = 0;
+#define LSTAMP(k)                                                                \
+  if (DBG) {                                                                     \
+    uint64_t t_;                                                                 \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
+    acc[k] += t_ - tprev;                                                        \
+    tprev = t_;                                                                  \
+  }
   LaneParams Q = Q0;
   Q.segb += P.sent_off[0];  // (staging index 0 = the segment's first byte)
   Q.bytes_end = P.sent_off[P.n_sent];
@@ -88,6 +98,7 @@ __global__ __launch_bounds__(64 * WAVES) void lane_kernel(TokParams P, LaneParam
   if (lane == 0) nbat = atomicAdd(Q.ctr, 1u);
   uint32_t iter = 0, slow_age = 0;
   uint64_t n_busy = 0, n_slow = 0;
+  if (DBG) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(tprev)::"memory");
   for (;;) {
     // ---- tiles for lanes that finished theirs (their loads land by the
     //      next iteration, where M_TILE reads them)
@@ -117,6 +128,7 @@ __global__ __launch_bounds__(64 * WAVES) void lane_kernel(TokParams P, LaneParam
       }
       bnext = min(bnext + (int64_t)__popcll(need), bend);
     }
+    LSTAMP(0)
     // ---- ring refill: every lane's missing 16-B chunks, one LDS-DMA per ring
     //      slot (the LDS address of an LDS-DMA is wave-uniform), then one wait
     if ((iter & (REFILL_EVERY - 1)) == 0) {
@@ -139,6 +151,7 @@ __global__ __launch_bounds__(64 * WAVES) void lane_kernel(TokParams P, LaneParam
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
+    LSTAMP(1)
     // ---- the batched slow path
     const uint64_t sw = __ballot(L.mode == M_SLOW);
     if (sw) {
@@ -150,8 +163,11 @@ __global__ __launch_bounds__(64 * WAVES) void lane_kernel(TokParams P, LaneParam
         ++n_slow;
       }
     }
+    LSTAMP(2)
     if (Q.stats) n_busy += __popcll(__ballot(L.mode >= M_TILE && L.mode != M_SLOW));
     lane_step(L, en);
+    if (DBG) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    LSTAMP(3)
     ++iter;
     if (__ballot(L.mode != M_IDLE) == 0) break;
   }
@@ -159,7 +175,10 @@ __global__ __launch_bounds__(64 * WAVES) void lane_kernel(TokParams P, LaneParam
     atomicAdd((unsigned long long*)&Q.stats[0], (unsigned long long)iter * 64ull);
     atomicAdd((unsigned long long*)&Q.stats[1], (unsigned long long)n_busy);
     atomicAdd((unsigned long long*)&Q.stats[2], (unsigned long long)n_slow);
+    if (DBG)
+      for (int k = 0; k < 4; ++k) atomicAdd((unsigned long long*)&Q.stats[3 + k], (unsigned long long)acc[k]);
   }
+#undef LSTAMP
 }
 
 // ------------------------------------------------------------- compact --
@@ -210,7 +229,7 @@ __global__ __launch_bounds__(256) void compact_kernel(TokParams P, const uint16_
 static int lane_blocks_per_cu() {
   static int per_cu = 0;
   if (per_cu == 0 &&
-      (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lane_kernel<LWAVES>, 64 * LWAVES, 0) != hipSuccess ||
+      (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lane_kernel<LWAVES, false>, 64 * LWAVES, 0) != hipSuccess ||
        per_cu < 1))
     per_cu = 1;
   return per_cu;
@@ -245,6 +264,7 @@ hipError_t launch_tokenize_lane(const TokParams& P, int64_t nbytes, int64_t* til
   Q.n_fallback = S.n_fallback;
   const int64_t seg = S.seg_tiles > 0 ? S.seg_tiles : SPLIT_SEG_TILES;
   const int grid = n_cu * tok6::lane_blocks_per_cu();
+  const bool dbg = Q.stats && getenv("LDDL_LANE_STATS") && getenv("LDDL_LANE_STATS")[0] == '2';
   for (int64_t t0 = 0; t0 < n_tiles; t0 += seg) {
     S.t0 = Q.t0 = t0;
     S.t1 = Q.t1 = std::min(n_tiles, t0 + seg);
@@ -252,8 +272,12 @@ hipError_t launch_tokenize_lane(const TokParams& P, int64_t nbytes, int64_t* til
     if ((e = hipMemsetAsync(S.chunk_ctr, 0, 8, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(S.fb_count, 0, 4, s)) != hipSuccess) return e;
     if ((e = mark(0, 0)) != hipSuccess) return e;
-    hipLaunchKernelGGL(tok6::lane_kernel<tok6::LWAVES>, dim3((unsigned)grid), dim3(64 * tok6::LWAVES), 0, s, P, Q,
-                       d_ctab);
+    if (dbg)
+      hipLaunchKernelGGL((tok6::lane_kernel<tok6::LWAVES, true>), dim3((unsigned)grid), dim3(64 * tok6::LWAVES), 0, s,
+                         P, Q, d_ctab);
+    else
+      hipLaunchKernelGGL((tok6::lane_kernel<tok6::LWAVES, false>), dim3((unsigned)grid), dim3(64 * tok6::LWAVES), 0,
+                         s, P, Q, d_ctab);
     if ((e = hipGetLastError()) != hipSuccess || (e = mark(0, 1)) != hipSuccess || (e = mark(2, 0)) != hipSuccess)
       return e;
     if ((e = finish_lane_segment(P, S, Q, n_cu, fb_grid, s)) != hipSuccess || (e = mark(2, 1)) != hipSuccess) return e;
