@@ -58,7 +58,7 @@ constexpr int REFILL_EVERY = 16;              // iterations between ring refills
 constexpr int SLOW_BATCH = 8;                 // waiting lanes that trigger the wave's slow pass
 constexpr int SLOW_AGE = 24;                  // ... or iterations the oldest has waited
 
-enum : uint32_t { M_IDLE = 0, M_NEED, M_TILE, M_SCAN, M_WORD, M_BUF, M_SKIP, M_SLOW };
+enum : uint32_t { M_IDLE = 0, M_NEED, M_TILE, M_TILE2, M_SCAN, M_WORD, M_BUF, M_SKIP, M_SLOW };
 enum : uint32_t { SL_UNIT = 1, SL_WORD = 2, SL_SKIPCH = 3 };
 
 struct LaneState {
@@ -68,7 +68,10 @@ struct LaneState {
   int64_t s, sb;          // sentence, one past the tile's last
   int64_t tb16;           // 16-aligned base of the tile's bytes: positions below are relative to it
   int64_t obase;          // staging index of the sentence's token 0 (M_TILE: the tile's first byte)
-  int32_t p, se, nse;     // byte cursor, sentence end, next sentence's end
+  int64_t sa1, sa2;       // sent_off[s + 1], sent_off[s + 2] as of the previous iteration: every
+                          // iteration loads them for the next, so a sentence start never waits
+                          // on a load it issued (and no branch merge copies a pending load)
+  int32_t p, se;          // byte cursor, sentence end
   int32_t w0, ps, la;     // word start, piece start, end of the longest accepted piece (< 0: none);
                           // BUF: buffer indices
   int32_t nt, wt;         // tokens of the sentence, tokens before the word
@@ -219,30 +222,30 @@ LDDL_HD void sentence_end(LaneState& L, const E& en) {
   }
   L.p = L.se;  // (a sentence cut at max_tok ends early)
   const int32_t ss = L.se;
-  L.se = L.nse;
-  const int64_t nx = L.s + 2 <= P.n_sent ? L.s + 2 : P.n_sent;
-  L.nse = (int32_t)(en.soff(nx) - L.tb16);
+  L.se = (int32_t)(L.sa2 - L.tb16);  // (sent_off[s + 1] of the new s)
   L.nt = 0;
   L.spec = 0;
   L.obase = L.tb16 - en.Q.segb + ss;
 }
 
-// the tile's first sentence (M_TILE: s, sb and the tile's first byte offset
-// in obase, loaded by the wave's hand-out in the previous iteration)
+// the tile's first sentence in two iterations: M_TILE has s, sb and the
+// tile's first byte offset (obase) from the wave's hand-out; M_TILE2 finds
+// sent_off[s + 1] in sa1 (loaded at the end of M_TILE's iteration)
 template <class E>
 LDDL_HD void tile_start(LaneState& L, const E& en) {
-  const TokParams& P = en.P;
-  if (L.s >= L.sb) {
-    L.mode = M_NEED;
+  if (L.mode == M_TILE) {
+    if (L.s >= L.sb) {
+      L.mode = M_NEED;
+      return;
+    }
+    const int64_t a = L.obase;
+    L.tb16 = a & ~(int64_t)15;
+    L.p = (int32_t)(a - L.tb16);
+    L.rlo = L.rhi = L.p >> 4;
+    L.mode = M_TILE2;
     return;
   }
-  const int64_t a = L.obase;
-  L.tb16 = a & ~(int64_t)15;
-  L.p = (int32_t)(a - L.tb16);
-  L.rlo = L.rhi = L.p >> 4;
-  L.se = (int32_t)(en.soff(L.s + 1) - L.tb16);
-  const int64_t nx = L.s + 2 <= P.n_sent ? L.s + 2 : P.n_sent;
-  L.nse = (int32_t)(en.soff(nx) - L.tb16);
+  L.se = (int32_t)(L.sa1 - L.tb16);
   L.nt = 0;
   L.spec = 0;
   L.obase = L.tb16 - en.Q.segb + L.p;
@@ -270,15 +273,36 @@ LDDL_HD int special_at(const E& en, int32_t p, int32_t se, int32_t* len) {
 template <class E>
 LDDL_HD void lane_step(LaneState& L, const E& en) {
   const TokParams& P = en.P;
-  if (L.mode == M_TILE) {
-    tile_start(L, en);
-    return;
+  const uint32_t mode = L.mode;
+  const bool buf = mode == M_BUF;
+  // every lane reads its ring at the cursor and one byte past it and issues
+  // one trie load, whatever its mode (lanes with nothing to feed load entry
+  // 0): branch-free up to the trie entry, which is then used whole
+  int32_t q = buf ? L.bi : L.p;
+  const uint32_t b = en.rbyte(q), c = en.ctab(b), cls = c >> 8;
+  const uint32_t c2 = en.ctab(en.rbyte(q + 1)) >> 8;
+  const int32_t need_scan = L.p + 6 < L.se ? L.p + 6 : L.se - 1;  // (a special's bytes)
+  const int32_t need_word = q + 1 < L.se ? q + 1 : q;
+  const bool av = ((mode == M_SCAN ? need_scan : need_word) >> 4) < L.rhi;
+  const bool scan = mode == M_SCAN && L.p < L.se && L.nt < P.max_tok && av;
+  bool startw = scan && (cls == LANE_CW || cls == LANE_CI || cls == LANE_CLB);
+  int32_t splen = 0;
+  int spk = -1;
+  if (startw && cls == LANE_CLB) {  // '[': a literal special, else an isolate
+    spk = special_at(en, L.p, L.se, &splen);
+    if (spk >= 0) startw = false;
   }
-  if (L.mode == M_SKIP) {
+  const bool walk = buf || (mode == M_WORD && av) || startw;
+  const uint32_t nbase = startw ? en.Q.rbase[0] : L.nbase;
+  const uint32_t lb = buf ? b : (c & 0xFFu);
+  const uint32_t idx = walk ? nbase + lb : 0u;
+  const uint2 t = en.trie(idx);
+  if (mode == M_TILE || mode == M_TILE2) {
+    tile_start(L, en);
+  } else if (mode == M_SKIP) {
     if (L.p >= L.se) {
       L.mode = M_SCAN;
     } else if ((L.p >> 4) < L.rhi) {
-      const uint32_t cls = en.ctab(en.rbyte(L.p)) >> 8;
       if (cls == LANE_CW || cls == LANE_CDR) {
         ++L.p;
       } else if (cls == LANE_CNA) {
@@ -288,132 +312,106 @@ LDDL_HD void lane_step(LaneState& L, const E& en) {
         L.mode = M_SCAN;
       }
     }
-    return;
-  }
-  if (L.mode == M_SCAN) {
+  } else if (mode == M_SCAN) {
     if (L.p >= L.se || L.nt >= P.max_tok) {
       sentence_end(L, en);
-      return;
-    }
-    const int32_t need = L.p + 6 < L.se ? L.p + 6 : L.se - 1;  // (a special's bytes)
-    if ((need >> 4) >= L.rhi) return;                          // ring not loaded yet
-    const uint32_t c = en.ctab(en.rbyte(L.p)), cls = c >> 8;
-    if (cls == LANE_CSP || cls == LANE_CDR) {
+    } else if (!av) {
+      // (ring not loaded yet)
+    } else if (cls == LANE_CSP || cls == LANE_CDR) {
       ++L.p;
-      return;
-    }
-    if (cls == LANE_CNA) {
+    } else if (cls == LANE_CNA) {
       L.slow = SL_UNIT;
       L.mode = M_SLOW;
-      return;
+    } else if (spk >= 0) {
+      emit_tok(L, en, P.special[spk]);
+      if ((spk == 2 || spk == 3) && L.nt <= P.max_tok) L.spec = 1;
+      L.p += splen;
+    } else {  // a word (or an isolated char) starts at p; its first byte is fed below
+      L.w0 = L.ps = L.p;
+      L.wt = L.nt;
+      L.node = 0;
+      L.nbase = nbase;
+      L.la = -1;
+      L.iso = cls != LANE_CW ? 1u : 0u;
+      L.mode = M_WORD;
     }
-    uint32_t iso = cls == LANE_CI ? 1u : 0u;
-    if (cls == LANE_CLB) {
-      int32_t len = 0;
-      const int k = special_at(en, L.p, L.se, &len);
-      if (k >= 0) {
-        emit_tok(L, en, P.special[k]);
-        if ((k == 2 || k == 3) && L.nt <= P.max_tok) L.spec = 1;
-        L.p += len;
-        return;
-      }
-      iso = 1u;
-    }
-    L.w0 = L.ps = L.p;
-    L.wt = L.nt;
-    L.node = 0;
-    L.nbase = en.Q.rbase[0];
-    L.la = -1;
-    L.iso = iso;
-    L.mode = M_WORD;
-  }
-  if (L.mode != M_WORD && L.mode != M_BUF) return;
-  const bool buf = L.mode == M_BUF;
-  int32_t q = buf ? L.bi : L.p;
-  if (!buf) {
-    const int32_t need = q + 1 < L.se ? q + 1 : q;
-    if ((need >> 4) >= L.rhi) {
-      const int32_t keep = L.la >= 0 ? L.la : q;
-      if (L.rhi - (keep >> 4) >= RING_SLOTS) {  // the piece outgrew the ring: the slow path
-        L.nt = L.wt;
-        L.slow = SL_WORD;
-        L.mode = M_SLOW;
-      }
-      return;
-    }
-  }
-  const uint32_t b = en.rbyte(q);
-  const uint32_t lb = buf ? b : (en.ctab(b) & 0xFFu);
-  bool more = false, slowish = false, space = false;
-  if (buf) {
-    more = q + 1 < L.bn;
-  } else if (!L.iso && q + 1 < L.se) {
-    const uint32_t c2 = en.ctab(en.rbyte(q + 1)) >> 8;
-    more = c2 == LANE_CW;
-    slowish = c2 == LANE_CNA || c2 == LANE_CDR;
-    space = c2 == LANE_CSP;
-  }
-  const uint32_t idx = L.nbase + lb;
-  const uint2 t = en.trie(idx);
-  const bool ok = trie_check(t) == L.node;
-  if (ok) {
-    L.node = idx;
-    L.nbase = trie_base(t);
-    ++q;
-    if (trie_accept(t)) {
-      L.la = q;
-      L.laid = trie_id(t);
-    }
-    if (slowish) {  // the word goes on with a char the fast path does not model
+  } else if (mode == M_WORD && !av) {
+    const int32_t keep = L.la >= 0 ? L.la : q;
+    if (L.rhi - (keep >> 4) >= RING_SLOTS) {  // the piece outgrew the ring: the slow path
       L.nt = L.wt;
       L.slow = SL_WORD;
       L.mode = M_SLOW;
-      return;
-    }
-    if (more) {
-      if (buf) L.bi = q;
-      else L.p = q;
-      return;
     }
   }
-  // the walk stopped at q: the word ends there (ok) or no key extends [ps, q] (!ok)
-  bool done = false;
-  if (ok && !buf && q - L.w0 > 100) {  // max_input_chars_per_word (an ASCII word: chars = bytes)
-    L.nt = L.wt;
-    emit_tok(L, en, P.unk);
-    done = true;
-  } else if (ok && L.la == q) {
-    emit_tok(L, en, L.laid);
-    done = true;
-  } else if (L.la >= 0) {  // the longest piece from ps, then "##" pieces from its end
-    emit_tok(L, en, L.laid);
-    q = L.ps = L.la;
-    L.la = -1;
-    L.node = 1;
-    L.nbase = en.Q.rbase[1];
-    if (buf) L.bi = q;
-    else L.p = q;
-    return;
-  } else {  // no piece: the word is [UNK]
-    L.nt = L.wt;
-    emit_tok(L, en, P.unk);
-    if (ok || buf || L.iso) {
-      done = true;
-      if (!ok && L.iso) q = L.w0 + 1;
-    } else {
-      L.p = q;
-      L.mode = M_SKIP;
-      return;
-    }
-  }
-  if (done) {
-    L.mode = M_SCAN;
+  if (walk) {
+    bool more = false, slowish = false, space = false;
     if (buf) {
-      L.rlo = L.rhi = L.p >> 4;  // (the buffer held the ring's bytes)
-    } else {
-      L.p = q + ((ok && space) ? 1 : 0);
+      more = q + 1 < L.bn;
+    } else if (!L.iso && q + 1 < L.se) {
+      more = c2 == LANE_CW;
+      slowish = c2 == LANE_CNA || c2 == LANE_CDR;
+      space = c2 == LANE_CSP;
+    }
+    const bool ok = trie_check(t) == L.node;
+    bool stop = true;
+    if (ok) {
+      L.node = idx;
+      L.nbase = trie_base(t);
+      ++q;
+      if (trie_accept(t)) {
+        L.la = q;
+        L.laid = trie_id(t);
+      }
+      if (slowish) {  // the word goes on with a char the fast path does not model
+        L.nt = L.wt;
+        L.slow = SL_WORD;
+        L.mode = M_SLOW;
+        stop = false;
+      } else if (more) {
+        if (buf) L.bi = q;
+        else L.p = q;
+        stop = false;
+      }
+    }
+    if (stop) {
+      // the walk stopped at q: the word ends there (ok) or no key extends [ps, q] (!ok)
+      bool done = false;
+      if (ok && !buf && q - L.w0 > 100) {  // max_input_chars_per_word (an ASCII word: chars = bytes)
+        L.nt = L.wt;
+        emit_tok(L, en, P.unk);
+        done = true;
+      } else if (ok && L.la == q) {
+        emit_tok(L, en, L.laid);
+        done = true;
+      } else if (L.la >= 0) {  // the longest piece from ps, then "##" pieces from its end
+        emit_tok(L, en, L.laid);
+        q = L.ps = L.la;
+        L.la = -1;
+        L.node = 1;
+        L.nbase = en.Q.rbase[1];
+        if (buf) L.bi = q;
+        else L.p = q;
+      } else {  // no piece: the word is [UNK]
+        L.nt = L.wt;
+        emit_tok(L, en, P.unk);
+        if (ok || buf || L.iso) {
+          done = true;
+          if (!ok && L.iso) q = L.w0 + 1;
+        } else {
+          L.p = q;
+          L.mode = M_SKIP;
+        }
+      }
+      if (done) {
+        L.mode = M_SCAN;
+        if (buf) L.rlo = L.rhi = L.p >> 4;  // (the buffer held the ring's bytes)
+        else L.p = q + ((ok && space) ? 1 : 0);
+      }
     }
   }
+  const int64_t n = P.n_sent;
+  L.sa1 = en.soff(L.s + 1 <= n ? L.s + 1 : n);
+  L.sa2 = en.soff(L.s + 2 <= n ? L.s + 2 : n);
 }
 
 }  // namespace tok6

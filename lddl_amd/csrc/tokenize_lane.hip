@@ -100,8 +100,60 @@ __global__ __launch_bounds__(64 * WAVES) void lane_kernel(TokParams P, LaneParam
   uint64_t n_busy = 0, n_slow = 0;
   if (DBG) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(tprev)::"memory");
   for (;;) {
-    // ---- tiles for lanes that finished theirs (their loads land by the
-    //      next iteration, where M_TILE reads them)
+    // ---- ring refill: every lane's missing 16-B chunks, all loads first, then
+    //      their LDS stores (no LDS-DMA: LLVM would then put a vmcnt(0) wait
+    //      in front of every ring read, serialising each iteration behind the
+    //      previous one's stores); one HBM round trip per REFILL_EVERY
+    //      iterations (vmcnt counts in order, so any later wait pays it anyway)
+    if ((iter & (REFILL_EVERY - 1)) == 0) {
+      const bool act = L.mode == M_SCAN || L.mode == M_WORD || L.mode == M_SKIP;
+      int nload = 0;
+      if (act) {
+        const int32_t keep = (L.mode == M_WORD && L.la >= 0) ? L.la : L.p;
+        if ((keep >> 4) > L.rlo) L.rlo = keep >> 4;
+        if (L.rhi < L.rlo) L.rhi = L.rlo;
+        const int64_t room = (Q.bytes_end - L.tb16 + 15) / 16 - L.rhi;  // chunks left before the corpus end
+        nload = (int)min((int64_t)(L.rlo + RING_SLOTS - L.rhi), max(room, (int64_t)0));
+      }
+      // (RING_SLOTS loads per lane, every one issued before the first LDS
+      // store -- a load per needed chunk under its own branch came out as
+      // load, wait, store, load ...; lanes needing fewer re-load their last)
+      if (__ballot(nload > 0)) {
+        uint4 v[RING_SLOTS];
+        const int64_t c0 = nload > 0 ? L.tb16 + 16 * (int64_t)L.rhi : 0;
+#pragma unroll
+        for (int r = 0; r < RING_SLOTS; ++r)
+          v[r] = *reinterpret_cast<const uint4*>(P.bytes + c0 + 16 * (int64_t)min(r, max(nload - 1, 0)));
+#pragma unroll
+        for (int r = 0; r < RING_SLOTS; ++r)  // (keeps the loads from sinking into the stores' branches)
+          asm volatile("" : "+v"(v[r].x), "+v"(v[r].y), "+v"(v[r].z), "+v"(v[r].w));
+#pragma unroll
+        for (int r = 0; r < RING_SLOTS; ++r)
+          if (r < nload) *reinterpret_cast<uint4*>(&rings[wv][(L.rhi + r) & (RING_SLOTS - 1)][lane * 16]) = v[r];
+      }
+      L.rhi += nload;
+    }
+    LSTAMP(1)
+    // ---- the batched slow path
+    const uint64_t sw = __ballot(L.mode == M_SLOW);
+    if (sw) {
+      ++slow_age;
+      const uint64_t other = __ballot(L.mode >= M_TILE && L.mode != M_SLOW);
+      if (__popcll(sw) >= SLOW_BATCH || slow_age >= SLOW_AGE || other == 0) {
+        if (L.mode == M_SLOW) lane_slow(L, en);
+        slow_age = 0;
+        ++n_slow;
+      }
+    }
+    LSTAMP(2)
+    if (Q.stats) n_busy += __popcll(__ballot(L.mode >= M_TILE && L.mode != M_SLOW));
+    lane_step(L, en);
+    if (DBG) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    LSTAMP(3)
+    // ---- tiles for lanes that finished theirs, last in the iteration: the
+    //      loads land during the next one's ring reads, where M_TILE reads them
+    //      (issued earlier, their results would be waited for -- and, vmcnt
+    //      counting in order, every store of the iteration with them)
     const uint64_t need = __ballot(L.mode == M_NEED);
     if (need) {
       if (bnext >= bend && !exhausted) {
@@ -129,45 +181,6 @@ __global__ __launch_bounds__(64 * WAVES) void lane_kernel(TokParams P, LaneParam
       bnext = min(bnext + (int64_t)__popcll(need), bend);
     }
     LSTAMP(0)
-    // ---- ring refill: every lane's missing 16-B chunks, one LDS-DMA per ring
-    //      slot (the LDS address of an LDS-DMA is wave-uniform), then one wait
-    if ((iter & (REFILL_EVERY - 1)) == 0) {
-      const bool act = L.mode == M_SCAN || L.mode == M_WORD || L.mode == M_SKIP;
-      if (act) {
-        const int32_t keep = (L.mode == M_WORD && L.la >= 0) ? L.la : L.p;
-        if ((keep >> 4) > L.rlo) L.rlo = keep >> 4;
-        if (L.rhi < L.rlo) L.rhi = L.rlo;
-      }
-#pragma unroll
-      for (int r = 0; r < 2 * RING_SLOTS; ++r) {
-        const int k = r & (RING_SLOTS - 1);
-        const bool want = act && L.rhi - L.rlo < RING_SLOTS && (L.rhi & (RING_SLOTS - 1)) == k &&
-                          L.tb16 + 16 * (int64_t)L.rhi < Q.bytes_end;
-        if (want) {
-          __builtin_amdgcn_global_load_lds((const uint32_t*)(P.bytes + L.tb16 + 16 * (int64_t)L.rhi),
-                                           (__attribute__((address_space(3))) uint32_t*)&rings[wv][k][0], 16, 0, 0);
-          ++L.rhi;
-        }
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    LSTAMP(1)
-    // ---- the batched slow path
-    const uint64_t sw = __ballot(L.mode == M_SLOW);
-    if (sw) {
-      ++slow_age;
-      const uint64_t other = __ballot(L.mode >= M_TILE && L.mode != M_SLOW);
-      if (__popcll(sw) >= SLOW_BATCH || slow_age >= SLOW_AGE || other == 0) {
-        if (L.mode == M_SLOW) lane_slow(L, en);
-        slow_age = 0;
-        ++n_slow;
-      }
-    }
-    LSTAMP(2)
-    if (Q.stats) n_busy += __popcll(__ballot(L.mode >= M_TILE && L.mode != M_SLOW));
-    lane_step(L, en);
-    if (DBG) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    LSTAMP(3)
     ++iter;
     if (__ballot(L.mode != M_IDLE) == 0) break;
   }

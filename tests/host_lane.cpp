@@ -148,34 +148,6 @@ int main(int argc, char** argv) {
             if (f(L[i])) m |= 1ull << i;
           return m;
         };
-        const uint64_t need = ballot([](const LaneState& l) { return l.mode == M_NEED; });
-        if (need) {
-          if (bnext >= bend && !exhausted) {
-            const int64_t b = Q.t0 + nbat * LANE_BATCH;
-            if (b < Q.t1) {
-              bnext = b;
-              bend = std::min(b + (int64_t)LANE_BATCH, Q.t1);
-              nbat = ctr++;
-            } else {
-              exhausted = true;
-            }
-          }
-          int k = 0;
-          for (int i = 0; i < 64; ++i) {
-            if (L[i].mode != M_NEED) continue;
-            const int64_t t = bnext + k++;
-            if (t < bend) {
-              L[i].t = t;
-              L[i].s = tile_sent[t];
-              L[i].sb = tile_sent[t + 1];
-              L[i].obase = tile_off[t];
-              L[i].mode = M_TILE;
-            } else if (exhausted) {
-              L[i].mode = M_IDLE;
-            }
-          }
-          bnext = std::min(bnext + (int64_t)__builtin_popcountll(need), bend);
-        }
         if ((iter & (REFILL_EVERY - 1)) == 0) {
           for (int i = 0; i < 64; ++i) {
             LaneState& l = L[i];
@@ -207,6 +179,34 @@ int main(int argc, char** argv) {
         for (int i = 0; i < 64; ++i) {
           const HostEnv en{P, Q, &rings[i * RING_BYTES], T.lane_ctab.data(), asct, &aborted};
           lane_step(L[i], en);
+        }
+        const uint64_t need = ballot([](const LaneState& l) { return l.mode == M_NEED; });
+        if (need) {
+          if (bnext >= bend && !exhausted) {
+            const int64_t b = Q.t0 + nbat * LANE_BATCH;
+            if (b < Q.t1) {
+              bnext = b;
+              bend = std::min(b + (int64_t)LANE_BATCH, Q.t1);
+              nbat = ctr++;
+            } else {
+              exhausted = true;
+            }
+          }
+          int k = 0;
+          for (int i = 0; i < 64; ++i) {
+            if (L[i].mode != M_NEED) continue;
+            const int64_t t = bnext + k++;
+            if (t < bend) {
+              L[i].t = t;
+              L[i].s = tile_sent[t];
+              L[i].sb = tile_sent[t + 1];
+              L[i].obase = tile_off[t];
+              L[i].mode = M_TILE;
+            } else if (exhausted) {
+              L[i].mode = M_IDLE;
+            }
+          }
+          bnext = std::min(bnext + (int64_t)__builtin_popcountll(need), bend);
         }
         ++iter;
         if (ballot([](const LaneState& l) { return l.mode != M_IDLE; }) == 0) break;
