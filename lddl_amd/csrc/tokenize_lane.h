@@ -57,6 +57,7 @@ constexpr int LANE_BATCH = 64;                // tiles handed to a wave per coun
 constexpr int REFILL_EVERY = 16;              // iterations between ring refills (a lane eats <= 1 B / iteration)
 constexpr int SLOW_BATCH = 8;                 // waiting lanes that trigger the wave's slow pass
 constexpr int SLOW_AGE = 24;                  // ... or iterations the oldest has waited
+constexpr int WALK_STEPS = 4;                 // trie steps a lane may take per iteration
 
 enum : uint32_t { M_IDLE = 0, M_NEED, M_TILE, M_TILE2, M_SCAN, M_WORD, M_BUF, M_SKIP, M_SLOW };
 enum : uint32_t { SL_UNIT = 1, SL_WORD = 2, SL_SKIPCH = 3 };
@@ -344,47 +345,59 @@ LDDL_HD void lane_step(LaneState& L, const E& en) {
     }
   }
   if (walk) {
-    bool more = false, slowish = false, space = false;
-    if (buf) {
-      more = q + 1 < L.bn;
-    } else if (!L.iso && q + 1 < L.se) {
-      more = c2 == LANE_CW;
-      slowish = c2 == LANE_CNA || c2 == LANE_CDR;
-      space = c2 == LANE_CSP;
-    }
-    const bool ok = trie_check(t) == L.node;
-    bool stop = true;
-    if (ok) {
-      L.node = idx;
-      L.nbase = trie_base(t);
+    // up to WALK_STEPS trie steps while the word goes on (one dependent trie
+    // load each); the iteration's one emit, if any, comes after the steps (a
+    // store in between would make the next step's wait include it: vmcnt
+    // counts in order)
+    uint2 te = t;
+    uint32_t ti = idx, c2n = c2;
+    bool ok, more, slowish, space;
+    for (int j = 1;; ++j) {
+      more = slowish = space = false;
+      if (buf) {
+        more = q + 1 < L.bn;
+      } else if (q + 1 < L.se) {
+        space = c2n == LANE_CSP;  // (consumed with the word's end)
+        if (!L.iso) {
+          more = c2n == LANE_CW;
+          slowish = c2n == LANE_CNA || c2n == LANE_CDR;
+        }
+      }
+      ok = trie_check(te) == L.node;
+      if (!ok) break;
+      L.node = ti;
+      L.nbase = trie_base(te);
       ++q;
-      if (trie_accept(t)) {
+      if (trie_accept(te)) {
         L.la = q;
-        L.laid = trie_id(t);
+        L.laid = trie_id(te);
       }
-      if (slowish) {  // the word goes on with a char the fast path does not model
-        L.nt = L.wt;
-        L.slow = SL_WORD;
-        L.mode = M_SLOW;
-        stop = false;
-      } else if (more) {
-        if (buf) L.bi = q;
-        else L.p = q;
-        stop = false;
-      }
+      if (slowish || !more || j == WALK_STEPS) break;
+      if (!buf && ((q + 1 < L.se ? q + 1 : q) >> 4) >= L.rhi) break;  // (ring: the next iteration)
+      const uint32_t bq = en.rbyte(q);
+      c2n = en.ctab(en.rbyte(q + 1)) >> 8;
+      ti = L.nbase + (buf ? bq : (en.ctab(bq) & 0xFFu));
+      te = en.trie(ti);
     }
-    if (stop) {
+    if (ok && slowish) {  // the word goes on with a char the fast path does not model
+      L.nt = L.wt;
+      L.slow = SL_WORD;
+      L.mode = M_SLOW;
+    } else if (ok && more) {  // (steps used up, or the ring's next chunk not loaded yet)
+      if (buf) L.bi = q;
+      else L.p = q;
+    } else {
       // the walk stopped at q: the word ends there (ok) or no key extends [ps, q] (!ok)
       bool done = false;
+      uint32_t eid = P.unk;
       if (ok && !buf && q - L.w0 > 100) {  // max_input_chars_per_word (an ASCII word: chars = bytes)
         L.nt = L.wt;
-        emit_tok(L, en, P.unk);
         done = true;
       } else if (ok && L.la == q) {
-        emit_tok(L, en, L.laid);
+        eid = L.laid;
         done = true;
       } else if (L.la >= 0) {  // the longest piece from ps, then "##" pieces from its end
-        emit_tok(L, en, L.laid);
+        eid = L.laid;
         q = L.ps = L.la;
         L.la = -1;
         L.node = 1;
@@ -393,7 +406,6 @@ LDDL_HD void lane_step(LaneState& L, const E& en) {
         else L.p = q;
       } else {  // no piece: the word is [UNK]
         L.nt = L.wt;
-        emit_tok(L, en, P.unk);
         if (ok || buf || L.iso) {
           done = true;
           if (!ok && L.iso) q = L.w0 + 1;
@@ -402,6 +414,7 @@ LDDL_HD void lane_step(LaneState& L, const E& en) {
           L.mode = M_SKIP;
         }
       }
+      emit_tok(L, en, eid);
       if (done) {
         L.mode = M_SCAN;
         if (buf) L.rlo = L.rhi = L.p >> 4;  // (the buffer held the ring's bytes)
