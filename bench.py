@@ -67,6 +67,9 @@ def parse():
   ap.add_argument('--launch-check', action='store_true',
                   help='multi-rank plumbing only (CPU, gloo, no GPU kernels): launch --gpus ranks, all-gather '
                        'synthetic per-(partition, bin) counts and print the line fields that depend on the world')
+  ap.add_argument('--build-check', action='store_true',
+                  help='with --launch-check: every rank also runs the library build (a no-op after the launching '
+                       'process built it), loads the library and reports its SHA-1')
   args = ap.parse_args()
   code = args.corpus == 'code'
   if args.unique_mb is None:
@@ -445,6 +448,12 @@ def launch_ranks(args):
     if args.gpus > have:
       print('bench.py: --gpus %d but %d GPU(s) visible' % (args.gpus, have), file=sys.stderr)
       return 2
+  if not args.launch_check or args.build_check:
+    # build once, here, before any rank exists (this process has not touched
+    # the GPU): N ranks finding a stale library would otherwise all compile
+    # (build_hip's lock serialises them, but each would wait for the first)
+    from lddl_amd import build
+    build.build_hip()
   with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
     s.bind(('127.0.0.1', 0))
     port = s.getsockname()[1]
@@ -478,9 +487,23 @@ def launch_check(args, rank, world):
   own = torch.arange(n_part * nbins, dtype=torch.int64).view(n_part, nbins) + 1000 * rank
   got = gather_bin_counts(own, rank * n_part) if world > 1 else own.numpy()
   n = check_gather(got, own.numpy(), rank, world)
+  libs = None
+  if args.build_check:  # every rank: build (a no-op now) and load the library it would run
+    import ctypes
+    import hashlib
+    from lddl_amd import build
+    path = build.build_hip()
+    ctypes.CDLL(path)
+    with open(path, 'rb') as f:
+      mine = (path, hashlib.sha1(f.read()).hexdigest())
+    libs = [None] * world
+    if world > 1:
+      dist.all_gather_object(libs, mine)
+    else:
+      libs = [mine]
   if rank == 0:
     print(json.dumps({'metric': METRIC, 'check': 'launch', 'n_gpus': world, 'gathered_partitions': n,
-                      'partitions_per_rank': n_part, 'parallelism': 'shard%d' % world}), flush=True)
+                      'partitions_per_rank': n_part, 'parallelism': 'shard%d' % world, 'libs': libs}), flush=True)
   if world > 1:
     dist.destroy_process_group()
 

@@ -22,10 +22,18 @@ def _newer(target, deps):
   return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build_hip(force=False, verbose=False, lib=LIB, defines=()):
+def build_hip(force=False, verbose=False, lib=None, defines=()):
   """Each .hip compiled to its own object in parallel (device code is per
   translation unit: the kernels share headers only), then linked.
-  lib / defines: A/B builds of variants (tools/ab_build.py)."""
+  lib / defines: A/B builds of variants (tools/ab_build.py).
+
+  Safe to call from several processes at once (the ranks of a multi-GPU
+  bench): one holds an exclusive lock on the build directory while it
+  compiles, into temporaries named by its pid, and the others, once they get
+  the lock, find the library up to date and return it.  LDDL_BUILD_LIB
+  redirects the default output, LDDL_HIPCC the compiler (tests)."""
+  import fcntl
+  lib = lib or os.environ.get('LDDL_BUILD_LIB') or LIB
   srcs = sorted(glob.glob(os.path.join(CSRC, '*.hip')))
   hdrs = glob.glob(os.path.join(CSRC, '*.h')) + [os.path.join(ROOT, 'include', 'lddl_amd.h')]
   if not force and not _newer(lib, srcs + hdrs):
@@ -33,25 +41,31 @@ def build_hip(force=False, verbose=False, lib=LIB, defines=()):
   from concurrent.futures import ThreadPoolExecutor
   odir = os.path.join(CSRC, 'build') if lib == LIB else os.path.splitext(lib)[0] + '_obj'
   os.makedirs(odir, exist_ok=True)
+  hipcc = os.environ.get('LDDL_HIPCC', 'hipcc')
   flags = ['--offload-arch=%s' % ARCH, '-O3', '-std=c++17', '-fPIC', '-Wno-unused-result'] + ['-D' + d for d in defines]
+  tag = '.tmp%d' % os.getpid()
+  with open(os.path.join(odir, '.build.lock'), 'w') as lk:
+    fcntl.flock(lk, fcntl.LOCK_EX)  # (released when the file closes)
+    if not force and not _newer(lib, srcs + hdrs):  # another process built it meanwhile
+      return lib
 
-  def obj(src):
-    o = os.path.join(odir, os.path.basename(src)[:-4] + '.o')
-    if force or _newer(o, [src] + hdrs):
-      cmd = ['hipcc'] + flags + ['-c', '-o', o + '.tmp', src]
-      if verbose:
-        print(' '.join(cmd))
-      subprocess.run(cmd, check=True, cwd=CSRC)
-      os.replace(o + '.tmp', o)
-    return o
+    def obj(src):
+      o = os.path.join(odir, os.path.basename(src)[:-4] + '.o')
+      if force or _newer(o, [src] + hdrs):
+        cmd = [hipcc] + flags + ['-c', '-o', o + tag, src]
+        if verbose:
+          print(' '.join(cmd))
+        subprocess.run(cmd, check=True, cwd=CSRC)
+        os.replace(o + tag, o)
+      return o
 
-  with ThreadPoolExecutor(max_workers=min(len(srcs), max(1, min(8, os.cpu_count() or 1)))) as ex:
-    objs = list(ex.map(obj, srcs))
-  cmd = ['hipcc', '--offload-arch=%s' % ARCH, '-shared', '-fPIC', '-o', lib + '.tmp'] + objs
-  if verbose:
-    print(' '.join(cmd))
-  subprocess.run(cmd, check=True, cwd=CSRC)
-  os.replace(lib + '.tmp', lib)
+    with ThreadPoolExecutor(max_workers=min(len(srcs), max(1, min(8, os.cpu_count() or 1)))) as ex:
+      objs = list(ex.map(obj, srcs))
+    cmd = [hipcc, '--offload-arch=%s' % ARCH, '-shared', '-fPIC', '-o', lib + tag] + objs
+    if verbose:
+      print(' '.join(cmd))
+    subprocess.run(cmd, check=True, cwd=CSRC)
+    os.replace(lib + tag, lib)
   return lib
 
 
