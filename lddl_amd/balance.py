@@ -243,7 +243,7 @@ def write_shards(shards, outdir, rank=0, world=1, compression='snappy'):
       raise ValueError('shard %s has no rows' % name)
     assert t.num_rows == n, (name, t.num_rows, n)
     path = os.path.join(outdir, name)
-    from .writer import DENSE_COLS
+    from .hostinfo import DENSE_COLS
     pq.write_table(t, path, compression=compression,
                    use_dictionary=[c for c in t.schema.names if c not in DENSE_COLS])
     written.append(path)
@@ -330,10 +330,17 @@ def rank_world():
 _JOB_ENV = ('PMIX_NAMESPACE', 'OMPI_MCA_ess_base_jobid', 'OMPI_MCA_orte_ess_jobid', 'PMI_JOBID', 'SLURM_JOB_ID')
 
 
+_MPI_ENV = ('OMPI_COMM_WORLD_SIZE', 'PMI_SIZE', 'PMIX_RANK', 'PMIX_NAMESPACE', 'MV2_COMM_WORLD_SIZE', 'PMI_RANK')
+
+
 def _mpi_joins(rank, world):
   """mpi4py is usable only when its COMM_WORLD is this launch's world: under
   srun without PMI wiring, or with an mpi4py built against another MPI, every
-  process is a singleton and Barrier() would return at once."""
+  process is a singleton and Barrier() would return at once.  mpi4py.MPI is
+  imported (MPI_Init) only when an MPI launcher's environment is present:
+  elsewhere MPI_Init can abort the process instead of raising."""
+  if not any(k in os.environ for k in _MPI_ENV):
+    return False
   try:
     from mpi4py import MPI
     c = MPI.COMM_WORLD
@@ -389,17 +396,39 @@ def _launch_start():
 _T_IMPORT = time.time()
 
 
-def _file_barrier(outdir, rank, world, timeout=24 * 3600.0, poll=0.05):
+def _barrier_tag():
+  return re.sub(r'[^A-Za-z0-9_.-]', '_', job_id() or 'nojob')
+
+
+def file_barrier_ref(outdir, rank):
+  """Rank 0, before any shard is written: a reference file on the shared
+  filesystem.  Markers are then judged fresh against ITS mtime (set by the
+  same file server clock as theirs), not against rank 0's local clock, which
+  may differ from the other nodes' by more than any margin."""
+  if rank == 0:
+    with open(os.path.join(outdir, '.lddl_barrier.%s.ref' % _barrier_tag()), 'w') as f:
+      f.write('%d\n' % os.getpid())
+
+
+def _file_barrier(outdir, rank, world, timeout=24 * 3600.0, poll=0.05, margin=60.0):
   """Every rank drops a marker file named by the job id; rank 0 waits for all
   of them and removes them.  Only rank 0 acts after the barrier (it removes
-  the inputs and writes .num_samples.json), so the other ranks need not wait."""
-  tag = re.sub(r'[^A-Za-z0-9_.-]', '_', job_id() or 'nojob')
+  the inputs and writes .num_samples.json), so the other ranks need not wait.
+  A marker counts when it is no older than rank 0's reference file
+  (file_barrier_ref) minus `margin` seconds: markers of an earlier launch
+  with the same job id (e.g. one that crashed) are older."""
+  tag = _barrier_tag()
   mk = lambda r: os.path.join(outdir, '.lddl_barrier.%s.%d' % (tag, r))
   with open(mk(rank), 'w') as f:
     f.write('done\n')
   if rank != 0:
     return
-  t0, start = time.time(), _launch_start() - 2.0
+  ref = os.path.join(outdir, '.lddl_barrier.%s.ref' % tag)
+  t0 = time.time()
+  try:
+    start = os.stat(ref).st_mtime - margin
+  except OSError:  # (no reference file: this process' start on the local clock)
+    start = _launch_start() - margin
 
   def fresh(p):
     try:
@@ -412,6 +441,8 @@ def _file_barrier(outdir, rank, world, timeout=24 * 3600.0, poll=0.05):
     time.sleep(poll)
   for r in range(world):
     os.remove(mk(r))
+  if os.path.exists(ref):
+    os.remove(ref)
 
 
 def _barrier(world, kind='dist', outdir=None, rank=0):
@@ -442,6 +473,8 @@ def main(args, rank=None, world=None):
   outdir = args.indir if args.outdir is None else os.path.abspath(os.path.expanduser(args.outdir))
   kind = barrier_kind(world, rank)  # fail before writing when the ranks cannot meet
   os.makedirs(outdir, exist_ok=True)
+  if kind == 'file':
+    file_barrier_ref(outdir, rank)
   paths = sorted(os.path.join(r, f) for r, _, fs in os.walk(args.indir) for f in fs
                  if '.parquet' in os.path.splitext(f)[1])
   counts = [pq.ParquetFile(p).metadata.num_rows for p in paths]

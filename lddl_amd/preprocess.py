@@ -269,8 +269,9 @@ def attach_args(parser=None, codebert=False):
                       'the writer on chunk k)')
   p.add_argument('--split-workers', type=int, default=None,
                  help='host processes splitting sentences ahead of the GPU (0: split inline; default: the cores '
-                      'of this process\'s affinity, as the reference\'s --local-n-workers defaults to '
-                      'os.cpu_count(), pretrain.py:678)')
+                      'of this process\'s affinity (the reference\'s --local-n-workers defaults to os.cpu_count(), '
+                      'pretrain.py:678) capped at LDDL_CPU_SHARE, default 16 -- one GPU\'s share of a GPU box, '
+                      'beside the parquet encode threads')
   p.add_argument('--num-shards', type=int, default=None,
                  help='balance the output into this many shard-{k}.parquet[_b] files (balance_dask_output, '
                       'load_balance.py) with counts all-gathered from the packer')
@@ -512,11 +513,9 @@ def main(args, codebert=False):
   # split workers: forked here, before anything touches the GPU; they read
   # their records from the index (integers only are inherited)
   sw = args.split_workers
-  if sw is None:
-    try:
-      sw = len(os.sched_getaffinity(0))
-    except (AttributeError, OSError):
-      sw = os.cpu_count() or 1
+  if sw is None:  # the host CPU share: affinity capped at LDDL_CPU_SHARE / 16 (hostinfo.cpu_share)
+    from .hostinfo import cpu_share
+    sw = cpu_share()
   # (a chunk's pieces are whole partitions: no more workers than partitions to split)
   n_todo = sum(chunks[c][1] - chunks[c][0] for c in todo)
   nw = min(max(0, sw), n_todo) if n_todo > 1 else 0

@@ -34,7 +34,7 @@ from . import _lib
 from .tokenizer import _ptr, _stream
 
 SEG0, SEG1, ROW, SPAN = 0, 1, 2, 3
-DENSE_COLS = ('A', 'B', 'doc', 'code', 'masked_lm_positions', 'masked_lm_labels')
+from .hostinfo import DENSE_COLS  # noqa: E402  (re-exported: writer.DENSE_COLS)
 
 BERT_SCHEMA = [('A', pa.string()), ('B', pa.string()), ('is_random_next', pa.bool_()),
                ('num_tokens', pa.uint16())]
@@ -204,6 +204,20 @@ def _arrow(typ, off, data, lo, hi):
   return pa.Array.from_buffers(big, hi - lo, [None, pa.py_buffer(o), pa.py_buffer(d)]).cast(typ)
 
 
+def file_table(sch, cols, raw, lo, hi, batch=None):
+  """rows [lo, hi) of a writer batch as one file's table.  batch: the batch's
+  table when every column fits its schema type (a zero-copy slice of it);
+  otherwise (a string column's batch bytes pass 2 GiB: large_string) each
+  string column is rebuilt from raw[name] = (type, int64 offsets, bytes)
+  with offsets rebased to the file's first row -- a slice of the large
+  column keeps absolute offsets, which a cast back to string rejects past
+  2^31 (the file's own bytes fit)"""
+  if batch is not None:
+    return batch.slice(lo, hi - lo)
+  arrs = [_arrow(*raw[nm], lo, hi) if nm in raw else cols[nm].slice(lo, hi - lo) for nm in sch.names]
+  return pa.Table.from_arrays(arrs, schema=sch)
+
+
 def write_shards(packer, res, out_dir, bin_size=None, codebert=False, masking=False, doc_ids=None,
                  part_base=0, compression='snappy', batch_rows=1 << 20, max_parts=None, stream=None,
                  executor=None, pending=None):
@@ -267,30 +281,28 @@ def write_shards(packer, res, out_dir, bin_size=None, codebert=False, masking=Fa
       lab = render(packer, res.mlm_label, res.mlm_off, r0, n, ROW, stream=stream)
       pos = npy_positions(moff_all[r0:r1 + 1] - m0, mpos_all[m0:int(moff_all[r1])])
     # one table over the batch's rows; a file is a zero-copy slice of it
-    cols = {}
+    cols, raw = {}, {}
     if codebert:
       cols['id'] = ids_col.slice(r0, n)
-      cols['doc'] = _arrow_rows(pa.string(), *c0, n)
-      cols['code'] = _arrow_rows(pa.string(), *c1, n)
+      raw['doc'], raw['code'] = (pa.string(),) + tuple(c0), (pa.string(),) + tuple(c1)
     else:
-      cols['A'] = _arrow_rows(pa.string(), *c0, n)
-      cols['B'] = _arrow_rows(pa.string(), *c1, n)
+      raw['A'], raw['B'] = (pa.string(),) + tuple(c0), (pa.string(),) + tuple(c1)
       cols['is_random_next'] = np_array((flags[r0:r1] & 1).astype(bool))
     cols['num_tokens'] = np_array(num_tokens[r0:r1])
     if masking and not codebert:
-      cols['masked_lm_positions'] = _arrow_rows(pa.binary(), *pos, n)
-      cols['masked_lm_labels'] = _arrow_rows(pa.string(), *lab, n)
+      raw['masked_lm_positions'] = (pa.binary(),) + tuple(pos)
+      raw['masked_lm_labels'] = (pa.string(),) + tuple(lab)
     if binned:
       cols['bin_id'] = np_array(bins[r0:r1])
+    for nm, (typ, off, data) in raw.items():
+      cols[nm] = _arrow_rows(typ, off, data, n)
     arrs = [cols[name] for name in sch.names]
     large = any(a.type != fd.type for a, fd in zip(arrs, sch))
-    tb = pa.Table.from_arrays(arrs, names=sch.names)
+    tb = None if large else pa.Table.from_arrays(arrs, names=sch.names)
     for fi in range(f, g):
       lo, hi = int(file_start[fi] - r0), int(file_start[fi + 1] - r0)
       p, b = divmod(fi, nbins)
-      t = tb.slice(lo, hi - lo)
-      if large:  # (a file's own bytes fit 32-bit offsets)
-        t = t.cast(sch)
+      t = file_table(sch, cols, raw, lo, hi, tb)
       name = 'part.%d.parquet' % (part_base + p)
       if binned:
         name += '_%d' % b
@@ -312,12 +324,9 @@ def write_shards(packer, res, out_dir, bin_size=None, codebert=False, masking=Fa
 
 
 def encode_workers():
-  """parquet encode threads: this process' cores, at most 16"""
-  try:
-    n = len(os.sched_getaffinity(0))
-  except (AttributeError, OSError):
-    n = os.cpu_count() or 1
-  return max(1, min(16, n))
+  """parquet encode threads: the host CPU share (hostinfo.cpu_share)"""
+  from .hostinfo import cpu_share
+  return cpu_share()
 
 
 def write_txt(packer, res, out_dir, bin_size=None, codebert=False, masking=False, doc_ids=None, part_base=0,

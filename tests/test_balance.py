@@ -3,6 +3,7 @@ outputs (tests/golden/balance.json.gz, tools/gen_golden_balance.py), and the
 multi-rank count gather / shard ownership over gloo (world size 2)."""
 import gzip
 import json
+import sys
 import os
 
 import numpy as np
@@ -235,5 +236,45 @@ def test_file_barrier_ignores_markers_of_an_earlier_launch(tmp_path, monkeypatch
   with pytest.raises(RuntimeError):
     balance._file_barrier(str(tmp_path), 0, 2, timeout=0.3)
   stale.write_text('done\n')  # a marker of this launch
+  balance._file_barrier(str(tmp_path), 0, 2, timeout=5)
+  assert not [n for n in os.listdir(str(tmp_path)) if n.startswith('.lddl_barrier')]
+
+
+def test_mpi4py_not_initialised_without_an_mpi_launcher(monkeypatch):
+  """outside mpirun / srun (no launcher environment) barrier_kind
+  never imports mpi4py.MPI (its MPI_Init can abort the process)"""
+  import types
+  for k in ('MASTER_ADDR', 'MASTER_PORT') + balance._JOB_ENV + balance._MPI_ENV:
+    monkeypatch.delenv(k, raising=False)
+  mod = types.ModuleType('mpi4py')
+
+  class _Boom(types.ModuleType):
+    def __getattr__(self, name):
+      raise AssertionError('mpi4py.MPI touched')
+  monkeypatch.setitem(sys.modules, 'mpi4py', mod)
+  monkeypatch.setitem(sys.modules, 'mpi4py.MPI', _Boom('mpi4py.MPI'))
+  mod.MPI = sys.modules['mpi4py.MPI']
+  monkeypatch.setenv('SLURM_JOB_ID', '5')
+  assert balance.barrier_kind(2, 0) == 'file'
+
+
+def test_file_barrier_judges_markers_by_the_shared_clock(tmp_path, monkeypatch):
+  """markers are judged against rank 0's reference file on the
+  shared filesystem (one clock), not rank 0's local start time: a marker a
+  little older than rank 0's process start (another node's clock behind)
+  still counts; one older than the reference by more than the margin does not"""
+  for k in balance._JOB_ENV:
+    monkeypatch.delenv(k, raising=False)
+  monkeypatch.setenv('PMIX_NAMESPACE', 'launch-c')
+  monkeypatch.setattr(balance, '_launch_start', lambda: 2e9)  # a local clock far ahead of the file server's
+  balance.file_barrier_ref(str(tmp_path), 0)
+  ref = tmp_path / '.lddl_barrier.launch-c.ref'
+  t_ref = os.stat(str(ref)).st_mtime
+  m1 = tmp_path / '.lddl_barrier.launch-c.1'
+  m1.write_text('done\n')
+  os.utime(str(m1), (t_ref - 3600, t_ref - 3600))  # an earlier launch's
+  with pytest.raises(RuntimeError):
+    balance._file_barrier(str(tmp_path), 0, 2, timeout=0.3)
+  os.utime(str(m1), (t_ref - 30, t_ref - 30))  # this launch, written by a node whose clock is behind
   balance._file_barrier(str(tmp_path), 0, 2, timeout=5)
   assert not [n for n in os.listdir(str(tmp_path)) if n.startswith('.lddl_barrier')]

@@ -362,3 +362,26 @@ def test_batch_columns_past_32bit_offsets(monkeypatch):
   assert t.schema.field('A').type == pa.string() and t.column('A').to_pylist() == ['', 'defg']
   monkeypatch.setattr(writer, 'OFF32_LIMIT', 2**31)
   assert writer._arrow_rows(pa.binary(), off, data, 4).type == pa.binary()
+
+
+def test_file_table_rebases_offsets_past_2gib():
+  """a writer batch whose string bytes really pass 2^31: the file
+  after the 2 GiB row is rebuilt with offsets rebased to its first row, not
+  sliced from the batch's large_string column (Arrow keeps a slice's absolute
+  offsets, and the cast back to string rejects them).  np.zeros leaves the
+  2 GiB buffer untouched: nothing reads its bytes."""
+  import pyarrow as pa
+  from lddl_amd import writer
+  big = 2**31 + 5
+  data = np.zeros(big + 3, np.uint8)
+  data[big:] = np.frombuffer(b'xyz', np.uint8)
+  off = np.array([0, big, big + 3], np.int64)
+  sch = pa.schema([('A', pa.string()), ('num_tokens', pa.uint16())])
+  raw = {'A': (pa.string(), off, data)}
+  cols = {'A': writer._arrow_rows(pa.string(), off, data, 2), 'num_tokens': writer.np_array(np.array([7, 9], np.uint16))}
+  assert cols['A'].type == pa.large_string()
+  t = writer.file_table(sch, cols, raw, 1, 2)
+  assert t.schema == sch
+  assert t.column('A').to_pylist() == ['xyz'] and t.column('num_tokens').to_pylist() == [9]
+  with pytest.raises(pa.ArrowInvalid):  # the old per-file slice + cast
+    pa.Table.from_arrays([cols['A']], names=['A']).slice(1, 1).cast(pa.schema([('A', pa.string())]))
