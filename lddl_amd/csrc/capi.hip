@@ -101,7 +101,7 @@ struct lddl_ctx {
   int pack_codebert = 0;
   // scratch
   int tok_grid = 0;
-  int tok_algo = 6;  // 6 = lane tokenizer, 5 = split tokenizer, 0 = every tile through the exact serial path
+  int tok_algo = 5;  // 5 = split tokenizer, 6 = lane tokenizer, 0 = every tile through the exact serial path
   uint8_t* d_ovf = nullptr;
   uint32_t* d_counter = nullptr;
   // collate: whole-token vocab table (built on first use)
@@ -233,15 +233,15 @@ extern "C" int lddl_create(const char* vocab_path, const char* table_path, int d
   if (hipGetDeviceProperties(&prop, device) != hipSuccess) { free_ctx(c); return set_err(LDDL_EHIP, "hipGetDeviceProperties"); }
   c->n_cu = prop.multiProcessorCount;
   if ((rc = load_table(c, table_path)) || (rc = load_vocab(c, vocab_path))) { free_ctx(c); return rc; }
-  // 6: the lane tokenizer (default); 5: the split tokenizer of rounds 2-4
-  // (A/B); 0: every tile through the exact serial path -- LDDL_TOKENIZE_ALGO
-  // selects (tests); an algorithm that does not model the tables falls back
+  // 5: the split tokenizer (default); 6: the lane tokenizer of round 5
+  // (measured slower; A/B); 0: every tile through the exact serial
+  // path -- LDDL_TOKENIZE_ALGO selects (tests); an algorithm that does not model the tables falls back
   // to the serial one (the lane tokenizer needs the trie and a table in which
   // no code point normalises to more chars than its UTF-8 bytes; the split
   // one keeps ids below SPLIT_EDEF and derives its byte classes from the
   // ASCII page)
   const char* algo = getenv("LDDL_TOKENIZE_ALGO");
-  c->tok_algo = !algo ? 6 : algo[0] == '0' ? 0 : algo[0] == '5' ? 5 : 6;
+  c->tok_algo = !algo ? 5 : algo[0] == '0' ? 0 : algo[0] == '6' ? 6 : 5;
   if (c->tok_algo == 6 && !c->lane_ok) c->tok_algo = 0;
   if (c->tok_algo == 5 && (!c->scan_ok || c->vocab_size > (int)SPLIT_EDEF)) c->tok_algo = 0;
   const char* mcap = getenv("LDDL_MLM_CAP");  // initial masking arena (tests force the regrow path)
@@ -330,6 +330,9 @@ extern "C" int lddl_tokenize(lddl_ctx* c, const uint8_t* d_bytes, int64_t nbytes
   P.vt = c->d_vt;
   P.vt_mask = c->vt_mask;
   P.vbloom = c->d_vbloom;
+  P.trie = c->d_trie;
+  P.trie_base[0] = c->trie_base[0];
+  P.trie_base[1] = c->trie_base[1];
   P.ovf = c->d_ovf;
   P.work_counter = c->d_counter;
   HIP_TRY(hipMemsetAsync(c->d_counter, 0, 64, st));

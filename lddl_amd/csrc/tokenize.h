@@ -38,6 +38,10 @@ struct TokParams {
   const uint4* vt;
   uint32_t vt_mask;  // #buckets - 1
   const uint32_t* vbloom;
+  // double-array trie of the vocab keys (common.h trie_*): the split
+  // tokenizer's WordPiece walk (wpt_kernel) and the lane tokenizer
+  const uint2* trie;
+  uint32_t trie_base[2];  // children bases of the whole-word and "##" roots
   // scratch
   uint8_t* ovf;
   uint32_t* work_counter;

@@ -32,6 +32,8 @@
 // Tiles the scan does not model (window > 2 KiB, > 64 sentences, > 256
 // units, a queued word longer than 56 bytes, record capacity) are
 // listed and re-run by tokenize_fallback_kernel (exact serial path).
+#include <string.h>
+
 #include "common.h"
 #include "tokenize.h"
 #include "wave.h"
@@ -1354,6 +1356,174 @@ __global__ __launch_bounds__(64 * WAVES) void wp_kernel(TokParams P, SplitParams
   }
 }
 
+// ---------------------------------------------------- WordPiece by trie --
+// The same records, pieces and counts as wp_kernel, found by walking the
+// vocab's double-array trie (tok_tables.h build_trie, common.h trie_*): per
+// step one byte of the key and one 8-B entry load; the walk from a piece
+// start ends where no key extends the bytes read, and the longest prefix it
+// accepted on the way is the piece (greedy longest-match-first, exactly
+// WordPiece's); the next piece's walk starts from the "##" root at its end.
+// No Bloom filter and no key hashing: ~30 instructions per step against
+// ~470 per step of wp_kernel's Bloom scan.  One record per lane with refill,
+// as wp_kernel (a lane whose word ends begins the next record in the same
+// step); WPT_STEPS steps per round of the refill bookkeeping.
+constexpr int WPT_STEPS = 2;
+
+template <int WAVES>
+__global__ __launch_bounds__(64 * WAVES) void wpt_kernel(TokParams P, SplitParams S) {
+  __shared__ uint32_t kbuf[WAVES * 64 * KB_DW];
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint32_t* kb = kbuf + wv * 64 * KB_DW + lane;  // dword i at kb[64 * i]
+  auto kbyte = [&](int i) { return (kb[64 * min(i >> 2, KB_DW - 1)] >> (8 * (i & 3))) & 0xFFu; };
+  const uint32_t nch = min(__builtin_amdgcn_readfirstlane(*S.chunk_ctr), S.n_chunks);
+  const uint32_t nwaves = gridDim.x * WAVES;
+  const uint2* const trie = P.trie;
+  const uint32_t rb0 = P.trie_base[0], rb1 = P.trie_base[1];
+  uint32_t* const wctr = S.chunk_ctr + 1;  // zeroed with chunk_ctr per segment
+  uint32_t c = blockIdx.x * WAVES + wv, off = 0, fill = 0;
+  uint32_t cn = 0;  // (lane 0) the next chunk
+  if (c < nch) {
+    fill = __builtin_amdgcn_readfirstlane(S.chunk_fill[c]);
+    if (lane == 0) cn = nwaves + atomicAdd(wctr, 1u);
+  }
+  auto advance = [&]() {
+    while (off >= fill && c < nch) {
+      c = (uint32_t)__builtin_amdgcn_readlane((int)cn, 0);
+      off = 0;
+      fill = 0u;
+      if (c < nch) {
+        fill = __builtin_amdgcn_readfirstlane(S.chunk_fill[c]);
+        if (lane == 0) cn = nwaves + atomicAdd(wctr, 1u);
+      }
+    }
+  };
+  advance();
+  uint32_t nrec = 0;
+  int r = -1;   // record slot being tokenised
+  int pr = -1;  // record slot loaded, not begun
+  uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0, q2 = q0, q3 = q0;
+  bool qlong = false;
+  int q = 0, len = 0, ps = 0, la = -1, np = 0;
+  uint32_t node = 0, nbase = 0, laid = 0;
+  uint4* const outs = S.pcs;
+  uint32_t pw01 = 0, pw23 = 0;
+  auto put_piece = [&](int k, uint32_t id) {
+    if (k < 4) {
+      const uint32_t sh = 16u * (uint32_t)(k & 1);
+      const uint32_t keep = ~(0xFFFFu << sh), val = id << sh;
+      if (k < 2) pw01 = (pw01 & keep) | val;
+      else pw23 = (pw23 & keep) | val;
+    } else {
+      reinterpret_cast<uint16_t*>(outs + (size_t)r * 4)[piece_at(k)] = (uint16_t)id;
+    }
+  };
+  auto finish = [&]() {
+    S.pch[r] = make_uint4((uint32_t)np, pw01, pw23, 0u);
+    S.cnt8[r] = (uint8_t)np;
+    r = -1;
+  };
+  for (;;) {
+    // ---- the walk: WPT_STEPS trie steps of each working lane
+#pragma unroll
+    for (int st = 0; st < WPT_STEPS; ++st) {
+      if (r >= 0) {
+        const uint32_t idx = nbase + kbyte(q);
+        const uint2 t = trie[idx];
+        if (trie_check(t) == node) {
+          node = idx;
+          nbase = trie_base(t);
+          ++q;
+          if (trie_accept(t)) {
+            la = q;
+            laid = trie_id(t);
+          }
+          if (q < len) continue;
+        }
+        // the walk stopped: at the word's end, or no key extends [ps, q]
+        if (la >= 0) {
+          put_piece(np, laid);
+          ++np;
+          if (la == len) {
+            finish();
+          } else {  // the next piece, "##", from the end of this one
+            q = ps = la;
+            la = -1;
+            node = 1;
+            nbase = rb1;
+          }
+        } else {  // some position has no match: the whole word is [UNK]
+          np = 0;
+          put_piece(0, (uint32_t)P.unk);
+          np = 1;
+          finish();
+        }
+      }
+    }
+    // ---- idle lanes take the next slots of the stream (one record ahead)
+    {
+      const uint64_t idle = __ballot(pr < 0);
+      if (idle != 0 && c < nch) {
+        const uint32_t avail = fill - off;
+        const int k = lane_rank(idle);
+        if (pr < 0 && (uint32_t)k < avail) {
+          pr = (int)(c * SPLIT_CHUNK + off + (uint32_t)k);
+          q0 = *recq(S, 0, (uint32_t)pr);
+          q1 = *recq(S, 1, (uint32_t)pr);
+          q2 = q3 = make_uint4(0, 0, 0, 0);
+          qlong = false;
+        }
+        off += min((uint32_t)__popcll(idle), avail);
+        advance();
+      }
+    }
+    // ---- an extension slot is dropped, a long key's bytes 24.. loaded, idle
+    //      lanes with a loaded record begin it
+    if (pr >= 0) {
+      if (q0.x == 0u) {
+        pr = -1;
+      } else if ((q0.x & 0xFFu) > 24u && !qlong) {
+        q2 = *recq(S, 2, (uint32_t)pr);
+        q3 = *recq(S, 3, (uint32_t)pr);
+        qlong = true;
+      } else if (r < 0) {
+        len = (int)(q0.x & 0xFFu);
+        kb[0] = q0.z; kb[64] = q0.w;
+        kb[128] = q1.x; kb[192] = q1.y; kb[256] = q1.z; kb[320] = q1.w;
+        kb[384] = q2.x; kb[448] = q2.y; kb[512] = q2.z; kb[576] = q2.w;
+        kb[640] = q3.x; kb[704] = q3.y; kb[768] = q3.z; kb[832] = q3.w;
+        kb[896] = 0u;
+        kb[960] = 0u;
+        r = pr;
+        pr = -1;
+        ++nrec;
+        q = ps = 0;
+        la = -1;
+        np = 0;
+        node = 0;
+        nbase = rb0;
+      }
+    }
+    if (__ballot(r >= 0 || pr >= 0) == 0 && c >= nch) break;
+  }
+  if (S.n_rec) {
+    const uint32_t tot = lane_get(wave_incl_add(nrec), 63);
+    if (lane == 0 && tot) atomicAdd(S.n_rec, (unsigned long long)tot);
+  }
+}
+
+template <int WAVES>
+static hipError_t launch_wpt(const TokParams& P, const SplitParams& S, int n_cu, hipStream_t s) {
+  static int per_cu = 0;
+  if (per_cu == 0 &&
+      (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, wpt_kernel<WAVES>, 64 * WAVES, 0) != hipSuccess ||
+       per_cu < 1))
+    per_cu = 1;
+  const int64_t grid = (int64_t)n_cu * per_cu;
+  hipLaunchKernelGGL(wpt_kernel<WAVES>, dim3((unsigned)grid), dim3(64 * WAVES), 0, s, P, S);
+  return hipGetLastError();
+}
+
 // ---------------------------------------------------------------- count --
 // Final token count per sentence of the segment: its direct ids (the scan's
 // entries that are vocab ids) + the pieces of its queued words (wp_kernel's
@@ -1547,7 +1717,7 @@ static hipError_t launch_wp(const TokParams& P, const SplitParams& S, int n_cu, 
 
 }  // namespace tok5
 
-constexpr int SCAN_WAVES = 4, WP_WAVES = 12;
+constexpr int SCAN_WAVES = 4, WP_WAVES = 12, WPT_WAVES = 8;
 hipError_t finish_segment(TokParams P, const SplitParams& S, int n_cu, int fb_grid, hipStream_t s);
 
 int64_t split_seg_slots(int64_t seg_tiles, int n_cu) {
@@ -1607,7 +1777,12 @@ hipError_t launch_tokenize_split(const TokParams& P, int64_t nbytes, int64_t* ti
     if (P.dbg) e = tok5::launch_scan<SCAN_WAVES, true, tok5::SCAN_OCC>(P, S, n_cu, s);
     else e = tok5::launch_scan<SCAN_WAVES, false, tok5::SCAN_OCC>(P, S, n_cu, s);
     if (e != hipSuccess || (e = mark(0, 1)) != hipSuccess || (e = mark(1, 0)) != hipSuccess) return e;
-    if ((e = tok5::launch_wp<WP_WAVES>(P, S, n_cu, s)) != hipSuccess) return e;
+    // WordPiece by trie walk (default) or by Bloom scan + bucket probes
+    // (LDDL_WP_ALGO=bloom, or tables without a trie: A/B)
+    static const bool bloom = getenv("LDDL_WP_ALGO") && strcmp(getenv("LDDL_WP_ALGO"), "bloom") == 0;
+    if ((e = (bloom || !P.trie) ? tok5::launch_wp<WP_WAVES>(P, S, n_cu, s) : tok5::launch_wpt<WPT_WAVES>(P, S, n_cu, s)) !=
+        hipSuccess)
+      return e;
     if ((e = mark(1, 1)) != hipSuccess || (e = mark(2, 0)) != hipSuccess) return e;
     if ((e = finish_segment(P, S, n_cu, fb_grid, s)) != hipSuccess || (e = mark(2, 1)) != hipSuccess) return e;
   }
