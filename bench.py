@@ -64,6 +64,16 @@ def parse():
   ap.add_argument('--parquet-parts', type=int, default=64,
                   help='after timing: write this many partitions as parquet shards and report the writer rate '
                        '(GPU string rendering + host Arrow/parquet encode; 0 = skip)')
+  ap.add_argument('--legs', default='mask512,mask128,code,wikibooks',
+                  help='after the headline (rank 0 at N=1, outside its timed region): the other BASELINE workloads '
+                       'as short legs, each with its own steps, kernel times and oracle check of one full-size '
+                       'partition -- mask512 / mask128: static masking at seq 512 / 128 over the same corpus '
+                       '(configs[3]), code: CodeBERT seq 512 (configs[2]), wikibooks: Wikipedia + Books seq 512 '
+                       '(configs[4]); comma list, "" = none')
+  ap.add_argument('--leg-steps', type=int, default=2)
+  ap.add_argument('--frontend-c2-mb', type=float, default=2048.0,
+                  help='MB of raw input for the C2-scale CLI leg (seq 512, bin 64: BASELINE configs[1] end to '
+                       'end through the preprocessor CLI, rank 0 at N=1, before the GPU is touched; 0: off)')
   ap.add_argument('--launch-check', action='store_true',
                   help='multi-rank plumbing only (CPU, gloo, no GPU kernels): launch --gpus ranks, all-gather '
                        'synthetic per-(partition, bin) counts and print the line fields that depend on the world')
@@ -266,20 +276,18 @@ def cpu_baseline(args, base, pdo, seconds):
           'host_cpus': hc}
 
 
-CPU_SHARE = 16  # host cores per GPU this harness lets a GPU command's worker pools use
-
-
 def host_cpus():
-  """The box's CPU count, this process's affinity and the share the CPU legs
-  run at: min(affinity, LDDL_CPU_SHARE or 16).  The GPU boxes of this harness
-  show the whole machine in os.cpu_count() / the affinity (256) but allot one
-  GPU's command a share of 16 cores for its worker pools."""
-  try:
-    aff = len(os.sched_getaffinity(0))
-  except (AttributeError, OSError):
-    aff = None
-  share = int(os.environ.get('LDDL_CPU_SHARE', CPU_SHARE))
-  return {'os_cpu_count': os.cpu_count(), 'affinity': aff, 'share': max(1, min(aff or share, share))}
+  """The box's CPU count, this process's affinity, the cgroup quota and the
+  share the CPU legs run at (lddl_amd.hostinfo): min(affinity, LDDL_CPU_SHARE
+  or 16).  The GPU boxes of this harness show the whole machine in
+  os.cpu_count() / the affinity (256) and allot one GPU's command a share of
+  16 cores for its worker pools -- the box exports OMP_NUM_THREADS / MAX_JOBS
+  = 16 to say so, and `evidence` carries those variables and the cgroup's
+  cpu.max as the box shows them."""
+  from lddl_amd import hostinfo
+  ev = hostinfo.cpu_evidence()
+  return {'os_cpu_count': ev['os_cpu_count'], 'affinity': ev['affinity'], 'share': hostinfo.cpu_share(),
+          'evidence': ev}
 
 
 def sample_partition_check(args, pk, res, base, pdo, reps, seed0):
@@ -398,36 +406,47 @@ def parquet_sample(args, pk, res, sh):
     shutil.rmtree(d, ignore_errors=True)
 
 
-def frontend_leg(mb, chunk_mb=32.0):
+def frontend_leg(mb, chunk_mb=32.0, seq=128, bin_size=None, unique_mb=256):
   """The preprocessor CLI end to end (lddl_amd.preprocess.main, the
-  reference's preprocess_bert_pretrain) on BASELINE.json configs[0]: mb MB of
-  synthetic Wikipedia-style raw input (one ``wiki-<id> <text>`` document per
-  line), seq 128, no static masking, unbinned parquet.  Runs first in the
-  process (its split workers fork before anything touches the GPU); wall,
-  host read / sentence split / GPU / parquet write seconds and the split time
-  hidden behind the GPU and the writer, as preprocess.main reports them."""
+  reference's preprocess_bert_pretrain) on mb MB of synthetic Wikipedia-style
+  raw input (one ``wiki-<id> <text>`` document per line): BASELINE.json
+  configs[0] (seq 128, no static masking, unbinned parquet) by default,
+  configs[1] with seq=512, bin_size=64.  Past unique_mb the documents repeat
+  (each line keeps its own id).  Runs first in the process (its split
+  workers fork before anything touches the GPU); wall, host read / sentence
+  split / GPU / parquet write seconds and the split time hidden behind the
+  GPU and the writer, as preprocess.main reports them."""
   import shutil
   import tempfile
   from lddl_amd import preprocess, synth
   d = tempfile.mkdtemp(prefix='lddl_bench_fe_')
   try:
     t0 = time.perf_counter()
-    c = synth.make_wiki(int(mb * (1 << 20)), seed=11)
+    c = synth.make_wiki(int(min(mb, unique_mb) * (1 << 20)), seed=11)
+    data, so, dso = c.data.tobytes(), c.sent_off, c.doc_sent_off
+    lines = [b' '.join(data[so[k]:so[k + 1]] for k in range(dso[q], dso[q + 1])) for q in range(c.n_doc)]
     os.makedirs(os.path.join(d, 'wiki', 'en'))
-    with open(os.path.join(d, 'wiki', 'en', 'a.txt'), 'w', encoding='utf-8') as f:
-      for i, doc in enumerate(c.documents()):
-        f.write('wiki-%d %s\n' % (i, ' '.join(doc)))
+    want, i = int(mb * (1 << 20)), 0
+    with open(os.path.join(d, 'wiki', 'en', 'a.txt'), 'wb') as f:
+      while f.tell() < want:
+        for doc in lines:
+          f.write(b'wiki-%d %s\n' % (i, doc))
+          i += 1
     gen_s = time.perf_counter() - t0
     raw = os.path.getsize(os.path.join(d, 'wiki', 'en', 'a.txt'))
-    a = preprocess.attach_args().parse_args(
-        ['--wikipedia', os.path.join(d, 'wiki'), '--sentence-splitter', 'rules', '--sink', os.path.join(d, 'out'),
-         '--target-seq-length', '128', '--block-size', '1M', '--chunk-mb', str(chunk_mb), '--seed', '7',
-         '--split-workers', str(host_cpus()['share'])])
+    argv = ['--wikipedia', os.path.join(d, 'wiki'), '--sentence-splitter', 'rules', '--sink', os.path.join(d, 'out'),
+            '--target-seq-length', str(seq), '--block-size', '1M', '--chunk-mb', str(chunk_mb), '--seed', '7',
+            '--split-workers', str(host_cpus()['share'])]
+    if bin_size:
+      argv += ['--bin-size', str(bin_size)]
+    a = preprocess.attach_args().parse_args(argv)
     t0 = time.perf_counter()
     files, t = preprocess.main(a)
     el = time.perf_counter() - t0
     t.pop('partitions', None)
-    out = {'what': 'preprocess CLI end to end, BERT seq 128 unbinned (BASELINE configs[0])', 'raw_mb': raw / 1e6,
+    out = {'what': 'preprocess CLI end to end, BERT seq %d %s (BASELINE configs[%d])' % (
+               seq, 'bin %d' % bin_size if bin_size else 'unbinned', 1 if bin_size else 0),
+           'raw_mb': raw / 1e6, 'documents': i, 'unique_mb': min(mb, unique_mb),
            'files': len(files), 'seconds': el, 'raw_mb_per_s': raw / 1e6 / el, 'gen_s': gen_s}
     out.update({k: v for k, v in t.items() if isinstance(v, (int, float, str))})
     return out
@@ -508,6 +527,72 @@ def launch_check(args, rank, world):
     dist.destroy_process_group()
 
 
+LEGS = {
+    'mask512': dict(corpus='wiki', masking=True, target_seq_length=512, bin_size=64, duplicate_factor=5),
+    'mask128': dict(corpus='wiki', masking=True, target_seq_length=128, bin_size=64, duplicate_factor=5),
+    'code': dict(corpus='code', masking=False, target_seq_length=512, bin_size=64, duplicate_factor=1),
+    'wikibooks': dict(corpus='wikibooks', masking=False, target_seq_length=512, bin_size=64, duplicate_factor=5),
+}
+
+
+def run_leg(args, name, local, device, shards=None):
+  """One BASELINE workload after the headline (never inside its timed
+  region): warmup + --leg-steps timed steps of tokenize + pack (+ masking)
+  + bin + row spans at full size, per-kernel tokenizer times of the last
+  step, and the oracle check of one full-size partition.  shards: the
+  headline's (same corpus) to reuse, else built here."""
+  import argparse
+  from lddl_amd.pipeline import Packer, VOCAB_BERT, VOCAB_CODEBERT
+  a = argparse.Namespace(**vars(args))
+  for k, v in LEGS[name].items():
+    setattr(a, k, v)
+  a.unique_mb = 16 if a.corpus == 'code' else 256
+  a.rows = 'spans'
+  t0 = time.perf_counter()
+  if shards is None:
+    sh, base, pdo, reps, _ = build_shards(a, 0, device)
+  else:
+    sh, base, pdo, reps = shards
+  code = a.corpus == 'code'
+  pk = Packer(VOCAB_CODEBERT if code else VOCAB_BERT, device=local, masking=a.masking)
+  pk.tok.set_timing(True)
+  kw = dict(target_seq_length=a.target_seq_length, short_seq_prob=0.1, duplicate_factor=a.duplicate_factor,
+       seed=a.seed, bin_size=a.bin_size, masking=a.masking, codebert=code, spans=True)
+  ev = []
+  for i in range(1 + a.leg_steps):
+    if i == 1:
+      torch.cuda.synchronize()
+      t = time.perf_counter()
+    s = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    ids, ntok, toff = pk.tokenize(sh)
+    e1.record(s)
+    res = pk.pack(sh, ids, ntok, toff, **kw)
+    if i:
+      ev.append((e0, e1))
+  torch.cuda.synchronize()
+  el = (time.perf_counter() - t) / a.leg_steps
+  n_tok = int(ntok[:sh.n_sent].sum().item())
+  ks = pk.tok.stats()
+  out = {'workload': '%s_seq%d_bin%d_%dGB_per_gpu%s' % ({'code': 'codebert', 'wiki': 'bert',
+                             'wikibooks': 'bert_wikibooks'}[a.corpus],
+                             a.target_seq_length, a.bin_size,
+                             round(sh.nbytes / (1 << 30)),
+                             '_masking' if a.masking else ''),
+     'baseline_config': {'mask512': 3, 'mask128': 3, 'code': 2, 'wikibooks': 4}[name],
+     'steps': a.leg_steps, 'warmup': 1, 'ms_per_step': el * 1e3, 'value': n_tok / el, 'unit': 'tokens/s',
+     'duplicate_factor': a.duplicate_factor, 'corpus_bytes': sh.nbytes, 'wordpiece_tokens': n_tok,
+     'pairs': res.n_pairs, 'packed_tokens': res.n_tokens, 'masked_positions': res.n_masked,
+     'tokenize_ms': float(np.mean([x.elapsed_time(y) for x, y in ev])),
+     'tokenize_kernels_ms': {'scan': ks['scan_ms'], 'wordpiece': ks['wordpiece_ms'], 'expand': ks['expand_ms']}}
+  if not args.no_sample_check:
+    out['sample_check'] = sample_partition_check(a, pk, res, base, pdo, reps, kw['seed'])
+  out['leg_seconds'] = time.perf_counter() - t0
+  del res, ids, ntok, toff, pk
+  return out
+
+
 def main():
   args = parse()
   if 'WORLD_SIZE' not in os.environ and (args.gpus or 1) > 1:
@@ -522,6 +607,8 @@ def main():
   if args.launch_check:
     return launch_check(args, rank, world)
   fe = frontend_leg(args.frontend_mb) if world == 1 and args.frontend_mb > 0 else None
+  fe2 = (frontend_leg(args.frontend_c2_mb, seq=512, bin_size=64)
+         if world == 1 and args.frontend_c2_mb > 0 else None)
   torch.cuda.set_device(local)
   device = torch.device('cuda', local)
   dist = None
@@ -664,10 +751,32 @@ def main():
     line['parquet_writer'] = parquet_sample(args, pk, res, sh)
   if fe is not None:
     line['frontend'] = fe
+  if fe2 is not None:
+    line['frontend_c2'] = fe2
   if not args.no_cpu_baseline and world == 1:  # the host leg (the oracle): rank 0 at N=1 only
     line['cpu_baseline'] = cpu_baseline(args, base, pdo, args.cpu_seconds)
     if not args.no_sample_check:  # the oracle as the checker of one full-size partition of the timed run
       line['cpu_baseline']['sample_check'] = sample_partition_check(args, pk, res, base, pdo, reps, kw['seed'])
+  if world == 1 and args.legs:
+    # the other BASELINE workloads, after everything above read the headline's
+    # results: its packer scratch goes first (a second context beside it would
+    # double the tokenizer / packer scratch), its shards stay for the legs on
+    # the same corpus
+    del res, pk, ntok
+    torch.cuda.empty_cache()
+    heads = (sh, base, pdo, reps) if args.corpus == 'wiki' else None
+    legs = {}
+    for name in [x for x in args.legs.split(',') if x]:
+      if LEGS[name]['corpus'] != 'wiki' and heads is not None:
+        heads = None
+        del sh
+        torch.cuda.empty_cache()
+      try:
+        legs[name] = run_leg(args, name, local, device, heads if LEGS[name]['corpus'] == 'wiki' else None)
+      except Exception as e:  # (recorded: the headline line still prints)
+        legs[name] = {'error': '%s: %s' % (type(e).__name__, e)}
+      torch.cuda.empty_cache()
+    line['legs'] = legs
   print(json.dumps(line), flush=True)
   if dist is not None:
     dist.destroy_process_group()

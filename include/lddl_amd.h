@@ -18,7 +18,12 @@
  *       create_pairs_from_document :241-365 and, with --masking,
  *       create_masked_lm_predictions :182-238; pretrain_codebert.py:460-477
  *       with :343-442) and the binned writer's grouping
- *       (binning.py:63-93 _to_dataframe_binned).
+ *       (binning.py:63-93 _to_dataframe_binned).  A pack call writes its
+ *       result into a caller-owned lddl_pack (lddl_pack_new; NULL = the
+ *       ctx's own) that the post-pack calls then name explicitly.
+ *   lddl_bin
+ *       replaces _to_dataframe_binned's grouping (binning.py:63-93) on its
+ *       own, for any column of row lengths.
  *
  * Conventions: every pointer named d_* is a DEVICE pointer on the ctx's
  * device; work is enqueued on `stream` (a hipStream_t, NULL = default) and is
@@ -47,6 +52,15 @@ extern "C" {
 #define LDDL_EASSERT -8
 
 typedef struct lddl_ctx lddl_ctx;
+/* The result of one lddl_pack_bert / lddl_pack_codebert call: pair records,
+ * their shuffled and binned order, per-partition counts, the masking draws.
+ * lddl_materialize / lddl_row_spans / lddl_masked_lm[_spans] / lddl_row_docs
+ * read the result they are given, so several results can be live at once
+ * (e.g. one shard set packed while the previous one is written).  Every call
+ * taking a `pack` accepts NULL = the ctx's own result.  A pack result's
+ * device buffers grow on demand and are reused by the next pack into it;
+ * a failed pack leaves it empty (post-pack calls return LDDL_EINVAL). */
+typedef struct lddl_pack lddl_pack;
 
 const char *lddl_last_error(void);
 
@@ -92,7 +106,14 @@ int lddl_tokenize_stats(lddl_ctx *ctx, double *out, int n);
  * over the ids.  Off by default (the unmasked path does not need them). */
 int lddl_set_special_flags(lddl_ctx *ctx, int on);
 
-/* Pack every partition of a tokenised shard set.
+/* A new, empty pack result on ctx's device (free with lddl_pack_free, before
+ * or after the ctx).  lddl_pack_rows: #rows of its last successful pack, -1
+ * when none. */
+int lddl_pack_new(lddl_ctx *ctx, lddl_pack **out);
+void lddl_pack_free(lddl_pack *pack);
+int lddl_pack_rows(const lddl_pack *pack, int64_t *out_npairs);
+
+/* Pack every partition of a tokenised shard set into `pack`.
  * Partition p = docs [d_part_doc_off[p], d_part_doc_off[p+1]); doc d =
  * sentences [d_doc_sent_off[d], d_doc_sent_off[d+1]); d_ids / d_ntok /
  * d_tok_off / d_sent_off are lddl_tokenize's output / input (d_ids may be
@@ -106,7 +127,7 @@ int lddl_set_special_flags(lddl_ctx *ctx, int on);
  * (:182-238) with vocab_words = the vocab file's tokens in file order
  * (target_seq_length <= 1024); the rows are then written by
  * lddl_materialize and masked by lddl_masked_lm. */
-int lddl_pack_bert(lddl_ctx *ctx, const uint16_t *d_ids, const int32_t *d_ntok, const int64_t *d_tok_off,
+int lddl_pack_bert(lddl_ctx *ctx, lddl_pack *pack, const uint16_t *d_ids, const int32_t *d_ntok, const int64_t *d_tok_off,
                    const int64_t *d_sent_off, int64_t n_sent, const int64_t *d_doc_sent_off, int64_t n_doc,
                    const int64_t *d_part_doc_off, int64_t n_part, int32_t target_seq_length, double short_seq_prob,
                    int32_t duplicate_factor, int32_t masking, double masked_lm_ratio, uint64_t seed, int32_t bin_size,
@@ -116,14 +137,14 @@ int lddl_pack_bert(lddl_ctx *ctx, const uint16_t *d_ids, const int32_t *d_ntok, 
 /* CodeBERT docstring/code packing (pretrain_codebert.py:343-442, :460-477).
  * Doc d's first d_doc_nseg_doc[d] sentences are its docstring segments, the
  * rest its code segments (one per source line, pretrain_codebert.py:126-159). */
-int lddl_pack_codebert(lddl_ctx *ctx, const int32_t *d_ntok, const int64_t *d_tok_off, const int64_t *d_sent_off,
+int lddl_pack_codebert(lddl_ctx *ctx, lddl_pack *pack, const int32_t *d_ntok, const int64_t *d_tok_off, const int64_t *d_sent_off,
                        int64_t n_sent, const int64_t *d_doc_sent_off, const int32_t *d_doc_nseg_doc, int64_t n_doc,
                        const int64_t *d_part_doc_off, int64_t n_part, int32_t target_seq_length,
                        double short_seq_prob, int32_t duplicate_factor, uint64_t seed, int32_t bin_size,
                        int64_t *out_totals, void *stream);
 
 /* d_ids: the dense ids lddl_tokenize wrote (and the pack call read).
- * Write the rows of the last pack call in output order (partition-major,
+ * Write the rows of `pack` in output order (partition-major,
  * bin-major, shuffled order within a bin = the reference's part.{p}.parquet_{b}
  * row order).  Row g: d_out_tokens[d_out_tok_off[g] .. d_out_tok_off[g+1]) =
  * [CLS] A [SEP] B [SEP] (CodeBERT: [CLS] doc [SEP] code [SEP], or
@@ -131,11 +152,11 @@ int lddl_pack_codebert(lddl_ctx *ctx, const int32_t *d_ntok, const int64_t *d_to
  * len(B); flags bit0 = is_random_next, bit1 = segment 0 is followed by [SEP];
  * bin = bin id; part = partition.  d_bin_count (optional) receives
  * int64[n_part][nbins] row counts. */
-int lddl_materialize(lddl_ctx *ctx, const uint16_t *d_ids, uint16_t *d_out_tokens, int64_t *d_out_tok_off,
+int lddl_materialize(lddl_ctx *ctx, lddl_pack *pack, const uint16_t *d_ids, uint16_t *d_out_tokens, int64_t *d_out_tok_off,
                      uint16_t *d_out_len0, uint16_t *d_out_len1, uint8_t *d_out_flags, uint8_t *d_out_bin,
                      int64_t *d_out_part, int64_t *d_bin_count, void *stream);
 
-/* The rows of the last pack call as SPANS of the dense ids, in
+/* The rows of `pack` as SPANS of the dense ids, in
  * lddl_materialize's row order, without copying a token: each segment of a
  * row is one contiguous run of lddl_tokenize's d_out_ids (a document's
  * sentences are contiguous there and a segment is a window of consecutive
@@ -147,7 +168,7 @@ int lddl_materialize(lddl_ctx *ctx, const uint16_t *d_ids, uint16_t *d_out_token
  * len0/len1/flags/bin/part/bin_count as lddl_materialize; d_out_tok_off
  * (optional, NULL = not written) = the materialised layout's row offsets.
  * The dense ids must stay live while the spans are read. */
-int lddl_row_spans(lddl_ctx *ctx, int64_t *d_out_src0, int64_t *d_out_src1, int64_t *d_out_tok_off,
+int lddl_row_spans(lddl_ctx *ctx, lddl_pack *pack, int64_t *d_out_src0, int64_t *d_out_src1, int64_t *d_out_tok_off,
                    uint16_t *d_out_len0, uint16_t *d_out_len1, uint8_t *d_out_flags, uint8_t *d_out_bin,
                    int64_t *d_out_part, int64_t *d_bin_count, void *stream);
 
@@ -159,7 +180,7 @@ int lddl_row_spans(lddl_ctx *ctx, int64_t *d_out_src0, int64_t *d_out_src1, int6
  * masked_lm_labels as token ids (pretrain.py:225-238, :340-361).  Reads
  * the rows and their partitions (d_out_tokens, d_out_tok_off, d_out_part)
  * of that lddl_materialize call, which must still be live. */
-int lddl_masked_lm(lddl_ctx *ctx, int64_t *d_out_mlm_off, uint16_t *d_out_mlm_pos, uint16_t *d_out_mlm_label,
+int lddl_masked_lm(lddl_ctx *ctx, lddl_pack *pack, int64_t *d_out_mlm_off, uint16_t *d_out_mlm_pos, uint16_t *d_out_mlm_label,
                    void *stream);
 
 /* After lddl_pack_bert(masking=1) + lddl_row_spans (no rows materialised):
@@ -170,7 +191,7 @@ int lddl_masked_lm(lddl_ctx *ctx, int64_t *d_out_mlm_off, uint16_t *d_out_mlm_po
  * branch left it, pretrain.py:212-225) -- what lddl_render_masked puts into
  * the A / B strings.  d_ids = the dense ids; d_src0 / d_src1 / d_len0 /
  * d_part = that lddl_row_spans call's outputs. */
-int lddl_masked_lm_spans(lddl_ctx *ctx, const uint16_t *d_ids, const int64_t *d_src0, const int64_t *d_src1,
+int lddl_masked_lm_spans(lddl_ctx *ctx, lddl_pack *pack, const uint16_t *d_ids, const int64_t *d_src0, const int64_t *d_src1,
                          const uint16_t *d_len0, const int64_t *d_part, int64_t *d_out_mlm_off,
                          uint16_t *d_out_mlm_pos, uint16_t *d_out_mlm_label, uint16_t *d_out_mlm_token,
                          void *stream);
@@ -207,11 +228,22 @@ int lddl_render_masked(lddl_ctx *ctx, const uint16_t *d_ids, const int64_t *d_sr
                        const uint16_t *d_mlm_token, int64_t row0, int64_t n_rows, int64_t *d_out_off,
                        uint8_t *d_out_bytes, int64_t out_cap, int64_t *out_nbytes, void *stream);
 
-/* Document index (into the corpus' documents) of every row of the last pack
- * call, in lddl_materialize's row order: the row's own document (seg0's; a
+/* Document index (into the corpus' documents) of every row of `pack`, in lddl_materialize's row order: the row's own document (seg0's; a
  * CodeBERT row without docstring: its code's) -- feeds CodeBERT's 'id'
  * column = document._id (pretrain_codebert.py:425-426). */
-int lddl_row_docs(lddl_ctx *ctx, int64_t *d_out_doc, void *stream);
+int lddl_row_docs(lddl_ctx *ctx, lddl_pack *pack, int64_t *d_out_doc, void *stream);
+
+/* Group n rows by length bin exactly as binning.py:63-93
+ * _to_dataframe_binned: row i goes to bin (num_tokens[i] - 1) // bin_size
+ * (Python floor division), capped at nbins - 1; a negative bin indexes the
+ * bins from the end as the reference's seqs[bin_id] does (length 0 -> the
+ * last bin), below -nbins is the reference's IndexError (LDDL_EINDEX).
+ * d_out_perm[0..n) = the row indices bin-major, ascending within a bin (the
+ * row order of the concatenated per-bin frames); d_out_bin_counts[0..nbins)
+ * = rows per bin.  1 <= nbins <= 1024, bin_size >= 1.  Synchronises the
+ * stream once (the IndexError check). */
+int lddl_bin(lddl_ctx *ctx, const int64_t *d_num_tokens, int64_t n, int32_t bin_size, int32_t nbins,
+             int64_t *d_out_perm, int64_t *d_out_bin_counts, void *stream);
 
 /* ---- training-time collate -------------------------
  * Replaces lddl/torch/bert.py:69-153 `_to_encoded_inputs` (+ :156-196

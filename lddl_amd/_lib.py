@@ -29,26 +29,30 @@ SIGNATURES = {
     'lddl_set_timing': (c_int, [c_void_p, c_int]),
     'lddl_set_special_flags': (c_int, [c_void_p, c_int]),
     'lddl_tokenize_stats': (c_int, [c_void_p, ctypes.POINTER(c_double), c_int]),
-    'lddl_pack_bert': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_int64,
+    'lddl_pack_new': (c_int, [c_void_p, ctypes.POINTER(c_void_p)]),
+    'lddl_pack_free': (None, [c_void_p]),
+    'lddl_pack_rows': (c_int, [c_void_p, ctypes.POINTER(c_int64)]),
+    'lddl_bin': (c_int, [c_void_p, c_void_p, c_int64, c_int32, c_int32, c_void_p, c_void_p, c_void_p]),
+    'lddl_pack_bert': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_int64,
                                c_void_p, c_int64, c_int32, c_double, c_int32, c_int32, c_double, c_uint64, c_int32,
                                ctypes.POINTER(c_int64), c_void_p]),
-    'lddl_pack_codebert': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int64,
+    'lddl_pack_codebert': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int64,
                                    c_void_p,
                                    c_int64, c_int32, c_double, c_int32, c_uint64, c_int32,
                                    ctypes.POINTER(c_int64), c_void_p]),
-    'lddl_materialize': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+    'lddl_materialize': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                  c_void_p, c_void_p, c_void_p, c_void_p]),
-    'lddl_row_spans': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+    'lddl_row_spans': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                c_void_p, c_void_p, c_void_p]),
-    'lddl_masked_lm': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
-    'lddl_masked_lm_spans': (c_int, [c_void_p] * 11),
+    'lddl_masked_lm': (c_int, [c_void_p] * 6),
+    'lddl_masked_lm_spans': (c_int, [c_void_p] * 12),
     'lddl_render_masked': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_void_p,
                                    c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_int64, ctypes.POINTER(c_int64),
                                    c_void_p]),
     'lddl_render_strings': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64,
                                     c_int32, c_int32, c_void_p, c_void_p, c_int64, ctypes.POINTER(c_int64),
                                     c_void_p]),
-    'lddl_row_docs': (c_int, [c_void_p, c_void_p, c_void_p]),
+    'lddl_row_docs': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
     'lddl_collate_seq_len': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int32,
                                      ctypes.POINTER(c_int64), c_void_p]),
     'lddl_collate_bert': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

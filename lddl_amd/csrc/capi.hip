@@ -12,6 +12,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <new>
 #include <string>
 #include <vector>
 
@@ -40,6 +41,30 @@ static int set_err(int code, const char* fmt, ...) {
     hipError_t _e = (expr);                                                            \
     if (_e != hipSuccess) return set_err(LDDL_EHIP, "%s: %s", #expr, hipGetErrorString(_e)); \
   } while (0)
+
+// a device buffer grown on demand
+struct WsBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+};
+
+// The result of one lddl_pack_* call, owned by the caller (lddl_pack_new):
+// the pair records, their shuffled / binned order, the per-partition counts
+// and offsets and (masking) the masked positions -- everything the post-pack
+// calls (lddl_materialize, lddl_row_spans, lddl_masked_lm[_spans],
+// lddl_row_docs) read.  A ctx holds one of its own for callers that pass
+// NULL.  Buffers grow on demand and are reused by later packs into it.
+struct lddl_pack {
+  int device = 0;
+  WsBuf ws[34];
+  PackParams pp{};
+  int64_t last_npairs = -1, last_ntok = -1, last_nmask = -1, last_nsent = 0, last_ndense = 0;
+  int pack_codebert = 0;
+  uint64_t mlm_cap = 0;  // masking arena capacity that last sufficed
+  uint16_t* last_tokens = nullptr;  // rows of the last lddl_materialize of this result
+  const int64_t* last_tok_off = nullptr;
+  const int64_t* last_part = nullptr;
+};
 
 struct lddl_ctx {
   int device = 0;
@@ -83,22 +108,11 @@ struct lddl_ctx {
   const void* spec_soff = nullptr;
   int64_t spec_nsent = -1;
   bool spec_flags = false;  // lddl_set_special_flags
-  // pack workspace (grown on demand)
-  struct Buf {
-    void* p = nullptr;
-    size_t cap = 0;
-  };
-  Buf ws[50];
-  PackParams pp{};
-  int64_t last_npairs = -1, last_ntok = -1;
+  // tokenizer / render / collate workspace (grown on demand)
+  WsBuf ws[50];
   int64_t* h_tot = nullptr;  // pinned [8]
-  int64_t last_nmask = -1;
-  int64_t last_nsent = 0, last_ndense = 0;  // sentences / tokens of the last pack (dense id array)
-  uint16_t* last_tokens = nullptr;  // rows of the last lddl_materialize
-  const int64_t* last_tok_off = nullptr;
-  const int64_t* last_part = nullptr;     // partition of every materialised row (lddl_materialize's out_part)   // masked entries of the last pack (-1: no masking)
-  uint64_t mlm_cap = 0;      // masking arena capacity that last sufficed
-  int pack_codebert = 0;
+  lddl_pack own;             // the pack result of calls that pass no lddl_pack
+  uint64_t mlm_cap0 = 0;     // initial masking arena (LDDL_MLM_CAP, tests)
   // scratch
   int tok_grid = 0;
   int tok_algo = 5;  // 5 = split tokenizer, 6 = lane tokenizer, 0 = every tile through the exact serial path
@@ -111,8 +125,8 @@ struct lddl_ctx {
 
 // ------------------------------------------------------------------ pack --
 template <class T>
-static int ws_get(lddl_ctx* c, int slot, size_t n, T** out) {
-  auto& b = c->ws[slot];
+static int ws_get(WsBuf* ws, int slot, size_t n, T** out) {
+  auto& b = ws[slot];
   const size_t bytes = (n ? n : 1) * sizeof(T);
   if (b.cap < bytes) {
     (void)hipFree(b.p);
@@ -123,6 +137,16 @@ static int ws_get(lddl_ctx* c, int slot, size_t n, T** out) {
   }
   *out = (T*)b.p;
   return 0;
+}
+template <class T>
+static int ws_get(lddl_ctx* c, int slot, size_t n, T** out) {
+  return ws_get(c->ws, slot, n, out);
+}
+static void free_pack(lddl_pack* k) {
+  for (auto& b : k->ws) {
+    (void)hipFree(b.p);
+    b = WsBuf{};
+  }
 }
 
 
@@ -157,6 +181,7 @@ static void free_ctx(lddl_ctx* c) {
     delete c->tm;
   }
   for (auto& b : c->ws) (void)hipFree(b.p);
+  free_pack(&c->own);
   if (c->h_tot) (void)hipHostFree(c->h_tot);
   delete c;
 }
@@ -245,7 +270,9 @@ extern "C" int lddl_create(const char* vocab_path, const char* table_path, int d
   if (c->tok_algo == 6 && !c->lane_ok) c->tok_algo = 0;
   if (c->tok_algo == 5 && (!c->scan_ok || c->vocab_size > (int)SPLIT_EDEF)) c->tok_algo = 0;
   const char* mcap = getenv("LDDL_MLM_CAP");  // initial masking arena (tests force the regrow path)
-  c->mlm_cap = mcap ? (uint64_t)atoll(mcap) : 0;
+  c->mlm_cap0 = mcap ? (uint64_t)atoll(mcap) : 0;
+  c->own.device = device;
+  c->own.mlm_cap = c->mlm_cap0;
   int per_cu = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, tokenize_fallback_kernel_ptr(), 256, 0) != hipSuccess ||
       per_cu < 1)
@@ -475,7 +502,7 @@ extern "C" int lddl_tokenize_stats(lddl_ctx* c, double* out, int n) {
   return 0;
 }
 
-static int pack_common(lddl_ctx* c, int codebert, const int32_t* d_ntok, const int64_t* d_tok_off,
+static int pack_common(lddl_ctx* c, lddl_pack* pk, int codebert, const int32_t* d_ntok, const int64_t* d_tok_off,
                        const int64_t* d_sent_off, int64_t n_sent,
                        const int64_t* d_doc_sent_off, const int32_t* d_doc_nseg_doc, int64_t n_doc,
                        const int64_t* d_part_doc_off, int64_t n_part, int32_t target_seq_length,
@@ -483,6 +510,8 @@ static int pack_common(lddl_ctx* c, int codebert, const int32_t* d_ntok, const i
                        int64_t* out_totals, void* stream, const uint16_t* d_ids = nullptr, int32_t masking = 0,
                        double masked_lm_ratio = 0.15) {
   if (!c) return set_err(LDDL_EINVAL, "null ctx");
+  lddl_pack* k = pk ? pk : &c->own;
+  if (k->device != c->device) return set_err(LDDL_EINVAL, "pack result of another device");
   if (masking) {
     if (!d_ids) return set_err(LDDL_EINVAL, "masking needs the tokenizer ids");
     if (target_seq_length > MLM_MAX_SEQ)
@@ -510,7 +539,10 @@ static int pack_common(lddl_ctx* c, int codebert, const int32_t* d_ntok, const i
   if (nbins > 255) return set_err(LDDL_EINVAL, "more than 255 bins");
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t st = (hipStream_t)stream;
-  PackParams& P = c->pp;
+  k->last_npairs = -1;  // until this pack succeeds, nothing to materialise
+  k->last_nmask = -1;
+  k->last_tokens = nullptr;
+  PackParams& P = k->pp;
   P = PackParams{};
   P.ntok = d_ntok;
   P.sent_off = d_sent_off;
@@ -526,22 +558,22 @@ static int pack_common(lddl_ctx* c, int codebert, const int32_t* d_ntok, const i
   P.nbins = nbins;
   const size_t npair_cap = (size_t)duplicate_factor * (size_t)(n_sent ? n_sent : 1);
   int rc;
-  if ((rc = ws_get(c, 0, n_sent, &P.fs_ntok)) || (rc = ws_get(c, 1, n_sent, &P.fs_base)) ||
-      (rc = ws_get(c, 2, n_doc, &P.fd_first)) || (rc = ws_get(c, 3, n_doc, &P.fd_n)) ||
-      (rc = ws_get(c, 4, n_doc, &P.fd_nd)) ||
-      (rc = ws_get(c, 6, npair_cap, &P.pairs)) || (rc = ws_get(c, 7, npair_cap, &P.order)) ||
-      (rc = ws_get(c, 8, npair_cap, &P.binned)) || (rc = ws_get(c, 9, npair_cap, &P.tok_local)) ||
-      (rc = ws_get(c, 10, n_part, &P.part_npairs)) || (rc = ws_get(c, 11, n_part, &P.part_ntok)) ||
-      (rc = ws_get(c, 12, (size_t)n_part * nbins, &P.bin_count)) ||
-      (rc = ws_get(c, 13, (size_t)n_part * nbins, &P.bin_cursor)) ||
-      (rc = ws_get(c, 14, n_part, &P.part_err)) || (rc = ws_get(c, 18, n_sent + n_part + 1, &P.kept)) ||
-      (rc = ws_get(c, 33, n_sent, &P.fs_dense)))
+  if ((rc = ws_get(k->ws, 0, n_sent, &P.fs_ntok)) || (rc = ws_get(k->ws, 1, n_sent, &P.fs_base)) ||
+      (rc = ws_get(k->ws, 2, n_doc, &P.fd_first)) || (rc = ws_get(k->ws, 3, n_doc, &P.fd_n)) ||
+      (rc = ws_get(k->ws, 4, n_doc, &P.fd_nd)) ||
+      (rc = ws_get(k->ws, 6, npair_cap, &P.pairs)) || (rc = ws_get(k->ws, 7, npair_cap, &P.order)) ||
+      (rc = ws_get(k->ws, 8, npair_cap, &P.binned)) || (rc = ws_get(k->ws, 9, npair_cap, &P.tok_local)) ||
+      (rc = ws_get(k->ws, 10, n_part, &P.part_npairs)) || (rc = ws_get(k->ws, 11, n_part, &P.part_ntok)) ||
+      (rc = ws_get(k->ws, 12, (size_t)n_part * nbins, &P.bin_count)) ||
+      (rc = ws_get(k->ws, 13, (size_t)n_part * nbins, &P.bin_cursor)) ||
+      (rc = ws_get(k->ws, 14, n_part, &P.part_err)) || (rc = ws_get(k->ws, 18, n_sent + n_part + 1, &P.kept)) ||
+      (rc = ws_get(k->ws, 33, n_sent, &P.fs_dense)))
     return rc;
   P.tokoff = d_tok_off;  // the tokenizer's dense offsets (lddl_tokenize d_out_tok_off)
   int64_t *pair_base, *tok_base;
   int32_t* err_any;
-  if ((rc = ws_get(c, 15, n_part + 1, &pair_base)) || (rc = ws_get(c, 16, n_part + 1, &tok_base)) ||
-      (rc = ws_get(c, 17, 4, &err_any)))
+  if ((rc = ws_get(k->ws, 15, n_part + 1, &pair_base)) || (rc = ws_get(k->ws, 16, n_part + 1, &tok_base)) ||
+      (rc = ws_get(k->ws, 17, 4, &err_any)))
     return rc;
   if (!c->h_tot) HIP_TRY(hipHostMalloc((void**)&c->h_tot, 8 * sizeof(int64_t)));
   int64_t *mask_base = nullptr, *mask_base2 = nullptr;
@@ -560,16 +592,17 @@ static int pack_common(lddl_ctx* c, int codebert, const int32_t* d_ntok, const i
     const bool spec_ok = c->spec_ids == d_ids && c->spec_ntok == d_ntok && c->spec_soff == d_sent_off &&
                          c->spec_nsent == n_sent;
     c->spec_ids = nullptr;
-    if ((rc = ws_get(c, spec_ok ? 41 : 22, n_sent, &sent_spec)) || (rc = ws_get(c, 23, n_sent, &fs_spec)) ||
-        (rc = ws_get(c, 24, npair_cap, &P.mref)) || (rc = ws_get(c, 25, npair_cap, &P.mloc)) ||
-        (rc = ws_get(c, 26, n_part, &P.part_nmask)) || (rc = ws_get(c, 27, n_part + 1, &mask_base)) ||
-        (rc = ws_get(c, 28, n_part + 1, &mask_base2)) || (rc = ws_get(c, 29, 1, &P.mcounter)) ||
-        (rc = ws_get(c, 31, (size_t)n_part * MLM_MAX_SEQ, &P.mcand)))
+    if ((rc = spec_ok ? ws_get(c->ws, 41, n_sent, &sent_spec) : ws_get(k->ws, 22, n_sent, &sent_spec)) ||
+        (rc = ws_get(k->ws, 23, n_sent, &fs_spec)) ||
+        (rc = ws_get(k->ws, 24, npair_cap, &P.mref)) || (rc = ws_get(k->ws, 25, npair_cap, &P.mloc)) ||
+        (rc = ws_get(k->ws, 26, n_part, &P.part_nmask)) || (rc = ws_get(k->ws, 27, n_part + 1, &mask_base)) ||
+        (rc = ws_get(k->ws, 28, n_part + 1, &mask_base2)) || (rc = ws_get(k->ws, 29, 1, &P.mcounter)) ||
+        (rc = ws_get(k->ws, 31, (size_t)n_part * MLM_MAX_SEQ, &P.mcand)))
       return rc;
     P.sent_spec = sent_spec;
     P.fs_spec = fs_spec;
     if (!spec_ok) HIP_TRY(launch_sent_special(d_ids, d_tok_off, d_ntok, n_sent, P.cls_id, P.sep_id, sent_spec, st));
-    if (!c->mlm_cap) c->mlm_cap = (uint64_t)n_part * 4 * MLM_CHUNK + (uint64_t)duplicate_factor * n_sent * 4;
+    if (!k->mlm_cap) k->mlm_cap = (uint64_t)n_part * 4 * MLM_CHUNK + (uint64_t)duplicate_factor * n_sent * 4;
   }
   if (!codebert) {
     // Wave packer: one 64-lane workgroup per partition runs a serial chain, so
@@ -592,8 +625,8 @@ static int pack_common(lddl_ctx* c, int codebert, const int32_t* d_ntok, const i
   }
   for (int attempt = 0;; ++attempt) {
     if (masking) {
-      if ((rc = ws_get(c, 30, c->mlm_cap, &P.marena))) return rc;
-      P.mcap = c->mlm_cap;
+      if ((rc = ws_get(k->ws, 30, k->mlm_cap, &P.marena))) return rc;
+      P.mcap = k->mlm_cap;
       HIP_TRY(hipMemsetAsync(P.mcounter, 0, 8, st));
     }
     static uint64_t* d_pdbg = nullptr;
@@ -630,53 +663,53 @@ static int pack_common(lddl_ctx* c, int codebert, const int32_t* d_ntok, const i
     HIP_TRY(hipStreamSynchronize(st));
     // the bump allocator overshot the arena: grow it and pack again (the
     // pack is deterministic, so the rerun reproduces the same rows)
-    if (masking && (uint64_t)c->h_tot[4] > c->mlm_cap && attempt == 0) {
-      c->mlm_cap = (uint64_t)c->h_tot[4] + (uint64_t)n_part * MLM_CHUNK;
+    if (masking && (uint64_t)c->h_tot[4] > k->mlm_cap && attempt == 0) {
+      k->mlm_cap = (uint64_t)c->h_tot[4] + (uint64_t)n_part * MLM_CHUNK;
       continue;
     }
-    if (masking && (uint64_t)c->h_tot[4] > c->mlm_cap) return set_err(LDDL_ECAPACITY, "masking arena overflow");
+    if (masking && (uint64_t)c->h_tot[4] > k->mlm_cap) return set_err(LDDL_ECAPACITY, "masking arena overflow");
     break;
   }
   const int32_t e = (int32_t)(c->h_tot[2] & 0xFFFFFFFF);
-  c->pack_codebert = codebert;
-  c->last_nmask = masking ? c->h_tot[3] : -1;
-  if (e & PACK_EINDEX) { c->last_npairs = -1; return set_err(LDDL_EINDEX, "IndexError in _truncate_seq (reference quirk)"); }
-  if (e & PACK_EASSERT) { c->last_npairs = -1; return set_err(LDDL_EASSERT, "AssertionError: empty segment after truncation"); }
-  c->last_npairs = c->h_tot[0];
-  c->last_ntok = c->h_tot[1];
-  c->last_nsent = n_sent;
-  c->last_ndense = c->h_tot[5];
-  out_totals[0] = c->last_npairs;
-  out_totals[1] = c->last_ntok;
+  k->pack_codebert = codebert;
+  k->last_nmask = masking ? c->h_tot[3] : -1;
+  if (e & PACK_EINDEX) { k->last_npairs = -1; return set_err(LDDL_EINDEX, "IndexError in _truncate_seq (reference quirk)"); }
+  if (e & PACK_EASSERT) { k->last_npairs = -1; return set_err(LDDL_EASSERT, "AssertionError: empty segment after truncation"); }
+  k->last_npairs = c->h_tot[0];
+  k->last_ntok = c->h_tot[1];
+  k->last_nsent = n_sent;
+  k->last_ndense = c->h_tot[5];
+  out_totals[0] = k->last_npairs;
+  out_totals[1] = k->last_ntok;
   out_totals[2] = nbins;
-  out_totals[3] = masking ? c->last_nmask : 0;
+  out_totals[3] = masking ? k->last_nmask : 0;
   return 0;
 }
 
-extern "C" int lddl_pack_bert(lddl_ctx* c, const uint16_t* d_ids, const int32_t* d_ntok, const int64_t* d_tok_off,
+extern "C" int lddl_pack_bert(lddl_ctx* c, lddl_pack* pk, const uint16_t* d_ids, const int32_t* d_ntok, const int64_t* d_tok_off,
                               const int64_t* d_sent_off, int64_t n_sent, const int64_t* d_doc_sent_off, int64_t n_doc,
                               const int64_t* d_part_doc_off, int64_t n_part, int32_t target_seq_length,
                               double short_seq_prob, int32_t duplicate_factor, int32_t masking,
                               double masked_lm_ratio, uint64_t seed, int32_t bin_size, int64_t* out_totals,
                               void* stream) {
-  return pack_common(c, 0, d_ntok, d_tok_off, d_sent_off, n_sent, d_doc_sent_off, nullptr, n_doc, d_part_doc_off, n_part,
+  return pack_common(c, pk, 0, d_ntok, d_tok_off, d_sent_off, n_sent, d_doc_sent_off, nullptr, n_doc, d_part_doc_off, n_part,
                      target_seq_length, short_seq_prob, duplicate_factor, seed, bin_size, out_totals, stream, d_ids,
                      masking, masked_lm_ratio);
 }
 
-extern "C" int lddl_pack_codebert(lddl_ctx* c, const int32_t* d_ntok, const int64_t* d_tok_off,
+extern "C" int lddl_pack_codebert(lddl_ctx* c, lddl_pack* pk, const int32_t* d_ntok, const int64_t* d_tok_off,
                                   const int64_t* d_sent_off, int64_t n_sent,
                                   const int64_t* d_doc_sent_off, const int32_t* d_doc_nseg_doc, int64_t n_doc,
                                   const int64_t* d_part_doc_off, int64_t n_part, int32_t target_seq_length,
                                   double short_seq_prob, int32_t duplicate_factor, uint64_t seed, int32_t bin_size,
                                   int64_t* out_totals, void* stream) {
-  return pack_common(c, 1, d_ntok, d_tok_off, d_sent_off, n_sent, d_doc_sent_off, d_doc_nseg_doc, n_doc, d_part_doc_off,
+  return pack_common(c, pk, 1, d_ntok, d_tok_off, d_sent_off, n_sent, d_doc_sent_off, d_doc_nseg_doc, n_doc, d_part_doc_off,
                      n_part, target_seq_length, short_seq_prob, duplicate_factor, seed, bin_size, out_totals, stream);
 }
 
 // MatParams of the last pack call (lddl_materialize / lddl_row_spans)
-static MatParams mat_params(lddl_ctx* c) {
-  const PackParams& P = c->pp;
+static MatParams mat_params(const lddl_ctx* c, const lddl_pack* k) {
+  const PackParams& P = k->pp;
   MatParams M{};
   M.fs_dense = P.fs_dense;
   M.sent_off = P.sent_off;
@@ -688,33 +721,35 @@ static MatParams mat_params(lddl_ctx* c) {
   M.binned = P.binned;
   M.tok_local = P.tok_local;
   M.part_npairs = P.part_npairs;
-  M.pair_base = (const int64_t*)c->ws[15].p;
-  M.tok_base = (const int64_t*)c->ws[16].p;
+  M.pair_base = (const int64_t*)k->ws[15].p;
+  M.tok_base = (const int64_t*)k->ws[16].p;
   M.n_part = P.n_part;
   M.dup = P.dup;
   M.bin_size = P.bin_size;
   M.nbins = P.nbins;
   M.cls_id = c->special[2];
   M.sep_id = c->special[3];
-  M.codebert = c->pack_codebert;
+  M.codebert = k->pack_codebert;
   return M;
 }
 
-extern "C" int lddl_materialize(lddl_ctx* c, const uint16_t* d_ids, uint16_t* d_out_tokens, int64_t* d_out_tok_off,
+extern "C" int lddl_materialize(lddl_ctx* c, lddl_pack* pk, const uint16_t* d_ids, uint16_t* d_out_tokens, int64_t* d_out_tok_off,
                                 uint16_t* d_out_len0, uint16_t* d_out_len1, uint8_t* d_out_flags, uint8_t* d_out_bin,
                                 int64_t* d_out_part, int64_t* d_bin_count, void* stream) {
   if (!c) return set_err(LDDL_EINVAL, "null ctx");
-  if (c->last_npairs < 0) return set_err(LDDL_EINVAL, "no successful lddl_pack_* call to materialise");
+  lddl_pack* k = pk ? pk : &c->own;
+  if (k->device != c->device) return set_err(LDDL_EINVAL, "pack result of another device");
+  if (k->last_npairs < 0) return set_err(LDDL_EINVAL, "no successful lddl_pack_* call to materialise");
   if (!d_ids || !d_out_tokens || !d_out_tok_off || !d_out_len0 || !d_out_len1 || !d_out_flags || !d_out_bin ||
       !d_out_part)
     return set_err(LDDL_EINVAL, "null pointer");
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t st = (hipStream_t)stream;
-  const PackParams& P = c->pp;
+  const PackParams& P = k->pp;
   // LDDL_MAT_ALGO=1: the wave-per-partition materialize kernel (also taken
   // for unaligned buffers); otherwise the chunked v2 kernel
   const int mat_algo = getenv("LDDL_MAT_ALGO") ? atoi(getenv("LDDL_MAT_ALGO")) : 2;
-  MatParams M = mat_params(c);
+  MatParams M = mat_params(c, k);
   M.dense = d_ids;
   M.out_tokens = d_out_tokens;
   M.out_tok_off = d_out_tok_off;
@@ -723,30 +758,32 @@ extern "C" int lddl_materialize(lddl_ctx* c, const uint16_t* d_ids, uint16_t* d_
   M.out_flags = d_out_flags;
   M.out_bin = d_out_bin;
   M.out_part = d_out_part;
-  if (c->last_npairs == 0) {
+  if (k->last_npairs == 0) {
     HIP_TRY(hipMemsetAsync(d_out_tok_off, 0, 8, st));
   } else {
-    HIP_TRY(launch_materialize(M, c->last_npairs, c->last_ndense + 16, mat_algo, st));
+    HIP_TRY(launch_materialize(M, k->last_npairs, k->last_ndense + 16, mat_algo, st));
   }
   if (d_bin_count)
     HIP_TRY(hipMemcpyAsync(d_bin_count, P.bin_count, (size_t)P.n_part * P.nbins * 8, hipMemcpyDeviceToDevice, st));
-  c->last_tokens = d_out_tokens;
-  c->last_tok_off = d_out_tok_off;
-  c->last_part = d_out_part;
+  k->last_tokens = d_out_tokens;
+  k->last_tok_off = d_out_tok_off;
+  k->last_part = d_out_part;
   return 0;
 }
 
-extern "C" int lddl_row_spans(lddl_ctx* c, int64_t* d_out_src0, int64_t* d_out_src1, int64_t* d_out_tok_off,
+extern "C" int lddl_row_spans(lddl_ctx* c, lddl_pack* pk, int64_t* d_out_src0, int64_t* d_out_src1, int64_t* d_out_tok_off,
                               uint16_t* d_out_len0, uint16_t* d_out_len1, uint8_t* d_out_flags, uint8_t* d_out_bin,
                               int64_t* d_out_part, int64_t* d_bin_count, void* stream) {
   if (!c) return set_err(LDDL_EINVAL, "null ctx");
-  if (c->last_npairs < 0) return set_err(LDDL_EINVAL, "no successful lddl_pack_* call");
+  lddl_pack* k = pk ? pk : &c->own;
+  if (k->device != c->device) return set_err(LDDL_EINVAL, "pack result of another device");
+  if (k->last_npairs < 0) return set_err(LDDL_EINVAL, "no successful lddl_pack_* call");
   if (!d_out_src0 || !d_out_src1 || !d_out_len0 || !d_out_len1 || !d_out_flags || !d_out_bin || !d_out_part)
     return set_err(LDDL_EINVAL, "null pointer");
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t st = (hipStream_t)stream;
-  const PackParams& P = c->pp;
-  MatParams M = mat_params(c);
+  const PackParams& P = k->pp;
+  MatParams M = mat_params(c, k);
   M.out_src0 = d_out_src0;
   M.out_src1 = d_out_src1;
   M.out_tok_off = d_out_tok_off;
@@ -755,85 +792,89 @@ extern "C" int lddl_row_spans(lddl_ctx* c, int64_t* d_out_src0, int64_t* d_out_s
   M.out_flags = d_out_flags;
   M.out_bin = d_out_bin;
   M.out_part = d_out_part;
-  if (c->last_npairs == 0) {
+  if (k->last_npairs == 0) {
     if (d_out_tok_off) HIP_TRY(hipMemsetAsync(d_out_tok_off, 0, 8, st));
   } else {
     int32_t* chunk_part = nullptr;
     int64_t* part_pb = nullptr;
     int rc;
-    if ((rc = ws_get(c, 48, (size_t)((c->last_npairs + 63) >> 6), &chunk_part)) ||
+    if ((rc = ws_get(c, 48, (size_t)((k->last_npairs + 63) >> 6), &chunk_part)) ||
         (rc = ws_get(c, 49, (size_t)P.n_part, &part_pb)))
       return rc;
     HIP_TRY(launch_chunk_parts(M.pair_base, P.doc_sent_off, P.part_doc_off, P.dup, P.n_part, chunk_part, part_pb, st));
     M.chunk_part = chunk_part;
     M.part_pb = part_pb;
-    HIP_TRY(launch_row_spans(M, c->last_npairs, st));
+    HIP_TRY(launch_row_spans(M, k->last_npairs, st));
   }
   if (d_bin_count)
     HIP_TRY(hipMemcpyAsync(d_bin_count, P.bin_count, (size_t)P.n_part * P.nbins * 8, hipMemcpyDeviceToDevice, st));
   return 0;
 }
 
-extern "C" int lddl_masked_lm(lddl_ctx* c, int64_t* d_out_mlm_off, uint16_t* d_out_mlm_pos, uint16_t* d_out_mlm_label,
+extern "C" int lddl_masked_lm(lddl_ctx* c, lddl_pack* pk, int64_t* d_out_mlm_off, uint16_t* d_out_mlm_pos, uint16_t* d_out_mlm_label,
                               void* stream) {
   if (!c) return set_err(LDDL_EINVAL, "null ctx");
-  if (c->last_npairs < 0 || c->last_nmask < 0 || !c->last_tokens)
+  lddl_pack* k = pk ? pk : &c->own;
+  if (k->device != c->device) return set_err(LDDL_EINVAL, "pack result of another device");
+  if (k->last_npairs < 0 || k->last_nmask < 0 || !k->last_tokens)
     return set_err(LDDL_EINVAL, "lddl_masked_lm needs lddl_pack_bert(masking=1) then lddl_materialize");
-  if (!d_out_mlm_off || (c->last_nmask > 0 && (!d_out_mlm_pos || !d_out_mlm_label)))
+  if (!d_out_mlm_off || (k->last_nmask > 0 && (!d_out_mlm_pos || !d_out_mlm_label)))
     return set_err(LDDL_EINVAL, "null pointer");
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t st = (hipStream_t)stream;
-  const PackParams& P = c->pp;
-  if (c->last_npairs == 0) {
+  const PackParams& P = k->pp;
+  if (k->last_npairs == 0) {
     HIP_TRY(hipMemsetAsync(d_out_mlm_off, 0, 8, st));
   } else {
     MlmParams M{};
     M.doc_sent_off = P.doc_sent_off;
     M.part_doc_off = P.part_doc_off;
-    M.pair_base = (const int64_t*)c->ws[15].p;
+    M.pair_base = (const int64_t*)k->ws[15].p;
     M.binned = P.binned;
     M.mref = P.mref;
     M.mloc = P.mloc;
-    M.mask_base = (const int64_t*)c->ws[27].p;
+    M.mask_base = (const int64_t*)k->ws[27].p;
     M.marena = P.marena;
     M.n_part = P.n_part;
     M.dup = P.dup;
-    M.tokens = c->last_tokens;
-    M.tok_off = c->last_tok_off;
-    M.row_part = c->last_part;
+    M.tokens = k->last_tokens;
+    M.tok_off = k->last_tok_off;
+    M.row_part = k->last_part;
     M.out_off = d_out_mlm_off;
     M.out_pos = d_out_mlm_pos;
     M.out_label = d_out_mlm_label;
     HIP_TRY(launch_masked_lm(M, st));
   }
-  c->last_nmask = -1;  // the rows are masked in place exactly once
+  k->last_nmask = -1;  // the rows are masked in place exactly once
   return 0;
 }
 
-extern "C" int lddl_masked_lm_spans(lddl_ctx* c, const uint16_t* d_ids, const int64_t* d_src0,
+extern "C" int lddl_masked_lm_spans(lddl_ctx* c, lddl_pack* pk, const uint16_t* d_ids, const int64_t* d_src0,
                                     const int64_t* d_src1, const uint16_t* d_len0, const int64_t* d_part,
                                     int64_t* d_out_mlm_off, uint16_t* d_out_mlm_pos, uint16_t* d_out_mlm_label,
                                     uint16_t* d_out_mlm_token, void* stream) {
   if (!c) return set_err(LDDL_EINVAL, "null ctx");
-  if (c->last_npairs < 0 || c->last_nmask < 0)
+  lddl_pack* k = pk ? pk : &c->own;
+  if (k->device != c->device) return set_err(LDDL_EINVAL, "pack result of another device");
+  if (k->last_npairs < 0 || k->last_nmask < 0)
     return set_err(LDDL_EINVAL, "lddl_masked_lm_spans needs lddl_pack_bert(masking=1) then lddl_row_spans");
-  if (!d_out_mlm_off || (c->last_npairs > 0 && (!d_ids || !d_src0 || !d_src1 || !d_len0 || !d_part)) ||
-      (c->last_nmask > 0 && (!d_out_mlm_pos || !d_out_mlm_label || !d_out_mlm_token)))
+  if (!d_out_mlm_off || (k->last_npairs > 0 && (!d_ids || !d_src0 || !d_src1 || !d_len0 || !d_part)) ||
+      (k->last_nmask > 0 && (!d_out_mlm_pos || !d_out_mlm_label || !d_out_mlm_token)))
     return set_err(LDDL_EINVAL, "null pointer");
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t st = (hipStream_t)stream;
-  const PackParams& P = c->pp;
-  if (c->last_npairs == 0) {
+  const PackParams& P = k->pp;
+  if (k->last_npairs == 0) {
     HIP_TRY(hipMemsetAsync(d_out_mlm_off, 0, 8, st));
   } else {
     MlmParams M{};
     M.doc_sent_off = P.doc_sent_off;
     M.part_doc_off = P.part_doc_off;
-    M.pair_base = (const int64_t*)c->ws[15].p;
+    M.pair_base = (const int64_t*)k->ws[15].p;
     M.binned = P.binned;
     M.mref = P.mref;
     M.mloc = P.mloc;
-    M.mask_base = (const int64_t*)c->ws[27].p;
+    M.mask_base = (const int64_t*)k->ws[27].p;
     M.marena = P.marena;
     M.n_part = P.n_part;
     M.dup = P.dup;
@@ -848,6 +889,55 @@ extern "C" int lddl_masked_lm_spans(lddl_ctx* c, const uint16_t* d_ids, const in
     M.out_token = d_out_mlm_token;
     HIP_TRY(launch_masked_lm(M, st));
   }
+  return 0;
+}
+
+extern "C" int lddl_pack_new(lddl_ctx* c, lddl_pack** out) {
+  if (!c || !out) return set_err(LDDL_EINVAL, "null pointer");
+  lddl_pack* k = new (std::nothrow) lddl_pack;
+  if (!k) return set_err(LDDL_ENOMEM, "out of host memory");
+  k->device = c->device;
+  k->mlm_cap = c->mlm_cap0;
+  *out = k;
+  return 0;
+}
+
+extern "C" void lddl_pack_free(lddl_pack* k) {
+  if (!k) return;
+  (void)hipSetDevice(k->device);
+  free_pack(k);
+  delete k;
+}
+
+extern "C" int lddl_pack_rows(const lddl_pack* k, int64_t* out_npairs) {
+  if (!k || !out_npairs) return set_err(LDDL_EINVAL, "null pointer");
+  *out_npairs = k->last_npairs;
+  return 0;
+}
+
+// ---------------------------------------------------------------- bin ----
+extern "C" int lddl_bin(lddl_ctx* c, const int64_t* d_num_tokens, int64_t n, int32_t bin_size, int32_t nbins,
+                        int64_t* d_out_perm, int64_t* d_out_bin_counts, void* stream) {
+  if (!c) return set_err(LDDL_EINVAL, "null ctx");
+  if (n < 0) return set_err(LDDL_EINVAL, "negative row count");
+  if (bin_size < 1) return set_err(LDDL_EINVAL, "bin_size %d < 1", bin_size);
+  if (nbins < 1 || nbins > 1024) return set_err(LDDL_EINVAL, "nbins %d not in [1, 1024]", nbins);
+  if (!d_out_bin_counts || (n > 0 && (!d_num_tokens || !d_out_perm))) return set_err(LDDL_EINVAL, "null pointer");
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t nh = bin_chunks(n) * nbins;
+  int32_t *hist, *err;
+  int64_t *base, *bsum;
+  int rc;
+  if ((rc = ws_get(c, 0, (size_t)(nh ? nh : 1), &hist)) || (rc = ws_get(c, 1, (size_t)nh + 1, &base)) ||
+      (rc = ws_get(c, 2, (size_t)scan_blocks(nh) + 1, &bsum)) || (rc = ws_get(c, 3, 1, &err)))
+    return rc;
+  if (!c->h_tot) HIP_TRY(hipHostMalloc((void**)&c->h_tot, 8 * sizeof(int64_t)));
+  HIP_TRY(launch_bin(d_num_tokens, n, bin_size, nbins, hist, base, bsum, d_out_perm, d_out_bin_counts, err, st));
+  HIP_TRY(hipMemcpyAsync(&c->h_tot[7], err, 4, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  if ((int32_t)(c->h_tot[7] & 0xFFFFFFFF))
+    return set_err(LDDL_EINDEX, "IndexError: list index out of range (a length bins below -nbins, binning.py:70-73)");
   return 0;
 }
 
@@ -939,22 +1029,24 @@ extern "C" int lddl_render_masked(lddl_ctx* c, const uint16_t* d_ids, const int6
   return 0;
 }
 
-extern "C" int lddl_row_docs(lddl_ctx* c, int64_t* d_out_doc, void* stream) {
+extern "C" int lddl_row_docs(lddl_ctx* c, lddl_pack* pk, int64_t* d_out_doc, void* stream) {
   if (!c) return set_err(LDDL_EINVAL, "null ctx");
-  if (c->last_npairs < 0) return set_err(LDDL_EINVAL, "no successful lddl_pack_* call");
+  lddl_pack* k = pk ? pk : &c->own;
+  if (k->device != c->device) return set_err(LDDL_EINVAL, "pack result of another device");
+  if (k->last_npairs < 0) return set_err(LDDL_EINVAL, "no successful lddl_pack_* call");
   if (!d_out_doc) return set_err(LDDL_EINVAL, "null pointer");
   HIP_TRY(hipSetDevice(c->device));
-  const PackParams& P = c->pp;
+  const PackParams& P = k->pp;
   RowDocParams D{};
   D.pairs = P.pairs;
   D.binned = P.binned;
-  D.pair_base = (const int64_t*)c->ws[15].p;
+  D.pair_base = (const int64_t*)k->ws[15].p;
   D.fs_base = P.fs_base;
   D.sent_off = P.sent_off;
   D.doc_sent_off = P.doc_sent_off;
   D.part_doc_off = P.part_doc_off;
   D.n_part = P.n_part;
-  D.n_rows = c->last_npairs;
+  D.n_rows = k->last_npairs;
   D.dup = P.dup;
   D.out_doc = d_out_doc;
   HIP_TRY(launch_row_docs(D, c->n_cu, (hipStream_t)stream));

@@ -154,6 +154,13 @@ hipError_t launch_scan_ntok(const int32_t* ntok, int64_t n, int64_t* tokoff, int
 // from tokoff[*d_lo]; blocksums: scan_blocks(max_items) + 1
 hipError_t launch_scan_ntok_range(const int32_t* ntok, const int64_t* d_lo, const int64_t* d_hi, int64_t max_items,
                                   int64_t* tokoff, int64_t* blocksums, hipStream_t s);
+// lddl_bin (bin.hip): stable grouping of rows by length bin.  hist:
+// bin_chunks(n) * nbins int32, base: that + 1 int64, scan_bsum:
+// scan_blocks(that) + 1 int64; err[0] = 1 when a bin is below -nbins
+int64_t bin_chunks(int64_t n);
+hipError_t launch_bin(const int64_t* num_tokens, int64_t n, int32_t bin_size, int32_t nbins, int32_t* hist,
+                      int64_t* base, int64_t* scan_bsum, int64_t* perm, int64_t* bin_counts, int32_t* err,
+                      hipStream_t s);
 hipError_t launch_sent_special(const uint16_t* ids, const int64_t* tok_off, const int32_t* ntok, int64_t n_sent,
                                uint32_t cls, uint32_t sep, uint8_t* out, hipStream_t s);
 hipError_t launch_masked_lm(const MlmParams& M, hipStream_t s);

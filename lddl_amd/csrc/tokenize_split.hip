@@ -1367,7 +1367,16 @@ __global__ __launch_bounds__(64 * WAVES) void wp_kernel(TokParams P, SplitParams
 // ~470 per step of wp_kernel's Bloom scan.  One record per lane with refill,
 // as wp_kernel (a lane whose word ends begins the next record in the same
 // step); WPT_STEPS steps per round of the refill bookkeeping.
-constexpr int WPT_STEPS = 2;
+// Measured, not kept as the default (LDDL_WP_ALGO=trie selects it):
+// 2.08 / 2.34 / 2.56 ms per GB of corpus at WPT_STEPS 8 / 4 / 2 against
+// wp_kernel's 1.28 (profiles/r5_wp_trie_ab.txt).  The steps are cheap but
+// each is a dependent ~L2 round trip (~13 per record), and the refill
+// bookkeeping per round costs what the Bloom scan saves.
+#ifdef LDDL_WPT_STEPS
+constexpr int WPT_STEPS = LDDL_WPT_STEPS;  // (A/B builds, tools/ab_build.py)
+#else
+constexpr int WPT_STEPS = 8;
+#endif
 
 template <int WAVES>
 __global__ __launch_bounds__(64 * WAVES) void wpt_kernel(TokParams P, SplitParams S) {
@@ -1777,10 +1786,10 @@ hipError_t launch_tokenize_split(const TokParams& P, int64_t nbytes, int64_t* ti
     if (P.dbg) e = tok5::launch_scan<SCAN_WAVES, true, tok5::SCAN_OCC>(P, S, n_cu, s);
     else e = tok5::launch_scan<SCAN_WAVES, false, tok5::SCAN_OCC>(P, S, n_cu, s);
     if (e != hipSuccess || (e = mark(0, 1)) != hipSuccess || (e = mark(1, 0)) != hipSuccess) return e;
-    // WordPiece by trie walk (default) or by Bloom scan + bucket probes
-    // (LDDL_WP_ALGO=bloom, or tables without a trie: A/B)
-    static const bool bloom = getenv("LDDL_WP_ALGO") && strcmp(getenv("LDDL_WP_ALGO"), "bloom") == 0;
-    if ((e = (bloom || !P.trie) ? tok5::launch_wp<WP_WAVES>(P, S, n_cu, s) : tok5::launch_wpt<WPT_WAVES>(P, S, n_cu, s)) !=
+    // WordPiece by Bloom scan + bucket probes (default) or by trie walk
+    // (LDDL_WP_ALGO=trie: A/B, slower)
+    const bool trie = getenv("LDDL_WP_ALGO") && strcmp(getenv("LDDL_WP_ALGO"), "trie") == 0;
+    if ((e = (trie && P.trie) ? tok5::launch_wpt<WPT_WAVES>(P, S, n_cu, s) : tok5::launch_wp<WP_WAVES>(P, S, n_cu, s)) !=
         hipSuccess)
       return e;
     if ((e = mark(1, 1)) != hipSuccess || (e = mark(2, 0)) != hipSuccess) return e;

@@ -153,6 +153,7 @@ class PackResult:
   src1: torch.Tensor = None       # of B / code; tokens is then None (no rows materialised)
   cls_id: int = 0
   sep_id: int = 0
+  pack: 'PackHandle' = None       # the lddl_pack this result was packed into (lddl_row_docs reads it)
 
   @property
   def spans(self):
@@ -210,14 +211,49 @@ class PackResult:
     return out
 
 
+class PackHandle:
+  """A pack result (lddl_pack_new / lddl_pack_free): what one
+  lddl_pack_bert / lddl_pack_codebert call leaves for the post-pack calls
+  (lddl_materialize, lddl_row_spans, lddl_masked_lm[_spans],
+  lddl_row_docs), which name it explicitly."""
+
+  def __init__(self, tok):
+    h = ctypes.c_void_p()
+    _lib.check(_lib.lib().lddl_pack_new(tok.handle, ctypes.byref(h)))
+    self._h = h.value
+
+  @property
+  def handle(self):
+    return self._h
+
+  def rows(self):
+    """#rows of the last successful pack into it (-1: none)"""
+    n = ctypes.c_int64()
+    _lib.check(_lib.lib().lddl_pack_rows(self._h, ctypes.byref(n)))
+    return n.value
+
+  def close(self):
+    if self._h:
+      _lib.lib().lddl_pack_free(self._h)
+      self._h = None
+
+  def __del__(self):
+    try:
+      self.close()
+    except Exception:
+      pass
+
+
 class Packer:
-  """One GPU's tokenize -> pack -> bin -> materialise pipeline (one lddl_ctx)."""
+  """One GPU's tokenize -> pack -> bin -> materialise pipeline (one lddl_ctx
+  and the pack result it packs into)."""
 
   def __init__(self, vocab_file=VOCAB_BERT, device=None, masking=False):
     self.tok = Tokenizer(vocab_file, device)
     if masking:  # the tokenizer records the [CLS]/[SEP] sentences the masked packer needs
       self.tok.set_special_flags(True)
     self.device = self.tok.device
+    self.result = PackHandle(self.tok)
     self._out = {}
 
   def _buf(self, name, n, dtype):
@@ -254,8 +290,9 @@ class Packer:
 
   def pack(self, shards, ids, ntok, tok_off=None, target_seq_length=128, short_seq_prob=0.1, duplicate_factor=5,
            seed=12345, bin_size=None, codebert=False, masking=False, masked_lm_ratio=0.15, stream=None,
-           spans=False):
-    """ids / ntok / tok_off: tokenize()'s dense CSR result (tok_off None:
+           spans=False, into=None):
+    """into: the PackHandle to pack into (default: the Packer's own).
+    ids / ntok / tok_off: tokenize()'s dense CSR result (tok_off None:
     the exclusive scan of ntok, for ids built by hand); ids must hold 16
     entries of padding past the last id (lddl_materialize's 16-B loads).
     spans: the rows as spans of the dense ids (lddl_row_spans, no token
@@ -269,15 +306,17 @@ class Packer:
       torch.cumsum(ntok[:shards.n_sent].to(torch.int64), 0, out=tok_off[1:])
     tot = (ctypes.c_int64 * 4)()
     s = _stream(stream)
+    into = into or self.result
+    h = into.handle
     if codebert:
       if shards.doc_nseg_doc is None:
         raise ValueError('CodeBERT packing needs doc_nseg_doc')
-      rc = L.lddl_pack_codebert(self.tok.handle, _ptr(ntok), _ptr(tok_off), _ptr(shards.sent_off), shards.n_sent,
+      rc = L.lddl_pack_codebert(self.tok.handle, h, _ptr(ntok), _ptr(tok_off), _ptr(shards.sent_off), shards.n_sent,
                                 _ptr(shards.doc_sent_off), _ptr(shards.doc_nseg_doc), shards.n_doc,
                                 _ptr(shards.part_doc_off), shards.n_part, target_seq_length, short_seq_prob,
                                 duplicate_factor, abs(int(seed)), bin_size or 0, tot, s)
     else:
-      rc = L.lddl_pack_bert(self.tok.handle, _ptr(ids) if masking else None, _ptr(ntok), _ptr(tok_off),
+      rc = L.lddl_pack_bert(self.tok.handle, h, _ptr(ids) if masking else None, _ptr(ntok), _ptr(tok_off),
                             _ptr(shards.sent_off), shards.n_sent,
                             _ptr(shards.doc_sent_off), shards.n_doc, _ptr(shards.part_doc_off), shards.n_part,
                             target_seq_length, short_seq_prob, duplicate_factor, 1 if masking else 0,
@@ -296,14 +335,15 @@ class Packer:
                      self._buf('part', n_pairs, torch.int64),
                      self._buf('bin_count', shards.n_part * nbins, torch.int64))
     res.cls_id, res.sep_id = self.tok.cls_id, self.tok.sep_id
+    res.pack = into
     if spans:
       res.src0 = self._buf('src0', n_pairs, torch.int64)
       res.src1 = self._buf('src1', n_pairs, torch.int64)
-      _lib.check(L.lddl_row_spans(self.tok.handle, _ptr(res.src0), _ptr(res.src1), _ptr(res.tok_off),
+      _lib.check(L.lddl_row_spans(self.tok.handle, h, _ptr(res.src0), _ptr(res.src1), _ptr(res.tok_off),
                                   _ptr(res.len0), _ptr(res.len1), _ptr(res.flags), _ptr(res.bins),
                                   _ptr(res.part), _ptr(res.bin_count), s))
     else:
-      _lib.check(L.lddl_materialize(self.tok.handle, _ptr(ids), _ptr(res.tokens), _ptr(res.tok_off),
+      _lib.check(L.lddl_materialize(self.tok.handle, h, _ptr(ids), _ptr(res.tokens), _ptr(res.tok_off),
                                     _ptr(res.len0), _ptr(res.len1), _ptr(res.flags), _ptr(res.bins),
                                     _ptr(res.part), _ptr(res.bin_count), s))
     res.bin_count = res.bin_count[:shards.n_part * nbins].view(shards.n_part, nbins)
@@ -315,15 +355,38 @@ class Packer:
       res.mlm_label = self._buf('mlm_label', res.n_masked, torch.int16)
       if spans:
         res.mlm_token = self._buf('mlm_token', res.n_masked, torch.int16)
-        _lib.check(L.lddl_masked_lm_spans(self.tok.handle, _ptr(ids), _ptr(res.src0), _ptr(res.src1),
+        _lib.check(L.lddl_masked_lm_spans(self.tok.handle, h, _ptr(ids), _ptr(res.src0), _ptr(res.src1),
                                           _ptr(res.len0), _ptr(res.part), _ptr(res.mlm_off), _ptr(res.mlm_pos),
                                           _ptr(res.mlm_label), _ptr(res.mlm_token), s))
       else:
-        _lib.check(L.lddl_masked_lm(self.tok.handle, _ptr(res.mlm_off), _ptr(res.mlm_pos), _ptr(res.mlm_label), s))
+        _lib.check(L.lddl_masked_lm(self.tok.handle, h, _ptr(res.mlm_off), _ptr(res.mlm_pos), _ptr(res.mlm_label), s))
     return res
 
   def run(self, shards, **kw):
     return self.pack(shards, *self.tokenize(shards), **kw)
+
+  def bin(self, num_tokens, bin_size, nbins, stream=None):
+    return bin_rows(self.tok, num_tokens, bin_size, nbins, stream)
+
+
+def bin_rows(tok, num_tokens, bin_size, nbins, stream=None):
+  """lddl_bin: group rows by length bin as binning.py:63-93
+  _to_dataframe_binned does.  num_tokens: int64 tensor on tok's device ->
+  (perm, bin_counts) on the device: the row indices bin-major, ascending
+  within a bin, and the rows per bin.  A length whose bin falls below -nbins
+  raises IndexError, as the reference's seqs[bin_id] does."""
+  if num_tokens.dtype != torch.int64 or not num_tokens.is_contiguous():
+    raise ValueError('num_tokens: a contiguous int64 tensor')
+  n = num_tokens.numel()
+  perm = torch.empty(max(n, 1), dtype=torch.int64, device=num_tokens.device)
+  counts = torch.empty(nbins, dtype=torch.int64, device=num_tokens.device)
+  L = _lib.lib()
+  rc = L.lddl_bin(tok.handle, _ptr(num_tokens), n, int(bin_size), int(nbins), _ptr(perm), _ptr(counts),
+                  _stream(stream))
+  if rc == -7:
+    raise IndexError(L.lddl_last_error().decode())
+  _lib.check(rc)
+  return perm[:n], counts
 
 
 def run_bert(corpus, vocab_file=VOCAB_BERT, target_seq_length=128, bin_size=None, n_partitions=1, seed=12345,

@@ -100,11 +100,13 @@ def seg_columns(packer, res, r0, n, codebert=False, stream=None):
           render(packer, res.tokens, res.tok_off, r0, n, SEG1, **kw))
 
 
-def row_docs(packer, n_rows, n_copy=None, stream=None):
-  """document index of every row of the last pack call (lddl_row_docs, all
-  n_rows rows on the device); the first n_copy of them copied to the host"""
+def row_docs(packer, res, n_copy=None, stream=None):
+  """document index of every row of the pack result `res` (lddl_row_docs
+  over res.pack, all rows on the device); the first n_copy of them copied to
+  the host"""
+  n_rows = res.n_pairs
   out = torch.empty(max(n_rows, 1), dtype=torch.int64, device=packer.device)
-  _lib.check(_lib.lib().lddl_row_docs(packer.tok.handle, _ptr(out), _stream(stream)))
+  _lib.check(_lib.lib().lddl_row_docs(packer.tok.handle, res.pack.handle, _ptr(out), _stream(stream)))
   return out[:n_rows if n_copy is None else min(n_copy, n_rows)].cpu().numpy()
 
 
@@ -256,7 +258,7 @@ def write_shards(packer, res, out_dir, bin_size=None, codebert=False, masking=Fa
   if codebert:
     if doc_ids is None:
       raise ValueError('CodeBERT shards need doc_ids (the id column)')
-    docs = np_array(row_docs(packer, res.n_pairs, n_rows, stream))
+    docs = np_array(row_docs(packer, res, n_rows, stream))
     ids_arr = doc_ids if isinstance(doc_ids, pa.Array) else str_array(doc_ids)
     ids_col = ids_arr.take(docs) if n_rows else str_array([])
   if masking and not codebert:
@@ -363,7 +365,7 @@ def write_txt(packer, res, out_dir, bin_size=None, codebert=False, masking=False
       raise ValueError('CodeBERT txt output needs doc_ids (the id field)')
     if isinstance(doc_ids, pa.Array):
       doc_ids = doc_ids.to_pylist()
-    docs = row_docs(packer, res.n_pairs, n_rows, stream)
+    docs = row_docs(packer, res, n_rows, stream)
   if masking and not codebert:
     moff_all = res.mlm_off[:n_rows + 1].cpu().numpy()
     mpos_all = res.mlm_pos[:int(moff_all[-1])].cpu().numpy().view(np.uint16)

@@ -123,13 +123,25 @@ def adversarial_sentences(rng, n):
   return out
 
 
-@pytest.mark.parametrize('algo', ['0', '5', '6'])
+# '5t': tok5 with its WordPiece by trie walk (LDDL_WP_ALGO=trie, the A/B option)
+ALGOS = ['0', '5', '5t', '6']
+
+
+def _set_algo(monkeypatch, algo):
+  monkeypatch.setenv('LDDL_TOKENIZE_ALGO', algo[0])
+  if algo.endswith('t'):
+    monkeypatch.setenv('LDDL_WP_ALGO', 'trie')
+  else:
+    monkeypatch.delenv('LDDL_WP_ALGO', raising=False)
+
+
+@pytest.mark.parametrize('algo', ALGOS)
 @pytest.mark.parametrize('name', ['bert', 'codebert'])
 def test_hip_tokenize_adversarial_vs_oracle(gpu, monkeypatch, algo, name):
   from lddl_amd.synth import corpus_from_sentences
   from lddl_amd.tokenizer import Tokenizer
-  monkeypatch.setenv('LDDL_TOKENIZE_ALGO', algo)
-  rng = np.random.default_rng(int(algo) * 7 + len(name))
+  _set_algo(monkeypatch, algo)
+  rng = np.random.default_rng(int(algo[0]) * 7 + len(name) + len(algo))
   sents = adversarial_sentences(rng, 6000)
   c = corpus_from_sentences(sents, [0, len(sents)])
   tok = Tokenizer(VOCABS[name])
@@ -142,11 +154,11 @@ def test_hip_tokenize_adversarial_vs_oracle(gpu, monkeypatch, algo, name):
       assert np.array_equal(a.astype(np.int64), b.astype(np.int64)), (i, repr(sents[i][:80]))
 
 
-@pytest.mark.parametrize('algo', ['0', '5', '6'])
+@pytest.mark.parametrize('algo', ALGOS)
 def test_hip_tokenize_algos_agree_on_wiki(gpu, monkeypatch, algo):
   from lddl_amd import synth
   from lddl_amd.tokenizer import Tokenizer
-  monkeypatch.setenv('LDDL_TOKENIZE_ALGO', algo)
+  _set_algo(monkeypatch, algo)
   c = synth.make_wiki(3_000_000, seed=17)
   ids, ntok = run_hip(Tokenizer(VOCABS['bert']), c.data, c.sent_off)
   oids, ontok = OracleTokenizer(VOCABS['bert']).run(c.data, c.sent_off, 512, nthreads=8)
