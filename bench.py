@@ -401,7 +401,8 @@ def parquet_sample(args, pk, res, sh):
     nb = res.nbins
     rows = int(res.bin_count[:args.parquet_parts].sum().item())
     return {'partitions': args.parquet_parts, 'files': len(files), 'rows': rows, 'seconds': el,
-            'rows_per_s': rows / el, 'parquet_mb': nbytes / 1e6, 'compression': 'snappy', 'nbins': nb}
+            'rows_per_s': rows / el, 'parquet_mb': nbytes / 1e6, 'compression': 'snappy', 'nbins': nb,
+            'sink': d, 'stages': dict(writer.LAST_STATS)}
   finally:
     shutil.rmtree(d, ignore_errors=True)
 
@@ -593,6 +594,15 @@ def run_leg(args, name, local, device, shards=None):
   return out
 
 
+_T0 = time.perf_counter()
+
+
+def progress(rank, msg):
+  """a stage mark on stderr (rank 0): long runs show they are alive"""
+  if rank == 0:
+    print('[bench %7.1fs] %s' % (time.perf_counter() - _T0, msg), file=sys.stderr, flush=True)
+
+
 def main():
   args = parse()
   if 'WORLD_SIZE' not in os.environ and (args.gpus or 1) > 1:
@@ -606,7 +616,9 @@ def main():
     raise SystemExit('bench.py: --gpus %d but WORLD_SIZE=%d' % (args.gpus, world))
   if args.launch_check:
     return launch_check(args, rank, world)
+  progress(rank, 'start')
   fe = frontend_leg(args.frontend_mb) if world == 1 and args.frontend_mb > 0 else None
+  progress(rank, 'frontend leg done')
   fe2 = (frontend_leg(args.frontend_c2_mb, seq=512, bin_size=64)
          if world == 1 and args.frontend_c2_mb > 0 else None)
   torch.cuda.set_device(local)
@@ -618,7 +630,9 @@ def main():
   from lddl_amd.pipeline import Packer
   from lddl_amd import build
   build.build_hip()
+  progress(rank, 'frontend_c2 leg done')
   sh, base, pdo, reps, gen_s = build_shards(args, rank, device)
+  progress(rank, 'shards built')
   from lddl_amd.pipeline import VOCAB_BERT, VOCAB_CODEBERT
   code = args.corpus == 'code'
   pk = Packer(VOCAB_CODEBERT if code else VOCAB_BERT, device=local, masking=args.masking)
@@ -747,6 +761,7 @@ def main():
         line['roofline']['traffic_source'] = e['source']
   except (OSError, ValueError, KeyError):
     pass
+  progress(rank, 'timed steps done')
   if args.parquet_parts > 0:
     line['parquet_writer'] = parquet_sample(args, pk, res, sh)
   if fe is not None:
@@ -754,6 +769,7 @@ def main():
   if fe2 is not None:
     line['frontend_c2'] = fe2
   if not args.no_cpu_baseline and world == 1:  # the host leg (the oracle): rank 0 at N=1 only
+    progress(rank, 'cpu baseline')
     line['cpu_baseline'] = cpu_baseline(args, base, pdo, args.cpu_seconds)
     if not args.no_sample_check:  # the oracle as the checker of one full-size partition of the timed run
       line['cpu_baseline']['sample_check'] = sample_partition_check(args, pk, res, base, pdo, reps, kw['seed'])
@@ -772,6 +788,7 @@ def main():
         del sh
         torch.cuda.empty_cache()
       try:
+        progress(rank, 'leg ' + name)
         legs[name] = run_leg(args, name, local, device, heads if LEGS[name]['corpus'] == 'wiki' else None)
       except Exception as e:  # (recorded: the headline line still prints)
         legs[name] = {'error': '%s: %s' % (type(e).__name__, e)}

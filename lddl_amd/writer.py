@@ -24,6 +24,7 @@ import concurrent.futures
 import ctypes
 import io
 import os
+import time
 
 import numpy as np
 import pyarrow as pa
@@ -51,6 +52,17 @@ def schema(codebert=False, masking=False, binned=False):
   return pa.schema(f)
 
 
+def _host(t, stream=None):
+  """device tensor -> numpy on the host through pinned memory (torch's
+  caching host allocator: the block returns to the cache when the last view
+  of it -- the Arrow buffers of the files still encoding -- is gone);
+  synchronises the stream"""
+  h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+  h.copy_(t, non_blocking=True)
+  (stream or torch.cuda.current_stream()).synchronize()
+  return h.numpy()
+
+
 def render(packer, tokens, row_off, row0, n_rows, segment, len0=None, len1=None, flags=None, codebert=False,
            stream=None):
   """One string column of rows [row0, row0 + n_rows) on the GPU.
@@ -67,7 +79,7 @@ def render(packer, tokens, row_off, row0, n_rows, segment, len0=None, len1=None,
   _lib.check(L.lddl_render_strings(*args, None, 0, ctypes.byref(nb), s))
   data = torch.empty(max(nb.value, 1), dtype=torch.uint8, device=dev)
   _lib.check(L.lddl_render_strings(*args, _ptr(data), nb.value, ctypes.byref(nb), s))
-  return off.cpu().numpy(), data[:nb.value].cpu().numpy()
+  return _host(off, stream), _host(data[:nb.value], stream)
 
 
 def render_masked(packer, res, row0, n_rows, segment, stream=None):
@@ -83,7 +95,7 @@ def render_masked(packer, res, row0, n_rows, segment, stream=None):
   _lib.check(L.lddl_render_masked(*args, None, 0, ctypes.byref(nb), s))
   data = torch.empty(max(nb.value, 1), dtype=torch.uint8, device=packer.device)
   _lib.check(L.lddl_render_masked(*args, _ptr(data), nb.value, ctypes.byref(nb), s))
-  return off.cpu().numpy(), data[:nb.value].cpu().numpy()
+  return _host(off, stream), _host(data[:nb.value], stream)
 
 
 def seg_columns(packer, res, r0, n, codebert=False, stream=None):
@@ -220,8 +232,11 @@ def file_table(sch, cols, raw, lo, hi, batch=None):
   return pa.Table.from_arrays(arrs, schema=sch)
 
 
+LAST_STATS = {}  # the last write_shards call's stage seconds (bench.py reports them)
+
+
 def write_shards(packer, res, out_dir, bin_size=None, codebert=False, masking=False, doc_ids=None,
-                 part_base=0, compression='snappy', batch_rows=1 << 20, max_parts=None, stream=None,
+                 part_base=0, compression='snappy', batch_rows=1 << 16, max_parts=None, stream=None,
                  executor=None, pending=None):
   """Write the rows of ``res`` (a pipeline.PackResult) as the reference's
   parquet files under out_dir.  Partition p of this pack call is file
@@ -232,7 +247,10 @@ def write_shards(packer, res, out_dir, bin_size=None, codebert=False, masking=Fa
   their futures to the caller's list, and this call returns once the string
   columns are rendered and on the host (the device buffers are free again):
   the encodes run on while the caller's next chunk splits and packs.
+  Rows are rendered in batches of whole files of about batch_rows rows, so
+  the files of one batch encode while the next renders.
   Returns the list of files (written once the futures are done)."""
+  t_start = time.perf_counter()
   os.makedirs(out_dir, exist_ok=True)
   binned = bin_size is not None
   nbins = res.nbins if binned else 1
@@ -267,6 +285,8 @@ def write_shards(packer, res, out_dir, bin_size=None, codebert=False, masking=Fa
   files = []
   f = 0
   workers = encode_workers()
+  st = {'setup_s': time.perf_counter() - t_start, 'render_s': 0.0, 'table_s': 0.0, 'backpressure_s': 0.0,
+        'drain_s': 0.0, 'batches': 0, 'workers': workers}
   own = executor is None
   pool = concurrent.futures.ThreadPoolExecutor(workers) if own else executor
   mine = []
@@ -277,11 +297,15 @@ def write_shards(packer, res, out_dir, bin_size=None, codebert=False, masking=Fa
       g += 1
     r0, r1 = int(file_start[f]), int(file_start[g])
     n = r1 - r0
+    t0 = time.perf_counter()
     c0, c1 = seg_columns(packer, res, r0, n, codebert, stream)
     if masking and not codebert:
       m0 = int(moff_all[r0])
       lab = render(packer, res.mlm_label, res.mlm_off, r0, n, ROW, stream=stream)
       pos = npy_positions(moff_all[r0:r1 + 1] - m0, mpos_all[m0:int(moff_all[r1])])
+    t1 = time.perf_counter()
+    st['render_s'] += t1 - t0
+    st['batches'] += 1
     # one table over the batch's rows; a file is a zero-copy slice of it
     cols, raw = {}, {}
     if codebert:
@@ -311,17 +335,25 @@ def write_shards(packer, res, out_dir, bin_size=None, codebert=False, masking=Fa
       path = os.path.join(out_dir, name)
       mine.append(pool.submit(pq.write_table, t, path, compression=compression, use_dictionary=dict_cols))
       files.append(path)
+    t2 = time.perf_counter()
+    st['table_s'] += t2 - t1
     # the parquet encoder releases the GIL: files of a batch encode in
     # parallel on the host cores while the next batch renders on the GPU
     while len(mine) > 4 * workers:
       mine.pop(0).result()
+    st['backpressure_s'] += time.perf_counter() - t2
     f = g
+  t3 = time.perf_counter()
   if own:
     for fu in mine:
       fu.result()
     pool.shutdown()
   else:
     pending.extend(mine)
+  st['drain_s'] = time.perf_counter() - t3
+  st['total_s'] = time.perf_counter() - t_start
+  LAST_STATS.clear()
+  LAST_STATS.update(st)
   return files
 
 
