@@ -61,7 +61,7 @@ def parse():
   ap.add_argument('--frontend-mb', type=float, default=100.0,
                   help='MB of raw input for the front-end leg (the preprocessor CLI end to end on BASELINE '
                        'configs[0]: seq 128, no binning; rank 0 at N=1, before the bench touches the GPU; 0: off)')
-  ap.add_argument('--parquet-parts', type=int, default=64,
+  ap.add_argument('--parquet-parts', type=int, default=256,
                   help='after timing: write this many partitions as parquet shards and report the writer rate '
                        '(GPU string rendering + host Arrow/parquet encode; 0 = skip)')
   ap.add_argument('--legs', default='mask512,mask128,code,wikibooks',
@@ -69,7 +69,7 @@ def parse():
                        'as short legs, each with its own steps, kernel times and oracle check of one full-size '
                        'partition -- mask512 / mask128: static masking at seq 512 / 128 over the same corpus '
                        '(configs[3]), code: CodeBERT seq 512 (configs[2]), wikibooks: Wikipedia + Books seq 512 '
-                       '(configs[4]); comma list, "" = none')
+                       '(configs[4]); comma list, "" or none = none')
   ap.add_argument('--leg-steps', type=int, default=2)
   ap.add_argument('--frontend-c2-mb', type=float, default=2048.0,
                   help='MB of raw input for the C2-scale CLI leg (seq 512, bin 64: BASELINE configs[1] end to '
@@ -773,7 +773,7 @@ def main():
     line['cpu_baseline'] = cpu_baseline(args, base, pdo, args.cpu_seconds)
     if not args.no_sample_check:  # the oracle as the checker of one full-size partition of the timed run
       line['cpu_baseline']['sample_check'] = sample_partition_check(args, pk, res, base, pdo, reps, kw['seed'])
-  if world == 1 and args.legs:
+  if world == 1 and args.legs and args.legs != 'none':
     # the other BASELINE workloads, after everything above read the headline's
     # results: its packer scratch goes first (a second context beside it would
     # double the tokenizer / packer scratch), its shards stay for the legs on
