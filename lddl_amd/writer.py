@@ -358,7 +358,11 @@ def write_shards(packer, res, out_dir, bin_size=None, codebert=False, masking=Fa
 
 
 def encode_workers():
-  """parquet encode threads: the host CPU share (hostinfo.cpu_share)"""
+  """parquet encode threads: the host CPU share (hostinfo.cpu_share), or
+  LDDL_ENCODE_WORKERS"""
+  e = os.environ.get('LDDL_ENCODE_WORKERS')
+  if e:
+    return max(1, int(e))
   from .hostinfo import cpu_share
   return cpu_share()
 

@@ -44,11 +44,29 @@ def main():
   ap.add_argument('--files', type=int, default=512)
   ap.add_argument('--threads', default='1,4,8,16')
   ap.add_argument('--dirs', default='/tmp,/dev/shm')
+  ap.add_argument('--pinned', action='store_true',
+                  help='the string buffers in pinned host memory (torch pin_memory), as the writer hands them over')
   a = ap.parse_args()
   tb = table(a.rows, 620)
+  if a.pinned:
+    import torch
+
+    def pin(arr):
+      bufs = arr.buffers()
+      out = []
+      for b in bufs:
+        if b is None:
+          out.append(None)
+          continue
+        h = torch.empty(b.size, dtype=torch.uint8, pin_memory=True)
+        h.numpy()[:] = np.frombuffer(b, dtype=np.uint8)
+        out.append(pa.py_buffer(h.numpy()))
+      return pa.Array.from_buffers(arr.type, len(arr), out)
+
+    tb = pa.Table.from_arrays([pin(c.combine_chunks()) for c in tb.columns], names=tb.column_names)
   per = a.rows // a.files
   dict_cols = ['is_random_next', 'num_tokens', 'bin_id']
-  out = {'rows': a.rows, 'files': a.files, 'table_mb': tb.nbytes / 1e6, 'cpu_count': os.cpu_count(), 'runs': []}
+  out = {'rows': a.rows, 'files': a.files, 'pinned': a.pinned, 'table_mb': tb.nbytes / 1e6, 'cpu_count': os.cpu_count(), 'runs': []}
 
   def go(k, sink):
     d = tempfile.mkdtemp(dir=sink) if sink else None
