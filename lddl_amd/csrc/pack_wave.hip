@@ -603,6 +603,10 @@ __global__ __launch_bounds__(64, PACK_OCC) void pack_bert_wave_kernel(PackParams
   // ---- filter: kept sentence slots via a running wave scan ---------------
   // kept_before[k] = #kept sentences before sentence s0 + k (k <= nsent)
   int32_t* kept_before = P.kept + s0 + p;
+  // masking: does any kept sentence of the partition hold a [CLS] / [SEP]
+  // token (literal specials in the text, rare)?  If none, every pair takes
+  // the implicit candidate list with no per-pair flag reads
+  bool part_spec = false;
   {
     int run = 0;
     for (int k = 0; k < nsent; k += 64) {
@@ -611,6 +615,7 @@ __global__ __launch_bounds__(64, PACK_OCC) void pack_bert_wave_kernel(PackParams
       if (kk < nsent) n = P.ntok[s0 + kk];
       const int keep = (kk < nsent && n > 0) ? 1 : 0;
       const int incl = wscan_incl(keep, lane);
+      bool sp = false;
       if (kk < nsent) {
         const int slot = run + incl - keep;
         kept_before[kk] = slot;
@@ -618,9 +623,14 @@ __global__ __launch_bounds__(64, PACK_OCC) void pack_bert_wave_kernel(PackParams
           P.fs_ntok[s0 + slot] = n;
           P.fs_base[s0 + slot] = P.sent_off[s0 + kk] - base;
           P.fs_dense[s0 + slot] = P.tokoff[s0 + kk];
-          if (MASK) P.fs_spec[s0 + slot] = P.sent_spec[s0 + kk];
+          if (MASK) {
+            const uint8_t f = P.sent_spec[s0 + kk];
+            P.fs_spec[s0 + slot] = f;
+            sp = f != 0;
+          }
         }
       }
+      if (MASK && __ballot(sp)) part_spec = true;
       run += lane_get(incl, 63);
     }
     if (lane == 0) kept_before[nsent] = run;
@@ -710,6 +720,7 @@ __global__ __launch_bounds__(64, PACK_OCC) void pack_bert_wave_kernel(PackParams
   auto any_spec = [&](int k0, int n) -> bool {
     bool f = false;
     if constexpr (MASK) {
+      if (!part_spec) return false;
       for (int k = 0; k < n; k += 64) {
         const int kk = k0 + k + lane;
         bool x = false;
