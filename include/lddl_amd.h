@@ -228,6 +228,20 @@ int lddl_render_masked(lddl_ctx *ctx, const uint16_t *d_ids, const int64_t *d_sr
                        const uint16_t *d_mlm_token, int64_t row0, int64_t n_rows, int64_t *d_out_off,
                        uint8_t *d_out_bytes, int64_t out_cap, int64_t *out_nbytes, void *stream);
 
+/* The 'masked_lm_positions' column (pretrain.py:356-360: serialize_np_array
+ * of the row's uint16 positions = np.save bytes, lddl/utils.py:98-102) of
+ * rows [row0, row0 + n_rows) as Arrow binary data: row r's k =
+ * d_mlm_off[r+1] - d_mlm_off[r] positions d_mlm_pos[d_mlm_off[r] ..] (from
+ * lddl_masked_lm[_spans], absolute row numbering) become header k + the k
+ * values little-endian, where d_hdr holds the np.save header of a uint16[k]
+ * array for every k in [0, kmax], hdr_len bytes each (np.save pads every 1-D
+ * header to the same length; even).  A row with more than kmax positions is
+ * LDDL_EINVAL.  Same two-phase size query / capacity rules as
+ * lddl_render_strings. */
+int lddl_render_npy(lddl_ctx *ctx, const int64_t *d_mlm_off, const uint16_t *d_mlm_pos, int64_t row0,
+                    int64_t n_rows, const uint16_t *d_hdr, int32_t hdr_len, int32_t kmax, int64_t *d_out_off,
+                    uint8_t *d_out_bytes, int64_t out_cap, int64_t *out_nbytes, void *stream);
+
 /* Document index (into the corpus' documents) of every row of `pack`, in lddl_materialize's row order: the row's own document (seg0's; a
  * CodeBERT row without docstring: its code's) -- feeds CodeBERT's 'id'
  * column = document._id (pretrain_codebert.py:425-426). */

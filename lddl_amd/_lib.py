@@ -52,6 +52,8 @@ SIGNATURES = {
     'lddl_render_strings': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64,
                                     c_int32, c_int32, c_void_p, c_void_p, c_int64, ctypes.POINTER(c_int64),
                                     c_void_p]),
+    'lddl_render_npy': (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_int32, c_int32, c_void_p,
+                                c_void_p, c_int64, ctypes.POINTER(c_int64), c_void_p]),
     'lddl_row_docs': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
     'lddl_collate_seq_len': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int32,
                                      ctypes.POINTER(c_int64), c_void_p]),

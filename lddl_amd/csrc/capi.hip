@@ -985,6 +985,47 @@ extern "C" int lddl_render_strings(lddl_ctx* c, const uint16_t* d_tokens, const 
   return 0;
 }
 
+extern "C" int lddl_render_npy(lddl_ctx* c, const int64_t* d_mlm_off, const uint16_t* d_mlm_pos, int64_t row0,
+                               int64_t n_rows, const uint16_t* d_hdr, int32_t hdr_len, int32_t kmax, int64_t* d_out_off,
+                               uint8_t* d_out_bytes, int64_t out_cap, int64_t* out_nbytes, void* stream) {
+  if (!c) return set_err(LDDL_EINVAL, "null ctx");
+  if (row0 < 0 || n_rows < 0) return set_err(LDDL_EINVAL, "negative row range");
+  if (hdr_len <= 0 || (hdr_len & 1) || kmax < 0) return set_err(LDDL_EINVAL, "header length %d must be even and > 0", hdr_len);
+  if (!d_out_off || !out_nbytes || (n_rows > 0 && (!d_mlm_off || !d_hdr))) return set_err(LDDL_EINVAL, "null pointer");
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t st = (hipStream_t)stream;
+  NpyParams N{};
+  N.moff = d_mlm_off;
+  N.mpos = d_mlm_pos;
+  N.row0 = row0;
+  N.n_rows = n_rows;
+  N.hdr = d_hdr;
+  N.hdr_u16 = hdr_len / 2;
+  N.kmax = kmax;
+  int64_t* bsum;
+  int rc;
+  if ((rc = ws_get(c, 35, (size_t)(n_rows ? n_rows : 1), &N.lens)) ||
+      (rc = ws_get(c, 36, (size_t)scan_blocks(n_rows) + 1, &bsum)) || (rc = ws_get(c, 4, 1, &N.err)))
+    return rc;
+  if (!c->h_tot) HIP_TRY(hipHostMalloc((void**)&c->h_tot, 8 * sizeof(int64_t)));
+  HIP_TRY(hipMemsetAsync(N.err, 0, 4, st));
+  HIP_TRY(launch_npy_len(N, c->n_cu, st));
+  HIP_TRY(launch_scan_ntok(N.lens, n_rows, d_out_off, bsum, st));
+  HIP_TRY(hipMemcpyAsync(&c->h_tot[6], d_out_off + n_rows, 8, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(&c->h_tot[7], N.err, 4, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  if ((int32_t)(c->h_tot[7] & 0xFFFFFFFF)) return set_err(LDDL_EINVAL, "a row has more than kmax = %d masked positions", kmax);
+  *out_nbytes = c->h_tot[6];
+  if (!d_out_bytes) return 0;  // size query
+  if (out_cap < c->h_tot[6])
+    return set_err(LDDL_ECAPACITY, "render needs %lld bytes, out_cap %lld", (long long)c->h_tot[6], (long long)out_cap);
+  if (n_rows > 0 && c->h_tot[6] > 2 * (int64_t)N.hdr_u16 * n_rows && !d_mlm_pos) return set_err(LDDL_EINVAL, "null pointer");
+  N.out_off = d_out_off;
+  N.out = d_out_bytes;
+  HIP_TRY(launch_npy_bytes(N, c->n_cu, st));
+  return 0;
+}
+
 extern "C" int lddl_render_masked(lddl_ctx* c, const uint16_t* d_ids, const int64_t* d_src, const uint16_t* d_len,
                                   const uint16_t* d_len0, int32_t segment, const int64_t* d_mlm_off,
                                   const uint16_t* d_mlm_pos, const uint16_t* d_mlm_token, int64_t row0, int64_t n_rows,

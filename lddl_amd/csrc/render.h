@@ -46,7 +46,24 @@ struct RowDocParams {
   int64_t* out_doc;
 };
 
+// masked_lm_positions as np.save bytes (lddl_render_npy): row r = header of
+// its count k (hdr[k], hdr_u16 u16 units, the same length for every k) +
+// its k positions as little-endian uint16
+struct NpyParams {
+  const int64_t* moff;      // [rows + 1] (absolute row numbering)
+  const uint16_t* mpos;
+  int64_t row0, n_rows;
+  const uint16_t* hdr;      // [(kmax + 1) * hdr_u16]
+  int32_t hdr_u16, kmax;
+  int32_t* lens;            // [n_rows] scratch
+  int32_t* err;             // set when a row has more than kmax positions
+  const int64_t* out_off;   // [n_rows + 1]
+  uint8_t* out;
+};
+
 hipError_t launch_render_len(const RenderParams& R, int n_cu, hipStream_t s);
+hipError_t launch_npy_len(const NpyParams& N, int n_cu, hipStream_t s);
+hipError_t launch_npy_bytes(const NpyParams& N, int n_cu, hipStream_t s);
 hipError_t launch_render_bytes(const RenderParams& R, int n_cu, hipStream_t s);
 hipError_t launch_row_docs(const RowDocParams& D, int n_cu, hipStream_t s);
 

@@ -169,6 +169,34 @@ __global__ __launch_bounds__(256) void row_docs_kernel(RowDocParams D) {
   }
 }
 
+// np.save bytes of each row's masked positions (pretrain.py:356-360 stores
+// serialize_np_array(np.array(positions, np.uint16)), lddl/utils.py:98-102)
+__global__ __launch_bounds__(256) void npy_len_kernel(NpyParams N) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N.n_rows; i += stride) {
+    int64_t k = N.moff[N.row0 + i + 1] - N.moff[N.row0 + i];
+    if (k < 0 || k > N.kmax) {
+      N.err[0] = 1;
+      k = 0;
+    }
+    N.lens[i] = 2 * (N.hdr_u16 + (int32_t)k);
+  }
+}
+
+// a wave per row, one u16 per lane (every row starts at an even byte offset)
+__global__ __launch_bounds__(256) void npy_bytes_kernel(NpyParams N) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  const int64_t o0 = N.out_off[0];
+  for (int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < N.n_rows; i += nw) {
+    const int64_t m0 = N.moff[N.row0 + i];
+    const int32_t k = (int32_t)(N.moff[N.row0 + i + 1] - m0);
+    uint16_t* dst = reinterpret_cast<uint16_t*>(N.out + (N.out_off[i] - o0));
+    const uint16_t* h = N.hdr + (int64_t)k * N.hdr_u16;
+    for (int32_t u = lane; u < N.hdr_u16 + k; u += 64) dst[u] = u < N.hdr_u16 ? h[u] : N.mpos[m0 + (u - N.hdr_u16)];
+  }
+}
+
 static unsigned grid_for(int64_t waves, int n_cu) {
   const int64_t cap = (int64_t)n_cu * 32;  // 32 blocks (128 waves) per CU, grid-stride beyond
   int64_t b = (waves + 3) / 4;
@@ -185,6 +213,19 @@ hipError_t launch_render_len(const RenderParams& R, int n_cu, hipStream_t s) {
 hipError_t launch_render_bytes(const RenderParams& R, int n_cu, hipStream_t s) {
   if (R.n_rows == 0) return hipSuccess;
   hipLaunchKernelGGL(render_bytes_kernel, dim3(grid_for(R.n_rows, n_cu)), dim3(256), 0, s, R);
+  return hipGetLastError();
+}
+
+hipError_t launch_npy_len(const NpyParams& N, int n_cu, hipStream_t s) {
+  if (N.n_rows == 0) return hipSuccess;
+  int64_t b = (N.n_rows + 255) / 256, cap = (int64_t)n_cu * 16;
+  hipLaunchKernelGGL(npy_len_kernel, dim3((unsigned)(b < cap ? b : cap)), dim3(256), 0, s, N);
+  return hipGetLastError();
+}
+
+hipError_t launch_npy_bytes(const NpyParams& N, int n_cu, hipStream_t s) {
+  if (N.n_rows == 0) return hipSuccess;
+  hipLaunchKernelGGL(npy_bytes_kernel, dim3(grid_for(N.n_rows, n_cu)), dim3(256), 0, s, N);
   return hipGetLastError();
 }
 

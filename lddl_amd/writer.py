@@ -122,6 +122,46 @@ def row_docs(packer, res, n_copy=None, stream=None):
   return out[:n_rows if n_copy is None else min(n_copy, n_rows)].cpu().numpy()
 
 
+_NPY_HDR = {}  # device -> (uint16 tensor [(kmax + 1) * H / 2], H bytes, kmax)
+
+
+def npy_header_table(device, kmax=1024):
+  """np.save's header of a uint16[k] array for every k <= kmax, back to
+  back on the device (what lddl_render_npy prepends to each row), or None
+  when the headers differ in length (then the host path builds the column)"""
+  t = _NPY_HDR.get(device)
+  if t is None or t[2] < kmax:
+    hdr = [_npy_header(k) for k in range(kmax + 1)]
+    if len({len(h) for h in hdr}) != 1 or len(hdr[0]) % 2:
+      return None
+    flat = np.concatenate(hdr).view(np.uint16)
+    t = (torch.from_numpy(flat.view(np.int16).copy()).to(device), len(hdr[0]), kmax)
+    _NPY_HDR[device] = t
+  return t
+
+
+def render_npy(packer, res, row0, n_rows, stream=None):
+  """masked_lm_positions of rows [row0, row0 + n_rows) as np.save bytes
+  per row on the GPU (lddl_render_npy): (offsets, bytes) on the host as
+  render(), or None when the header table does not apply"""
+  if os.environ.get('LDDL_NPY_HOST'):  # (A/B: the host path)
+    return None
+  kmax = 1024
+  t = npy_header_table(packer.device, kmax)
+  if t is None:
+    return None
+  hdr, hlen, kmax = t
+  L = _lib.lib()
+  off = torch.empty(n_rows + 1, dtype=torch.int64, device=packer.device)
+  nb = ctypes.c_int64(0)
+  s = _stream(stream)
+  args = (packer.tok.handle, _ptr(res.mlm_off), _ptr(res.mlm_pos), row0, n_rows, _ptr(hdr), hlen, kmax, _ptr(off))
+  _lib.check(L.lddl_render_npy(*args, None, 0, ctypes.byref(nb), s))
+  data = torch.empty(max(nb.value, 1), dtype=torch.uint8, device=packer.device)
+  _lib.check(L.lddl_render_npy(*args, _ptr(data), nb.value, ctypes.byref(nb), s))
+  return _host(off, stream), _host(data[:nb.value], stream)
+
+
 def _npy_header(k):
   b = io.BytesIO()
   np.save(b, np.zeros(k, dtype=np.uint16))  # serialize_np_array, lddl/utils.py:98-102
@@ -279,9 +319,13 @@ def write_shards(packer, res, out_dir, bin_size=None, codebert=False, masking=Fa
     docs = np_array(row_docs(packer, res, n_rows, stream))
     ids_arr = doc_ids if isinstance(doc_ids, pa.Array) else str_array(doc_ids)
     ids_col = ids_arr.take(docs) if n_rows else str_array([])
-  if masking and not codebert:
-    moff_all = res.mlm_off[:n_rows + 1].cpu().numpy()
-    mpos_all = res.mlm_pos[:int(moff_all[-1])].cpu().numpy().view(np.uint16)
+  host_mlm = []  # (offsets, positions) on the host, fetched only for the host npy path
+
+  def mlm_host():
+    if not host_mlm:
+      moff = res.mlm_off[:n_rows + 1].cpu().numpy()
+      host_mlm.extend([moff, res.mlm_pos[:int(moff[-1])].cpu().numpy().view(np.uint16)])
+    return host_mlm
   files = []
   f = 0
   workers = encode_workers()
@@ -300,9 +344,12 @@ def write_shards(packer, res, out_dir, bin_size=None, codebert=False, masking=Fa
     t0 = time.perf_counter()
     c0, c1 = seg_columns(packer, res, r0, n, codebert, stream)
     if masking and not codebert:
-      m0 = int(moff_all[r0])
       lab = render(packer, res.mlm_label, res.mlm_off, r0, n, ROW, stream=stream)
-      pos = npy_positions(moff_all[r0:r1 + 1] - m0, mpos_all[m0:int(moff_all[r1])])
+      pos = render_npy(packer, res, r0, n, stream)
+      if pos is None:
+        moff_all, mpos_all = mlm_host()
+        m0 = int(moff_all[r0])
+        pos = npy_positions(moff_all[r0:r1 + 1] - m0, mpos_all[m0:int(moff_all[r1])])
     t1 = time.perf_counter()
     st['render_s'] += t1 - t0
     st['batches'] += 1

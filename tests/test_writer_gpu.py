@@ -426,3 +426,33 @@ def test_cli_resume_skips_completed_chunks(gpu, tmp_path):
   assert all(open(f, 'rb').read() == blobs[f] for f in files)
   _, t4 = preprocess.main(preprocess.attach_args().parse_args(common + ['--duplicate-factor', '2']))
   assert t4['chunks_skipped'] == 0
+
+
+def test_render_npy_matches_host(packer):
+  """lddl_render_npy (the masked_lm_positions column on the GPU) against
+  the host restatement npy_positions (numpy's own np.save header per
+  length): rows with 0..300 positions, a row range inside the rows"""
+  import ctypes
+  import torch
+  from types import SimpleNamespace
+  from lddl_amd import _lib, writer
+  rng = np.random.default_rng(3)
+  k = rng.integers(0, 301, size=5000)
+  k[::97] = 0
+  off = np.zeros(len(k) + 1, np.int64)
+  np.cumsum(k, out=off[1:])
+  pos = rng.integers(0, 65536, size=int(off[-1])).astype(np.uint16)
+  res = SimpleNamespace(mlm_off=torch.from_numpy(off).cuda(), mlm_pos=torch.from_numpy(pos.view(np.int16)).cuda())
+  for r0, n in ((0, len(k)), (123, 2000), (len(k), 0)):
+    got = writer.render_npy(packer, res, r0, n)
+    exp = writer.npy_positions(off[r0:r0 + n + 1] - off[r0], pos[off[r0]:off[r0 + n]])
+    assert np.array_equal(got[0], exp[0]) and np.array_equal(got[1], exp[1]), (r0, n)
+  # a row longer than the header table is refused
+  hdr, hlen, _ = writer.npy_header_table(packer.device)
+  o = torch.empty(2, dtype=torch.int64, device='cuda')
+  nb = ctypes.c_int64()
+  big = int(np.argmax(k))
+  rc = _lib.lib().lddl_render_npy(packer.tok.handle, ctypes.c_void_p(res.mlm_off.data_ptr()),
+                                  ctypes.c_void_p(res.mlm_pos.data_ptr()), big, 1, ctypes.c_void_p(hdr.data_ptr()),
+                                  hlen, int(k[big]) - 1, ctypes.c_void_p(o.data_ptr()), None, 0, ctypes.byref(nb), None)
+  assert rc == -1
