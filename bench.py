@@ -374,9 +374,11 @@ def sample_partition_check(args, pk, res, base, pdo, reps, seed0):
   return {'partition': p, 'rows': n, 'sentences': s1 - s0, 'identical': True, 'seconds': time.time() - t0}
 
 
-def parquet_sample(args, pk, res, sh):
+def parquet_sample(args, pk, res, sh, enc=None):
   """Writer throughput on the first --parquet-parts partitions (outside the
-  timed step; the reference's to_parquet_binned stage, reported separately)"""
+  timed step; the reference's to_parquet_binned stage, reported separately).
+  enc: the process encoder (writer.ProcessEncoder, started before the GPU),
+  else the writer's thread pool"""
   import shutil
   import tempfile
   from lddl_amd import writer
@@ -389,20 +391,26 @@ def parquet_sample(args, pk, res, sh):
   try:
     # one untimed partition first: pyarrow's lazily imported modules (compute,
     # pandas compat: ~0.55 s once per process) stay out of the rate
+    pend = []
     writer.write_shards(pk, res, os.path.join(d, 'warm'), bin_size=args.bin_size, masking=args.masking,
-                        codebert=args.corpus == 'code', doc_ids=doc_ids, max_parts=1)
+                        codebert=args.corpus == 'code', doc_ids=doc_ids, max_parts=1, executor=enc, pending=pend)
+    for f_ in pend:
+      f_.result()
+    pend = []
     torch.cuda.synchronize()
     t = time.perf_counter()
     files = writer.write_shards(pk, res, d, bin_size=args.bin_size, masking=args.masking,
                                 codebert=args.corpus == 'code', doc_ids=doc_ids,
-                                max_parts=args.parquet_parts)
+                                max_parts=args.parquet_parts, executor=enc, pending=pend)
+    for f_ in pend:
+      f_.result()
     el = time.perf_counter() - t
     nbytes = sum(os.path.getsize(f) for f in files)
     nb = res.nbins
     rows = int(res.bin_count[:args.parquet_parts].sum().item())
     return {'partitions': args.parquet_parts, 'files': len(files), 'rows': rows, 'seconds': el,
             'rows_per_s': rows / el, 'parquet_mb': nbytes / 1e6, 'compression': 'snappy', 'nbins': nb,
-            'sink': d, 'stages': dict(writer.LAST_STATS)}
+            'sink': d, 'encoder': 'processes' if enc is not None else 'threads', 'stages': dict(writer.LAST_STATS)}
   finally:
     shutil.rmtree(d, ignore_errors=True)
 
@@ -617,6 +625,12 @@ def main():
   if args.launch_check:
     return launch_check(args, rank, world)
   progress(rank, 'start')
+  # the writer sample's encode processes, forked while the process is GPU-free
+  # (LDDL_ENCODE_PROCS=0: the thread pool instead)
+  enc = None
+  if args.parquet_parts > 0 and os.environ.get('LDDL_ENCODE_PROCS', '1') != '0':
+    from lddl_amd import writer
+    enc = writer.ProcessEncoder()
   fe = frontend_leg(args.frontend_mb) if world == 1 and args.frontend_mb > 0 else None
   progress(rank, 'frontend leg done')
   fe2 = (frontend_leg(args.frontend_c2_mb, seq=512, bin_size=64)
@@ -763,7 +777,9 @@ def main():
     pass
   progress(rank, 'timed steps done')
   if args.parquet_parts > 0:
-    line['parquet_writer'] = parquet_sample(args, pk, res, sh)
+    line['parquet_writer'] = parquet_sample(args, pk, res, sh, enc)
+  if enc is not None:
+    enc.close()
   if fe is not None:
     line['frontend'] = fe
   if fe2 is not None:

@@ -558,6 +558,15 @@ def main(args, codebert=False):
   # the device tables
   ahead = 2  # chunks split ahead of the GPU
   futs = {c: submit(c) for c in todo[:ahead]} if pool is not None else {}
+  # the parquet encodes: a pool of processes forked here, before the GPU is
+  # touched (writer.ProcessEncoder; LDDL_ENCODE_PROCS=0: a thread pool)
+  import concurrent.futures
+  enc = None
+  if args.output_format != 'txt':
+    if os.environ.get('LDDL_ENCODE_PROCS', '1') != '0':
+      enc = writer.ProcessEncoder()
+    else:
+      enc = concurrent.futures.ThreadPoolExecutor(writer.encode_workers())
   t0 = time.perf_counter()
   device = torch.device('cuda', local)
   try:
@@ -567,6 +576,8 @@ def main(args, codebert=False):
     if pool is not None:
       pool.terminate()
       pool.join()
+    if enc is not None:
+      enc.close() if isinstance(enc, writer.ProcessEncoder) else enc.shutdown(wait=False)
     raise
   t['gpu_init_s'] = time.perf_counter() - t0
   out = []
@@ -581,8 +592,6 @@ def main(args, codebert=False):
   # parquet encodes of chunk k run on this pool while chunk k+1 splits,
   # uploads, tokenizes and packs; a chunk's --resume marker is saved once
   # all of its files are encoded (in chunk order)
-  import concurrent.futures
-  enc = concurrent.futures.ThreadPoolExecutor(writer.encode_workers()) if args.output_format != 'txt' else None
   inflight = []  # (a, b, files, futures, counts, n_pairs) per chunk, oldest first
 
   def settle(keep):
@@ -643,7 +652,7 @@ def main(args, codebert=False):
       pool.terminate()
       pool.join()
     if enc is not None:
-      enc.shutdown(wait=True)
+      enc.close() if isinstance(enc, writer.ProcessEncoder) else enc.shutdown(wait=True)
     index.close()
     t['teardown_s'] = time.perf_counter() - t0
   if args.num_shards:

@@ -64,7 +64,7 @@ def _host(t, stream=None):
 
 
 def render(packer, tokens, row_off, row0, n_rows, segment, len0=None, len1=None, flags=None, codebert=False,
-           stream=None):
+           stream=None, host=True):
   """One string column of rows [row0, row0 + n_rows) on the GPU.
 
   Returns (offsets int64[n_rows + 1] starting at 0, bytes uint8) on the host.
@@ -79,10 +79,12 @@ def render(packer, tokens, row_off, row0, n_rows, segment, len0=None, len1=None,
   _lib.check(L.lddl_render_strings(*args, None, 0, ctypes.byref(nb), s))
   data = torch.empty(max(nb.value, 1), dtype=torch.uint8, device=dev)
   _lib.check(L.lddl_render_strings(*args, _ptr(data), nb.value, ctypes.byref(nb), s))
+  if not host:  # (device tensors: the process encoder copies them into its shared slot)
+    return off, data[:nb.value]
   return _host(off, stream), _host(data[:nb.value], stream)
 
 
-def render_masked(packer, res, row0, n_rows, segment, stream=None):
+def render_masked(packer, res, row0, n_rows, segment, stream=None, host=True):
   """A (segment 0) / B (1) of span rows with the static masking applied
   (lddl_render_masked): (offsets, bytes) on the host as render()"""
   L = _lib.lib()
@@ -95,19 +97,21 @@ def render_masked(packer, res, row0, n_rows, segment, stream=None):
   _lib.check(L.lddl_render_masked(*args, None, 0, ctypes.byref(nb), s))
   data = torch.empty(max(nb.value, 1), dtype=torch.uint8, device=packer.device)
   _lib.check(L.lddl_render_masked(*args, _ptr(data), nb.value, ctypes.byref(nb), s))
+  if not host:
+    return off, data[:nb.value]
   return _host(off, stream), _host(data[:nb.value], stream)
 
 
-def seg_columns(packer, res, r0, n, codebert=False, stream=None):
+def seg_columns(packer, res, r0, n, codebert=False, stream=None, host=True):
   """the two segment string columns (A / B, or doc / code) of rows
   [r0, r0 + n): rendered from the spans over the dense ids (res.spans) or
   from the materialised rows"""
   if res.spans and res.mlm_token is not None:
-    return (render_masked(packer, res, r0, n, 0, stream), render_masked(packer, res, r0, n, 1, stream))
+    return (render_masked(packer, res, r0, n, 0, stream, host), render_masked(packer, res, r0, n, 1, stream, host))
   if res.spans:
-    return (render(packer, res.ids, res.src0, r0, n, SPAN, len0=res.len0, stream=stream),
-            render(packer, res.ids, res.src1, r0, n, SPAN, len0=res.len1, stream=stream))
-  kw = dict(len0=res.len0, len1=res.len1, flags=res.flags, codebert=codebert, stream=stream)
+    return (render(packer, res.ids, res.src0, r0, n, SPAN, len0=res.len0, stream=stream, host=host),
+            render(packer, res.ids, res.src1, r0, n, SPAN, len0=res.len1, stream=stream, host=host))
+  kw = dict(len0=res.len0, len1=res.len1, flags=res.flags, codebert=codebert, stream=stream, host=host)
   return (render(packer, res.tokens, res.tok_off, r0, n, SEG0, **kw),
           render(packer, res.tokens, res.tok_off, r0, n, SEG1, **kw))
 
@@ -140,7 +144,7 @@ def npy_header_table(device, kmax=1024):
   return t
 
 
-def render_npy(packer, res, row0, n_rows, stream=None):
+def render_npy(packer, res, row0, n_rows, stream=None, host=True):
   """masked_lm_positions of rows [row0, row0 + n_rows) as np.save bytes
   per row on the GPU (lddl_render_npy): (offsets, bytes) on the host as
   render(), or None when the header table does not apply"""
@@ -159,6 +163,8 @@ def render_npy(packer, res, row0, n_rows, stream=None):
   _lib.check(L.lddl_render_npy(*args, None, 0, ctypes.byref(nb), s))
   data = torch.empty(max(nb.value, 1), dtype=torch.uint8, device=packer.device)
   _lib.check(L.lddl_render_npy(*args, _ptr(data), nb.value, ctypes.byref(nb), s))
+  if not host:
+    return off, data[:nb.value]
   return _host(off, stream), _host(data[:nb.value], stream)
 
 
@@ -272,6 +278,145 @@ def file_table(sch, cols, raw, lo, hi, batch=None):
   return pa.Table.from_arrays(arrs, schema=sch)
 
 
+def _warm(_):
+  from . import encode_worker  # noqa: F401  (imported before the first batch)
+  return os.getpid()
+
+
+class ProcessEncoder:
+  """Parquet encodes in a pool of host processes (encode_worker.encode).
+
+  The per-file part of pyarrow's writer holds the GIL, so a thread pool
+  serialises on small files (CodeBERT's, ~100 rows each); processes each
+  have their own.  A batch's columns are copied once into a shared slot
+  file under /dev/shm (device columns straight from the GPU, through the
+  slot pinned with hipHostRegister when the runtime allows), then each task
+  writes a run of the batch's files from it.  `slots` batches can be in
+  flight; a slot is reused once its batch's files are written.  Create it
+  before the process touches the GPU (its workers are forked); close() ends
+  the workers and removes the slot files."""
+
+  def __init__(self, workers=None, slots=3, context='fork'):
+    import multiprocessing as mp
+    self.workers = workers or encode_workers()
+    self.ex = concurrent.futures.ProcessPoolExecutor(self.workers, mp_context=mp.get_context(context))
+    list(self.ex.map(_warm, range(self.workers)))  # start the workers now, not in the first batch
+    d = '/dev/shm' if os.path.isdir('/dev/shm') and os.access('/dev/shm', os.W_OK) else None
+    import tempfile
+    self.dir = tempfile.mkdtemp(prefix='lddl_enc_', dir=d)
+    self.slots = [dict(path=os.path.join(self.dir, 'slot%d' % i), size=0, mm=None, t=None, pinned=False, futs=[])
+                  for i in range(slots)]
+    self.next = 0
+
+  def submit(self, fn, *a, **kw):  # (a plain task, as an executor)
+    return self.ex.submit(fn, *a, **kw)
+
+  def _unpin(self, sl):
+    if sl['pinned']:
+      torch.cuda.cudart().cudaHostUnregister(sl['t'].data_ptr())
+      sl['pinned'] = False
+
+  def _acquire(self, size):
+    sl = self.slots[self.next]
+    self.next = (self.next + 1) % len(self.slots)
+    for f_ in sl['futs']:
+      f_.result()
+    sl['futs'] = []
+    if sl['size'] < size:
+      import mmap
+      self._unpin(sl)
+      sl['t'] = None
+      if sl['mm'] is not None:
+        sl['mm'].close()
+      new = max(size, 2 * sl['size'], 64 << 20)
+      new = (new + (1 << 21) - 1) & ~((1 << 21) - 1)
+      fd = os.open(sl['path'], os.O_RDWR | os.O_CREAT, 0o600)
+      try:
+        os.ftruncate(fd, new)
+        sl['mm'] = mmap.mmap(fd, new)
+      finally:
+        os.close(fd)
+      sl['size'] = new
+      sl['t'] = torch.frombuffer(sl['mm'], dtype=torch.uint8)
+      if torch.cuda.is_initialized():
+        try:
+          sl['pinned'] = torch.cuda.cudart().cudaHostRegister(sl['t'].data_ptr(), new, 0) == 0
+        except Exception:  # (not available: pageable copies)
+          sl['pinned'] = False
+    return sl
+
+  def submit_batch(self, n, specs, sch, files, compression, dict_cols, stream=None):
+    """specs: (name, kind, a, b) per schema column: 'str' / 'bin' with
+    a = int64 offsets [n + 1] from 0 and b = bytes (device tensors or numpy),
+    or 'bool' / 'u16' / 'i64' with a = numpy values [n]; files: (path, lo, hi)
+    row ranges.  Returns the tasks' futures."""
+    def nbytes(x):
+      return x.numel() * x.element_size() if isinstance(x, torch.Tensor) else x.nbytes
+
+    lay, pos = [], 0
+    for name, kind, a, b in specs:
+      p0 = (pos + 63) & ~63
+      if kind in ('str', 'bin'):
+        p1 = (p0 + nbytes(a) + 63) & ~63
+        lay.append((name, kind, p0, p1))
+        pos = p1 + nbytes(b)
+      else:
+        lay.append((name, kind, p0, 0))
+        pos = p0 + nbytes(a)
+    sl = self._acquire(max(pos, 64))
+    dst = sl['t']
+    dev = False
+    for (name, kind, a, b), (_, _, p0, p1) in zip(specs, lay):
+      for x, at in ((a, p0), (b, p1)) if kind in ('str', 'bin') else ((a, p0),):
+        k = nbytes(x)
+        if k == 0:
+          continue
+        if isinstance(x, torch.Tensor):
+          dst[at:at + k].copy_(x.reshape(-1).view(torch.uint8), non_blocking=sl['pinned'])
+          dev = True
+        else:
+          dst[at:at + k].numpy()[:] = np.ascontiguousarray(x).reshape(-1).view(np.uint8)
+    if dev:
+      (stream or torch.cuda.current_stream()).synchronize()
+    from . import encode_worker
+    # tasks of about equal rows, at least one file each, ~2 per worker
+    ntask = max(1, min(len(files), 2 * self.workers))
+    bounds = np.searchsorted(np.array([f_[2] for f_ in files]), np.linspace(0, n, ntask + 1)[1:-1], side='left')
+    cuts = [0] + sorted(set(int(x) + 1 for x in bounds if 0 <= x < len(files) - 1)) + [len(files)]
+    cols = [(name, kind, p0, p1) for name, kind, p0, p1 in lay]
+    futs = [self.ex.submit(encode_worker.encode, sl['path'], sl['size'], n, cols, sch, files[a:b], compression,
+                           dict_cols) for a, b in zip(cuts[:-1], cuts[1:]) if b > a]
+    sl['futs'] = list(futs)
+    return futs
+
+  def close(self):
+    for sl in self.slots:
+      for f_ in sl['futs']:
+        try:
+          f_.result()
+        except Exception:
+          pass
+    self.ex.shutdown(wait=True)
+    for sl in self.slots:
+      self._unpin(sl)
+      sl['t'] = None
+      if sl['mm'] is not None:
+        sl['mm'].close()
+        sl['mm'] = None
+    import shutil
+    shutil.rmtree(self.dir, ignore_errors=True)
+
+
+def _host_var(arr, r0, n):
+  """rows [r0, r0 + n) of an Arrow string array as (int64 offsets from 0, bytes)"""
+  a = arr.slice(r0, n)
+  wide = a.type in (pa.large_string(), pa.large_binary())
+  off = np.frombuffer(a.buffers()[1], dtype=np.int64 if wide else np.int32, count=a.offset + n + 1)[a.offset:]
+  off = off.astype(np.int64)
+  data = np.frombuffer(a.buffers()[2], dtype=np.uint8, count=int(off[-1]))[int(off[0]):] if n else np.zeros(0, np.uint8)
+  return off - off[0], data
+
+
 LAST_STATS = {}  # the last write_shards call's stage seconds (bench.py reports them)
 
 
@@ -332,6 +477,9 @@ def write_shards(packer, res, out_dir, bin_size=None, codebert=False, masking=Fa
   st = {'setup_s': time.perf_counter() - t_start, 'render_s': 0.0, 'table_s': 0.0, 'backpressure_s': 0.0,
         'drain_s': 0.0, 'batches': 0, 'workers': workers}
   own = executor is None
+  proc = isinstance(executor, ProcessEncoder)
+  if proc:
+    st['workers'] = executor.workers
   pool = concurrent.futures.ThreadPoolExecutor(workers) if own else executor
   mine = []
   # render in batches of whole files (>= batch_rows rows, or one big file)
@@ -342,6 +490,38 @@ def write_shards(packer, res, out_dir, bin_size=None, codebert=False, masking=Fa
     r0, r1 = int(file_start[f]), int(file_start[g])
     n = r1 - r0
     t0 = time.perf_counter()
+    if proc:
+      c0, c1 = seg_columns(packer, res, r0, n, codebert, stream, host=False)
+      var = {('doc' if codebert else 'A'): c0, ('code' if codebert else 'B'): c1}
+      if masking and not codebert:
+        var['masked_lm_labels'] = render(packer, res.mlm_label, res.mlm_off, r0, n, ROW, stream=stream, host=False)
+        pos = render_npy(packer, res, r0, n, stream, host=False)
+        if pos is None:
+          moff_all, mpos_all = mlm_host()
+          m0 = int(moff_all[r0])
+          pos = npy_positions(moff_all[r0:r1 + 1] - m0, mpos_all[m0:int(moff_all[r1])])
+        var['masked_lm_positions'] = pos
+      if codebert:
+        var['id'] = _host_var(ids_col, r0, n)
+      fixed = {'is_random_next': ('bool', (flags[r0:r1] & 1).astype(bool)), 'num_tokens': ('u16', num_tokens[r0:r1]),
+               'bin_id': ('i64', bins[r0:r1])}
+      specs = [(nm, 'bin' if nm == 'masked_lm_positions' else 'str') + tuple(var[nm]) if nm in var else
+               (nm, fixed[nm][0], fixed[nm][1], None) for nm in sch.names]
+      flist = []
+      for fi in range(f, g):
+        p, b = divmod(fi, nbins)
+        name = 'part.%d.parquet' % (part_base + p)
+        if binned:
+          name += '_%d' % b
+        flist.append((os.path.join(out_dir, name), int(file_start[fi] - r0), int(file_start[fi + 1] - r0)))
+      t1 = time.perf_counter()
+      st['render_s'] += t1 - t0
+      st['batches'] += 1
+      mine.extend(executor.submit_batch(n, specs, sch, flist, compression, dict_cols, stream))
+      files.extend(f_[0] for f_ in flist)
+      st['table_s'] += time.perf_counter() - t1
+      f = g
+      continue
     c0, c1 = seg_columns(packer, res, r0, n, codebert, stream)
     if masking and not codebert:
       lab = render(packer, res.mlm_label, res.mlm_off, r0, n, ROW, stream=stream)

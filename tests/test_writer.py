@@ -2,6 +2,7 @@
 equal lddl/utils.py:98-102 serialize_np_array, schemas match
 pretrain.py:450-471 / pretrain_codebert.py:499-510."""
 import io
+import os
 
 import numpy as np
 import pyarrow as pa
@@ -48,3 +49,46 @@ def test_arrow_slices_and_large_offsets():
   off = np.array([0, 2, 2, 5, 10], dtype=np.int64)
   assert writer._arrow(pa.string(), off, data, 1, 4).to_pylist() == ['', 'cde', 'fghij']
   assert writer._arrow(pa.string(), off, data, 2, 2).to_pylist() == []
+
+
+def test_process_encoder_writes_what_pyarrow_writes(tmp_path):
+  """writer.ProcessEncoder (forked workers, the batch's columns in a shared
+  slot file) writes files with the same tables as pq.write_table of the same
+  row ranges, for every column kind, across slot reuse and growth"""
+  import pyarrow.parquet as pq
+  rng = np.random.default_rng(5)
+  enc = writer.ProcessEncoder(workers=2, slots=2)
+  try:
+    sch = writer.schema(masking=True, binned=True)
+    for batch, n in enumerate((50, 3000, 0, 700)):
+      def var(binary=False):
+        lens = rng.integers(0, 40, size=n)
+        off = np.zeros(n + 1, np.int64)
+        np.cumsum(lens, out=off[1:])
+        data = rng.integers(97, 123, size=int(off[-1])).astype(np.uint8)
+        return off, data
+      cols = {nm: var() for nm in ('A', 'B', 'masked_lm_positions', 'masked_lm_labels')}
+      fixed = {'is_random_next': ('bool', rng.random(n) < 0.5), 'num_tokens': ('u16', rng.integers(0, 600, n).astype(np.uint16)),
+               'bin_id': ('i64', rng.integers(0, 8, n).astype(np.int64))}
+      specs = [(nm, 'bin' if nm == 'masked_lm_positions' else 'str') + cols[nm] if nm in cols else
+               (nm, fixed[nm][0], fixed[nm][1], None) for nm in sch.names]
+      cuts = np.unique(np.concatenate([[0, n], rng.integers(0, n + 1, size=7)]))
+      files = [(str(tmp_path / ('b%d_f%d.parquet' % (batch, i))), int(a), int(b))
+               for i, (a, b) in enumerate(zip(cuts[:-1], cuts[1:]))]
+      futs = enc.submit_batch(n, specs, sch, files, 'snappy', ['is_random_next', 'num_tokens', 'bin_id'])
+      for f_ in futs:
+        f_.result()
+      for path, lo, hi in files:
+        got = pq.read_table(path)
+        arrs = []
+        for nm, fd in zip(sch.names, sch):
+          if nm in cols:
+            off, data = cols[nm]
+            arrs.append(writer._arrow(fd.type, off, data, lo, hi))
+          else:
+            arrs.append(writer.np_array(fixed[nm][1][lo:hi]))
+        exp = pa.Table.from_arrays(arrs, schema=sch)
+        assert got.equals(exp), (batch, path)
+  finally:
+    enc.close()
+  assert not os.path.exists(enc.dir)
