@@ -307,6 +307,11 @@ class ProcessEncoder:
     self.slots = [dict(path=os.path.join(self.dir, 'slot%d' % i), size=0, mm=None, t=None, pinned=False, futs=[])
                   for i in range(slots)]
     self.next = 0
+    # the slot files are memory: removed at exit even when close() is never
+    # reached (an exception on the caller's path)
+    import shutil
+    import weakref
+    self._fin = weakref.finalize(self, shutil.rmtree, self.dir, True)
 
   def submit(self, fn, *a, **kw):  # (a plain task, as an executor)
     return self.ex.submit(fn, *a, **kw)
@@ -403,8 +408,7 @@ class ProcessEncoder:
       if sl['mm'] is not None:
         sl['mm'].close()
         sl['mm'] = None
-    import shutil
-    shutil.rmtree(self.dir, ignore_errors=True)
+    self._fin()
 
 
 def _host_var(arr, r0, n):
