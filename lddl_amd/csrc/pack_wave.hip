@@ -388,16 +388,20 @@ struct WaveRng {
       if (idx >= MT_N) refill();
       const int lim = min(MT_N - idx, 64);
       const uint32_t w = lane < lim ? temper(L.mt[idx + lane]) : 0u;
-      const uint32_t w1 = (uint32_t)__shfl((int)w, min(lane + 1, 63)), w2 = (uint32_t)__shfl((int)w, min(lane + 2, 63));
+      // (the next two words by DPP wave shifts, not LDS permutes; lanes 62-63
+      // read 0 there, and their picks need words past the window anyway)
+      const uint32_t w1 = wave_shl1(w), w2 = wave_shl1(w1);
       const uint64_t accV = __ballot(lane < lim && (w >> (32 - kV)) < V);
-      const double x = ((double)(w >> 5) * 67108864.0 + (double)(w1 >> 6)) * (1.0 / 9007199254740992.0);
+      // random() < 0.8 on integers: random() = v * 2^-53 exactly, v = (w >> 5) * 2^26 + (w1 >> 6),
+      // and 0.8 as a double is 7205759403792794 * 2^-53
+      const bool lt08 = ((((uint64_t)(w >> 5)) << 26) | (uint64_t)(w1 >> 6)) < 7205759403792794ull;
       const uint64_t rest = lane + 4 < 64 ? accV & (~0ull << (lane + 4)) : 0ull;
       const int p = rest ? __ffsll((unsigned long long)rest) - 1 : 64;
       const uint32_t rv = (uint32_t)__shfl((int)(w >> (32 - kV)), p < 64 ? p : 63);
       bool res = false;
       int len = 0;
       uint32_t nid = 0;
-      if (lane + 1 < lim && x < 0.8) {
+      if (lane + 1 < lim && lt08) {
         res = true; len = 2; nid = mask_id;
       } else if (lane + 3 < lim && (w2 >> 31) == 0u) {
         res = true; len = 4; nid = keep_id;

@@ -15,6 +15,7 @@ enum : int {
   DPP_ROW_SHR2 = 0x112,
   DPP_ROW_SHR4 = 0x114,
   DPP_ROW_SHR8 = 0x118,
+  DPP_WAVE_SHL1 = 0x130,
   DPP_WAVE_SHR1 = 0x138,
   DPP_ROW_BCAST15 = 0x142,
   DPP_ROW_BCAST31 = 0x143,
@@ -53,6 +54,9 @@ __device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {
 // lane l receives lane l-1's value, lane 0 receives 0
 __device__ __forceinline__ uint32_t wave_shr1(uint32_t x) { return dpp0<DPP_WAVE_SHR1>(x); }
 __device__ __forceinline__ int wave_shr1(int x) { return (int)dpp0<DPP_WAVE_SHR1>((uint32_t)x); }
+
+// lane l receives lane l+1's value, lane 63 receives 0
+__device__ __forceinline__ uint32_t wave_shl1(uint32_t x) { return dpp0<DPP_WAVE_SHL1>(x); }
 
 // value of a (wave-uniform) lane
 __device__ __forceinline__ uint32_t lane_get(uint32_t x, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)x, l); }
