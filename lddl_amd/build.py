@@ -1,7 +1,9 @@
-"""Build liblddl_amd.so (gfx950) and the oracle's liboracle.so in-tree.
+"""Build liblddl_amd.so (gfx950), the host splitter libsplit.so and the
+oracle's liboracle.so in-tree.
 
-    python -m lddl_amd.build          # both
-The HIP library is the product; the oracle build is test infrastructure.
+    python -m lddl_amd.build          # all
+The HIP library and libsplit.so are the product; the oracle build is test
+infrastructure.
 """
 import glob
 import os
@@ -20,6 +22,26 @@ def _newer(target, deps):
     return True
   t = os.path.getmtime(target)
   return any(os.path.getmtime(d) > t for d in deps)
+
+
+SPLIT_LIB = os.path.join(PKG, 'libsplit.so')
+
+
+def build_split(force=False, verbose=False):
+  """lddl_amd/host/split_rules.c -> libsplit.so (plain C, gcc: the CLI's
+  split workers load it without the HIP runtime)"""
+  src = os.path.join(PKG, 'host', 'split_rules.c')
+  if not force and not _newer(SPLIT_LIB, [src]):
+    return SPLIT_LIB
+  tmp = SPLIT_LIB + '.tmp%d' % os.getpid()
+  cmd = [os.environ.get('CC', 'gcc'), '-O2', '-shared', '-fPIC', '-std=c99', '-Wall', '-o', tmp, src]
+  if verbose:
+    print(' '.join(cmd))
+  subprocess.run(cmd, check=True)
+  os.replace(tmp, SPLIT_LIB)
+  from lddl_amd import splitnative  # its code point table, cached next to the library
+  splitnative.props_table()
+  return SPLIT_LIB
 
 
 def build_hip(force=False, verbose=False, lib=None, defines=()):
@@ -78,4 +100,5 @@ def build_oracle(force=False):
 if __name__ == '__main__':
   force = '--force' in sys.argv
   print(build_hip(force, verbose=True))
+  print(build_split(force, verbose=True))
   print(build_oracle(force))

@@ -276,6 +276,19 @@ class RecordIndex:
   def texts(self, idx):
     return [self.text(int(i)) for i in idx]
 
+  def raw(self, i):
+    """record i's bytes (not decoded: the native splitter validates them)"""
+    f = int(self.fid[i])
+    mm = self._mm.get(f)
+    if mm is None:
+      with open(self.files[f], 'rb') as fh:
+        mm = self._mm[f] = mmap.mmap(fh.fileno(), 0, access=mmap.ACCESS_READ)
+    o = int(self.off[i])
+    return mm[o:o + int(self.len[i])]
+
+  def raws(self, idx):
+    return [self.raw(int(i)) for i in idx]
+
   def close(self):
     for mm in self._mm.values():
       mm.close()
