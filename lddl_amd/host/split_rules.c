@@ -273,3 +273,53 @@ int64_t lddl_split_rules(const uint8_t *buf, const int64_t *rec_off, int64_t n_r
   }
   return k.n_sent;
 }
+
+/* The line spans of buf[0, n) as readers._line_spans makes them (terminators
+ * excluded; universal newlines: CR LF, lone CR and lone LF each end a line;
+ * crlf_only: CR LF alone; no final line after a last terminator).  Returns
+ * the number of lines; starts / ends are written when it is <= cap (a first
+ * call with cap 0 counts them). */
+int64_t lddl_line_spans(const uint8_t *buf, int64_t n, int32_t crlf_only, int64_t *starts, int64_t *ends,
+                        int64_t cap) {
+  int64_t m = 0, a = 0;
+  const int cr = !crlf_only && n > 0 && memchr(buf, '\r', (size_t)n) != NULL;
+#define LINE(s_, e_)              \
+  do {                            \
+    if (m < cap) {                \
+      starts[m] = (s_);           \
+      ends[m] = (e_);             \
+    }                             \
+    ++m;                          \
+  } while (0)
+  if (!cr) {  /* LF only (universal, no CR in the text) or CR LF pairs */
+    int64_t p = 0;
+    while (p < n) {
+      const uint8_t *f = memchr(buf + p, '\n', (size_t)(n - p));
+      if (!f) break;
+      const int64_t t = f - buf;
+      p = t + 1;
+      if (crlf_only) {
+        if (t == 0 || buf[t - 1] != '\r') continue;
+        LINE(a, t - 1);
+      } else {
+        LINE(a, t);
+      }
+      a = t + 1;
+    }
+  } else {
+    for (int64_t t = 0; t < n; ++t) {
+      const uint8_t b = buf[t];
+      if (b == '\n') {
+        LINE(a, t);
+        a = t + 1;
+      } else if (b == '\r') {
+        LINE(a, t);
+        if (t + 1 < n && buf[t + 1] == '\n') ++t;
+        a = t + 1;
+      }
+    }
+  }
+  if (a < n) LINE(a, n);
+#undef LINE
+  return m;
+}

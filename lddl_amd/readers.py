@@ -207,6 +207,13 @@ class RecordIndex:
     if size == 0:
       return np.zeros(0, np.int64), np.zeros(0, np.int64)
     buf = np.memmap(path, dtype=np.uint8, mode='r')
+    # the whole file in one C pass when the host library is there (the same
+    # spans; LDDL_SPLIT_NATIVE=0 keeps the numpy windows below)
+    if os.environ.get('LDDL_SPLIT_NATIVE', '1') != '0':
+      from . import splitnative
+      got = splitnative.line_spans(buf, linedelimiter == '\r\n')
+      if got is not None:
+        return _strip_spans(buf, *got)
     # windows of ~INDEX_WINDOW bytes, each cut right after a line feed (a
     # window starts a line; a \r\n pair never splits), so the per-byte masks
     # and indices live for one window at a time, not the whole file

@@ -62,6 +62,9 @@ def _lib():
     f.restype = ctypes.c_int64
     f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
                   ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64)]
+    g = L.lddl_line_spans
+    g.restype = ctypes.c_int64
+    g.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
     _STATE['lib'] = L
   return L
 
@@ -109,3 +112,19 @@ def split_raw(raws):
   idl = ids.tolist()
   doc_ids = [joined[idl[2 * r]:idl[2 * r + 1]].decode('utf-8') for r in range(n)]
   return corpus, doc_ids
+
+
+def line_spans(buf, crlf_only):
+  """readers._line_spans in one C pass (memchr): (starts, ends) int64, or
+  None without the library"""
+  L = _lib()
+  if L is None:
+    return None
+  n = len(buf)
+  if n == 0:
+    return np.zeros(0, np.int64), np.zeros(0, np.int64)
+  p = ctypes.c_void_p(buf.ctypes.data)
+  m = L.lddl_line_spans(p, n, 1 if crlf_only else 0, None, None, 0)
+  s, e = np.empty(max(m, 1), np.int64), np.empty(max(m, 1), np.int64)
+  L.lddl_line_spans(p, n, 1 if crlf_only else 0, _p(s), _p(e), m)
+  return s[:m], e[:m]

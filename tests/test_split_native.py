@@ -93,3 +93,19 @@ def test_random_code_points():
            (int(rng.integers(65, 123)) if rng.random() < 0.6 else pool[int(rng.integers(0, len(pool)))]) for _ in range(n)]
     recs.append(''.join(map(chr, cps)))
   _check(recs)
+
+
+@pytest.mark.parametrize('crlf', [False, True])
+def test_line_spans_match_numpy(crlf):
+  """the C line scan (the record index's lines) against readers._line_spans
+  on buffers dense in CR / LF / CR LF, with and without a final terminator"""
+  from lddl_amd import readers
+  rng = np.random.default_rng(int(crlf))
+  for trial in range(300):
+    n = int(rng.integers(0, 400))
+    alphabet = np.array([10, 13, 65, 66, 32, 0xC2, 0xA0], dtype=np.uint8)
+    p = np.array([0.15, 0.1, 0.4, 0.2, 0.1, 0.03, 0.02]) if trial % 3 else np.array([0.1, 0, 0.5, 0.3, 0.1, 0, 0])
+    buf = rng.choice(alphabet, size=n, p=p / p.sum()).astype(np.uint8)
+    got = splitnative.line_spans(buf, crlf)
+    exp = readers._line_spans(buf, crlf)
+    assert np.array_equal(got[0], exp[0]) and np.array_equal(got[1], exp[1]), (trial, bytes(buf))
