@@ -301,7 +301,11 @@ class ProcessEncoder:
     self.workers = workers or encode_workers()
     self.ex = concurrent.futures.ProcessPoolExecutor(self.workers, mp_context=mp.get_context(context))
     list(self.ex.map(_warm, range(self.workers)))  # start the workers now, not in the first batch
-    d = '/dev/shm' if os.path.isdir('/dev/shm') and os.access('/dev/shm', os.W_OK) else None
+    d = None
+    if os.path.isdir('/dev/shm') and os.access('/dev/shm', os.W_OK):
+      st = os.statvfs('/dev/shm')
+      if st.f_bavail * st.f_frsize >= (1 << 30) * slots:  # (a small /dev/shm would fault on the slot writes)
+        d = '/dev/shm'
     import tempfile
     self.dir = tempfile.mkdtemp(prefix='lddl_enc_', dir=d)
     self.slots = [dict(path=os.path.join(self.dir, 'slot%d' % i), size=0, mm=None, t=None, pinned=False, futs=[])
