@@ -217,7 +217,12 @@ static int load_table(lddl_ctx* c, const char* path) {
 static int load_vocab(lddl_ctx* c, const char* path) {
   VocabTables V;
   std::string err;
-  int rc = build_vocab_tables(path, V, err);
+  // the trie only for the options that read it (its build is the bulk of
+  // the table setup)
+  const char* algo = getenv("LDDL_TOKENIZE_ALGO");
+  const char* wp = getenv("LDDL_WP_ALGO");
+  const bool want_trie = (algo && algo[0] == '6') || (wp && strcmp(wp, "trie") == 0);
+  int rc = build_vocab_tables(path, V, err, want_trie);
   if (rc) return set_err(rc, "%s", err.c_str());
   c->vocab_size = (int)V.vocab.size();
   for (int k = 0; k < 5; ++k) c->special[k] = V.special[k];

@@ -79,22 +79,40 @@ inline bool build_trie(const std::vector<std::string>& vocab, std::vector<uint2>
     }
     nodes[n].id = (int32_t)i;
   }
-  // place breadth-first: slot[node], base[node]; first fit over a used map
+  // place breadth-first: slot[node], base[node]; first fit over a used map,
+  // the candidates for a node's first child walked over free slots only
+  // (nxt: the next free slot at or after p, path-halved)
+  const uint32_t CAPS = 1u << 20;
   std::vector<uint32_t> slot(nodes.size(), 0), base(nodes.size(), 0);
-  std::vector<uint8_t> used(1u << 20, 0);
-  used[0] = used[1] = 1;
+  std::vector<uint8_t> used(CAPS + 256, 0);
+  std::vector<uint32_t> nxt(CAPS + 257);
+  for (uint32_t p = 0; p < nxt.size(); ++p) nxt[p] = p;
+  auto find = [&](uint32_t p) {
+    while (nxt[p] != p) {
+      nxt[p] = nxt[nxt[p]];
+      p = nxt[p];
+    }
+    return p;
+  };
+  auto take = [&](uint32_t p) {
+    used[p] = 1;
+    nxt[p] = p + 1;
+  };
+  take(0);
+  take(1);
   slot[0] = 0;
   slot[1] = 1;
   std::vector<uint32_t> order = {0, 1};
-  uint32_t first_free = 2, top = 2;
+  uint32_t top = 2;
   for (size_t qi = 0; qi < order.size(); ++qi) {
     Node& nd = nodes[order[qi]];
     if (nd.kids.empty()) continue;
     std::sort(nd.kids.begin(), nd.kids.end());
     const uint32_t c0 = nd.kids[0].first;
-    uint32_t b = first_free > c0 ? first_free - c0 : 0;
-    for (;; ++b) {
-      if (b + 256 >= used.size()) return false;
+    uint32_t b = 0;
+    for (uint32_t p = find(c0);; p = find(p + 1)) {  // p: a free slot for the first child
+      b = p - c0;
+      if (b + 256 >= CAPS) return false;
       bool fit = true;
       for (auto& kc : nd.kids)
         if (used[b + kc.first]) { fit = false; break; }
@@ -102,12 +120,11 @@ inline bool build_trie(const std::vector<std::string>& vocab, std::vector<uint2>
     }
     base[order[qi]] = b;
     for (auto& kc : nd.kids) {
-      used[b + kc.first] = 1;
+      take(b + kc.first);
       slot[kc.second] = b + kc.first;
       order.push_back(kc.second);
       if (b + kc.first + 1 > top) top = b + kc.first + 1;
     }
-    while (used[first_free]) ++first_free;
   }
   uint32_t maxb = 0;
   for (uint32_t b : base) maxb = b > maxb ? b : maxb;
@@ -228,7 +245,9 @@ inline int build_uni_tables(const char* path, UniTables& T, std::string& err) {
   return 0;
 }
 
-inline int build_vocab_tables(const char* path, VocabTables& V, std::string& err) {
+// with_trie: also the double-array trie (the lane tokenizer and the trie
+// WordPiece read it; the default tok5 path does not)
+inline int build_vocab_tables(const char* path, VocabTables& V, std::string& err, bool with_trie = true) {
   FILE* f = fopen(path, "rb");
   if (!f) { err = std::string("cannot open vocab ") + path; return LDDL_EIO; }
   std::string cur;
@@ -365,7 +384,7 @@ inline int build_vocab_tables(const char* path, VocabTables& V, std::string& err
     V.rpool.resize((V.rpool.size() + 3) & ~(size_t)3, 0);
   }
   V.rpool.resize(V.rpool.size() + 16, 0);
-  if (!build_trie(V.vocab, V.trie, V.trie_base)) V.trie.clear();  // (the lane tokenizer then stays off)
+  if (with_trie && !build_trie(V.vocab, V.trie, V.trie_base)) V.trie.clear();  // (the lane tokenizer then stays off)
   return 0;
 }
 
