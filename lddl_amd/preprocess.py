@@ -374,6 +374,15 @@ def split_chunk(index, idx, codebert, split):
   return split_records(index.texts(idx), codebert, split)
 
 
+def _nice_worker():
+  n = int(os.environ.get('LDDL_WORKER_NICE', '5'))
+  if n > 0:
+    try:
+      os.nice(n)
+    except OSError:
+      pass
+
+
 def _split_worker(a, b):
   ts = time.perf_counter()
   corpus, ids = split_chunk(_FE['index'], _FE['order'][a:b], _FE['codebert'], _FE['split'])
@@ -542,7 +551,9 @@ def main(args, codebert=False):
     import multiprocessing
     _FE.update(index=index, order=order, codebert=codebert, split=split)
     t0 = time.perf_counter()
-    pool = multiprocessing.get_context('fork').Pool(nw)
+    # (niced: the CPU share is shared with this process, whose thread drives
+    # the GPU and the writer; LDDL_WORKER_NICE=0 keeps the default priority)
+    pool = multiprocessing.get_context('fork').Pool(nw, initializer=_nice_worker)
     t['pool_start_s'] = time.perf_counter() - t0
     _FE.clear()
 

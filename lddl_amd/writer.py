@@ -278,8 +278,17 @@ def file_table(sch, cols, raw, lo, hi, batch=None):
   return pa.Table.from_arrays(arrs, schema=sch)
 
 
-def _warm(_):
+def _worker_init():
   from . import encode_worker  # noqa: F401  (imported before the first batch)
+  n = int(os.environ.get('LDDL_WORKER_NICE', '5'))  # (niced as the CLI's split workers)
+  if n > 0:
+    try:
+      os.nice(n)
+    except OSError:
+      pass
+
+
+def _warm(_):
   return os.getpid()
 
 
@@ -299,7 +308,8 @@ class ProcessEncoder:
   def __init__(self, workers=None, slots=3, context='fork'):
     import multiprocessing as mp
     self.workers = workers or encode_workers()
-    self.ex = concurrent.futures.ProcessPoolExecutor(self.workers, mp_context=mp.get_context(context))
+    self.ex = concurrent.futures.ProcessPoolExecutor(self.workers, mp_context=mp.get_context(context),
+                                                     initializer=_worker_init)
     list(self.ex.map(_warm, range(self.workers)))  # start the workers now, not in the first batch
     d = None
     if os.path.isdir('/dev/shm') and os.access('/dev/shm', os.W_OK):
