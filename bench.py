@@ -19,6 +19,7 @@ Prints ONE JSON line on rank 0.
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -421,13 +422,14 @@ def frontend_leg(mb, chunk_mb=32.0, seq=128, bin_size=None, unique_mb=256):
   raw input (one ``wiki-<id> <text>`` document per line): BASELINE.json
   configs[0] (seq 128, no static masking, unbinned parquet) by default,
   configs[1] with seq=512, bin_size=64.  Past unique_mb the documents repeat
-  (each line keeps its own id).  Runs first in the process (its split
-  workers fork before anything touches the GPU); wall, host read / sentence
-  split / GPU / parquet write seconds and the split time hidden behind the
-  GPU and the writer, as preprocess.main reports them."""
+  (each line keeps its own id).  Runs in a child process of its own, as the
+  command line does, started before this process touches the GPU; wall,
+  host read / sentence split / GPU / parquet write seconds and the split
+  time hidden behind the GPU and the writer, as preprocess.main reports
+  them (main() itself: interpreter start-up and imports excluded)."""
   import shutil
   import tempfile
-  from lddl_amd import preprocess, synth
+  from lddl_amd import synth
   d = tempfile.mkdtemp(prefix='lddl_bench_fe_')
   try:
     t0 = time.perf_counter()
@@ -448,11 +450,23 @@ def frontend_leg(mb, chunk_mb=32.0, seq=128, bin_size=None, unique_mb=256):
             '--split-workers', str(host_cpus()['share'])]
     if bin_size:
       argv += ['--bin-size', str(bin_size)]
-    a = preprocess.attach_args().parse_args(argv)
-    t0 = time.perf_counter()
-    files, t = preprocess.main(a)
-    el = time.perf_counter() - t0
-    t.pop('partitions', None)
+    # a child process per CLI run, as the command line runs it: its GPU
+    # context, split pool and encoders start and end with it (run in this
+    # process, the second leg paid the first leg's context teardown); the
+    # module imports (torch, ~1.5 s cold) are timed on their own: imports_s
+    code = ('import json, sys, time; t0 = time.perf_counter(); import torch; '
+            'from lddl_amd import preprocess, pipeline, writer, balance; imp = time.perf_counter() - t0; '
+            'a = preprocess.attach_args().parse_args(json.loads(sys.argv[1])); '
+            't0 = time.perf_counter(); files, t = preprocess.main(a); el = time.perf_counter() - t0; '
+            't.pop("partitions", None); t["files"] = len(files); t["el"] = el; t["imports_s"] = imp; '
+            'print("LDDL_LEG " + json.dumps({k: v for k, v in t.items() if isinstance(v, (int, float, str))}))')
+    p = subprocess.run([sys.executable, '-c', code, json.dumps(argv)], stdout=subprocess.PIPE,
+                       cwd=os.path.dirname(os.path.abspath(__file__)), timeout=900)
+    rows = [ln for ln in p.stdout.decode().splitlines() if ln.startswith('LDDL_LEG ')]
+    if p.returncode != 0 or not rows:
+      raise RuntimeError('preprocess CLI leg failed (exit %d)' % p.returncode)
+    t = json.loads(rows[-1][len('LDDL_LEG '):])
+    files, el = [None] * t.pop('files'), t.pop('el')
     out = {'what': 'preprocess CLI end to end, BERT seq %d %s (BASELINE configs[%d])' % (
                seq, 'bin %d' % bin_size if bin_size else 'unbinned', 1 if bin_size else 0),
            'raw_mb': raw / 1e6, 'documents': i, 'unique_mb': min(mb, unique_mb),
