@@ -47,6 +47,12 @@ namespace tok5 {
 // (a 1.5 KiB window for 6 waves/SIMD measured slower: 0.2 % of the tiles fall
 // back to the serial path, finish 0.97 -> 3.2 ms per GiB, and the 80-VGPR
 // scan spills: 3.80 vs 3.49)
+// LDDL_PROBE_REC (measurement builds only, results not exact): 1 stores
+// only a record's first 16 B, 2 no record bytes (the scan-side bound of
+// smaller WordPiece records)
+#ifndef LDDL_PROBE_REC
+#define LDDL_PROBE_REC 0
+#endif
 constexpr int CAP = 2048;                // window bytes (32 per lane)
 constexpr int DCAP = 256;                // side buffer for dirty words
 constexpr int SCAN_OCC = 5;              // waves per SIMD the scan's LDS admits (4 measured 5 % slower)
@@ -981,10 +987,10 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
 #pragma unroll
               for (int i = 0; i < 6; ++i) kd[i] = __builtin_amdgcn_alignbyte(xx[i + 1], xx[i], sh);
             }
-            *recq(S, 0, slot) = make_uint4((uint32_t)len | (nsl << 8) | 0x80000000u, 0u, kd[0], kd[1]);
-            *recq(S, 1, slot) = make_uint4(kd[2], kd[3], kd[4], kd[5]);
+            if (LDDL_PROBE_REC < 2) *recq(S, 0, slot) = make_uint4((uint32_t)len | (nsl << 8) | 0x80000000u, 0u, kd[0], kd[1]);
+            if (LDDL_PROBE_REC < 1) *recq(S, 1, slot) = make_uint4(kd[2], kd[3], kd[4], kd[5]);
             // key bytes 24..55 (wp_kernel reads them only for a longer key)
-            if (len > 24) {
+            if (LDDL_PROBE_REC < 1 && len > 24) {
               uint32_t xx[9];
 #pragma unroll
               for (int i = 0; i < 9; ++i) xx[i] = L.nb[a + 6 + i];
