@@ -362,6 +362,9 @@ __global__ __launch_bounds__(256) void materialize2_kernel(MatParams M, int64_t 
   mat_copy(W, G0, G1, M.dense, n_src, M.out_tokens, M.cls_id, M.sep_id, lane);
 }
 
+#ifndef LDDL_ROWSPAN_XCD
+#define LDDL_ROWSPAN_XCD 1
+#endif
 // Row spans (lddl_row_spans): the rows of materialize2 without the token
 // copy.  Each segment of a row is ONE contiguous run of the tokenizer's dense
 // ids (a document's sentences are contiguous there and a segment is a window
@@ -392,9 +395,11 @@ hipError_t launch_chunk_parts(const int64_t* pair_base, const int64_t* doc_sent_
   return hipGetLastError();
 }
 
+// (XCD-aware blocks, as materialize2: a partition's rows run on one XCD, so
+// its pair records and binned order are fetched into one L2, not all eight)
 __global__ __launch_bounds__(256) void rowspan_kernel(MatParams M, int64_t total) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int64_t gbase = ((int64_t)blockIdx.x * 4 + wv) * 64;
+  const int64_t gbase = (LDDL_ROWSPAN_XCD ? xcd_block(blockIdx.x, gridDim.x) * 4 + wv : (int64_t)blockIdx.x * 4 + wv) * 64;
   if (gbase >= total) return;
   const int64_t g = gbase + lane;
   if (g >= total) return;
@@ -420,7 +425,8 @@ __global__ __launch_bounds__(256) void rowspan_kernel(MatParams M, int64_t total
 }
 
 hipError_t launch_row_spans(const MatParams& M, int64_t total_pairs, hipStream_t s) {
-  const int64_t nblk = (total_pairs + 255) / 256;
+  int64_t nblk = (total_pairs + 255) / 256;
+  if (LDDL_ROWSPAN_XCD && nblk >= 64) nblk = (nblk + 7) & ~(int64_t)7;  // xcd_block: 8 equal ranges (extra blocks exit)
   hipLaunchKernelGGL(rowspan_kernel, dim3((unsigned)nblk), dim3(256), 0, s, M, total_pairs);
   return hipGetLastError();
 }

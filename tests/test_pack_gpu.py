@@ -400,15 +400,16 @@ def test_masked_special_flags_from_tokenizer(gpu):
   assert len(a) == len(b) and a == b
 
 
-@pytest.mark.parametrize('codebert', [False, True])
-def test_row_spans_equal_materialized_rows(gpu, codebert):
+@pytest.mark.parametrize('codebert,nbytes', [(False, 500_000), (True, 0), (False, 6_000_000)])
+def test_row_spans_equal_materialized_rows(gpu, codebert, nbytes):
   """lddl_row_spans describes exactly lddl_materialize's rows: the same
   row offsets, lengths, flags, bins, partitions and bin counts, and the
-  tokens the spans select from the dense ids equal the materialised rows"""
+  tokens the spans select from the dense ids equal the materialised rows
+  (6 MB: > 64 row-span blocks, so their XCD-aware order is in play)"""
   from lddl_amd import synth, pipeline
-  c = synth.make_code(300, seed=8) if codebert else synth.make_wiki(500_000, seed=8)
+  c = synth.make_code(300, seed=8) if codebert else synth.make_wiki(nbytes, seed=8)
   vocab = pipeline.VOCAB_CODEBERT if codebert else pipeline.VOCAB_BERT
-  pdo = pipeline.partition_by_bytes(c, 4)
+  pdo = pipeline.partition_by_bytes(c, 4 if nbytes <= 500_000 else 23)
   pk = pipeline.Packer(vocab, 0)
   sh = pipeline.upload(c, pdo, gpu)
   ids, ntok, toff = pk.tokenize(sh)
@@ -420,6 +421,8 @@ def test_row_spans_equal_materialized_rows(gpu, codebert):
   mbc = m.bin_count.cpu().numpy().copy()
   s = pk.pack(sh, ids, ntok, toff, spans=True, **kw)
   assert s.spans and s.tokens is None and s.n_pairs == m.n_pairs and s.n_pairs > 0
+  if nbytes > 500_000:
+    assert (s.n_pairs + 255) // 256 >= 64 and ((s.n_pairs + 255) // 256) % 8, s.n_pairs  # (rounded-up grid)
   for k, v in mcopy.items():
     assert np.array_equal(getattr(s, k)[:s.n_pairs + (1 if k == 'tok_off' else 0)].cpu().numpy(), v), k
   assert np.array_equal(s.bin_count.cpu().numpy(), mbc)
