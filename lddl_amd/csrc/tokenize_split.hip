@@ -53,6 +53,13 @@ namespace tok5 {
 #ifndef LDDL_PROBE_REC
 #define LDDL_PROBE_REC 0
 #endif
+// LDDL_PROBE_L2 (measurement builds only, results not exact): the whole-word
+// probe reads 1 MB of the table (L2-resident); 2: and takes every probed word
+// as found (no records from probe misses); 3: the whole table, every probed
+// word taken as found
+#ifndef LDDL_PROBE_L2
+#define LDDL_PROBE_L2 0
+#endif
 constexpr int CAP = 2048;                // window bytes (32 per lane)
 constexpr int DCAP = 256;                // side buffer for dirty words
 constexpr int SCAN_OCC = 5;              // waves per SIMD the scan's LDS admits (4 measured 5 % slower)
@@ -914,9 +921,10 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
           }
           STAMP(6);
           if (w != 0 && len <= 24 && len <= mb0) {
-            const uint4* bk = P.vt + 4 * (key_hash(key, len, 0u) & vmask);
+            const uint4* bk =
+                P.vt + 4 * (key_hash(key, len, 0u) & vmask & ((LDDL_PROBE_L2 == 1 || LDDL_PROBE_L2 == 2) ? 0x3FFFu : ~0u));
             const uint4 fa = bk[0], fb = bk[1];
-            if (slot_eq(fa, fb, key, ((uint32_t)len << 16) | 0x80000000u)) {
+            if (LDDL_PROBE_L2 >= 2 || slot_eq(fa, fb, key, ((uint32_t)len << 16) | 0x80000000u)) {
               id = (uint16_t)(fb.z & 0xFFFFu);
               w = 0;
             }
