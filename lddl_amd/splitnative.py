@@ -102,8 +102,8 @@ def split_raw(raws):
     soff = np.zeros(cap + 1, dtype=np.int64)
     ns = L.lddl_split_rules(_p(buf), _p(rec_off), n, _p(tab), _p(out), out.size, _p(soff), cap, _p(doc), _p(ids),
                             ctypes.byref(bad))
-    if ns == -3:
-      cap *= 4
+    if ns == -3 and cap <= total:  # (non-empty sentences: at most one per byte)
+      cap = min(cap * 4, total + 1)
       continue
     if ns < 0:
       return None

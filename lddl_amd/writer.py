@@ -58,8 +58,10 @@ def _host(t, stream=None):
   of it -- the Arrow buffers of the files still encoding -- is gone);
   synchronises the stream"""
   h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
-  h.copy_(t, non_blocking=True)
-  (stream or torch.cuda.current_stream()).synchronize()
+  s = stream or torch.cuda.current_stream()
+  with torch.cuda.stream(s):  # (the copy on the stream the render ran on)
+    h.copy_(t, non_blocking=True)
+  s.synchronize()
   return h.numpy()
 
 
@@ -385,18 +387,21 @@ class ProcessEncoder:
     sl = self._acquire(max(pos, 64))
     dst = sl['t']
     dev = False
+    st = None
     for (name, kind, a, b), (_, _, p0, p1) in zip(specs, lay):
       for x, at in ((a, p0), (b, p1)) if kind in ('str', 'bin') else ((a, p0),):
         k = nbytes(x)
         if k == 0:
           continue
         if isinstance(x, torch.Tensor):
-          dst[at:at + k].copy_(x.reshape(-1).view(torch.uint8), non_blocking=sl['pinned'])
+          st = st or stream or torch.cuda.current_stream()
+          with torch.cuda.stream(st):  # (the copies on the stream the columns were rendered on)
+            dst[at:at + k].copy_(x.reshape(-1).view(torch.uint8), non_blocking=sl['pinned'])
           dev = True
         else:
           dst[at:at + k].numpy()[:] = np.ascontiguousarray(x).reshape(-1).view(np.uint8)
     if dev:
-      (stream or torch.cuda.current_stream()).synchronize()
+      st.synchronize()
     from . import encode_worker
     # tasks of about equal rows, at least one file each, ~2 per worker
     ntask = max(1, min(len(files), 2 * self.workers))

@@ -101,10 +101,12 @@ def test_codebert_parquet_golden(cpacker, tmp_path, k, spans):
   assert got['num_tokens'] == [e['num_tokens'] for e in exp]
 
 
-@pytest.mark.parametrize('spans', [False, True])
-def test_end_to_end_parquet_vs_oracle(gpu, tmp_path, spans):
+@pytest.mark.parametrize('spans,side', [(False, False), (True, False), (True, True)])
+def test_end_to_end_parquet_vs_oracle(gpu, tmp_path, spans, side):
   """synthetic corpus, several partitions (some empty), binned seq 128:
-  every file's rows equal the oracle's rendering of its pairs"""
+  every file's rows equal the oracle's rendering of its pairs (side: the
+  writer renders and copies on a stream that is not the current one)"""
+  import torch
   from lddl_amd import synth, pipeline, writer
   from oracle.oracle import OracleTokenizer
   c = synth.make_wiki(400_000, seed=77)
@@ -113,7 +115,11 @@ def test_end_to_end_parquet_vs_oracle(gpu, tmp_path, spans):
   pk = pipeline.Packer(pipeline.VOCAB_BERT, 0)
   sh = pipeline.upload(c, pdo, gpu)
   res = pk.run(sh, target_seq_length=128, bin_size=32, seed=99, spans=spans)
-  files = writer.write_shards(pk, res, str(tmp_path), bin_size=32, batch_rows=500)
+  st = None
+  if side:
+    st = torch.cuda.Stream(device=gpu)
+    st.wait_stream(torch.cuda.current_stream())
+  files = writer.write_shards(pk, res, str(tmp_path), bin_size=32, batch_rows=500, stream=st)
   assert len(files) == (len(pdo) - 1) * 4
   oids, ontok = OracleTokenizer(pipeline.VOCAB_BERT).run(c.data, c.sent_off, 512, nthreads=8)
   exp = po.run_bert_shards(c, oids, ontok, pdo, 128, 0.1, 5, 99, 32)
