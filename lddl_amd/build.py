@@ -44,7 +44,7 @@ def build_split(force=False, verbose=False):
   return SPLIT_LIB
 
 
-def build_hip(force=False, verbose=False, lib=None, defines=()):
+def build_hip(force=False, verbose=False, lib=None, defines=(), extra=()):
   """Each .hip compiled to its own object in parallel (device code is per
   translation unit: the kernels share headers only), then linked.
   lib / defines: A/B builds of variants (tools/ab_build.py).
@@ -64,7 +64,8 @@ def build_hip(force=False, verbose=False, lib=None, defines=()):
   odir = os.path.join(CSRC, 'build') if lib == LIB else os.path.splitext(lib)[0] + '_obj'
   os.makedirs(odir, exist_ok=True)
   hipcc = os.environ.get('LDDL_HIPCC', 'hipcc')
-  flags = ['--offload-arch=%s' % ARCH, '-O3', '-std=c++17', '-fPIC', '-Wno-unused-result'] + ['-D' + d for d in defines]
+  flags = ['--offload-arch=%s' % ARCH, '-O3', '-std=c++17', '-fPIC', '-Wno-unused-result'] + ['-D' + d for d in defines] + \
+      list(extra)
   tag = '.tmp%d' % os.getpid()
   with open(os.path.join(odir, '.build.lock'), 'w') as lk:
     fcntl.flock(lk, fcntl.LOCK_EX)  # (released when the file closes)
