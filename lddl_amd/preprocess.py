@@ -583,19 +583,29 @@ def main(args, codebert=False):
     got = [f_.get() for f_ in fs]
     return [g[0] for g in got], concat_ids([g[1] for g in got]), sum(g[2] for g in got)
 
+  # the parquet encodes: a pool of processes forked here, before the GPU is
+  # touched and before the split workers get busy (16 forks beside 16 busy
+  # split workers took 0.17-0.29 s of the CPU share; writer.ProcessEncoder;
+  # LDDL_ENCODE_PROCS=0: a thread pool)
+  import concurrent.futures
+  enc = None
+  t0 = time.perf_counter()
+  try:
+    if args.output_format != 'txt':
+      if os.environ.get('LDDL_ENCODE_PROCS', '1') != '0':
+        enc = writer.ProcessEncoder()
+      else:
+        enc = concurrent.futures.ThreadPoolExecutor(writer.encode_workers())
+  except BaseException:
+    if pool is not None:
+      pool.terminate()
+      pool.join()
+    raise
+  t['enc_start_s'] = time.perf_counter() - t0
   # the first chunks split while this process brings up the GPU context and
   # the device tables
   ahead = 2  # chunks split ahead of the GPU
   futs = {c: submit(c) for c in todo[:ahead]} if pool is not None else {}
-  # the parquet encodes: a pool of processes forked here, before the GPU is
-  # touched (writer.ProcessEncoder; LDDL_ENCODE_PROCS=0: a thread pool)
-  import concurrent.futures
-  enc = None
-  if args.output_format != 'txt':
-    if os.environ.get('LDDL_ENCODE_PROCS', '1') != '0':
-      enc = writer.ProcessEncoder()
-    else:
-      enc = concurrent.futures.ThreadPoolExecutor(writer.encode_workers())
   t0 = time.perf_counter()
   device = torch.device('cuda', local)
   try:
