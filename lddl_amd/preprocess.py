@@ -677,6 +677,8 @@ def main(args, codebert=False):
         wrote = writer.write_txt(pk, res, sink, **kw)
       else:
         wrote = writer.write_shards(pk, res, sink, executor=enc, pending=cf, **kw)
+        for k_ in ('setup_s', 'render_s', 'table_s'):  # (the writer's stages: table_s = slot copies + hand-off)
+          t['writer_' + k_] = t.get('writer_' + k_, 0.0) + writer.LAST_STATS.get(k_, 0.0)
       out += wrote
       inflight.append((a, b, wrote, cf, counts[a - lo:b - lo].tolist(), res.n_pairs))
       settle(2)  # at most two chunks' encodes behind the GPU
@@ -685,6 +687,8 @@ def main(args, codebert=False):
     t0 = time.perf_counter()
     settle(0)
     t['drain_s'] = time.perf_counter() - t0  # the last chunks' encodes
+    if isinstance(enc, writer.ProcessEncoder):
+      t['enc_slot_wait_s'], t['enc_copy_s'] = enc.wait_s, enc.copy_s
   finally:
     t0 = time.perf_counter()
     if pool is not None:

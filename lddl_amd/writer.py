@@ -323,6 +323,8 @@ class ProcessEncoder:
     self.slots = [dict(path=os.path.join(self.dir, 'slot%d' % i), size=0, mm=None, t=None, pinned=False, futs=[])
                   for i in range(slots)]
     self.next = 0
+    self.wait_s = 0.0  # waiting for a slot's previous batch to finish encoding
+    self.copy_s = 0.0  # columns into the slots (device copies included)
     # the slot files are memory: removed at exit even when close() is never
     # reached (an exception on the caller's path)
     import shutil
@@ -340,8 +342,10 @@ class ProcessEncoder:
   def _acquire(self, size):
     sl = self.slots[self.next]
     self.next = (self.next + 1) % len(self.slots)
+    t0 = time.perf_counter()
     for f_ in sl['futs']:
       f_.result()
+    self.wait_s += time.perf_counter() - t0
     sl['futs'] = []
     if sl['size'] < size:
       import mmap
@@ -385,6 +389,7 @@ class ProcessEncoder:
         lay.append((name, kind, p0, 0))
         pos = p0 + nbytes(a)
     sl = self._acquire(max(pos, 64))
+    t0 = time.perf_counter()
     dst = sl['t']
     dev = False
     st = None
@@ -402,6 +407,7 @@ class ProcessEncoder:
           dst[at:at + k].numpy()[:] = np.ascontiguousarray(x).reshape(-1).view(np.uint8)
     if dev:
       st.synchronize()
+    self.copy_s += time.perf_counter() - t0
     from . import encode_worker
     # tasks of about equal rows, at least one file each, ~2 per worker
     ntask = max(1, min(len(files), 2 * self.workers))
