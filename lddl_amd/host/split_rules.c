@@ -281,8 +281,7 @@ int64_t lddl_split_rules(const uint8_t *buf, const int64_t *rec_off, int64_t n_r
  * call with cap 0 counts them). */
 int64_t lddl_line_spans(const uint8_t *buf, int64_t n, int32_t crlf_only, int64_t *starts, int64_t *ends,
                         int64_t cap) {
-  int64_t m = 0, a = 0;
-  const int cr = !crlf_only && n > 0 && memchr(buf, '\r', (size_t)n) != NULL;
+  int64_t m = 0, a = 0, p = 0;
 #define LINE(s_, e_)              \
   do {                            \
     if (m < cap) {                \
@@ -291,33 +290,36 @@ int64_t lddl_line_spans(const uint8_t *buf, int64_t n, int32_t crlf_only, int64_
     }                             \
     ++m;                          \
   } while (0)
-  if (!cr) {  /* LF only (universal, no CR in the text) or CR LF pairs */
-    int64_t p = 0;
-    while (p < n) {
-      const uint8_t *f = memchr(buf + p, '\n', (size_t)(n - p));
+  /* one streaming pass: memchr to the next LF; in universal mode the bytes
+   * before it (still in cache) are checked for CR (a lone CR ends a line;
+   * CR LF ends one line) */
+  while (p < n) {
+    const uint8_t *f = memchr(buf + p, '\n', (size_t)(n - p));
+    const int64_t t = f ? (int64_t)(f - buf) : n;
+    if (crlf_only) {
       if (!f) break;
-      const int64_t t = f - buf;
       p = t + 1;
-      if (crlf_only) {
-        if (t == 0 || buf[t - 1] != '\r') continue;
-        LINE(a, t - 1);
-      } else {
-        LINE(a, t);
-      }
+      if (t == 0 || buf[t - 1] != '\r') continue;
+      LINE(a, t - 1);
       a = t + 1;
+      continue;
     }
-  } else {
-    for (int64_t t = 0; t < n; ++t) {
-      const uint8_t b = buf[t];
-      if (b == '\n') {
-        LINE(a, t);
-        a = t + 1;
-      } else if (b == '\r') {
-        LINE(a, t);
-        if (t + 1 < n && buf[t + 1] == '\n') ++t;
-        a = t + 1;
+    int crlf = 0;
+    const uint8_t *r = memchr(buf + p, '\r', (size_t)(t - p));
+    while (r) {
+      const int64_t c = (int64_t)(r - buf);
+      LINE(a, c);
+      a = c + 1;
+      if (c + 1 == t) {  /* CR LF: one terminator */
+        crlf = 1;
+        break;
       }
+      r = memchr(buf + a, '\r', (size_t)(t - a));
     }
+    if (!f) break;
+    if (!crlf) LINE(a, t);
+    a = t + 1;
+    p = t + 1;
   }
   if (a < n) LINE(a, n);
 #undef LINE

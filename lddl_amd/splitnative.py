@@ -114,17 +114,66 @@ def split_raw(raws):
   return corpus, doc_ids
 
 
-def line_spans(buf, crlf_only):
-  """readers._line_spans in one C pass (memchr): (starts, ends) int64, or
-  None without the library"""
+def _spans_piece(L, base, lo, hi, crlf_only):
+  """the line spans of buf[lo, hi) (base = the buffer's address), offsets
+  relative to lo"""
+  n = hi - lo
+  if n <= 0:
+    return np.zeros(0, np.int64), np.zeros(0, np.int64)
+  p = ctypes.c_void_p(base + lo)
+  cap = n // 32 + 1024  # (one call for lines of >= 32 B on average; else count, then fill)
+  s, e = np.empty(cap, np.int64), np.empty(cap, np.int64)
+  m = L.lddl_line_spans(p, n, 1 if crlf_only else 0, _p(s), _p(e), cap)
+  if m > cap:
+    s, e = np.empty(m, np.int64), np.empty(m, np.int64)
+    L.lddl_line_spans(p, n, 1 if crlf_only else 0, _p(s), _p(e), m)
+  return s[:m], e[:m]
+
+
+def _cut_after_terminator(buf, b, crlf_only):
+  """the first position after a line terminator at or past b (a piece may
+  start there: no CR LF pair straddles it), or len(buf)"""
+  n, w = len(buf), 1 << 16
+  pat = b'\r\n' if crlf_only else b'\n'
+  lo = max(b - 1, 0) if crlf_only else b
+  while lo < n:
+    hi = min(n, lo + w)
+    k = bytes(buf[lo:hi]).find(pat)
+    if k >= 0:
+      return lo + k + len(pat)
+    lo = hi - (len(pat) - 1)
+    if hi == n:
+      break
+    w *= 4
+  return n
+
+
+def line_spans(buf, crlf_only, threads=None, min_piece=64 << 20):
+  """readers._line_spans in C (memchr): (starts, ends) int64, or None
+  without the library.  A large buffer is cut after line terminators into
+  pieces indexed on threads (ctypes releases the GIL): a file read through
+  a memory map spends most of a single pass in first-touch page faults."""
   L = _lib()
   if L is None:
     return None
   n = len(buf)
   if n == 0:
     return np.zeros(0, np.int64), np.zeros(0, np.int64)
-  p = ctypes.c_void_p(buf.ctypes.data)
-  m = L.lddl_line_spans(p, n, 1 if crlf_only else 0, None, None, 0)
-  s, e = np.empty(max(m, 1), np.int64), np.empty(max(m, 1), np.int64)
-  L.lddl_line_spans(p, n, 1 if crlf_only else 0, _p(s), _p(e), m)
-  return s[:m], e[:m]
+  base = buf.ctypes.data
+  if threads is None:
+    from .hostinfo import cpu_share
+    threads = cpu_share()
+  k = max(1, min(int(threads), n // max(1, min_piece)))
+  if k == 1:
+    return _spans_piece(L, base, 0, n, crlf_only)
+  cuts = [0]
+  for i in range(1, k):
+    c = _cut_after_terminator(buf, max(i * n // k, cuts[-1]), crlf_only)
+    if cuts[-1] < c < n:
+      cuts.append(c)
+  cuts.append(n)
+  from concurrent.futures import ThreadPoolExecutor
+  with ThreadPoolExecutor(len(cuts) - 1) as ex:
+    parts = list(ex.map(lambda i: _spans_piece(L, base, cuts[i], cuts[i + 1], crlf_only), range(len(cuts) - 1)))
+  return (np.concatenate([s + cuts[i] for i, (s, _) in enumerate(parts)]),
+          np.concatenate([e + cuts[i] for i, (_, e) in enumerate(parts)]))

@@ -109,3 +109,22 @@ def test_line_spans_match_numpy(crlf):
     got = splitnative.line_spans(buf, crlf)
     exp = readers._line_spans(buf, crlf)
     assert np.array_equal(got[0], exp[0]) and np.array_equal(got[1], exp[1]), (trial, bytes(buf))
+
+
+@pytest.mark.parametrize('crlf', [False, True])
+def test_line_spans_threaded_pieces(crlf):
+  """the line index of a buffer cut into pieces after line terminators and
+  indexed on threads equals the single pass: CR / LF / CR LF-dense buffers,
+  tiny pieces (cuts land next to every kind of terminator), lines longer
+  than a piece, no terminator at all"""
+  from lddl_amd import readers
+  rng = np.random.default_rng(10 + int(crlf))
+  alphabet = np.array([10, 13, 65, 66, 32], dtype=np.uint8)
+  for trial in range(200):
+    n = int(rng.integers(0, 3000))
+    p = [np.array([0.1, 0.1, 0.5, 0.2, 0.1]), np.array([0.005, 0.005, 0.6, 0.3, 0.09]),
+         np.array([0, 0, 0.6, 0.3, 0.1])][trial % 3]
+    buf = rng.choice(alphabet, size=n, p=p / p.sum()).astype(np.uint8)
+    got = splitnative.line_spans(buf, crlf, threads=int(rng.integers(2, 9)), min_piece=int(rng.integers(1, 200)))
+    exp = readers._line_spans(buf, crlf)
+    assert np.array_equal(got[0], exp[0]) and np.array_equal(got[1], exp[1]), (trial, bytes(buf))
