@@ -383,6 +383,10 @@ def _nice_worker():
       pass
 
 
+def _split_warm(_):
+  return os.getpid()
+
+
 def _split_worker(a, b):
   ts = time.perf_counter()
   corpus, ids = split_chunk(_FE['index'], _FE['order'][a:b], _FE['codebert'], _FE['split'])
@@ -548,14 +552,21 @@ def main(args, codebert=False):
     if splitnative.available():
       splitnative.props_table()  # (loaded here once; the forked workers share it)
   if nw > 0:
+    import concurrent.futures
     import multiprocessing
     _FE.update(index=index, order=order, codebert=codebert, split=split)
     t0 = time.perf_counter()
     # (niced: the CPU share is shared with this process, whose thread drives
-    # the GPU and the writer; LDDL_WORKER_NICE=0 keeps the default priority)
-    pool = multiprocessing.get_context('fork').Pool(nw, initializer=_nice_worker)
+    # the GPU and the writer; LDDL_WORKER_NICE=0 keeps the default priority.
+    # An executor, not multiprocessing.Pool: the Pool's handler threads poll
+    # at 0.1 s, and its terminate / join took 0.12-0.25 s at the end)
+    pool = concurrent.futures.ProcessPoolExecutor(nw, mp_context=multiprocessing.get_context('fork'),
+                                                  initializer=_nice_worker)
+    try:
+      list(pool.map(_split_warm, range(nw)))  # (the first task forks every worker, while _FE holds the state)
+    finally:
+      _FE.clear()
     t['pool_start_s'] = time.perf_counter() - t0
-    _FE.clear()
 
   # a chunk is split as pieces of ~1/(2 nw) of it (whole partitions) on all
   # the workers at once: the GPU packs a chunk's partitions in parallel, one
@@ -567,20 +578,20 @@ def main(args, codebert=False):
 
   def submit(c):
     if pool is not None:
-      return [pool.apply_async(_split_worker, (int(pro[a]), int(pro[b]))) for a, b in pieces(c)]
+      return [pool.submit(_split_worker, int(pro[a]), int(pro[b])) for a, b in pieces(c)]
     ts = time.perf_counter()
     a, b = chunks[c]
     corpus, ids = split_chunk(index, order[int(pro[a]):int(pro[b])], codebert, split)
 
     class Done:
-      def get(self):
+      def result(self):
         return corpus, ids, time.perf_counter() - ts
     return [Done()]
 
   def gather(fs):
     """the pieces of a chunk, in order: (corpora, doc ids, split seconds);
     pipeline.upload_pieces stages them for the GPU without a host concat"""
-    got = [f_.get() for f_ in fs]
+    got = [f_.result() for f_ in fs]
     return [g[0] for g in got], concat_ids([g[1] for g in got]), sum(g[2] for g in got)
 
   # the parquet encodes: a pool of processes forked here, before the GPU is
@@ -598,8 +609,7 @@ def main(args, codebert=False):
         enc = concurrent.futures.ThreadPoolExecutor(writer.encode_workers())
   except BaseException:
     if pool is not None:
-      pool.terminate()
-      pool.join()
+      pool.shutdown(wait=True, cancel_futures=True)
     raise
   t['enc_start_s'] = time.perf_counter() - t0
   # the first chunks split while this process brings up the GPU context and
@@ -613,8 +623,7 @@ def main(args, codebert=False):
     pk = pipeline.Packer(vocab, local, masking=args.masking and not codebert)
   except BaseException:
     if pool is not None:
-      pool.terminate()
-      pool.join()
+      pool.shutdown(wait=True, cancel_futures=True)
     if enc is not None:
       enc.close() if isinstance(enc, writer.ProcessEncoder) else enc.shutdown(wait=False)
     raise
@@ -657,6 +666,10 @@ def main(args, codebert=False):
       t['host_split_s'] += ts
       if pool is not None and i + ahead < len(todo):
         futs[todo[i + ahead]] = submit(todo[i + ahead])  # overlaps this chunk's GPU work and parquet writes
+      elif pool is not None and not futs and os.environ.get('LDDL_SPLIT_EARLY_EXIT', '1') != '0':
+        # every split is in: the workers exit (0.2-0.4 s after a C2-size
+        # run) beside the last chunks' GPU work and writes
+        pool.shutdown(wait=False)
       t0 = time.perf_counter()
       sh = pipeline.upload_pieces(corpus, pro[a:b + 1] - pro[a], device)
       ids_d, ntok, toff = pk.tokenize(sh)
@@ -692,12 +705,14 @@ def main(args, codebert=False):
   finally:
     t0 = time.perf_counter()
     if pool is not None:
-      pool.terminate()
-      pool.join()
+      pool.shutdown(wait=True, cancel_futures=True)
+    t['teardown_split_s'] = time.perf_counter() - t0
     if enc is not None:
       enc.close() if isinstance(enc, writer.ProcessEncoder) else enc.shutdown(wait=True)
     index.close()
     t['teardown_s'] = time.perf_counter() - t0
+    if isinstance(enc, writer.ProcessEncoder):
+      t['teardown_enc_exit_s'], t['teardown_enc_unpin_s'], t['teardown_enc_rm_s'] = enc.close_s
   if args.num_shards:
     # balance_dask_output's job (load_balance.py:321-369) from the packer's
     # counts: one all-gather (RCCL) instead of its per-file count pass + MPI

@@ -426,14 +426,18 @@ class ProcessEncoder:
           f_.result()
         except Exception:
           pass
+    t0 = time.perf_counter()
     self.ex.shutdown(wait=True)
+    t1 = time.perf_counter()
     for sl in self.slots:
       self._unpin(sl)
       sl['t'] = None
       if sl['mm'] is not None:
         sl['mm'].close()
         sl['mm'] = None
+    t2 = time.perf_counter()
     self._fin()
+    self.close_s = (t1 - t0, t2 - t1, time.perf_counter() - t2)  # workers' exit, slot unpin / unmap, slot files
 
 
 def _host_var(arr, r0, n):
