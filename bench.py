@@ -470,7 +470,8 @@ def frontend_leg(mb, chunk_mb=32.0, seq=128, bin_size=None, unique_mb=256):
     out = {'what': 'preprocess CLI end to end, BERT seq %d %s (BASELINE configs[%d])' % (
                seq, 'bin %d' % bin_size if bin_size else 'unbinned', 1 if bin_size else 0),
            'raw_mb': raw / 1e6, 'documents': i, 'unique_mb': min(mb, unique_mb),
-           'files': len(files), 'seconds': el, 'raw_mb_per_s': raw / 1e6 / el, 'gen_s': gen_s}
+           'files': len(files), 'seconds': el, 'raw_mb_per_s': raw / 1e6 / el, 'gen_s': gen_s,
+           'rows_per_s': t.get('pairs', 0) / el, 'work_dir': tempfile.gettempdir()}
     out.update({k: v for k, v in t.items() if isinstance(v, (int, float, str))})
     return out
   finally:
