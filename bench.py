@@ -646,9 +646,15 @@ def main():
   if args.parquet_parts > 0 and os.environ.get('LDDL_ENCODE_PROCS', '1') != '0':
     from lddl_amd import writer
     enc = writer.ProcessEncoder()
-  fe = frontend_leg(args.frontend_mb) if world == 1 and args.frontend_mb > 0 else None
+  def cli_leg(*a, **kw):  # (a failed CLI leg is recorded in the line; the headline still runs)
+    try:
+      return frontend_leg(*a, **kw)
+    except Exception as e:  # noqa: BLE001
+      return {'error': '%s: %s' % (type(e).__name__, e)}
+
+  fe = cli_leg(args.frontend_mb) if world == 1 and args.frontend_mb > 0 else None
   progress(rank, 'frontend leg done')
-  fe2 = (frontend_leg(args.frontend_c2_mb, seq=512, bin_size=64)
+  fe2 = (cli_leg(args.frontend_c2_mb, seq=512, bin_size=64)
          if world == 1 and args.frontend_c2_mb > 0 else None)
   torch.cuda.set_device(local)
   device = torch.device('cuda', local)
@@ -792,7 +798,10 @@ def main():
     pass
   progress(rank, 'timed steps done')
   if args.parquet_parts > 0:
-    line['parquet_writer'] = parquet_sample(args, pk, res, sh, enc)
+    try:
+      line['parquet_writer'] = parquet_sample(args, pk, res, sh, enc)
+    except Exception as e:  # (recorded: the headline line still prints)
+      line['parquet_writer'] = {'error': '%s: %s' % (type(e).__name__, e)}
   if enc is not None:
     enc.close()
   if fe is not None:
@@ -801,9 +810,15 @@ def main():
     line['frontend_c2'] = fe2
   if not args.no_cpu_baseline and world == 1:  # the host leg (the oracle): rank 0 at N=1 only
     progress(rank, 'cpu baseline')
-    line['cpu_baseline'] = cpu_baseline(args, base, pdo, args.cpu_seconds)
+    try:
+      line['cpu_baseline'] = cpu_baseline(args, base, pdo, args.cpu_seconds)
+    except Exception as e:  # (recorded: the headline line still prints)
+      line['cpu_baseline'] = {'error': '%s: %s' % (type(e).__name__, e)}
     if not args.no_sample_check:  # the oracle as the checker of one full-size partition of the timed run
-      line['cpu_baseline']['sample_check'] = sample_partition_check(args, pk, res, base, pdo, reps, kw['seed'])
+      try:
+        line['cpu_baseline']['sample_check'] = sample_partition_check(args, pk, res, base, pdo, reps, kw['seed'])
+      except Exception as e:  # (recorded, never as a pass: identical is absent)
+        line['cpu_baseline']['sample_check'] = {'error': '%s: %s' % (type(e).__name__, e)}
   if world == 1 and args.legs and args.legs != 'none':
     # the other BASELINE workloads, after everything above read the headline's
     # results: its packer scratch goes first (a second context beside it would
