@@ -89,6 +89,8 @@ struct lddl_ctx {
   uint4* d_vt = nullptr;         // v4 bucketed vocab table
   uint32_t vt_mask = 0;
   uint32_t* d_vbloom = nullptr;  // its Bloom filter
+  uint4* d_st = nullptr;         // the scan's whole-word table
+  uint32_t st_mask = 0;
   bool scan_ok = false;          // the ASCII page fits the split scan's per-byte class table
   // lane tokenizer (tokenize_lane.hip): the vocab trie, its roots, the byte classes
   uint2* d_trie = nullptr;
@@ -167,6 +169,7 @@ static void free_ctx(lddl_ctx* c) {
   (void)hipFree(c->d_rinfo);
   (void)hipFree(c->d_vt);
   (void)hipFree(c->d_vbloom);
+  (void)hipFree(c->d_st);
   (void)hipFree(c->d_ovf);
   (void)hipFree(c->d_counter);
   (void)hipFree(c->d_ctab);
@@ -233,6 +236,8 @@ static int load_vocab(lddl_ctx* c, const char* path) {
   if ((rc = upload(&c->d_bloom, V.bloom.data(), V.bloom.size() * 4))) return rc;
   if ((rc = upload(&c->d_vt, V.vt.data(), V.vt.size() * 4))) return rc;
   if ((rc = upload(&c->d_vbloom, V.vbloom.data(), V.vbloom.size() * 4))) return rc;
+  c->st_mask = V.st_mask;
+  if ((rc = upload(&c->d_st, V.st.data(), V.st.size() * 4))) return rc;
   if ((rc = upload(&c->d_slots, V.slots.data(), V.slots.size() * sizeof(uint4)))) return rc;
   if ((rc = upload(&c->d_pool, V.pool.data(), V.pool.size()))) return rc;
   if ((rc = upload(&c->d_voff, V.voff.data(), V.voff.size() * 4))) return rc;
@@ -362,6 +367,14 @@ extern "C" int lddl_tokenize(lddl_ctx* c, const uint8_t* d_bytes, int64_t nbytes
   P.vt = c->d_vt;
   P.vt_mask = c->vt_mask;
   P.vbloom = c->d_vbloom;
+  // LDDL_SCAN_TABLE=1: the scan probes its two-choice whole-word table
+  // (half the scan's fetch, 3 % fewer WordPiece records, but the scan 3.5 %
+  // slower: profiles/r5_scan_table.txt); default: slot 0 of the vt bucket
+  {
+    const char* e = getenv("LDDL_SCAN_TABLE");
+    P.st = (e && e[0] == '1') ? c->d_st : nullptr;
+    P.st_mask = c->st_mask;
+  }
   P.trie = c->d_trie;
   P.trie_base[0] = c->trie_base[0];
   P.trie_base[1] = c->trie_base[1];

@@ -74,6 +74,10 @@ LDDL_HD uint32_t vfinal(uint32_t h, uint32_t len, uint32_t cont) {
   h ^= h >> 15;
   return h;
 }
+// The scan's whole-word table (tok_tables.h build_vocab_tables): 32-B slots
+// in the v4 slot layout, a key in one of two slots, at vhash & mask and at
+// st_second(vhash) & mask (two-choice cuckoo placement)
+LDDL_HD uint32_t st_second(uint32_t h) { return ((h >> 16) | (h << 16)) ^ 0x9E3779B9u; }
 // Bucket index of a candidate piece: its first 12 bytes (three dwords, zero
 // past the key), its byte length and the "##" flag -- always three mixes, so
 // the scan's whole-word probe hashes a key without selecting among prefix

@@ -45,6 +45,8 @@ struct VocabTables {
   std::vector<uint32_t> vt;               // v4 buckets: two 32-B slots each
   uint32_t vt_mask = 0;
   std::vector<uint32_t> vbloom;           // [BLOOM_WORDS] over the v4 keys + extension keys
+  std::vector<uint32_t> st;               // the scan's whole-word table: 32-B slots, two choices per key
+  uint32_t st_mask = 0;
   std::vector<uint8_t> rpool;             // vocab entries verbatim, 4-aligned (rendering)
   std::vector<uint32_t> rinfo;            // [V] offset << 8 | length into rpool
   std::vector<uint2> trie;                // lane tokenizer's double-array trie (trie_* below)
@@ -373,6 +375,68 @@ inline int build_vocab_tables(const char* path, VocabTables& V, std::string& err
     }
   }
   V.vt_mask = nbk - 1;
+  // the scan's whole-word table: every whole-word key of <= 24 bytes (the
+  // keys the scan probes) in one of its two slots (st_second), placed by
+  // cuckoo moves, >= 2.5 slots per key: 64 K slots (2 MB) for BERT, so the
+  // probes of words outside the vocab hit L2 instead of random lines of the
+  // 32 MB bucket table.  A duplicate line: the last id wins, as in vt.
+  {
+    std::vector<size_t> keys;
+    for (size_t i : order)
+      if (vcont[i] == 0 && vlen[i] <= 24) keys.push_back(i);
+    uint32_t ns = 1024;
+    while (ns < keys.size() * 5 / 2) ns <<= 1;
+    auto key_of = [&](size_t i, uint32_t* d) {
+      for (int q = 0; q < VKEY_DW; ++q) d[q] = 0;
+      memcpy(d, &pool[V.voff[i]], vlen[i]);
+    };
+    for (;;) {
+      V.st.assign((size_t)ns * 8, 0u);
+      const uint32_t m = ns - 1;
+      bool ok = true;
+      for (size_t i : keys) {
+        uint32_t e[8];
+        key_of(i, e);
+        e[6] = slot_info((uint32_t)i, vlen[i], 0);
+        e[7] = V.voff[i];
+        const uint32_t h = vhash(e, vlen[i], 0);
+        const uint32_t p1 = h & m, p2 = st_second(h) & m;
+        bool dup = false;
+        for (uint32_t p : {p1, p2}) {
+          uint32_t* s = &V.st[(size_t)p * 8];
+          if (s[6] != 0 && same(s[6] & 0xFFFFu, i)) {
+            s[6] = e[6];  // (last id wins)
+            dup = true;
+            break;
+          }
+        }
+        if (dup) continue;
+        uint32_t pos = V.st[(size_t)p1 * 8 + 6] == 0 ? p1 : p2;
+        bool placed = false;
+        for (int kick = 0; kick < 1000 && !placed; ++kick) {
+          uint32_t* s = &V.st[(size_t)pos * 8];
+          if (s[6] == 0) {
+            memcpy(s, e, sizeof e);
+            placed = true;
+            break;
+          }
+          uint32_t out[8];
+          memcpy(out, s, sizeof out);
+          memcpy(s, e, sizeof e);
+          memcpy(e, out, sizeof out);
+          const uint32_t hl = vhash(e, (e[6] >> 16) & 0xFFu, 0);
+          pos = (pos == (hl & m)) ? (st_second(hl) & m) : (hl & m);
+        }
+        if (!placed) {
+          ok = false;
+          break;
+        }
+      }
+      if (ok) break;
+      ns <<= 1;  // (a cycle: a larger table)
+    }
+    V.st_mask = ns - 1;
+  }
   // rendering tables: the vocab entries verbatim (pretrain.py:348-353 joins them)
   V.rpool.clear();
   V.rinfo.assign(n, 0);

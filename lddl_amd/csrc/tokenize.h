@@ -38,6 +38,10 @@ struct TokParams {
   const uint4* vt;
   uint32_t vt_mask;  // #buckets - 1
   const uint32_t* vbloom;
+  // the scan's whole-word table (two 32-B slots per key, common.h
+  // st_second); null: the scan probes slot 0 of the key's vt bucket instead
+  const uint4* st;
+  uint32_t st_mask;
   // double-array trie of the vocab keys (common.h trie_*): the split
   // tokenizer's WordPiece walk (wpt_kernel) and the lane tokenizer
   const uint2* trie;

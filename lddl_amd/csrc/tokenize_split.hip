@@ -921,12 +921,24 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
           }
           STAMP(6);
           if (w != 0 && len <= 24 && len <= mb0) {
-            const uint4* bk =
-                P.vt + 4 * (key_hash(key, len, 0u) & vmask & ((LDDL_PROBE_L2 == 1 || LDDL_PROBE_L2 == 2) ? 0x3FFFu : ~0u));
-            const uint4 fa = bk[0], fb = bk[1];
-            if (LDDL_PROBE_L2 >= 2 || slot_eq(fa, fb, key, ((uint32_t)len << 16) | 0x80000000u)) {
-              id = (uint16_t)(fb.z & 0xFFFFu);
-              w = 0;
+            const uint32_t hk = key_hash(key, len, 0u), want = ((uint32_t)len << 16) | 0x80000000u;
+            if (P.st && !LDDL_PROBE_L2) {
+              // the scan table: both candidate slots loaded before either compare
+              const uint4* s1 = P.st + 2 * (hk & P.st_mask);
+              const uint4* s2 = P.st + 2 * (st_second(hk) & P.st_mask);
+              const uint4 fa = s1[0], fb = s1[1], ga = s2[0], gb = s2[1];
+              const bool h1 = slot_eq(fa, fb, key, want), h2 = slot_eq(ga, gb, key, want);
+              if (h1 || h2) {
+                id = (uint16_t)((h1 ? fb.z : gb.z) & 0xFFFFu);
+                w = 0;
+              }
+            } else {
+              const uint4* bk = P.vt + 4 * (hk & vmask & ((LDDL_PROBE_L2 == 1 || LDDL_PROBE_L2 == 2) ? 0x3FFFu : ~0u));
+              const uint4 fa = bk[0], fb = bk[1];
+              if (LDDL_PROBE_L2 >= 2 || slot_eq(fa, fb, key, want)) {
+                id = (uint16_t)(fb.z & 0xFFFFu);
+                w = 0;
+              }
             }
           }
           if (__any(lovf)) {

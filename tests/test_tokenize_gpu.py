@@ -123,8 +123,9 @@ def adversarial_sentences(rng, n):
   return out
 
 
-# '5t': tok5 with its WordPiece by trie walk (LDDL_WP_ALGO=trie, the A/B option)
-ALGOS = ['0', '5', '5t', '6']
+# '5t': tok5 with its WordPiece by trie walk (LDDL_WP_ALGO=trie, the A/B option);
+# '5s': tok5 whose scan probes its two-choice whole-word table (LDDL_SCAN_TABLE=1)
+ALGOS = ['0', '5', '5t', '5s', '6']
 
 
 def _set_algo(monkeypatch, algo):
@@ -133,6 +134,10 @@ def _set_algo(monkeypatch, algo):
     monkeypatch.setenv('LDDL_WP_ALGO', 'trie')
   else:
     monkeypatch.delenv('LDDL_WP_ALGO', raising=False)
+  if algo.endswith('s'):
+    monkeypatch.setenv('LDDL_SCAN_TABLE', '1')
+  else:
+    monkeypatch.delenv('LDDL_SCAN_TABLE', raising=False)
 
 
 @pytest.mark.parametrize('algo', ALGOS)
