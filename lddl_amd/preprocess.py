@@ -711,7 +711,7 @@ def main(args, codebert=False):
       enc.close() if isinstance(enc, writer.ProcessEncoder) else enc.shutdown(wait=True)
     index.close()
     t['teardown_s'] = time.perf_counter() - t0
-    if isinstance(enc, writer.ProcessEncoder):
+    if getattr(enc, 'close_s', None):  # (absent when close() raised: that error propagates)
       t['teardown_enc_exit_s'], t['teardown_enc_unpin_s'], t['teardown_enc_rm_s'] = enc.close_s
   if args.num_shards:
     # balance_dask_output's job (load_balance.py:321-369) from the packer's
