@@ -405,7 +405,7 @@ extern "C" int lddl_tokenize(lddl_ctx* c, const uint8_t* d_bytes, int64_t nbytes
   int rc;
   // (the entry / staging buffer: u16 per byte of a segment + the last
   // sentence's ids past its end)
-  if ((rc = ws_get(c, 19, nt + 1, &tile_sent)) || (rc = ws_get(c, 20, nt, &S.fb_list)) ||
+  if ((rc = ws_get(c, 19, nt + 1, &tile_sent)) || (rc = ws_get(c, 20, (size_t)fb_list_cap(seg), &S.fb_list)) ||
       (rc = ws_get(c, 21, 16, &S.fb_count)) ||
       (rc = ws_get(c, 34, (size_t)seg * 1024 + (size_t)max_tok + 4096, &S.ent)) ||
       (rc = ws_get(c, 36, (size_t)n_chunks + 16, &S.chunk_fill)) ||

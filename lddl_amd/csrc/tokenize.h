@@ -55,11 +55,16 @@ struct TokParams {
 int64_t tile_count(int64_t nbytes);
 hipError_t launch_tile_bounds(const int64_t* sent_off, int64_t n_sent, int64_t n_tiles, int64_t* tile_sent,
                               int64_t* tile_off, hipStream_t s);
-hipError_t launch_tokenize_fallback(const TokParams& P, const int64_t* tile_sent, const int32_t* fb_list,
-                                    const int32_t* fb_count, int grid, hipStream_t s);
+// fb_list: *fb_count sentence ranges [fb_list[2k], fb_list[2k+1]) for the
+// exact serial path (a scan window or a tile it did not model)
+hipError_t launch_tokenize_fallback(const TokParams& P, const int64_t* fb_list, const int32_t* fb_count, int grid,
+                                    hipStream_t s);
 const void* tokenize_fallback_kernel_ptr();
-// fb_list = every tile of [0, n_tiles), *fb_count = n_tiles
-hipError_t launch_list_all_tiles(int64_t n_tiles, int32_t* fb_list, int32_t* fb_count, hipStream_t s);
+// fb_list = the sentence range of every tile of [0, n_tiles), *fb_count = n_tiles
+hipError_t launch_list_all_tiles(int64_t n_tiles, const int64_t* tile_sent, int64_t* fb_list, int32_t* fb_count,
+                                 hipStream_t s);
+// fallback ranges a segment of seg_tiles tiles can list (its scan windows)
+int64_t fb_list_cap(int64_t seg_tiles);
 
 // v5 (tokenize_split.hip): the tile scan resolves whole-word vocab hits and
 // hands every other word to a WordPiece record queue; a full-occupancy
@@ -103,8 +108,8 @@ struct SplitParams {
   uint8_t* cnt8;           // per record slot: pieces of the word (0 for an extension slot)
   int64_t* scan_bsum;      // scan_blocks(seg_sent_cap) + 1
   int64_t seg_sent_cap;    // bound on the sentences of a segment (the count scan's grid)
-  int32_t* fb_list;
-  int32_t* fb_count;       // tiles listed for the serial path in this segment
+  int64_t* fb_list;        // sentence ranges for the serial path (pairs, launch_tokenize_fallback)
+  int32_t* fb_count;       // ranges listed in this segment
   uint32_t* n_fallback;    // tiles listed over the call (lddl_tokenize_stats)
   unsigned long long* n_rec;  // optional: records run by wp_kernel (summed over the call)
 };
@@ -137,7 +142,7 @@ struct LaneParams {
   const int64_t* tile_off;
   int64_t t0, t1;         // the segment's tiles
   uint32_t* ctr;          // [0] tile batches handed out
-  int32_t* fb_list;
+  int64_t* fb_list;       // sentence-range pairs (SplitParams::fb_list)
   int32_t* fb_count;
   uint32_t* n_fallback;
   uint64_t* stats;        // optional: [0] iterations x 64, [1] lane-iterations busy, [2] slow passes

@@ -5,12 +5,13 @@
 // tile, so every tile is independent.  tile_sent[t] = first sentence of tile
 // t (tile_bounds_kernel, one pass over the sentences).
 //
-// tokenize_fallback_kernel re-runs listed tiles one lane per sentence
+// tokenize_fallback_kernel re-runs listed sentence ranges (the split
+// tokenizer's scan windows it did not model, or whole tiles) one lane per sentence
 // (tokenize_serial.h: the serial restatement of HF tokenizers'
 // BertNormalizer / BertPreTokenizer / WordPiece behind
 // tokenizer.tokenize(s, max_length=512, truncation=True),
 // lddl/dask/bert/pretrain.py:79-80, as oracle/tokenizer_oracle.c).  The
-// split tokenizer (tokenize_split.hip) lists the tiles it does not model;
+// split tokenizer (tokenize_split.hip) lists the windows it does not model;
 // launch_tokenize_serial_dense lists every tile (vocabularies / unicode
 // tables the split tokenizer does not take: > 61440 ids, or an ASCII page
 // with more than the A-Z -> a-z mapping).  Its ids are written sparse by
@@ -42,9 +43,10 @@ __global__ void tile_bounds_kernel(const int64_t* sent_off, int64_t n_sent, int6
   }
 }
 
-// Exact serial path for the listed tiles: lane per sentence (tokenize_serial.h).
-__global__ __launch_bounds__(256) void tokenize_fallback_kernel(TokParams P, const int64_t* tile_sent,
-                                                                const int32_t* fb_list, const int32_t* fb_count) {
+// Exact serial path for the listed sentence ranges (a scan window or a tile
+// the split tokenizer did not model): lane per sentence (tokenize_serial.h).
+__global__ __launch_bounds__(256) void tokenize_fallback_kernel(TokParams P, const int64_t* fb_list,
+                                                                const int32_t* fb_count) {
   __shared__ uint32_t ascii_tab[128];
   if (threadIdx.x < 128) ascii_tab[threadIdx.x] = P.pages[(uint32_t)P.top[0] * 256u + threadIdx.x];
   __syncthreads();
@@ -54,8 +56,7 @@ __global__ __launch_bounds__(256) void tokenize_fallback_kernel(TokParams P, con
   const int wave = (blockIdx.x * 256 + threadIdx.x) >> 6, lane = threadIdx.x & 63;
   const int nw = (gridDim.x * 256) >> 6;
   for (int k = wave; k < n; k += nw) {
-    const int64_t t = fb_list[k];
-    const int64_t sa = tile_sent[t], sb = tile_sent[t + 1];
+    const int64_t sa = fb_list[2 * k], sb = fb_list[2 * k + 1];
     for (int64_t s = sa + lane; s < sb; s += 64) {
       SentState st{P.sent_off[s], P.sent_off[s + 1], P.sent_off[s] - base, 0};
       while (st.p < st.e && st.ntok < P.max_tok) step(P, st, wb, ascii_tab);
@@ -72,17 +73,26 @@ __global__ __launch_bounds__(256) void tokenize_fallback_kernel(TokParams P, con
 }
 
 int64_t tile_count(int64_t nbytes) { return (nbytes >> TILE_SHIFT) + 1; }
+// (the scan's windows: two consecutive windows of a super-tile cover more
+// than 2 KiB - 16 B, a window longer than 2 KiB holds one sentence, plus a
+// partly filled last window per super-tile -> fewer than 2 per tile; the
+// serial path lists one range per tile)
+int64_t fb_list_cap(int64_t seg_tiles) { return 2 * (2 * seg_tiles + 64); }
 const void* tokenize_fallback_kernel_ptr() { return reinterpret_cast<const void*>(&tokenize_fallback_kernel); }
 
 
-__global__ void list_all_tiles_kernel(int64_t n_tiles, int32_t* fb_list, int32_t* fb_count) {
-  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n_tiles; t += (int64_t)gridDim.x * blockDim.x)
-    fb_list[t] = (int32_t)t;
+__global__ void list_all_tiles_kernel(int64_t n_tiles, const int64_t* tile_sent, int64_t* fb_list,
+                                      int32_t* fb_count) {
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n_tiles; t += (int64_t)gridDim.x * blockDim.x) {
+    fb_list[2 * t] = tile_sent[t];
+    fb_list[2 * t + 1] = tile_sent[t + 1];
+  }
   if (blockIdx.x == 0 && threadIdx.x == 0) *fb_count = (int32_t)n_tiles;
 }
 
-hipError_t launch_list_all_tiles(int64_t n_tiles, int32_t* fb_list, int32_t* fb_count, hipStream_t s) {
-  hipLaunchKernelGGL(list_all_tiles_kernel, dim3(1024), dim3(256), 0, s, n_tiles, fb_list, fb_count);
+hipError_t launch_list_all_tiles(int64_t n_tiles, const int64_t* tile_sent, int64_t* fb_list, int32_t* fb_count,
+                                 hipStream_t s) {
+  hipLaunchKernelGGL(list_all_tiles_kernel, dim3(1024), dim3(256), 0, s, n_tiles, tile_sent, fb_list, fb_count);
   return hipGetLastError();
 }
 
@@ -92,9 +102,9 @@ hipError_t launch_tile_bounds(const int64_t* sent_off, int64_t n_sent, int64_t n
   return hipGetLastError();
 }
 
-hipError_t launch_tokenize_fallback(const TokParams& P, const int64_t* tile_sent, const int32_t* fb_list,
-                                    const int32_t* fb_count, int grid, hipStream_t s) {
-  hipLaunchKernelGGL(tokenize_fallback_kernel, dim3(grid), dim3(256), 0, s, P, tile_sent, fb_list, fb_count);
+hipError_t launch_tokenize_fallback(const TokParams& P, const int64_t* fb_list, const int32_t* fb_count, int grid,
+                                    hipStream_t s) {
+  hipLaunchKernelGGL(tokenize_fallback_kernel, dim3(grid), dim3(256), 0, s, P, fb_list, fb_count);
   return hipGetLastError();
 }
 

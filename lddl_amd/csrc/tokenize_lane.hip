@@ -59,7 +59,8 @@ struct DevEnv {
   }
   __device__ __forceinline__ void abort_tile(const LaneState& L) const {
     const int at = atomicAdd(Q.fb_count, 1);
-    Q.fb_list[at] = (int32_t)L.t;
+    Q.fb_list[2 * at] = Q.tile_sent[L.t];
+    Q.fb_list[2 * at + 1] = Q.tile_sent[L.t + 1];
     atomicAdd(Q.n_fallback, 1u);
   }
 };
@@ -302,7 +303,7 @@ hipError_t finish_lane_segment(TokParams P, const SplitParams& S, const tok6::La
                                hipStream_t s) {
   TokParams F = P;
   F.out_ids = S.ent - (S.t0 << 10);  // the serial path writes at sent_off[s] - sent_off[0]
-  hipError_t e = launch_tokenize_fallback(F, S.tile_sent, S.fb_list, S.fb_count, fb_grid, s);
+  hipError_t e = launch_tokenize_fallback(F, S.fb_list, S.fb_count, fb_grid, s);
   if (e != hipSuccess) return e;
   if ((e = launch_scan_ntok_range(P.out_ntok, S.tile_sent + S.t0, S.tile_sent + S.t1, S.seg_sent_cap, P.out_tok_off,
                                   S.scan_bsum, s)) != hipSuccess)

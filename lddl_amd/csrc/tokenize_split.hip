@@ -63,9 +63,13 @@ namespace tok5 {
 constexpr int CAP = 2048;                // window bytes (32 per lane)
 constexpr int DCAP = 256;                // side buffer for dirty words
 constexpr int SCAN_OCC = 5;              // waves per SIMD the scan's LDS admits (4 measured 5 % slower)
+#ifndef LDDL_SCAN_SUPER
+#define LDDL_SCAN_SUPER 16
+#endif
+constexpr int SUPER = LDDL_SCAN_SUPER;   // tiles per super-tile (a wave's unit of hand-out, packed into windows)
 constexpr int NBUF = CAP + DCAP + 64;    // + over-read pad of the key loads
 constexpr int UCAP = 256;                // units per round
-constexpr int NSCAP = 64;                // sentences per tile
+constexpr int NSCAP = 32;                // sentences per window (< NSCAP: NSCAP sentence offsets staged)
 constexpr int XCAP = 32;                 // expansion markers per tile
 constexpr int KEYMAX = 56;               // key bytes a record holds
 constexpr int KEY1 = 28;                 // keys up to 28 bytes take one slot (<= 28 pieces)
@@ -90,7 +94,11 @@ __device__ __forceinline__ uint32_t lx_make(int nxt_brk, int nxt_dirty, int sbb)
 struct alignas(16) Lds {
   uint32_t rp[CAP / 4 + 4];    // raw bytes of the tile (LDS-DMA); free after the exception pass, when the
                                // next tile's bytes are prefetched into it
-  uint32_t pb[8];              // the tile's bounds: tile_sent[t], tile_sent[t+1], sent_off of both (LDS-DMA)
+  uint32_t pb[4];              // the next super-tile's bounds: tile_sent of its first tile and of its end (LDS-DMA)
+  int64_t soff[NSCAP];         // the next window's sent_off[c_s .. c_s + 32) (LDS-DMA; read by stage2, then its
+                               // sentence starts by the window's first steps)
+  int64_t wst[3];              // window staging: the super-tile's next sentence, its end, the super-tile (kept
+                               // here, not in registers, across the window's work)
   uint32_t nb[NBUF / 4];       // normalised bytes in window coordinates; side buffer at [CAP, CAP+DCAP)
   uint32_t brk[64];            // break bits: unit starts, spaces, sentence starts
   uint32_t um[64];             // unit-start bits
@@ -352,48 +360,91 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
   // record chunk of this wave (wave-uniform): slots [cur, cend)
   uint32_t cur = 0, cend = 0, cbase = 0, tbase = 0, tsl = 0;
   int chunk = -1;
-  // The tile's bounds (pb) and raw bytes (rp) arrive by LDS-DMA (no VGPRs,
-  // no register-to-LDS copy of the bytes).  (A software-pipelined variant
-  // that loaded the next tile while this one ran measured no faster: the
-  // kernel is bound by its LDS round trips and instruction issue.)
-  int64_t n_sa = 0, n_sb = 0, n_A = 0, n_B = 0, n_spos = 0;
+  // Windows.  The wave walks super-tiles of SUPER tiles (its wave index, then
+  // + nwaves) and packs each one's sentences greedily into windows: as many
+  // whole sentences (<= 63) as fit in CAP bytes from the first one's 16-B
+  // aligned start.  A window is about twice a tile's bytes, so the per-window
+  // work (classification, exception pass, unit scans, per-sentence records)
+  // runs over a nearly full 2 KiB window instead of a ~1 KiB tile in it.  A
+  // sentence longer than the window is a window of its own and falls back.
+  // The next window is staged inside the current one: stage1 loads
+  // sent_off[c_s + lane] (its sentences' starts and ends) right after this
+  // window's own bytes arrived, stage2 (before this window's unit steps)
+  // finds how many sentences fit and moves their raw bytes into rp (free
+  // after this window's exception pass) by LDS-DMA, so both round trips fly
+  // behind this window's work; the loop top finishes whatever a window that
+  // returned early left undone.  A super-tile's bounds (tile_sent) arrive by
+  // LDS-DMA into pb while the one before it runs.
+  int64_t n_sa = 0, n_sb = 0, n_A = 0, n_B = 0;
   int nst = 0;
   bool dma_pending = false;  // raw-byte DMA issued and not yet waited for
-  int64_t tn = S.t0 + (int64_t)blockIdx.x * WAVES + wv;
+  const int64_t ng = (S.t1 - S.t0 + SUPER - 1) / SUPER;
   // (LDS-DMA: lane i of the instruction writes dword i at the LDS base)
   auto dma4 = [&](const void* g, uint32_t* l) {
     __builtin_amdgcn_global_load_lds((const uint32_t*)g, (__attribute__((address_space(3))) uint32_t*)l, 4, 0, 0);
   };
   auto drain = [&]() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); };
-  // The next tile's staging runs inside the current one: stage1 (its bounds
-  // and byte offsets, tile_sent / tile_off, by LDS-DMA) right after this
-  // tile's own arrived, stage2 (its raw bytes into rp -- free after this
-  // tile's exception pass -- and its sentence starts) before this tile's
-  // unit steps, so both round trips fly behind this tile's work; the loop
-  // top finishes whatever a tile that returned early left undone.
+  // (lanes 0-1: tile_sent of super-tile g's first tile, lanes 2-3: of its end -> pb[0..3])
+  auto st_bounds = [&](int64_t g) {
+    if (g < ng && lane < 4) {
+      const int64_t t = min(S.t1, S.t0 + (g + (lane >> 1)) * SUPER);
+      dma4(reinterpret_cast<const uint32_t*>(S.tile_sent + t) + (lane & 1), L.pb);
+    }
+  };
+  {
+    const int64_t g = (int64_t)blockIdx.x * WAVES + wv;
+    int64_t cs = 0, ce = 0;
+    if (g < ng) {
+      cs = uni64(S.tile_sent[S.t0 + g * SUPER]);
+      ce = uni64(S.tile_sent[min(S.t1, S.t0 + (g + 1) * SUPER)]);
+    }
+    L.wst[0] = cs;
+    L.wst[1] = ce;
+    L.wst[2] = g;
+    wsync();
+    st_bounds(g + nwaves);
+  }
   auto stage1 = [&]() {
     if (nst != 0) return;
     nst = 1;
-    // (lanes 0-3: tile_sent[tn], [tn + 1] -> pb[0..3]; lanes 4-7: tile_off -> pb[4..7])
-    if (tn < S.t1 && lane < 8)
-      dma4(reinterpret_cast<const uint32_t*>(lane < 4 ? S.tile_sent + tn : S.tile_off + tn) + (lane & 3), L.pb);
+    int64_t cs = uni64(L.wst[0]), ce = uni64(L.wst[1]), g = uni64(L.wst[2]);
+    if (cs >= ce && g < ng) {
+      while (cs >= ce && g < ng) {  // the super-tile is done: the next one's bounds (pb)
+        g += nwaves;
+        if (g >= ng) break;
+        drain();
+        cs = uni64(*reinterpret_cast<const int64_t*>(&L.pb[0]));
+        ce = uni64(*reinterpret_cast<const int64_t*>(&L.pb[2]));
+        st_bounds(g + nwaves);
+      }
+      L.wst[0] = cs;
+      L.wst[1] = ce;
+      L.wst[2] = g;
+    }
+    // (lane l: dword l of sent_off[cs ..], the offsets up to ce)
+    if (cs < ce && cs + (lane_here() >> 1) <= ce) dma4(reinterpret_cast<const uint32_t*>(P.sent_off + cs) + lane_here(), reinterpret_cast<uint32_t*>(L.soff));
   };
   auto stage2 = [&]() {
     if (nst != 1) return;
     nst = 2;
     n_sa = n_sb = 0;
-    if (tn >= S.t1) return;
+    const int64_t cs = uni64(L.wst[0]), ce = uni64(L.wst[1]);
+    if (cs >= ce) return;
     drain();
-    n_sa = uni64(*reinterpret_cast<const int64_t*>(&L.pb[0]));
-    n_sb = uni64(*reinterpret_cast<const int64_t*>(&L.pb[2]));
-    if (n_sa >= n_sb) return;
-    n_A = uni64(*reinterpret_cast<const int64_t*>(&L.pb[4]));
-    n_B = uni64(*reinterpret_cast<const int64_t*>(&L.pb[6]));
+    const int64_t a = uni64(L.soff[0]);
+    const int aoff = (int)(reinterpret_cast<uintptr_t>(P.bytes + a) & 15u);
+    // (sentence i < NSCAP - 1 of the window ends at offset i + 1: a prefix of the lanes fits)
     const int ln = lane_here();
-    if (ln < n_sb - n_sa) n_spos = P.sent_off[n_sa + ln];
-    const int aoff = (int)(reinterpret_cast<uintptr_t>(P.bytes + n_A) & 15u);
+    const bool in = ln >= 1 && ln < NSCAP && cs + ln <= ce;
+    const uint64_t fit = __ballot(in && L.soff[in ? ln : 0] <= a - aoff + CAP);
+    const int ns = max(__popcll(fit), 1);  // (0: the first sentence alone is longer; it falls back)
+    n_sa = cs;
+    n_sb = cs + ns;
+    n_A = a;
+    n_B = uni64(L.soff[ns]);
+    L.wst[0] = cs + ns;
     const int64_t nb64 = (n_B - n_A) + aoff;
-    if (nb64 > CAP || n_sb - n_sa > NSCAP) return;  // the tile falls back: no bytes needed
+    if (nb64 > CAP) return;  // the window falls back: no bytes needed
     dma_pending = true;
     // streamed once: non-temporal (aux bit 1), keep L2 for the vocab table
     const uint8_t* g = P.bytes + (n_A - aoff) + 16 * ln;
@@ -403,26 +454,26 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
       __builtin_amdgcn_global_load_lds((const uint32_t*)(g + 1024), (__attribute__((address_space(3))) uint32_t*)(L.rp + 256), 16, 0, 2);
   };
   if (DBG) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(tprev)::"memory");
-  for (int64_t t = tn; t < S.t1; t = tn) {
+  for (;;) {
     wsync();
     stage1();
     stage2();
-    const int64_t sa = n_sa, sb = n_sb, A = n_A, B = n_B, spos = n_spos;
+    if (n_sa >= n_sb) break;  // no window left
+    const int64_t sa = n_sa, sb = n_sb, A = n_A, B = n_B;
     STAMP(0);
-    if (dma_pending) drain();  // this tile's raw bytes
+    if (dma_pending) drain();  // this window's raw bytes
     dma_pending = false;
     nst = 0;
-    tn = t + nwaves;
-    stage1();
     [&]() {
     if (sa >= sb) return;
     const int ns = (int)(sb - sa);
-    // the tile goes to the exact serial kernel; its sentences are no-ops for
+    // the window goes to the exact serial kernel; its sentences are no-ops for
     // the count / expand passes
     auto fallback = [&]() {
       if (lane == 0) {
         const int at = atomicAdd(S.fb_count, 1);
-        S.fb_list[at] = (int32_t)t;
+        S.fb_list[2 * at] = sa;
+        S.fb_list[2 * at + 1] = sb;
         atomicAdd(S.n_fallback, 1u);
       }
       for (int j = lane_here(); j < ns; j += 64) {
@@ -448,10 +499,12 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
     if (lane < ns) L.sacc[lane] = 0;
     wsync();
     if (lane < ns) {
-      const int pos = (int)(spos - A) + aoff;
+      const int pos = (int)(L.soff[lane] - A) + aoff;
       L.sst[lane] = (uint16_t)pos;
       if (pos < nb) atomicOr(&L.sb[pos >> 5], 1u << (pos & 31));
     }
+    wsync();
+    stage1();  // (soff is read: the next window's offsets may land)
     STAMP(1);
     // ---- 1: raw bytes -> masks + normalised bytes in place ------------------
     uint32_t W, I, S_, CS, D, X, inwin;
@@ -1731,7 +1784,8 @@ static hipError_t launch_scan(const TokParams& P, const SplitParams& S, int n_cu
        per_cu < 1))
     per_cu = 1;
   int64_t grid = (int64_t)n_cu * per_cu;
-  const int64_t need = (S.t1 - S.t0 + WAVES - 1) / WAVES;
+  const int64_t ng = (S.t1 - S.t0 + SUPER - 1) / SUPER;  // super-tiles
+  const int64_t need = (ng + WAVES - 1) / WAVES;
   if (grid > need) grid = need;
   if (grid < 1) grid = 1;
   hipLaunchKernelGGL((scan_kernel<WAVES, DBG, OCC>), dim3((unsigned)grid), dim3(64 * WAVES), 0, s, P, S);
@@ -1782,7 +1836,7 @@ hipError_t launch_tokenize_serial_dense(const TokParams& P, int64_t nbytes, int6
   S.tile_sent = tile_sent;
   S.t0 = 0;
   S.t1 = n_tiles;
-  if ((e = launch_list_all_tiles(n_tiles, S.fb_list, S.fb_count, s)) != hipSuccess) return e;
+  if ((e = launch_list_all_tiles(n_tiles, tile_sent, S.fb_list, S.fb_count, s)) != hipSuccess) return e;
   hipLaunchKernelGGL(smeta_fallback_kernel, dim3(1024), dim3(256), 0, s, S.smeta, P.n_sent);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   return finish_segment(P, S, n_cu, fb_grid, s);
@@ -1831,7 +1885,7 @@ hipError_t launch_tokenize_split(const TokParams& P, int64_t nbytes, int64_t* ti
 hipError_t finish_segment(TokParams P, const SplitParams& S, int n_cu, int fb_grid, hipStream_t s) {
   TokParams F = P;
   F.out_ids = S.ent - (S.t0 << 10);  // the serial path writes at sent_off[s] - sent_off[0]
-  hipError_t e = launch_tokenize_fallback(F, S.tile_sent, S.fb_list, S.fb_count, fb_grid, s);
+  hipError_t e = launch_tokenize_fallback(F, S.fb_list, S.fb_count, fb_grid, s);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(tok5::count_kernel, dim3((unsigned)std::max(1, n_cu * 8)), dim3(256), 0, s, P, S);
   if ((e = hipGetLastError()) != hipSuccess) return e;
