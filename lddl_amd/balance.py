@@ -38,7 +38,8 @@ import time
 
 import numpy as np
 
-__all__ = ['plan', 'plan_files', 'write_shards', 'gather_bin_counts', 'balance_counts', 'main']
+__all__ = ['plan', 'plan_files', 'write_shards', 'gather_bin_counts', 'balance_counts', 'main', 'num_samples_cache',
+           'generate_num_samples_cache']
 
 
 class _Shard:
@@ -402,36 +403,57 @@ def _barrier_tag():
 
 def file_barrier_ref(outdir, rank):
   """Rank 0, before any shard is written: a reference file on the shared
-  filesystem.  Markers are then judged fresh against ITS mtime (set by the
-  same file server clock as theirs), not against rank 0's local clock, which
-  may differ from the other nodes' by more than any margin."""
+  filesystem holding a nonce of this launch.  Every rank's marker carries
+  the nonce it read there, so a marker left by an earlier launch with the
+  same job tag (one that crashed, or a fast requeue in the same allocation)
+  never counts, whatever the clocks say."""
   if rank == 0:
-    with open(os.path.join(outdir, '.lddl_barrier.%s.ref' % _barrier_tag()), 'w') as f:
-      f.write('%d\n' % os.getpid())
+    ref = os.path.join(outdir, '.lddl_barrier.%s.ref' % _barrier_tag())
+    tmp = ref + '.%d' % os.getpid()
+    with open(tmp, 'w') as f:
+      f.write('%d.%.6f.%s\n' % (os.getpid(), time.time(), os.urandom(8).hex()))
+    os.replace(tmp, ref)  # (readers see the whole nonce or none)
 
 
-def _file_barrier(outdir, rank, world, timeout=24 * 3600.0, poll=0.05, margin=60.0):
-  """Every rank drops a marker file named by the job id; rank 0 waits for all
-  of them and removes them.  Only rank 0 acts after the barrier (it removes
-  the inputs and writes .num_samples.json), so the other ranks need not wait.
-  A marker counts when it is no older than rank 0's reference file
-  (file_barrier_ref) minus `margin` seconds: markers of an earlier launch
-  with the same job id (e.g. one that crashed) are older."""
+def _read_nonce(ref):
+  try:
+    with open(ref) as f:
+      v = f.read()
+    return v if v.endswith('\n') else None
+  except OSError:
+    return None
+
+
+def _file_barrier(outdir, rank, world, timeout=24 * 3600.0, poll=0.05, margin=60.0, ref_wait=600.0):
+  """Every rank drops a marker file named by the job tag; rank 0 waits for
+  all of them and removes them.  Only rank 0 acts after the barrier (it
+  removes the inputs and writes .num_samples.json), so the other ranks need
+  not wait.  With rank 0's reference file (file_barrier_ref) a marker counts
+  when it holds that file's nonce (the other ranks wait up to ref_wait
+  seconds for it to appear); without one, when it is no older than rank 0's
+  start minus `margin` seconds."""
   tag = _barrier_tag()
   mk = lambda r: os.path.join(outdir, '.lddl_barrier.%s.%d' % (tag, r))
-  with open(mk(rank), 'w') as f:
-    f.write('done\n')
+  ref = os.path.join(outdir, '.lddl_barrier.%s.ref' % tag)
+  nonce = _read_nonce(ref)
+  if rank != 0:
+    t0 = time.time()
+    while nonce is None and time.time() - t0 < ref_wait and os.path.exists(os.path.dirname(ref)):
+      time.sleep(poll)
+      nonce = _read_nonce(ref)
+  with open(mk(rank) + '.tmp', 'w') as f:
+    f.write(nonce or 'done\n')
+  os.replace(mk(rank) + '.tmp', mk(rank))
   if rank != 0:
     return
-  ref = os.path.join(outdir, '.lddl_barrier.%s.ref' % tag)
   t0 = time.time()
-  try:
-    start = os.stat(ref).st_mtime - margin
-  except OSError:  # (no reference file: this process' start on the local clock)
-    start = _launch_start() - margin
+  start = _launch_start() - margin
 
   def fresh(p):
     try:
+      if nonce is not None:
+        with open(p) as f:
+          return f.read() == nonce
       return os.stat(p).st_mtime >= start
     except OSError:
       return False
@@ -491,6 +513,67 @@ def main(args, rank=None, world=None):
   return written, ns
 
 
+def _parquets_under(indir):
+  """lddl/utils.py get_all_parquets_under: every file under indir whose
+  extension holds '.parquet' (shards and their _<bin> forms), sorted by path"""
+  return sorted(os.path.join(r, f) for r, _, fs in os.walk(indir) for f in fs
+                if '.parquet' in os.path.splitext(f)[1])
+
+
+def num_samples_cache(indir, rank=None, world=None):
+  """load_balance.py:generate_num_samples_cache (:428-455): .num_samples.json
+  for already balanced shards, {basename: rows} in sorted path order, written
+  into indir.  The reference reads every table (get_num_samples_of_parquet,
+  utils.py:77-78) strided over its MPI ranks and Allreduces the counts; here
+  each rank reads the parquet footers (num_rows, no table reads) of one
+  contiguous block of the files and one all-gather (gather_bin_counts, the
+  RCCL / gloo path of the balancer) gives every rank all counts.  Under the
+  file barrier (no collective) rank 0 reads every footer.  Rank 0 writes the
+  file (the reference has every rank write the same bytes).  Returns the
+  dict."""
+  import pyarrow.parquet as pq
+  if rank is None or world is None:
+    rank, world = rank_world()
+  paths = _parquets_under(indir)
+  n = len(paths)
+  kind = barrier_kind(world, rank)
+  counts = np.zeros(n, dtype=np.int64)
+  if kind in ('none', 'file'):
+    if kind == 'file' and rank != 0:
+      return None
+    for i, p in enumerate(paths):
+      counts[i] = pq.ParquetFile(p).metadata.num_rows
+  else:
+    lo, hi = n * rank // world, n * (rank + 1) // world
+    mine = np.array([pq.ParquetFile(p).metadata.num_rows for p in paths[lo:hi]], dtype=np.int64).reshape(-1, 1)
+    if kind == 'mpi4py':
+      from mpi4py import MPI
+      full = np.zeros(n, dtype=np.int64)
+      full[lo:hi] = mine[:, 0]
+      MPI.COMM_WORLD.Allreduce(MPI.IN_PLACE, full, op=MPI.SUM)
+      counts = full
+    else:
+      import torch
+      import torch.distributed as dist
+      if not dist.is_initialized():
+        dist.init_process_group('gloo', rank=rank, world_size=world)
+      dev = torch.device('cuda', torch.cuda.current_device()) if dist.get_backend() == 'nccl' else torch.device('cpu')
+      counts = gather_bin_counts(torch.from_numpy(mine).to(dev), lo)[:, 0]
+  ns = {os.path.basename(p): int(c) for p, c in zip(paths, counts)}
+  if rank == 0:
+    store_num_samples(ns, indir)
+  return ns
+
+
+def generate_num_samples_cache(argv=None):
+  """The reference's `generate_num_samples_cache` console script (setup.py:72)."""
+  parser = argparse.ArgumentParser('Generate .num_samples.json for the balanced parquets.')
+  parser.add_argument('--indir', type=str, default=None, help='path to the dir that contains the balanced shards')
+  parser.add_argument('--num-samples-cache', action='store_true', help=argparse.SUPPRESS)
+  args = parser.parse_args(argv)
+  num_samples_cache(args.indir)
+
+
 def console_script():
   tic = time.perf_counter()
   main(attach_args().parse_args())
@@ -498,4 +581,8 @@ def console_script():
 
 
 if __name__ == '__main__':
-  console_script()
+  import sys
+  if '--num-samples-cache' in sys.argv[1:]:  # python -m lddl_amd.balance --num-samples-cache --indir DIR
+    generate_num_samples_cache()
+  else:
+    console_script()

@@ -67,6 +67,10 @@ constexpr int SCAN_OCC = 5;              // waves per SIMD the scan's LDS admits
 #define LDDL_SCAN_SUPER 16
 #endif
 constexpr int SUPER = LDDL_SCAN_SUPER;   // tiles per super-tile (a wave's unit of hand-out, packed into windows)
+#ifndef LDDL_SCAN_FK
+#define LDDL_SCAN_FK 2
+#endif
+constexpr int FK = LDDL_SCAN_FK;         // fast steps per batch (their probe loads in flight together)
 constexpr int NBUF = CAP + DCAP + 64;    // + over-read pad of the key loads
 constexpr int UCAP = 256;                // units per round
 constexpr int NSCAP = 32;                // sentences per window (< NSCAP: NSCAP sentence offsets staged)
@@ -126,6 +130,29 @@ __device__ __forceinline__ void wsync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+// LDS-DMA (global_load_lds: lane i's bytes land at the LDS base + i * size,
+// M0 = the LDS base) issued from inline asm.  The compiler's wait insertion
+// does not see these loads, so it places no conservative vmcnt wait before
+// every later LDS read (it cannot tell the DMA's target from the arrays the
+// window's steps read, and a wait there also waits for every probe load in
+// flight); the scan drains them itself (drain(): s_waitcnt vmcnt(0)) before
+// it reads what they wrote.  vmcnt counts in issue order, so a wait the
+// compiler places for one of its own loads stays correct: an unseen younger
+// DMA only makes it stricter.  M0 is saved and restored around the load.
+__device__ __forceinline__ void lds_dma4(const void* g, uint32_t* l) {
+  uint32_t t;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(t)
+               : "v"(g), "s"((uint32_t)(uintptr_t)l)
+               : "memory");
+}
+__device__ __forceinline__ void lds_dma16_nt(const void* g, uint32_t* l) {
+  uint32_t t;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+               : "=&s"(t)
+               : "v"(g), "s"((uint32_t)(uintptr_t)l)
+               : "memory");
 }
 // record slot k (of 4 16-B quarters) of slot i, quarter-major: the lanes of a
 // refill, on consecutive slots, load one contiguous run per quarter
@@ -380,9 +407,7 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
   bool dma_pending = false;  // raw-byte DMA issued and not yet waited for
   const int64_t ng = (S.t1 - S.t0 + SUPER - 1) / SUPER;
   // (LDS-DMA: lane i of the instruction writes dword i at the LDS base)
-  auto dma4 = [&](const void* g, uint32_t* l) {
-    __builtin_amdgcn_global_load_lds((const uint32_t*)g, (__attribute__((address_space(3))) uint32_t*)l, 4, 0, 0);
-  };
+  auto dma4 = [&](const void* g, uint32_t* l) { lds_dma4(g, l); };
   auto drain = [&]() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); };
   // (lanes 0-1: tile_sent of super-tile g's first tile, lanes 2-3: of its end -> pb[0..3])
   auto st_bounds = [&](int64_t g) {
@@ -448,10 +473,8 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
     dma_pending = true;
     // streamed once: non-temporal (aux bit 1), keep L2 for the vocab table
     const uint8_t* g = P.bytes + (n_A - aoff) + 16 * ln;
-    if (16 * ln < nb64)
-      __builtin_amdgcn_global_load_lds((const uint32_t*)g, (__attribute__((address_space(3))) uint32_t*)L.rp, 16, 0, 2);
-    if (1024 + 16 * ln < nb64)
-      __builtin_amdgcn_global_load_lds((const uint32_t*)(g + 1024), (__attribute__((address_space(3))) uint32_t*)(L.rp + 256), 16, 0, 2);
+    if (16 * ln < nb64) lds_dma16_nt(g, L.rp);
+    if (1024 + 16 * ln < nb64) lds_dma16_nt(g + 1024, L.rp + 256);
   };
   if (DBG) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(tprev)::"memory");
   for (;;) {
@@ -826,6 +849,7 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
     const bool wbad = __any(bad);
     STAMP(3);
     wsync();
+    stage2();  // (rp is free after the exception pass: the next window's bytes fly behind the rest)
     // ---- 2: units -----------------------------------------------------------
     uint32_t U, SBm;
     int ub, sbb, n, nstarts;
@@ -907,37 +931,40 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
           if (u >= rb && u < rb + nr) up[u - rb] = (uint16_t)(p0 + __ffs(m) - 1);
       }
       wsync();
-      stage2();  // (rp is free: the next tile's bytes fly behind the unit steps)
       STAMP(5);
-      // ---- 3+4, 64 units per step (one per lane), in unit order: prep
-      //      (dirty words, specials, long words), the whole-word probe (slot 0
-      //      of the home bucket; the key loaded and hashed once, a special's
-      //      marker is its key's first byte), then the unit's entry and, for a
-      //      word the probe did not resolve, its WordPiece record from the key
-      //      still in registers.  A unit's entry index is its rank in its
-      //      sentence (ebs); record slots are tile-relative, in unit order,
-      //      from two ballots (a sentence's slots are then contiguous and its
-      //      first is the exclusive sum of the earlier sentences' at the end).
+      // ---- 3, fast steps: 64 units per step (one per lane), in unit order.
+      //      A clean unit of <= 24 bytes (no filler / expansion byte, not a
+      //      literal special) loads its key from the window, hashes it and
+      //      probes slot 0 of its home bucket (one 32-B load, an xor / or
+      //      compare); a hit writes its entry (the vocab id at the unit's rank
+      //      in its sentence, ebs).  Every other unit -- a probe miss, a dirty
+      //      span, a special, a key longer than 24 bytes -- is listed for the
+      //      record pass (its unit index, flagged MISS when the probe already
+      //      missed).  The fast step holds no per-mode code: one path, no LDS
+      //      writes but the list.
+      // ---- 4, record pass over the listed units, 64 per step, in unit order:
+      //      dirty words normalised, specials, > 100-char words -> [UNK], the
+      //      probe of a dirty word, then the entries and, for a word no probe
+      //      resolved, its WordPiece record from the key in registers.  Record
+      //      slots are tile-relative, in unit order, from two ballots (a
+      //      sentence's slots are then contiguous and its first is the
+      //      exclusive sum of the earlier sentences' at the end).
       {
         const int mb0 = (int)P.maxb[0];
         const uint32_t vmask = P.vt_mask;
-        for (int r = 0; r < nr; r += 64) {
-          const int u = r + lane;
-          const bool valid = u < nr;
-          uint32_t w = 0;
-          uint16_t id = U_EMPTY;
-          // the unit: start p (window position), span end q = the next break
-          // (the owning lane's own bits, else its later-lane position), dirty
-          // (a filler / expansion byte in [p, q)) and sentence sj
-          const int p = valid ? (int)reinterpret_cast<const uint16_t*>(L.xm)[u] : 0;
+        const int mbf = min(mb0, 24);
+        // the unit: start p (window position), span end q = the next break
+        // (the owning lane's own bits, else its later-lane position), dirty
+        // (a filler / expansion byte in [p, q)) and sentence sj
+        auto decode = [&](int u, bool valid, int& p, int& q, bool& dirty, uint32_t& sj) {
+          p = valid ? (int)reinterpret_cast<const uint16_t*>(L.xm)[u] : 0;
           const int wl = p >> 5, b = p & 31, p0 = p & ~31;
           const uint32_t brk = L.brk[wl], Dl = L.dm[wl], SBl = L.sb[wl], lx = L.xm[128 + wl];
           const uint32_t rest = brk & ~((2u << b) - 1u);
-          const int q = rest ? min(p0 + __ffs(rest) - 1, nb) : (int)(lx & 0xFFFu);
+          q = rest ? min(p0 + __ffs(rest) - 1, nb) : (int)(lx & 0xFFFu);
           uint32_t own = Dl & ~((1u << b) - 1u);
           if (q < p0 + 32) own &= (1u << (q - p0)) - 1u;
-          const bool dirty = valid && (own != 0 || (q > p0 + 32 && (int)((lx >> 12) & 0xFFFu) < q));
-          uint32_t sj;
+          dirty = valid && (own != 0 || (q > p0 + 32 && (int)((lx >> 12) & 0xFFFu) < q));
           if (starts_distinct) {
             sj = (lx >> 24) + (uint32_t)__popc(SBl & ((2u << b) - 1u)) - 1u;
           } else {
@@ -949,6 +976,86 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
             }
             sj = (uint32_t)lo;
           }
+        };
+        // the deferred units of the round (u16: unit | MISS << 15), in the
+        // lanes' unit bases' place (free once the sentences' first units are set)
+        uint16_t* const dl = reinterpret_cast<uint16_t*>(L.xm + 192);
+        constexpr uint32_t DL_MISS = 0x8000u;
+        uint32_t ndef = 0;
+        // FK steps per batch: every step's key, hash and probe loads first,
+        // then the compares, so the batch's probe round trips overlap (the
+        // loads of a batch are issued back to back; no store sits between
+        // them and their first use)
+        const bool fprobe = P.st == nullptr || LDDL_PROBE_L2;  // (the two-choice scan table: probed in the record pass)
+        // (the entry buffer's last element: no unit's entry, no serial-path id reaches it,
+        // capi.hip sizes it seg_tiles * 1 KiB + max_tok + 4096)
+        const int64_t ent_spare = S.seg_tiles * 1024 + max_tok + 4095;
+        for (int r = 0; r < nr; r += 64 * FK) {
+          Key6 key[FK];
+          uint4 fa[FK], fb[FK];
+          bool probe[FK], dirty[FK];
+          int len[FK];
+          uint32_t sj[FK];
+#pragma unroll
+          for (int k = 0; k < FK; ++k) {
+            const int u = r + 64 * k + lane;
+            const bool valid = u < nr;
+            int p, q;
+            decode(u, valid, p, q, dirty[k], sj[k]);
+            len[k] = q - p;
+            probe[k] = fprobe && valid && !dirty[k] && len[k] <= mbf;
+            // (every lane: the key's reads depend on p alone and fly with the mask reads)
+            key[k] = load_key(L.nb, p, len[k]);
+            probe[k] = probe[k] && !((key[k].d0 & 0xFFu) >= BS && (key[k].d0 & 0xFFu) < BS + 5);
+            // (every lane loads: a lane with nothing to probe reads bucket 0)
+            const uint32_t hk = probe[k] ? key_hash(key[k], len[k], 0u) : 0u;
+            const uint4* bk = P.vt + 4 * (hk & vmask & ((LDDL_PROBE_L2 == 1 || LDDL_PROBE_L2 == 2) ? 0x3FFFu : ~0u));
+            fa[k] = bk[0];
+            fb[k] = bk[1];
+          }
+          STAMP(12);
+#pragma unroll
+          for (int k = 0; k < FK; ++k) {
+            const int u = r + 64 * k + lane;
+            const bool valid = u < nr;
+            const uint32_t want = ((uint32_t)len[k] << 16) | 0x80000000u;
+            // (branch-free: a branch around the compare leaves the batch's loads
+            // pending on one path, and the join then waits for every store too)
+            const bool eq = LDDL_PROBE_L2 >= 2 || slot_eq(fa[k], fb[k], key[k], want);
+            const bool hit = probe[k] & eq;
+            const uint32_t id = fb[k].z & 0xFFFFu;
+            // every lane stores (no branch around a store: the join after one
+            // waits for it): a hit its id, a deferred unit a hole the record
+            // pass overwrites (same wave, same address, in order), a lane past
+            // the round's units the segment buffer's spare last entry
+            S.ent[valid ? ent0 + (int)L.ebs[sj[k]] + rb + u : ent_spare] = (uint16_t)(hit ? id : SPLIT_EHOLE);
+            // ([CLS] / [SEP] come only from literal specials, never from WordPiece;
+            // a flag past the sentence's max_tok cut is harmless: the masked
+            // packer then checks the ids themselves)
+            const bool spc = hit && (id == P.special[2] || id == P.special[3]);
+            if (__ballot(spc) != 0 && spc) atomicOr(&L.sspec[sj[k] >> 5], 1u << (sj[k] & 31));
+            // (a clean key longer than any whole-word key misses without a probe)
+            const bool dfr = valid && !hit;
+            const uint64_t D = __ballot(dfr);
+            if (dfr)
+              dl[ndef + lane_rank(D)] =
+                  (uint16_t)((uint32_t)u | (!dirty[k] && len[k] <= 24 && (probe[k] || len[k] > mb0) ? DL_MISS : 0u));
+            ndef += (uint32_t)__popcll(D);
+          }
+          STAMP(7);
+        }
+        wsync();
+        for (int r = 0; r < (int)ndef; r += 64) {
+          const bool valid = r + lane < (int)ndef;
+          const uint32_t de = valid ? dl[r + lane] : 0u;
+          const int u = (int)(de & 0x7FFFu);
+          const bool miss = (de & DL_MISS) != 0;
+          uint32_t w = 0;
+          uint16_t id = U_EMPTY;
+          int p, q;
+          bool dirty;
+          uint32_t sj;
+          decode(u, valid, p, q, dirty, sj);
           STAMP(12);
           int src = p, len = valid ? q - p : 0;
           bool lovf = false;  // the tile falls back: side buffer full, or a queued word too long for a record
@@ -973,7 +1080,7 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
             }
           }
           STAMP(6);
-          if (w != 0 && len <= 24 && len <= mb0) {
+          if (w != 0 && !miss && len <= 24 && len <= mb0) {
             const uint32_t hk = key_hash(key, len, 0u), want = ((uint32_t)len << 16) | 0x80000000u;
             if (P.st && !LDDL_PROBE_L2) {
               // the scan table: both candidate slots loaded before either compare

@@ -221,6 +221,7 @@ class PackHandle:
     h = ctypes.c_void_p()
     _lib.check(_lib.lib().lddl_pack_new(tok.handle, ctypes.byref(h)))
     self._h = h.value
+    self._out = {}  # the PackResult columns of packs into this handle (Packer._buf)
 
   @property
   def handle(self):
@@ -256,11 +257,15 @@ class Packer:
     self.result = PackHandle(self.tok)
     self._out = {}
 
-  def _buf(self, name, n, dtype):
-    t = self._out.get(name)
+  def _buf(self, name, n, dtype, owner=None):
+    """a cached device buffer of >= n entries; owner: the PackHandle whose
+    PackResult columns it holds (each handle its own, so that several pack
+    results stay live at once), else the Packer's (the tokenizer output)"""
+    out = self._out if owner is None else owner._out
+    t = out.get(name)
     if t is None or t.numel() < n or t.dtype != dtype:
       t = torch.empty(max(n, 1), dtype=dtype, device=self.device)
-      self._out[name] = t
+      out[name] = t
     return t
 
   @staticmethod
@@ -327,18 +332,21 @@ class Packer:
       raise AssertionError(L.lddl_last_error().decode())
     _lib.check(rc)
     n_pairs, n_tokens, nbins = int(tot[0]), int(tot[1]), int(tot[2])
+
+    def buf(name, n, dtype):
+      return self._buf(name, n, dtype, into)
     res = PackResult(n_pairs, n_tokens, nbins,
-                     None if spans else self._buf('tokens', n_tokens, torch.int16),
-                     self._buf('tok_off', n_pairs + 1, torch.int64),
-                     self._buf('len0', n_pairs, torch.int16), self._buf('len1', n_pairs, torch.int16),
-                     self._buf('flags', n_pairs, torch.uint8), self._buf('bins', n_pairs, torch.uint8),
-                     self._buf('part', n_pairs, torch.int64),
-                     self._buf('bin_count', shards.n_part * nbins, torch.int64))
+                     None if spans else buf('tokens', n_tokens, torch.int16),
+                     buf('tok_off', n_pairs + 1, torch.int64),
+                     buf('len0', n_pairs, torch.int16), buf('len1', n_pairs, torch.int16),
+                     buf('flags', n_pairs, torch.uint8), buf('bins', n_pairs, torch.uint8),
+                     buf('part', n_pairs, torch.int64),
+                     buf('bin_count', shards.n_part * nbins, torch.int64))
     res.cls_id, res.sep_id = self.tok.cls_id, self.tok.sep_id
     res.pack = into
     if spans:
-      res.src0 = self._buf('src0', n_pairs, torch.int64)
-      res.src1 = self._buf('src1', n_pairs, torch.int64)
+      res.src0 = buf('src0', n_pairs, torch.int64)
+      res.src1 = buf('src1', n_pairs, torch.int64)
       _lib.check(L.lddl_row_spans(self.tok.handle, h, _ptr(res.src0), _ptr(res.src1), _ptr(res.tok_off),
                                   _ptr(res.len0), _ptr(res.len1), _ptr(res.flags), _ptr(res.bins),
                                   _ptr(res.part), _ptr(res.bin_count), s))
@@ -350,11 +358,11 @@ class Packer:
     res.ids, res.ntok, res.ids_off = ids, ntok, tok_off
     if masking and not codebert:
       res.n_masked = int(tot[3])
-      res.mlm_off = self._buf('mlm_off', n_pairs + 1, torch.int64)
-      res.mlm_pos = self._buf('mlm_pos', res.n_masked, torch.int16)
-      res.mlm_label = self._buf('mlm_label', res.n_masked, torch.int16)
+      res.mlm_off = buf('mlm_off', n_pairs + 1, torch.int64)
+      res.mlm_pos = buf('mlm_pos', res.n_masked, torch.int16)
+      res.mlm_label = buf('mlm_label', res.n_masked, torch.int16)
       if spans:
-        res.mlm_token = self._buf('mlm_token', res.n_masked, torch.int16)
+        res.mlm_token = buf('mlm_token', res.n_masked, torch.int16)
         _lib.check(L.lddl_masked_lm_spans(self.tok.handle, h, _ptr(ids), _ptr(res.src0), _ptr(res.src1),
                                           _ptr(res.len0), _ptr(res.part), _ptr(res.mlm_off), _ptr(res.mlm_pos),
                                           _ptr(res.mlm_label), _ptr(res.mlm_token), s))

@@ -322,6 +322,7 @@ class ProcessEncoder:
     self.dir = tempfile.mkdtemp(prefix='lddl_enc_', dir=d)
     self.slots = [dict(path=os.path.join(self.dir, 'slot%d' % i), size=0, mm=None, t=None, pinned=False, futs=[])
                   for i in range(slots)]
+    self.disk_dir = None  # (slots that outgrew /dev/shm: _grow)
     self.next = 0
     self.wait_s = 0.0  # waiting for a slot's previous batch to finish encoding
     self.copy_s = 0.0  # columns into the slots (device copies included)
@@ -339,6 +340,41 @@ class ProcessEncoder:
       torch.cuda.cudart().cudaHostUnregister(sl['t'].data_ptr())
       sl['pinned'] = False
 
+  def _grow(self, sl, new):
+    """The slot file at `new` bytes, its space reserved (posix_fallocate), so
+    a full tmpfs is an OSError here and not a SIGBUS in the copy into the
+    mapping (the /dev/shm check at construction sees neither the slots'
+    growth nor the other ranks of the node).  A slot that no longer fits in
+    /dev/shm moves to a directory on disk."""
+    import errno
+    import mmap
+    for attempt in range(2):
+      fd = os.open(sl['path'], os.O_RDWR | os.O_CREAT, 0o600)
+      try:
+        os.ftruncate(fd, new)
+        try:
+          os.posix_fallocate(fd, 0, new)
+        except OSError as e:
+          if e.errno not in (errno.ENOSPC, errno.EFBIG, errno.EDQUOT) or attempt:
+            raise OSError(e.errno, 'parquet encoder slot of %d MB: no space in %s (%s)' % (
+                new >> 20, os.path.dirname(sl['path']), e.strerror)) from e
+          os.ftruncate(fd, 0)
+          if self.disk_dir is None:
+            import shutil
+            import tempfile
+            import weakref
+            self.disk_dir = tempfile.mkdtemp(prefix='lddl_enc_')
+            self._fin_disk = weakref.finalize(self, shutil.rmtree, self.disk_dir, True)
+          os.close(fd)
+          fd = -1
+          os.remove(sl['path'])
+          sl['path'] = os.path.join(self.disk_dir, os.path.basename(sl['path']))
+          continue
+        return mmap.mmap(fd, new)
+      finally:
+        if fd >= 0:
+          os.close(fd)
+
   def _acquire(self, size):
     sl = self.slots[self.next]
     self.next = (self.next + 1) % len(self.slots)
@@ -355,12 +391,7 @@ class ProcessEncoder:
         sl['mm'].close()
       new = max(size, 2 * sl['size'], 64 << 20)
       new = (new + (1 << 21) - 1) & ~((1 << 21) - 1)
-      fd = os.open(sl['path'], os.O_RDWR | os.O_CREAT, 0o600)
-      try:
-        os.ftruncate(fd, new)
-        sl['mm'] = mmap.mmap(fd, new)
-      finally:
-        os.close(fd)
+      sl['mm'] = self._grow(sl, new)
       sl['size'] = new
       sl['t'] = torch.frombuffer(sl['mm'], dtype=torch.uint8)
       if torch.cuda.is_initialized():
@@ -437,6 +468,8 @@ class ProcessEncoder:
         sl['mm'] = None
     t2 = time.perf_counter()
     self._fin()
+    if self.disk_dir is not None:
+      self._fin_disk()
     self.close_s = (t1 - t0, t2 - t1, time.perf_counter() - t2)  # workers' exit, slot unpin / unmap, slot files
 
 
@@ -446,7 +479,10 @@ def _host_var(arr, r0, n):
   wide = a.type in (pa.large_string(), pa.large_binary())
   off = np.frombuffer(a.buffers()[1], dtype=np.int64 if wide else np.int32, count=a.offset + n + 1)[a.offset:]
   off = off.astype(np.int64)
-  data = np.frombuffer(a.buffers()[2], dtype=np.uint8, count=int(off[-1]))[int(off[0]):] if n else np.zeros(0, np.uint8)
+  buf = a.buffers()[2]
+  # (Arrow may leave the data buffer out when every string of the slice is empty)
+  data = np.frombuffer(buf, dtype=np.uint8, count=int(off[-1]))[int(off[0]):] if n and buf is not None and off[-1] \
+      else np.zeros(0, np.uint8)
   return off - off[0], data
 
 

@@ -28,7 +28,7 @@ def test_plan_matches_reference(k, strict):
     return
   if c['error'] == 'TimeoutError':  # the reference never finishes
     if strict:
-      with pytest.raises(RuntimeError):
+      with pytest.raises(RuntimeError, match='load balance cannot finish'):
         balance.plan_files(c['files'], c['counts'], c['num_shards'], c['bin_ids'], strict)
       return
     shards, ns = balance.plan_files(c['files'], c['counts'], c['num_shards'], c['bin_ids'], strict)
@@ -258,23 +258,98 @@ def test_mpi4py_not_initialised_without_an_mpi_launcher(monkeypatch):
   assert balance.barrier_kind(2, 0) == 'file'
 
 
-def test_file_barrier_judges_markers_by_the_shared_clock(tmp_path, monkeypatch):
-  """markers are judged against rank 0's reference file on the
-  shared filesystem (one clock), not rank 0's local start time: a marker a
-  little older than rank 0's process start (another node's clock behind)
-  still counts; one older than the reference by more than the margin does not"""
+def test_file_barrier_markers_carry_the_launch_nonce(tmp_path, monkeypatch):
+  """with rank 0's reference file a marker counts when it holds
+  the file's nonce: a marker of an earlier launch with the same job tag is
+  refused however fresh its mtime (a fast requeue), one of this launch is
+  taken however old (another node's clock behind)"""
   for k in balance._JOB_ENV:
     monkeypatch.delenv(k, raising=False)
   monkeypatch.setenv('PMIX_NAMESPACE', 'launch-c')
   monkeypatch.setattr(balance, '_launch_start', lambda: 2e9)  # a local clock far ahead of the file server's
-  balance.file_barrier_ref(str(tmp_path), 0)
+  d = str(tmp_path)
+  balance.file_barrier_ref(d, 0)
+  old_nonce = (tmp_path / '.lddl_barrier.launch-c.ref').read_text()
+  balance._file_barrier(d, 1, 2)  # an earlier launch's rank 1 ...
+  balance.file_barrier_ref(d, 0)  # ... then this launch's rank 0
   ref = tmp_path / '.lddl_barrier.launch-c.ref'
-  t_ref = os.stat(str(ref)).st_mtime
+  assert ref.read_text() != old_nonce
   m1 = tmp_path / '.lddl_barrier.launch-c.1'
-  m1.write_text('done\n')
-  os.utime(str(m1), (t_ref - 3600, t_ref - 3600))  # an earlier launch's
+  assert m1.read_text() == old_nonce
   with pytest.raises(RuntimeError):
-    balance._file_barrier(str(tmp_path), 0, 2, timeout=0.3)
-  os.utime(str(m1), (t_ref - 30, t_ref - 30))  # this launch, written by a node whose clock is behind
-  balance._file_barrier(str(tmp_path), 0, 2, timeout=5)
-  assert not [n for n in os.listdir(str(tmp_path)) if n.startswith('.lddl_barrier')]
+    balance._file_barrier(d, 0, 2, timeout=0.3)
+  balance._file_barrier(d, 1, 2)  # this launch's rank 1
+  os.utime(str(m1), (1e9, 1e9))
+  balance._file_barrier(d, 0, 2, timeout=5)
+  assert not [n for n in os.listdir(d) if n.startswith('.lddl_barrier')]
+
+
+NSC = json.load(open(os.path.join(os.path.dirname(__file__), 'golden', 'num_samples_cache.json')))
+
+
+def _nsc_tree(d):
+  for rel, n in NSC['files']:
+    p = os.path.join(d, rel)
+    os.makedirs(os.path.dirname(p), exist_ok=True)
+    pq.write_table(pa.table({'A': pa.array(['a %d' % i for i in range(n)], pa.string()),
+                             'num_tokens': pa.array(np.arange(n, dtype=np.uint16))}), p)
+  for rel in NSC['other']:
+    with open(os.path.join(d, rel), 'w') as f:
+      f.write('x\n')
+
+
+def test_num_samples_cache_matches_reference(tmp_path):
+  """generate_num_samples_cache (load_balance.py:428-455): the same bytes as
+  the reference's .num_samples.json over the same tree (golden written by
+  tools/gen_golden_num_samples.py from the reference with a one-rank MPI stub)"""
+  _nsc_tree(str(tmp_path))
+  ns = balance.num_samples_cache(str(tmp_path), 0, 1)
+  with open(str(tmp_path / '.num_samples.json')) as f:
+    assert f.read() == NSC['num_samples_json']
+  assert list(ns.items()) == list(json.loads(NSC['num_samples_json']).items())
+
+
+def test_num_samples_cache_console(tmp_path):
+  import subprocess
+  _nsc_tree(str(tmp_path))
+  root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+  p = subprocess.run([sys.executable, '-m', 'lddl_amd.balance', '--num-samples-cache', '--indir', str(tmp_path)],
+                     cwd=root, capture_output=True, text=True, timeout=120, env=_clean_env())
+  assert p.returncode == 0, p.stderr
+  with open(str(tmp_path / '.num_samples.json')) as f:
+    assert f.read() == NSC['num_samples_json']
+
+
+def _nsc_rank(rank, world, port, d, q):
+  os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+  import torch.distributed as dist
+  dist.init_process_group('gloo', rank=rank, world_size=world)
+  try:
+    q.put((rank, balance.num_samples_cache(d, rank, world)))
+  finally:
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('world', [2, 3])
+def test_num_samples_cache_gloo(tmp_path, world):
+  """ranks read the footers of one block of the files each and all-gather the
+  counts (gather_bin_counts): every rank gets the whole dict, rank 0 writes
+  the reference's bytes"""
+  import socket
+  _nsc_tree(str(tmp_path))
+  with socket.socket() as s:
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+  ctx = mp.get_context('spawn')
+  q = ctx.Queue()
+  ps = [ctx.Process(target=_nsc_rank, args=(r, world, port, str(tmp_path), q)) for r in range(world)]
+  for p in ps:
+    p.start()
+  got = dict(q.get(timeout=120) for _ in range(world))
+  for p in ps:
+    p.join(60)
+  assert all(p.exitcode == 0 for p in ps)
+  want = json.loads(NSC['num_samples_json'])
+  assert all(list(got[r].items()) == list(want.items()) for r in range(world))
+  with open(str(tmp_path / '.num_samples.json')) as f:
+    assert f.read() == NSC['num_samples_json']

@@ -183,6 +183,29 @@ def test_two_pack_results_coexist(packer):
     h.close()
 
 
+def test_packer_results_into_two_handles_stay_live(packer):
+  """Packer.pack into a second PackHandle keeps its PackResult
+  columns in buffers of that handle, so the first result's columns are not
+  overwritten (each equals the same pack done alone)"""
+  from lddl_amd import synth, pipeline
+  cs = [synth.make_wiki(300_000, seed=15), synth.make_wiki(250_000, seed=16)]
+  cfg = [dict(target_seq_length=128, bin_size=32, seed=3), dict(target_seq_length=256, bin_size=64, seed=4)]
+  sets = []
+  for c in cs:
+    sh = pipeline.upload(c, pipeline.partition_by_bytes(c, 2), 'cuda')
+    ids, ntok, toff = packer.tokenize(sh)
+    sets.append((sh, ids.clone(), ntok.clone(), toff.clone()))
+  alone = [packer.pack(sh, ids, ntok, toff, spans=True, **kw).rows() for (sh, ids, ntok, toff), kw in zip(sets, cfg)]
+  h2 = pipeline.PackHandle(packer.tok)
+  try:
+    r1 = packer.pack(*sets[0], spans=True, **cfg[0])
+    r2 = packer.pack(*sets[1], spans=True, into=h2, **cfg[1])
+    assert r2.rows() == alone[1]
+    assert r1.rows() == alone[0]  # (read after the second pack)
+  finally:
+    h2.close()
+
+
 def test_pack_result_states(packer):
   """a fresh result has nothing to materialise; a failed pack empties the
   result it was packing into and leaves the others alone"""

@@ -92,3 +92,49 @@ def test_process_encoder_writes_what_pyarrow_writes(tmp_path):
   finally:
     enc.close()
   assert not os.path.exists(enc.dir)
+
+
+def test_process_encoder_slot_moves_to_disk_when_tmpfs_is_full(tmp_path, monkeypatch):
+  """a slot that grows past the tmpfs' free space reserves it
+  (posix_fallocate) and so sees ENOSPC as an OSError, and moves to a
+  directory on disk instead of faulting (SIGBUS) in the copy"""
+  import errno
+  import pyarrow.parquet as pq
+  enc = writer.ProcessEncoder(workers=1, slots=1)
+  real = os.posix_fallocate
+  full = enc.dir
+
+  def falloc(fd, off, n):
+    if os.readlink('/proc/self/fd/%d' % fd).startswith(full):
+      raise OSError(errno.ENOSPC, 'No space left on device')
+    return real(fd, off, n)
+  monkeypatch.setattr(os, 'posix_fallocate', falloc)
+  try:
+    sch = writer.schema()
+    n = 300
+    off = np.arange(n + 1, dtype=np.int64) * 3
+    data = np.frombuffer(b'abc' * n, dtype=np.uint8)
+    specs = [('A', 'str', off, data), ('B', 'str', off, data), ('is_random_next', 'bool', np.zeros(n, bool), None),
+             ('num_tokens', 'u16', np.full(n, 7, np.uint16), None)]
+    f = str(tmp_path / 'x.parquet')
+    for f_ in enc.submit_batch(n, specs, sch, [(f, 0, n)], 'snappy', ['is_random_next', 'num_tokens']):
+      f_.result()
+    assert enc.disk_dir is not None and enc.slots[0]['path'].startswith(enc.disk_dir)
+    t = pq.read_table(f)
+    assert t.column('A').to_pylist() == ['abc'] * n and t.column('num_tokens').to_pylist() == [7] * n
+  finally:
+    enc.close()
+  assert not os.path.exists(enc.dir) and not os.path.exists(enc.disk_dir)
+
+
+def test_host_var_all_empty_strings():
+  """Arrow may leave the data buffer out of a slice whose strings
+  are all empty"""
+  a = pa.array(['', '', ''], pa.string())
+  off, data = writer._host_var(a, 0, 3)
+  assert off.tolist() == [0, 0, 0, 0] and data.size == 0
+  b = pa.array(['x', '', '', 'yz'], pa.string())
+  off, data = writer._host_var(b, 1, 2)
+  assert off.tolist() == [0, 0, 0] and data.size == 0
+  off, data = writer._host_var(b, 2, 2)
+  assert off.tolist() == [0, 0, 2] and bytes(data) == b'yz'

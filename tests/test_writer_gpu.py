@@ -208,10 +208,9 @@ def test_cli_bert_end_to_end(gpu, tmp_path):
   # load balancer over the written shards: every row lands exactly once
   bargs = balance.attach_args().parse_args(['--indir', str(sink), '--outdir', str(tmp_path / 'bal'),
                                             '--num-shards', '3', '--keep-orig'])
-  try:
-    written, ns = balance.main(bargs)
-  except RuntimeError:
-    pytest.skip('counts hit the reference load balancer non-termination case')
+  # (these counts are ones the reference's balancer finishes; its non-terminating
+  # case is a CPU test of balance.plan: tests/test_balance.py)
+  written, ns = balance.main(bargs)
   for b in range(4):
     n_in = sum(len(_bin_rows(rows, 32, 4)[b]) for rows in exp)
     assert sum(v for k, v in ns.items() if k.endswith('_%d' % b)) == n_in
