@@ -71,6 +71,10 @@ constexpr int SUPER = LDDL_SCAN_SUPER;   // tiles per super-tile (a wave's unit 
 #define LDDL_SCAN_FK 2
 #endif
 constexpr int FK = LDDL_SCAN_FK;         // fast steps per batch (their probe loads in flight together)
+#ifndef LDDL_SCAN_FKEY
+#define LDDL_SCAN_FKEY 16
+#endif
+constexpr int FKEY = LDDL_SCAN_FKEY;     // longest key the fast step probes (16 or 24 bytes)
 constexpr int NBUF = CAP + DCAP + 64;    // + over-read pad of the key loads
 constexpr int UCAP = 256;                // units per round
 constexpr int NSCAP = 32;                // sentences per window (< NSCAP: NSCAP sentence offsets staged)
@@ -317,6 +321,21 @@ __device__ __forceinline__ Key6 load_key(const uint32_t* nb, int s, int len) {
   k.d5 = keep_bytes(__builtin_amdgcn_alignbyte(x6, x5, sh), lc - 20);
   return k;
 }
+// the first min(len, 16) bytes at s, zero beyond (d4 = d5 = 0): the fast
+// step's key (a whole word of <= 16 bytes: five LDS reads, four byte aligns)
+__device__ __forceinline__ Key6 load_key16(const uint32_t* nb, int s, int len) {
+  const int a = s >> 2;
+  const uint32_t sh = (uint32_t)(s & 3);
+  const uint32_t x0 = nb[a], x1 = nb[a + 1], x2 = nb[a + 2], x3 = nb[a + 3], x4 = nb[a + 4];
+  const int lc = min(len, 16);
+  Key6 k;
+  k.d0 = keep_bytes(__builtin_amdgcn_alignbyte(x1, x0, sh), lc);
+  k.d1 = keep_bytes(__builtin_amdgcn_alignbyte(x2, x1, sh), lc - 4);
+  k.d2 = keep_bytes(__builtin_amdgcn_alignbyte(x3, x2, sh), lc - 8);
+  k.d3 = keep_bytes(__builtin_amdgcn_alignbyte(x4, x3, sh), lc - 12);
+  k.d4 = k.d5 = 0;
+  return k;
+}
 // a value the optimiser cannot see through: keeps the xor / or reduction
 // below (v_xor + v_or3) from being rewritten into one compare per dword,
 // materialised bools and 16-bit shifts
@@ -462,7 +481,7 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
     const int ln = lane_here();
     const bool in = ln >= 1 && ln < NSCAP && cs + ln <= ce;
     const uint64_t fit = __ballot(in && L.soff[in ? ln : 0] <= a - aoff + CAP);
-    const int ns = max(__popcll(fit), 1);  // (0: the first sentence alone is longer; it falls back)
+    const int ns = max((int)__popcll(fit), 1);  // (0: the first sentence alone is longer; it falls back)
     n_sa = cs;
     n_sb = cs + ns;
     n_A = a;
@@ -923,12 +942,24 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
         // bits: the loop runs the wave's largest count at about half the
         // lanes busy, so a unit's span end, dirtiness and sentence are
         // derived in the unit step below, one unit per lane)
+        // Four units per iteration, every write unconditional: a rank outside
+        // the round ([k0, k1) are the lane's units in it) writes a spare LDS
+        // word instead (only the lane the round starts in skips any)
         uint16_t* const up = reinterpret_cast<uint16_t*>(L.xm);
+        uint16_t* const spare = reinterpret_cast<uint16_t*>(&L.misc[3]);
         const uint32_t Ul = L.um[lane];
         const int p0 = lane * 32;
-        int u = ub;
-        for (uint32_t m = Ul; m; m &= m - 1, ++u)
-          if (u >= rb && u < rb + nr) up[u - rb] = (uint16_t)(p0 + __ffs(m) - 1);
+        const int k0 = max(rb - ub, 0), k1 = min(rb + nr - ub, (int)__popc(Ul));
+        uint32_t m = Ul;
+        for (int k = 0; k < k1; k += 4) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int kk = k + j;
+            uint16_t* const dst = kk >= k0 && kk < k1 ? up + (ub + kk - rb) : spare;
+            *dst = (uint16_t)(p0 + __builtin_ctz(m | 0x80000000u));
+            m &= m - 1;
+          }
+        }
       }
       wsync();
       STAMP(5);
@@ -952,7 +983,7 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
       {
         const int mb0 = (int)P.maxb[0];
         const uint32_t vmask = P.vt_mask;
-        const int mbf = min(mb0, 24);
+        const int mbf = min(mb0, FKEY);  // (a clean key of FKEY < len <= 24 bytes: probed in the record pass)
         // the unit: start p (window position), span end q = the next break
         // (the owning lane's own bits, else its later-lane position), dirty
         // (a filler / expansion byte in [p, q)) and sentence sj
@@ -1005,7 +1036,7 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
             len[k] = q - p;
             probe[k] = fprobe && valid && !dirty[k] && len[k] <= mbf;
             // (every lane: the key's reads depend on p alone and fly with the mask reads)
-            key[k] = load_key(L.nb, p, len[k]);
+            key[k] = FKEY == 16 ? load_key16(L.nb, p, len[k]) : load_key(L.nb, p, len[k]);
             probe[k] = probe[k] && !((key[k].d0 & 0xFFu) >= BS && (key[k].d0 & 0xFFu) < BS + 5);
             // (every lane loads: a lane with nothing to probe reads bucket 0)
             const uint32_t hk = probe[k] ? key_hash(key[k], len[k], 0u) : 0u;
