@@ -419,7 +419,7 @@ extern "C" int lddl_tokenize(lddl_ctx* c, const uint8_t* d_bytes, int64_t nbytes
        (rc = ws_get(c, 43, n_sent, &S.snslot)) || (rc = ws_get(c, 44, (size_t)slots, &S.cnt8))))
     return rc;
   int64_t* tile_off = nullptr;
-  if (c->tok_algo != 0 && (rc = ws_get(c, 46, nt + 1, &tile_off))) return rc;
+  if (c->tok_algo == 6 && (rc = ws_get(c, 46, nt + 1, &tile_off))) return rc;  // (the lane tokenizer's tile starts)
   S.tile_off = tile_off;
   S.chunk_ctr = S.chunk_fill + n_chunks;
   S.n_chunks = (uint32_t)n_chunks;

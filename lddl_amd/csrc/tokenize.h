@@ -53,8 +53,10 @@ struct TokParams {
 };
 
 int64_t tile_count(int64_t nbytes);
+// tile_sent (and tile_off) of every tile, or with sup > 1 only of the tiles
+// (t % seg) % sup == 0 and of n_tiles (what the split scan reads)
 hipError_t launch_tile_bounds(const int64_t* sent_off, int64_t n_sent, int64_t n_tiles, int64_t* tile_sent,
-                              int64_t* tile_off, hipStream_t s);
+                              int64_t* tile_off, hipStream_t s, int64_t seg = 0, int sup = 1);
 // fb_list: *fb_count sentence ranges [fb_list[2k], fb_list[2k+1]) for the
 // exact serial path (a scan window or a tile it did not model)
 hipError_t launch_tokenize_fallback(const TokParams& P, const int64_t* fb_list, const int32_t* fb_count, int grid,

@@ -25,9 +25,12 @@ namespace lddl {
 
 constexpr int TILE_SHIFT = 10;  // nominal tile: sentences starting in 1 KiB
 
-// tile_sent[t] = first sentence whose start (relative) >= t * TILE
+// tile_sent[t] = first sentence whose start (relative) >= t * TILE, for the
+// tiles t the caller reads: (t % seg) % sup == 0 (the split scan's
+// super-tile starts in each segment of seg tiles; sup = 1: every tile) and
+// t = n_tiles
 __global__ void tile_bounds_kernel(const int64_t* sent_off, int64_t n_sent, int64_t n_tiles, int64_t* tile_sent,
-                                   int64_t* tile_off) {
+                                   int64_t* tile_off, int64_t seg, int sup) {
   const int64_t base = sent_off[0];
   for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s <= n_sent; s += (int64_t)gridDim.x * blockDim.x) {
     // tiles t with off[s-1] < t*TILE <= off[s] map to s (s = n_sent: the rest)
@@ -37,6 +40,7 @@ __global__ void tile_bounds_kernel(const int64_t* sent_off, int64_t n_sent, int6
     if (lo < 0) t0 = 0;
     const int64_t t1 = hi >> TILE_SHIFT;  // last t with t*TILE <= hi
     for (int64_t t = t0; t <= t1 && t <= n_tiles; ++t) {
+      if ((t % seg) % sup != 0 && t != n_tiles) continue;
       tile_sent[t] = s;
       if (tile_off) tile_off[t] = sent_off[s];
     }
@@ -97,8 +101,9 @@ hipError_t launch_list_all_tiles(int64_t n_tiles, const int64_t* tile_sent, int6
 }
 
 hipError_t launch_tile_bounds(const int64_t* sent_off, int64_t n_sent, int64_t n_tiles, int64_t* tile_sent,
-                              int64_t* tile_off, hipStream_t s) {
-  hipLaunchKernelGGL(tile_bounds_kernel, dim3(4096), dim3(256), 0, s, sent_off, n_sent, n_tiles, tile_sent, tile_off);
+                              int64_t* tile_off, hipStream_t s, int64_t seg, int sup) {
+  hipLaunchKernelGGL(tile_bounds_kernel, dim3(4096), dim3(256), 0, s, sent_off, n_sent, n_tiles, tile_sent, tile_off,
+                     seg > 0 ? seg : n_tiles + 1, sup > 0 ? sup : 1);
   return hipGetLastError();
 }
 

@@ -1990,11 +1990,12 @@ hipError_t launch_tokenize_split(const TokParams& P, int64_t nbytes, int64_t* ti
     return e;
   };
   const int64_t n_tiles = tile_count(nbytes);
-  hipError_t e = launch_tile_bounds(P.sent_off, P.n_sent, n_tiles, tile_sent, const_cast<int64_t*>(S.tile_off), s);
+  const int64_t seg = S.seg_tiles > 0 ? S.seg_tiles : SPLIT_SEG_TILES;
+  // (the scan reads tile_sent at its super-tile starts and the segment bounds only)
+  hipError_t e = launch_tile_bounds(P.sent_off, P.n_sent, n_tiles, tile_sent, nullptr, s, seg, tok5::SUPER);
   if (e != hipSuccess) return e;
   if ((e = hipMemsetAsync(P.out_tok_off, 0, sizeof(int64_t), s)) != hipSuccess) return e;
   S.tile_sent = tile_sent;
-  const int64_t seg = S.seg_tiles > 0 ? S.seg_tiles : SPLIT_SEG_TILES;
   for (int64_t t0 = 0; t0 < n_tiles; t0 += seg) {
     S.t0 = t0;
     S.t1 = std::min(n_tiles, t0 + seg);
