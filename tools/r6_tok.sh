@@ -6,15 +6,16 @@
 set -o pipefail
 TAG=${1:-r6tok}; MB=${2:-1024}
 cd "${GRAFT_REPO_ROOT:-.}" && export TMPDIR=/tmp && mkdir -p gpurun_out/$TAG
-# (each library twice, in alternating order: the first run of a call measured
-# ~1 % slower with identical code, profiles/r6/h1_*; compare the min)
-for R in 1 2; do
-  for L in lddl_amd/liblddl_amd.so ${LIBS}; do
-    N=$(basename $L .so)
-    LDDL_LIB=$PWD/$L timeout -k 10 300 python -u tools/tok_check.py $MB 5 >> gpurun_out/$TAG/$N.txt 2>&1 || { tail -5 gpurun_out/$TAG/$N.txt; exit 1; }
-  done
-  [ -z "${LIBS}" ] && break
-  LIBS_R=""; for L in ${LIBS}; do LIBS_R="$L $LIBS_R"; done
+# (each library twice, the second time in reverse order: the first run of a
+# call measured ~1 % slower with identical code, profiles/r6/h1_*; compare
+# the min of each library's lines)
+ORDER="lddl_amd/liblddl_amd.so ${LIBS}"
+REV=""; for L in $ORDER; do REV="$L $REV"; done
+[ -n "${LIBS}" ] && ORDER="$ORDER $REV"
+for L in $ORDER; do
+  N=$(basename $L .so)
+  LDDL_LIB=$PWD/$L timeout -k 10 300 python -u tools/tok_check.py $MB 5 >> gpurun_out/$TAG/$N.txt 2>&1 || { tail -5 gpurun_out/$TAG/$N.txt; exit 1; }
+done
 done
 if [ -n "$STAMPS" ]; then
   LDDL_TOK_DEBUG=1 NOCHECK=1 timeout -k 10 300 python -u tools/tok_check.py $MB 5 > gpurun_out/$TAG/stamps.txt 2>&1 || exit $?
