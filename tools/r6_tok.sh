@@ -16,7 +16,6 @@ for L in $ORDER; do
   N=$(basename $L .so)
   LDDL_LIB=$PWD/$L timeout -k 10 300 python -u tools/tok_check.py $MB 5 >> gpurun_out/$TAG/$N.txt 2>&1 || { tail -5 gpurun_out/$TAG/$N.txt; exit 1; }
 done
-done
 if [ -n "$STAMPS" ]; then
   LDDL_TOK_DEBUG=1 NOCHECK=1 timeout -k 10 300 python -u tools/tok_check.py $MB 5 > gpurun_out/$TAG/stamps.txt 2>&1 || exit $?
 fi
