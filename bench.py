@@ -72,6 +72,10 @@ def parse():
                        '(configs[3]), code: CodeBERT seq 512 (configs[2]), wikibooks: Wikipedia + Books seq 512 '
                        '(configs[4]); comma list, "" or none = none')
   ap.add_argument('--leg-steps', type=int, default=2)
+  # (measured slower: 124.6 vs 122.0 ms per step, profiles/r6/ov1_*; not the default)
+  ap.add_argument('--overlap', dest='overlap', action='store_true', default=False,
+                  help='step k pack beside step k+1 tokenize on two streams (unmasked)')
+  ap.add_argument('--no-overlap', dest='overlap', action='store_false')
   ap.add_argument('--frontend-c2-mb', type=float, default=2048.0,
                   help='MB of raw input for the C2-scale CLI leg (seq 512, bin 64: BASELINE configs[1] end to '
                        'end through the preprocessor CLI, rank 0 at N=1, before the GPU is touched; 0: off)')
@@ -678,18 +682,51 @@ def main():
   tok_ms = []
   gathered = []
 
+  # Steps overlap pairwise with --overlap (unmasked): step k's pack (scalar-unit
+  # bound) runs on its own stream beside step k+1's tokenize (vector-unit and
+  # latency bound) on another.  The tokenizer writes alternating output sets
+  # (pipeline.TokBuffers), so step k+1's tokenize waits only for the pack
+  # of step k-1, the last reader of the set it overwrites.  Every step still
+  # tokenizes, packs, bins and writes the row spans of the whole 20 GB; the
+  # timed region ends when both streams are idle.
+  overlap = args.overlap and not args.masking
+  if overlap:
+    from lddl_amd.pipeline import TokBuffers
+    st_tok, st_pack = torch.cuda.Stream(device), torch.cuda.Stream(device)
+    tbufs = [TokBuffers(), TokBuffers()]
+    ov = {'k': 0, 'packed': [None, None]}
+
   def step(timed):
-    s = torch.cuda.current_stream()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(s)
-    ids, ntok, toff = pk.tokenize(sh)
-    e1.record(s)
-    res = pk.pack(sh, ids, ntok, toff, **kw)
+    if overlap:
+      i = ov['k'] % 2
+      ov['k'] += 1
+      s = st_tok
+      with torch.cuda.stream(st_tok):
+        if ov['packed'][i] is not None:
+          st_tok.wait_event(ov['packed'][i])  # (the pack that last read set i)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        ids, ntok, toff = pk.tokenize(sh, stream=st_tok, bufs=tbufs[i])
+        e1.record(s)
+      with torch.cuda.stream(st_pack):
+        st_pack.wait_event(e1)
+        res = pk.pack(sh, ids, ntok, toff, stream=st_pack, **kw)
+        done = torch.cuda.Event()
+        done.record(st_pack)
+        ov['packed'][i] = done
+    else:
+      s = torch.cuda.current_stream()
+      e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+      e0.record(s)
+      ids, ntok, toff = pk.tokenize(sh)
+      e1.record(s)
+      res = pk.pack(sh, ids, ntok, toff, **kw)
     if dist is not None:
       # per-(partition, bin) row counts of every rank: the load balancer's
       # input (lddl_amd/balance.py), one RCCL all-gather per step
       from lddl_amd.balance import gather_bin_counts
-      g = gather_bin_counts(res.bin_count, rank * sh.n_part)
+      with torch.cuda.stream(st_pack if overlap else torch.cuda.current_stream()):
+        g = gather_bin_counts(res.bin_count, rank * sh.n_part)
       if timed:
         gathered.append(g)
     if timed:
@@ -771,7 +808,9 @@ def main():
                  'masked_positions_per_gpu': res.n_masked,
                  'parallelism': 'shard%d' % world, 'gathered_partitions': n_gathered,
                  # the step's row output: spans of the dense ids (what the writer renders from) or materialised rows
-                 'rows': 'spans' if res.spans else 'materialize'},
+                 'rows': 'spans' if res.spans else 'materialize',
+                 # steps pipelined pairwise over two streams (pack k beside tokenize k+1)
+                 'step_overlap': bool(overlap)},
       'roofline': {'bound': 'hbm', 'kernel': 'lddl::tok5::scan_kernel', 'achieved': achieved, 'peak': HBM_PEAK_GBS,
                    'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS, 'traffic': None,
                    'algorithmic_bytes_per_launch': alg, 'avg_launch_ms': ks['scan_ms'] / nl,

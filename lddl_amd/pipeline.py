@@ -245,6 +245,15 @@ class PackHandle:
       pass
 
 
+class TokBuffers:
+  """A set of Packer.tokenize output buffers (ids, ntok, tok_off).  Passing
+  alternating sets (bufs=) lets one batch's pack read its tokenizer output
+  while the next batch tokenizes into the other set on another stream."""
+
+  def __init__(self):
+    self._out = {}
+
+
 class Packer:
   """One GPU's tokenize -> pack -> bin -> materialise pipeline (one lddl_ctx
   and the pack result it packs into)."""
@@ -260,7 +269,8 @@ class Packer:
   def _buf(self, name, n, dtype, owner=None):
     """a cached device buffer of >= n entries; owner: the PackHandle whose
     PackResult columns it holds (each handle its own, so that several pack
-    results stay live at once), else the Packer's (the tokenizer output)"""
+    results stay live at once) or the TokBuffers of a tokenize call, else
+    the Packer's own"""
     out = self._out if owner is None else owner._out
     t = out.get(name)
     if t is None or t.numel() < n or t.dtype != dtype:
@@ -275,17 +285,18 @@ class Packer:
     re-runs with the exact total (tokenize).  #tokens <= #bytes always."""
     return min(nbytes, nbytes * 3 // 8 + (1 << 16))
 
-  def tokenize(self, shards, max_tok=512, stream=None):
+  def tokenize(self, shards, max_tok=512, stream=None, bufs=None):
     """-> (ids, ntok, tok_off): the dense CSR ids (lddl_tokenize).  The ids
     buffer is sized by ids_estimate, not by the byte count (20 GB of corpus:
     ~8 GB instead of 43 GB); the total is read back (one stream sync) and a
-    corpus with more tokens runs again into a buffer of exactly its size."""
+    corpus with more tokens runs again into a buffer of exactly its size.
+    bufs: a TokBuffers to write into (default: the Packer's own buffers)."""
     from .tokenizer import CapacityError
-    ntok = self._buf('ntok', shards.n_sent, torch.int32)
-    toff = self._buf('tok_off_in', shards.n_sent + 1, torch.int64)
+    ntok = self._buf('ntok', shards.n_sent, torch.int32, bufs)
+    toff = self._buf('tok_off_in', shards.n_sent + 1, torch.int64, bufs)
     cap = self.ids_estimate(shards.nbytes)
     for _ in range(2):
-      ids = self._buf('ids', cap + 16, torch.int16)
+      ids = self._buf('ids', cap + 16, torch.int16, bufs)
       try:
         return self.tok.tokenize_device(shards.data, shards.sent_off, max_tok, ids, ntok, toff, stream,
                                         nbytes=shards.nbytes)
