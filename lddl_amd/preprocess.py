@@ -537,6 +537,25 @@ def main(args, codebert=False):
         done[c] = m
   todo = [c for c in range(len(chunks)) if c not in done]
 
+  # the parquet encodes: a pool of processes forked first, before the GPU is
+  # touched and before the split pool exists (a process forked beside a live
+  # executor's threads can inherit their locks held; 16 forks beside 16 busy
+  # split workers had also taken 0.17-0.29 s of the CPU share;
+  # writer.ProcessEncoder; LDDL_ENCODE_PROCS=0: a thread pool)
+  import concurrent.futures
+  enc = None
+  t0 = time.perf_counter()
+  if args.output_format != 'txt':
+    if os.environ.get('LDDL_ENCODE_PROCS', '1') != '0':
+      enc = writer.ProcessEncoder()
+    else:
+      enc = concurrent.futures.ThreadPoolExecutor(writer.encode_workers())
+  t['enc_start_s'] = time.perf_counter() - t0
+
+  def close_enc():
+    if enc is not None:
+      enc.close() if isinstance(enc, writer.ProcessEncoder) else enc.shutdown(wait=False)
+
   # split workers: forked here, before anything touches the GPU; they read
   # their records from the index (integers only are inherited)
   sw = args.split_workers
@@ -560,12 +579,18 @@ def main(args, codebert=False):
     # the GPU and the writer; LDDL_WORKER_NICE=0 keeps the default priority.
     # An executor, not multiprocessing.Pool: the Pool's handler threads poll
     # at 0.1 s, and its terminate / join took 0.12-0.25 s at the end)
-    pool = concurrent.futures.ProcessPoolExecutor(nw, mp_context=multiprocessing.get_context('fork'),
-                                                  initializer=_nice_worker)
     try:
-      list(pool.map(_split_warm, range(nw)))  # (the first task forks every worker, while _FE holds the state)
-    finally:
-      _FE.clear()
+      pool = concurrent.futures.ProcessPoolExecutor(nw, mp_context=multiprocessing.get_context('fork'),
+                                                    initializer=_nice_worker)
+      try:
+        list(pool.map(_split_warm, range(nw)))  # (the first task forks every worker, while _FE holds the state)
+      finally:
+        _FE.clear()
+    except BaseException:
+      if pool is not None:
+        pool.shutdown(wait=True, cancel_futures=True)
+      close_enc()
+      raise
     t['pool_start_s'] = time.perf_counter() - t0
 
   # a chunk is split as pieces of ~1/(2 nw) of it (whole partitions) on all
@@ -594,24 +619,6 @@ def main(args, codebert=False):
     got = [f_.result() for f_ in fs]
     return [g[0] for g in got], concat_ids([g[1] for g in got]), sum(g[2] for g in got)
 
-  # the parquet encodes: a pool of processes forked here, before the GPU is
-  # touched and before the split workers get busy (16 forks beside 16 busy
-  # split workers took 0.17-0.29 s of the CPU share; writer.ProcessEncoder;
-  # LDDL_ENCODE_PROCS=0: a thread pool)
-  import concurrent.futures
-  enc = None
-  t0 = time.perf_counter()
-  try:
-    if args.output_format != 'txt':
-      if os.environ.get('LDDL_ENCODE_PROCS', '1') != '0':
-        enc = writer.ProcessEncoder()
-      else:
-        enc = concurrent.futures.ThreadPoolExecutor(writer.encode_workers())
-  except BaseException:
-    if pool is not None:
-      pool.shutdown(wait=True, cancel_futures=True)
-    raise
-  t['enc_start_s'] = time.perf_counter() - t0
   # the first chunks split while this process brings up the GPU context and
   # the device tables
   ahead = 2  # chunks split ahead of the GPU
@@ -624,8 +631,7 @@ def main(args, codebert=False):
   except BaseException:
     if pool is not None:
       pool.shutdown(wait=True, cancel_futures=True)
-    if enc is not None:
-      enc.close() if isinstance(enc, writer.ProcessEncoder) else enc.shutdown(wait=False)
+    close_enc()
     raise
   t['gpu_init_s'] = time.perf_counter() - t0
   out = []
