@@ -267,3 +267,39 @@ def test_tokenize_without_truncation_refuses_what_it_cannot_return(gpu):
   assert len(tok.tokenize('! ' * 600, truncation=False)) == 600
   with pytest.raises(ValueError):
     tok.tokenize('!' * (TOKENS_MAX + 10), truncation=False)
+
+
+@pytest.mark.parametrize('seed', [0, 1])
+def test_hip_tokenize_window_packing_edges(gpu, seed):
+  """The scan's greedy 2 KiB windows: sentences whose lengths put the window
+  end exactly at, just below and just past 2 KiB of the first sentence's
+  16-B aligned start, at every start alignment; a sentence longer than a
+  window (alone, to the serial path); runs of 40 one-word sentences (more
+  than a window's 31); empty sentences between them"""
+  from lddl_amd.synth import corpus_from_sentences
+  from lddl_amd.tokenizer import Tokenizer
+  rng = np.random.default_rng(seed)
+  words = ['the', 'of', 'naïve', 'hello', 'electroencephalographically', '[SEP]', ',', 'x' * 120]
+
+  def sent(nbytes):  # a sentence of exactly nbytes UTF-8 bytes
+    out = ''
+    while len(out.encode()) < nbytes - 4:
+      out += words[int(rng.integers(0, len(words)))] + ' '
+    out = out.encode()[:max(0, nbytes - 4)].decode('utf-8', 'ignore')
+    return out + 'a' * (nbytes - len(out.encode()))
+  sents = []
+  for align in range(16):
+    sents.append('z' * align)
+    for target in (2032, 2040, 2047, 2048, 2049, 2064, 1024, 3000):
+      a = int(rng.integers(1, target - 1))
+      sents += [sent(a), sent(target - a), '']
+    sents += ['w%d' % k for k in range(40)]
+    sents += [sent(int(rng.integers(2040, 2100)))]
+  tok = Tokenizer(VOCABS['bert'])
+  c = corpus_from_sentences(sents, [0, len(sents)])
+  ids, ntok = run_hip(tok, c.data, c.sent_off)
+  oids, ontok = OracleTokenizer(VOCABS['bert']).run(c.data, c.sent_off, 512)
+  assert np.array_equal(ntok, ontok)
+  got, exp = compact(ids, ntok, c.sent_off), compact(oids, ontok, c.sent_off)
+  bad = [i for i, (a, b) in enumerate(zip(got, exp)) if not np.array_equal(a, b)]
+  assert not bad, bad[:10]
