@@ -648,11 +648,17 @@ static int pack_common(lddl_ctx* c, lddl_pack* pk, int codebert, const int32_t* 
       HIP_TRY(hipMemsetAsync(P.mcounter, 0, 8, st));
     }
     static uint64_t* d_pdbg = nullptr;
+    static int64_t pdbg_cap = 0;
     const char* pdbg = getenv("LDDL_PACK_DEBUG");
     P.dbg = nullptr;
+    const int64_t pdbg_n = 16 + 2 * (int64_t)n_part;  // counters + the BERT packer's per-wave start / end
     if (pdbg && pdbg[0] == '1') {
-      if (!d_pdbg) HIP_TRY(hipMalloc((void**)&d_pdbg, 16 * 8));
-      HIP_TRY(hipMemsetAsync(d_pdbg, 0, 16 * 8, st));
+      if (pdbg_cap < pdbg_n) {
+        if (d_pdbg) HIP_TRY(hipFree(d_pdbg));
+        HIP_TRY(hipMalloc((void**)&d_pdbg, pdbg_n * 8));
+        pdbg_cap = pdbg_n;
+      }
+      HIP_TRY(hipMemsetAsync(d_pdbg, 0, pdbg_n * 8, st));
       P.dbg = d_pdbg;
     }
     HIP_TRY(codebert ? launch_pack_codebert_wave(P, st) : launch_pack_bert_wave(P, st));
@@ -667,6 +673,56 @@ static int pack_common(lddl_ctx* c, lddl_pack* pk, int codebert, const int32_t* 
       for (int k = 0; k < 13; ++k)
         fprintf(stderr, " %s=%llu", k < 8 || P.masking ? nm[k] : gn[k - 8], (unsigned long long)h[k]);
       fprintf(stderr, "\n");
+      // occupancy timeline (100 MHz ticks): the span from the first wave's
+      // start to the last one's end, the summed wave time, the most waves
+      // resident at once, and how long the residency stays below 90 % / 50 %
+      // of that maximum after the peak (the tail)
+      std::vector<uint64_t> tl(2 * (size_t)n_part);
+      HIP_TRY(hipMemcpyAsync(tl.data(), P.dbg + 16, tl.size() * 8, hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipStreamSynchronize(st));
+      std::vector<std::pair<uint64_t, int>> ev;
+      ev.reserve(tl.size());
+      uint64_t busy = 0, t_lo = ~0ull, t_hi = 0;
+      for (int64_t q = 0; q < n_part; ++q) {
+        const uint64_t a = tl[2 * q], b = tl[2 * q + 1];
+        if (b < a || a == 0) continue;
+        ev.push_back({a, 1});
+        ev.push_back({b, -1});
+        busy += b - a;
+        t_lo = std::min(t_lo, a);
+        t_hi = std::max(t_hi, b);
+      }
+      std::sort(ev.begin(), ev.end());
+      int cur = 0, mx = 0;
+      uint64_t t_peak = t_lo;
+      for (auto& e : ev) {
+        cur += e.second;
+        if (cur > mx) { mx = cur; t_peak = e.first; }
+      }
+      uint64_t below90 = 0, below50 = 0, prev = t_lo;
+      cur = 0;
+      for (auto& e : ev) {
+        if (e.first > t_peak) {
+          if (cur < 0.9 * mx) below90 += e.first - prev;
+          if (cur < 0.5 * mx) below50 += e.first - prev;
+        }
+        prev = e.first;
+        cur += e.second;
+      }
+      std::vector<uint64_t> du;
+      uint64_t last_start = 0;
+      for (int64_t q = 0; q < n_part; ++q)
+        if (tl[2 * q] && tl[2 * q + 1] >= tl[2 * q]) {
+          du.push_back(tl[2 * q + 1] - tl[2 * q]);
+          last_start = std::max(last_start, tl[2 * q] - t_lo);
+        }
+      std::sort(du.begin(), du.end());
+      auto pct = [&](double f) { return du.empty() ? 0.0 : du[std::min(du.size() - 1, (size_t)(f * du.size()))] / 100.0; };
+      fprintf(stderr, "[lddl pack tl] wave_us p10=%.0f p50=%.0f p90=%.0f max=%.0f last_start_us=%.0f\n", pct(0.1), pct(0.5),
+              pct(0.9), pct(1.0), last_start / 100.0);
+      fprintf(stderr, "[lddl pack tl] waves=%zu span_us=%.0f busy_wave_us=%.0f max_resident=%d mean_resident=%.0f tail_below90_us=%.0f tail_below50_us=%.0f mean_wave_us=%.0f\n",
+              ev.size() / 2, (t_hi - t_lo) / 100.0, busy / 100.0, mx, t_hi > t_lo ? (double)busy / (double)(t_hi - t_lo) : 0.0,
+              below90 / 100.0, below50 / 100.0, ev.empty() ? 0.0 : busy / 100.0 / (ev.size() / 2));
     }
     HIP_TRY(launch_scan_parts(P.part_npairs, P.part_ntok, n_part, pair_base, tok_base, P.part_err, err_any, st));
     HIP_TRY(hipMemcpyAsync(c->h_tot, pair_base + n_part, 8, hipMemcpyDeviceToHost, st));

@@ -590,6 +590,9 @@ __global__ __launch_bounds__(64, PACK_OCC) void pack_bert_wave_kernel(PackParams
   // pair generation, shuffle, binning; masking: candidates, shuffle draws,
   // pick trace, 80/10/10 choices, sorted writes
   uint64_t ph[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, tprev = DBG ? __builtin_amdgcn_s_memtime() : 0;
+  // (DBG: the wave's start and end on the 100 MHz device clock, for the
+  // host's occupancy timeline: P.dbg[16 + 2p], [16 + 2p + 1])
+  const uint64_t rt0 = DBG ? __builtin_amdgcn_s_memrealtime() : 0;
 // generate sub-phases of the unmasked packer reuse the masking slots 6-10
 #define PW_GSTAMP(k)                                    \
   if (!MASK && DBG) {                                   \
@@ -1194,6 +1197,8 @@ __global__ __launch_bounds__(64, PACK_OCC) void pack_bert_wave_kernel(PackParams
     atomicAdd((unsigned long long*)&P.dbg[6], (unsigned long long)np);
     atomicAdd((unsigned long long*)&P.dbg[7], 1ull);
     for (int k = 6; k < 11; ++k) atomicAdd((unsigned long long*)&P.dbg[k + 2], (unsigned long long)ph[k]);
+    P.dbg[16 + 2 * p] = rt0;
+    P.dbg[16 + 2 * p + 1] = __builtin_amdgcn_s_memrealtime();
   }
 #undef PW_STAMP
 #undef PW_GSTAMP

@@ -1772,8 +1772,11 @@ __global__ __launch_bounds__(256) void count_kernel(TokParams P, SplitParams S) 
 // --------------------------------------------------------------- expand --
 // Dense output: a wave per group of 64 sentences; their entries (a vocab id,
 // a hole, or a queued word's record) in steps of 64, one per lane.  An entry's
-// sentence comes from a scatter of the sentences' first entries (LDS max) and
-// a wave max-scan; the step's entries are loaded one step ahead, so each
+// sentence: the group's non-empty sentences are numbered in order, each marks
+// its first entry's lane in an LDS tag array (tagged by the step, so nothing
+// is cleared), one ballot reads the marks back, and an entry's sentence is
+// the marks at or below its lane (v_mbcnt) plus those of earlier steps; the
+// step's entries are loaded one step ahead, so each
 // step's record loads (count + first 4 pieces, one 12-B load) fly with the
 // next step's entry loads.  A segmented scan of the token counts gives each
 // token's position in its sentence, written at out_tok_off[s] + position
@@ -1787,8 +1790,8 @@ struct ExpSent {
   uint32_t pad;
 };
 struct ExpLds {
-  ExpSent sn[64];
-  uint32_t own[64];  // scatter: the sentence whose first entry is the step's entry k
+  ExpSent sn[64];    // the group's non-empty sentences, in order
+  uint32_t hf[64];   // hf[k] = the step's tag: some sentence's first entry is the step's entry k
 };
 
 __global__ __launch_bounds__(256) void expand_kernel(TokParams P, SplitParams S) {
@@ -1802,6 +1805,8 @@ __global__ __launch_bounds__(256) void expand_kernel(TokParams P, SplitParams S)
   typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
   const uint4* const pcs = S.pcs;
   const uint4* const pch = S.pch;
+  uint32_t tag = 0;  // per step, across the groups: hf needs no clearing
+  E.hf[lane] = 0u;
   for (int64_t g0 = sA + ((int64_t)blockIdx.x * 4 + wv) * 64; g0 < sB; g0 += nwaves * 64) {
     const int64_t s = g0 + lane;
     uint32_t ne = 0;
@@ -1827,16 +1832,18 @@ __global__ __launch_bounds__(256) void expand_kernel(TokParams P, SplitParams S)
     es.lim = lim;
     es.e0 = e0;
     es.pad = 0;
-    E.sn[lane] = es;
-    // the sentence of each entry of step st (entries st + lane)
-    uint32_t own_carry = 0;
-    auto owner = [&](uint32_t st) -> uint32_t {
-      E.own[lane] = 0u;
+    const uint64_t nzm = __ballot(ne != 0);
+    if (ne != 0) E.sn[bits_below(nzm)] = es;
+    // the sentence (non-empty rank) of each entry of step st (entries st + lane)
+    uint32_t hcar = 0;  // non-empty sentences that start before the step
+    auto owner = [&](uint32_t st, bool& head) -> uint32_t {
+      ++tag;
+      if (ne != 0 && e0 - st < 64u) E.hf[e0 - st] = tag;
       wsync();
-      if (ne != 0 && e0 >= st && e0 < st + 64) atomicMax(&E.own[e0 - st], (uint32_t)lane);
-      wsync();
-      const uint32_t o = max(wave_incl_max(E.own[lane]), own_carry);
-      own_carry = lane_get(o, 63);
+      const uint64_t hm = __ballot(E.hf[lane] == tag);
+      head = (hm >> lane) & 1ull;
+      const uint32_t o = hcar + (uint32_t)bits_below(hm) + (head ? 0u : (uint32_t)-1);
+      hcar += (uint32_t)__popcll(hm);
       return o;
     };
     // EXP_K steps at a time, in three phases: the entry loads of all of them,
@@ -1858,10 +1865,11 @@ __global__ __launch_bounds__(256) void expand_kernel(TokParams P, SplitParams S)
         xin[k] = xhead[k] = false;
         if (st < T) {
           const uint32_t g = st + (uint32_t)lane;
-          xj[k] = owner(st);
+          bool hd;
+          xj[k] = min(owner(st, hd), 63u);
           xin[k] = g < T;
           const ExpSent sj = E.sn[xj[k]];
-          xhead[k] = xin[k] && g == sj.e0;
+          xhead[k] = xin[k] && hd;
           xv[k] = S.ent[xin[k] ? sj.eb + g : 0];  // (every lane loads: no branch around the load)
         }
       }
