@@ -103,7 +103,7 @@ struct SplitParams {
   uint4* pch;              // WordPiece head per slot: {#pieces, pieces 0-1, pieces 2-3, 0}: dense 16 B, what
                            // expand reads for nearly every record (one 16-B line share instead of a 64-B stride)
   uint32_t* chunk_fill;
-  uint32_t* chunk_ctr;     // [0] chunks handed out by the scan, [1] by wp_kernel
+  uint32_t* chunk_ctr;     // [0] chunks handed out by the scan, [1] by wp_kernel, [2] super-tiles claimed by the scan
   uint32_t n_chunks;
   uint2* smeta;            // per sentence: #entries | first slot - the tile's << 16, the tile's first slot
   uint16_t* snslot;        // per sentence: its record slots (count_kernel sums their piece counts)

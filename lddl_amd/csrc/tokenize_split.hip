@@ -105,8 +105,8 @@ struct alignas(16) Lds {
   uint32_t pb[4];              // the next super-tile's bounds: tile_sent of its first tile and of its end (LDS-DMA)
   int64_t soff[NSCAP];         // the next window's sent_off[c_s .. c_s + 32) (LDS-DMA; read by stage2, then its
                                // sentence starts by the window's first steps)
-  int64_t wst[3];              // window staging: the super-tile's next sentence, its end, the super-tile (kept
-                               // here, not in registers, across the window's work)
+  int64_t wst[4];              // window staging: the super-tile's next sentence, its end, the super-tile, the
+                               // next super-tile (kept here, not in registers, across the window's work)
   uint32_t nb[NBUF / 4];       // normalised bytes in window coordinates; side buffer at [CAP, CAP+DCAP)
   uint32_t brk[64];            // break bits: unit starts, spaces, sentence starts
   uint32_t um[64];             // unit-start bits
@@ -407,7 +407,7 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
   uint32_t cur = 0, cend = 0, cbase = 0, tbase = 0, tsl = 0;
   int chunk = -1;
   // Windows.  The wave walks super-tiles of SUPER tiles (its wave index, then
-  // + nwaves) and packs each one's sentences greedily into windows: as many
+  // the ones it claims from a counter) and packs each one's sentences greedily into windows: as many
   // whole sentences (<= 63) as fit in CAP bytes from the first one's 16-B
   // aligned start.  A window is about twice a tile's bytes, so the per-window
   // work (classification, exception pass, unit scans, per-sentence records)
@@ -420,7 +420,13 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
   // after this window's exception pass) by LDS-DMA, so both round trips fly
   // behind this window's work; the loop top finishes whatever a window that
   // returned early left undone.  A super-tile's bounds (tile_sent) arrive by
-  // LDS-DMA into pb while the one before it runs.
+  // LDS-DMA into pb while the one before it runs.  Super-tiles past the
+  // first are claimed from a per-segment counter (chunk_ctr[2]) one
+  // transition ahead (the claim's return is read at the next transition), so
+  // a wave that starts late -- its CU still busy with another kernel's waves
+  // -- takes fewer of them instead of finishing the launch late.  A wave
+  // claims only what it will run: a claim made after another is larger, so
+  // when a wave's next super-tile is past the end, so is every one it holds.
   int64_t n_sa = 0, n_sb = 0, n_A = 0, n_B = 0;
   int nst = 0;
   bool dma_pending = false;  // raw-byte DMA issued and not yet waited for
@@ -435,35 +441,48 @@ __global__ __launch_bounds__(64 * WAVES, OCC) void scan_kernel(TokParams P, Spli
       dma4(reinterpret_cast<const uint32_t*>(S.tile_sent + t) + (lane & 1), L.pb);
     }
   };
+  uint32_t* const sctr = S.chunk_ctr + 2;  // zeroed with chunk_ctr per segment
+  uint32_t gq = 0;                         // lane 0: the claim after the next super-tile (in flight)
+  auto claim = [&]() {
+    if (lane == 0) gq = atomicAdd(sctr, 1u);
+  };
   {
     const int64_t g = (int64_t)blockIdx.x * WAVES + wv;
-    int64_t cs = 0, ce = 0;
+    int64_t cs = 0, ce = 0, gn = ng;
     if (g < ng) {
       cs = uni64(S.tile_sent[S.t0 + g * SUPER]);
       ce = uni64(S.tile_sent[min(S.t1, S.t0 + (g + 1) * SUPER)]);
+      claim();
+      gn = nwaves + (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)gq, 0);
+      claim();
     }
     L.wst[0] = cs;
     L.wst[1] = ce;
     L.wst[2] = g;
+    L.wst[3] = gn;
     wsync();
-    st_bounds(g + nwaves);
+    st_bounds(gn);
   }
   auto stage1 = [&]() {
     if (nst != 0) return;
     nst = 1;
     int64_t cs = uni64(L.wst[0]), ce = uni64(L.wst[1]), g = uni64(L.wst[2]);
     if (cs >= ce && g < ng) {
+      int64_t gn = uni64(L.wst[3]);
       while (cs >= ce && g < ng) {  // the super-tile is done: the next one's bounds (pb)
-        g += nwaves;
+        g = gn;
         if (g >= ng) break;
         drain();
         cs = uni64(*reinterpret_cast<const int64_t*>(&L.pb[0]));
         ce = uni64(*reinterpret_cast<const int64_t*>(&L.pb[2]));
-        st_bounds(g + nwaves);
+        gn = nwaves + (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)gq, 0);
+        claim();
+        st_bounds(gn);
       }
       L.wst[0] = cs;
       L.wst[1] = ce;
       L.wst[2] = g;
+      L.wst[3] = gn;
     }
     // (lane l: dword l of sent_off[cs ..], the offsets up to ce)
     if (cs < ce && cs + (lane_here() >> 1) <= ce) dma4(reinterpret_cast<const uint32_t*>(P.sent_off + cs) + lane_here(), reinterpret_cast<uint32_t*>(L.soff));
@@ -2007,7 +2026,7 @@ hipError_t launch_tokenize_split(const TokParams& P, int64_t nbytes, int64_t* ti
   for (int64_t t0 = 0; t0 < n_tiles; t0 += seg) {
     S.t0 = t0;
     S.t1 = std::min(n_tiles, t0 + seg);
-    if ((e = hipMemsetAsync(S.chunk_ctr, 0, 8, s)) != hipSuccess) return e;  // scan's and wp's chunk counters
+    if ((e = hipMemsetAsync(S.chunk_ctr, 0, 12, s)) != hipSuccess) return e;  // scan's and wp's chunk counters, scan's super-tiles
     if ((e = hipMemsetAsync(S.fb_count, 0, 4, s)) != hipSuccess) return e;
     if ((e = mark(0, 0)) != hipSuccess) return e;
     if (P.dbg) e = tok5::launch_scan<SCAN_WAVES, true, tok5::SCAN_OCC>(P, S, n_cu, s);
