@@ -106,6 +106,16 @@ int lddl_tokenize_stats(lddl_ctx *ctx, double *out, int n);
  * over the ids.  Off by default (the unmasked path does not need them). */
 int lddl_set_special_flags(lddl_ctx *ctx, int on);
 
+/* The tokenizer algorithm of the following lddl_tokenize calls (A/B and
+ * tests; every algorithm gives identical ids): 5 = the split tokenizer (the
+ * default), 6 = the lane tokenizer, 0 = every tile through the exact serial
+ * path.  An algorithm that does not model the loaded tables falls back to 0;
+ * so does 6 on a ctx created without LDDL_TOKENIZE_ALGO=6 or
+ * LDDL_WP_ALGO=trie in the environment (its trie is built only then).
+ * *out_algo (may be NULL) receives the one selected.  Scratch is kept across
+ * a switch; each call allocates what its algorithm reads. */
+int lddl_set_tokenize_algo(lddl_ctx *ctx, int algo, int *out_algo);
+
 /* A new, empty pack result on ctx's device (free with lddl_pack_free, before
  * or after the ctx).  lddl_pack_rows: #rows of its last successful pack, -1
  * when none. */

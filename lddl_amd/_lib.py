@@ -28,6 +28,7 @@ SIGNATURES = {
                               c_void_p, c_void_p, c_void_p]),
     'lddl_set_timing': (c_int, [c_void_p, c_int]),
     'lddl_set_special_flags': (c_int, [c_void_p, c_int]),
+    'lddl_set_tokenize_algo': (c_int, [c_void_p, c_int, ctypes.POINTER(c_int)]),
     'lddl_tokenize_stats': (c_int, [c_void_p, ctypes.POINTER(c_double), c_int]),
     'lddl_pack_new': (c_int, [c_void_p, ctypes.POINTER(c_void_p)]),
     'lddl_pack_free': (None, [c_void_p]),

@@ -254,6 +254,17 @@ static int load_vocab(lddl_ctx* c, const char* path) {
   return 0;
 }
 
+// the tokenizer algorithm: the one asked for, or the serial path (0) when it
+// does not model the loaded tables (the lane tokenizer needs the trie and a
+// table in which no code point normalises to more chars than its UTF-8
+// bytes; the split one keeps ids below SPLIT_EDEF and derives its byte
+// classes from the ASCII page)
+static void select_tok_algo(lddl_ctx* c, int algo) {
+  c->tok_algo = algo;
+  if (c->tok_algo == 6 && !c->lane_ok) c->tok_algo = 0;
+  if (c->tok_algo == 5 && (!c->scan_ok || c->vocab_size > (int)SPLIT_EDEF)) c->tok_algo = 0;
+}
+
 extern "C" int lddl_create(const char* vocab_path, const char* table_path, int device, lddl_ctx** out) {
   if (!out || !vocab_path || !table_path) return set_err(LDDL_EINVAL, "null argument");
   *out = nullptr;
@@ -276,9 +287,7 @@ extern "C" int lddl_create(const char* vocab_path, const char* table_path, int d
   // one keeps ids below SPLIT_EDEF and derives its byte classes from the
   // ASCII page)
   const char* algo = getenv("LDDL_TOKENIZE_ALGO");
-  c->tok_algo = !algo ? 5 : algo[0] == '0' ? 0 : algo[0] == '6' ? 6 : 5;
-  if (c->tok_algo == 6 && !c->lane_ok) c->tok_algo = 0;
-  if (c->tok_algo == 5 && (!c->scan_ok || c->vocab_size > (int)SPLIT_EDEF)) c->tok_algo = 0;
+  select_tok_algo(c, !algo ? 5 : algo[0] == '0' ? 0 : algo[0] == '6' ? 6 : 5);
   const char* mcap = getenv("LDDL_MLM_CAP");  // initial masking arena (tests force the regrow path)
   c->mlm_cap0 = mcap ? (uint64_t)atoll(mcap) : 0;
   c->own.device = device;
@@ -418,6 +427,10 @@ extern "C" int lddl_tokenize(lddl_ctx* c, const uint8_t* d_bytes, int64_t nbytes
        (rc = ws_get(c, 47, (size_t)slots, &S.pch)) || (rc = ws_get(c, 37, n_sent, &S.smeta)) ||
        (rc = ws_get(c, 43, n_sent, &S.snslot)) || (rc = ws_get(c, 44, (size_t)slots, &S.cnt8))))
     return rc;
+  // (the finish pass -- count_kernel and expand_kernel of algorithms 5 and 0
+  // -- reads these unconditionally: refuse to run it without them)
+  if (c->tok_algo != 6 && (!S.pch || !S.smeta || !S.snslot || !S.cnt8 || !S.rec || !S.pcs))
+    return set_err(LDDL_EINVAL, "tokenize: finish scratch not allocated");
   int64_t* tile_off = nullptr;
   if (c->tok_algo == 6 && (rc = ws_get(c, 46, nt + 1, &tile_off))) return rc;  // (the lane tokenizer's tile starts)
   S.tile_off = tile_off;
@@ -479,6 +492,14 @@ extern "C" int lddl_tokenize(lddl_ctx* c, const uint8_t* d_bytes, int64_t nbytes
 extern "C" int lddl_set_special_flags(lddl_ctx* c, int on) {
   if (!c) return set_err(LDDL_EINVAL, "null ctx");
   c->spec_flags = on != 0;
+  return 0;
+}
+
+extern "C" int lddl_set_tokenize_algo(lddl_ctx* c, int algo, int* out_algo) {
+  if (!c) return set_err(LDDL_EINVAL, "null ctx");
+  if (algo != 0 && algo != 5 && algo != 6) return set_err(LDDL_EINVAL, "tokenize algo must be 0, 5 or 6");
+  select_tok_algo(c, algo);
+  if (out_algo) *out_algo = c->tok_algo;
   return 0;
 }
 

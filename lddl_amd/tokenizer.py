@@ -115,6 +115,14 @@ class Tokenizer:
     masked pack over the same buffers (lddl_set_special_flags)"""
     _lib.check(_lib.lib().lddl_set_special_flags(self.handle, 1 if on else 0))
 
+  def set_algo(self, algo):
+    """the tokenizer algorithm of the following calls (lddl_set_tokenize_algo:
+    5 split, the default; 6 lane; 0 the exact serial path -- identical ids);
+    returns the one selected (0 when the tables rule the asked one out)"""
+    out = ctypes.c_int(-1)
+    _lib.check(_lib.lib().lddl_set_tokenize_algo(self.handle, int(algo), ctypes.byref(out)))
+    return out.value
+
   def set_timing(self, on=True):
     """per-kernel timing of the following tokenize calls (lddl_set_timing)"""
     _lib.check(_lib.lib().lddl_set_timing(self.handle, 1 if on else 0))

@@ -303,3 +303,27 @@ def test_hip_tokenize_window_packing_edges(gpu, seed):
   got, exp = compact(ids, ntok, c.sent_off), compact(oids, ontok, c.sent_off)
   bad = [i for i, (a, b) in enumerate(zip(got, exp)) if not np.array_equal(a, b)]
   assert not bad, bad[:10]
+
+
+def test_algorithms_switched_on_one_ctx(gpu, monkeypatch):
+  """Scratch reused across tokenizer algorithms on one ctx: the lane
+  tokenizer (6, which allocates no finish scratch of its own) then the
+  serial path (0) and the split tokenizer (5), whose finish pass reads
+  pch / smeta / snslot / cnt8, then back -- every call identical to the
+  oracle (the fault of round 5: the finish pass ran over scratch another
+  algorithm had not allocated)"""
+  from lddl_amd import synth
+  from lddl_amd.tokenizer import Tokenizer
+  c = synth.make_wiki(400_000, seed=41)
+  oids, ontok = OracleTokenizer(VOCABS['bert']).run(c.data, c.sent_off, 512, nthreads=8)
+  exp = compact(oids, ontok, c.sent_off)
+  monkeypatch.setenv('LDDL_TOKENIZE_ALGO', '6')  # (the ctx builds the lane tokenizer's trie only when asked)
+  tok = Tokenizer(VOCABS['bert'])
+  for algo in (6, 0, 5, 6, 5, 0):
+    assert tok.set_algo(algo) == algo
+    ids, ntok = run_hip(tok, c.data, c.sent_off)
+    assert np.array_equal(ntok, ontok), algo
+    got = compact(ids, ntok, c.sent_off)
+    assert all(np.array_equal(a.astype(np.int64), b.astype(np.int64)) for a, b in zip(got, exp)), algo
+  with pytest.raises(Exception):
+    tok.set_algo(3)
