@@ -684,14 +684,15 @@ static int pack_common(lddl_ctx* c, lddl_pack* pk, int codebert, const int32_t* 
     }
     HIP_TRY(codebert ? launch_pack_codebert_wave(P, st) : launch_pack_bert_wave(P, st));
     if (P.dbg && !codebert) {
-      uint64_t h[13];
+      uint64_t h[16];
       HIP_TRY(hipMemcpyAsync(h, P.dbg, sizeof h, hipMemcpyDeviceToHost, st));
       HIP_TRY(hipStreamSynchronize(st));
-      const char* nm[13] = {"filter", "ldsfill", "seed", "generate", "shuffle", "bin", "pairs", "parts",
-                            "m_cand", "m_draws", "m_trace", "m_choices", "m_write"};
+      const char* nm[16] = {"filter", "ldsfill", "seed", "generate", "shuffle", "bin", "pairs", "parts",
+                            "m_cand", "m_draws", "m_trace", "m_choices", "m_write", "m_trace_fbuild", "m_trace_chains",
+                            "unused"};
       const char* gn[5] = {"g_doc", "g_fill", "g_pairB", "g_trunc", "g_store"};  // unmasked: generate sub-phases
       fprintf(stderr, "[lddl pack dbg]");
-      for (int k = 0; k < 13; ++k)
+      for (int k = 0; k < (P.masking ? 15 : 13); ++k)
         fprintf(stderr, " %s=%llu", k < 8 || P.masking ? nm[k] : gn[k - 8], (unsigned long long)h[k]);
       fprintf(stderr, "\n");
       // occupancy timeline (100 MHz ticks): the span from the first wave's

@@ -611,7 +611,7 @@ __global__ __launch_bounds__(256) void masked_lm_kernel(MlmParams M) {
 // never include [CLS] / [SEP], pretrain.py:187-190) and the token the masked
 // row shows there (the replacement, or the label when kept) goes to
 // out_token for the writer (lddl_render_masked).
-constexpr int MLM_SPAN_UNROLL = 4;  // masked positions per lane with loads in flight together
+constexpr int MLM_SPAN_UNROLL = 8;  // masked positions per lane with loads in flight together
 
 __global__ __launch_bounds__(256) void masked_lm_spans_kernel(MlmParams M) {
   // A wave per 64 rows.  First every lane resolves one row (partition, its

@@ -589,7 +589,7 @@ __global__ __launch_bounds__(64, PACK_OCC) void pack_bert_wave_kernel(PackParams
   // optional phase stamps (wave-uniform branch): filter, LDS fill, seed,
   // pair generation, shuffle, binning; masking: candidates, shuffle draws,
   // pick trace, 80/10/10 choices, sorted writes
-  uint64_t ph[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, tprev = DBG ? __builtin_amdgcn_s_memtime() : 0;
+  uint64_t ph[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, tprev = DBG ? __builtin_amdgcn_s_memtime() : 0;
   // (DBG: the wave's start and end on the 100 MHz device clock, for the
   // host's occupancy timeline: P.dbg[16 + 2p], [16 + 2p + 1])
   const uint64_t rt0 = DBG ? __builtin_amdgcn_s_memrealtime() : 0;
@@ -989,6 +989,7 @@ __global__ __launch_bounds__(64, PACK_OCC) void pack_bert_wave_kernel(PackParams
             static_assert(sizeof(ML.mpos) + sizeof(ML.mid) >= 2 * MCAP, "F spans mpos + mid");
             for (int k = lane; k < m; k += 64) F[k] = 0xFFFFu;
             wsync();
+            PW_STAMP(8)  // (trace sub-phases: the list reset above -> m_trace; F build -> 11, chains -> 12)
             for (int qb = nm + ((m - nm - 1) & ~63); qb >= nm; qb -= 64) {
               const int q = qb + lane;
               uint32_t j = 0;
@@ -1004,6 +1005,7 @@ __global__ __launch_bounds__(64, PACK_OCC) void pack_bert_wave_kernel(PackParams
                 wsync();
               }
             }
+            PW_STAMP(11)
             // element at v after the early swaps -> jb[nm8 + v]
             for (int v = lane; v < nm; v += 64) {
               uint32_t val = (uint32_t)v, t = F[v];
@@ -1013,6 +1015,7 @@ __global__ __launch_bounds__(64, PACK_OCC) void pack_bert_wave_kernel(PackParams
               }
               ML.jb[nm8 + v] = (uint16_t)val;
             }
+            PW_STAMP(12)
           }
           {
             // identity swaps pad the traced list: jb[0] = 0, jb[q] = q for q in
@@ -1196,7 +1199,7 @@ __global__ __launch_bounds__(64, PACK_OCC) void pack_bert_wave_kernel(PackParams
     for (int k = 0; k < 6; ++k) atomicAdd((unsigned long long*)&P.dbg[k], (unsigned long long)ph[k]);
     atomicAdd((unsigned long long*)&P.dbg[6], (unsigned long long)np);
     atomicAdd((unsigned long long*)&P.dbg[7], 1ull);
-    for (int k = 6; k < 11; ++k) atomicAdd((unsigned long long*)&P.dbg[k + 2], (unsigned long long)ph[k]);
+    for (int k = 6; k < 14; ++k) atomicAdd((unsigned long long*)&P.dbg[k + 2], (unsigned long long)ph[k]);
     P.dbg[16 + 2 * p] = rt0;
     P.dbg[16 + 2 * p + 1] = __builtin_amdgcn_s_memrealtime();
   }
