@@ -1299,24 +1299,34 @@ __global__ __launch_bounds__(64 * WAVES) void wp_kernel(TokParams P, SplitParams
   const uint32_t nwaves = gridDim.x * WAVES;
   const int mb0 = (int)P.maxb[0], mb1 = (int)P.maxb[1];
   const uint32_t vmask = P.vt_mask;
-  // the wave's slot stream: chunk gw first, then chunks handed out by a
+  // the wave's slot stream: unit gw first, then units handed out by a
   // counter (chunks hold different work: dynamic hand-out balances the
-  // launch's tail); the next chunk is fetched one chunk ahead, so the
-  // atomic's round trip flies with the current chunk's loads
+  // launch's tail); a unit is half a chunk's filled slots (the launch's
+  // last units are shorter); the next unit is fetched one unit ahead, so
+  // the atomic's round trip flies with the current unit's loads.  (A record
+  // and its extension slot may fall in different halves: the extension
+  // slot's zero header is skipped wherever it is.)
   uint32_t* const wctr = S.chunk_ctr + 1;  // zeroed with chunk_ctr per segment
-  uint32_t c = blockIdx.x * WAVES + wv, off = 0, fill = 0;
-  uint32_t cn = 0;  // (lane 0) the next chunk
-  if (c < nch) {
-    fill = __builtin_amdgcn_readfirstlane(S.chunk_fill[c]);
+  const uint32_t nun = 2 * nch;
+  uint32_t u = blockIdx.x * WAVES + wv, c = u >> 1, off = 0, fill = 0;
+  uint32_t cn = 0;  // (lane 0) the next unit
+  auto take = [&]() {  // unit u: slots [off, fill) of chunk c
+    const uint32_t f = __builtin_amdgcn_readfirstlane(S.chunk_fill[c]);
+    off = (u & 1u) ? f >> 1 : 0u;
+    fill = (u & 1u) ? f : f >> 1;
+  };
+  if (u < nun) {
+    take();
     if (lane == 0) cn = nwaves + atomicAdd(wctr, 1u);
   }
   auto advance = [&]() {
-    while (off >= fill && c < nch) {
-      c = (uint32_t)__builtin_amdgcn_readlane((int)cn, 0);
+    while (off >= fill && u < nun) {
+      u = (uint32_t)__builtin_amdgcn_readlane((int)cn, 0);
+      c = u >> 1;
       off = 0;
       fill = 0u;
-      if (c < nch) {
-        fill = __builtin_amdgcn_readfirstlane(S.chunk_fill[c]);
+      if (u < nun) {
+        take();
         if (lane == 0) cn = nwaves + atomicAdd(wctr, 1u);
       }
     }
@@ -1485,7 +1495,7 @@ __global__ __launch_bounds__(64 * WAVES) void wp_kernel(TokParams P, SplitParams
     //      instead of idling a step); their loads fly with the bucket loads
     {
       const uint64_t idle = __ballot(pr < 0);
-      if (idle != 0 && c < nch) {
+      if (idle != 0 && u < nun) {
         const uint32_t avail = fill - off;
         const int k = lane_rank(idle);
         if (pr < 0 && (uint32_t)k < avail) {
@@ -1581,7 +1591,7 @@ __global__ __launch_bounds__(64 * WAVES) void wp_kernel(TokParams P, SplitParams
       wacc[4] += 1;
       wacc[5] += __popcll(__ballot(r >= 0));
     }
-    if (__ballot(r >= 0 || pr >= 0) == 0 && c >= nch) break;
+    if (__ballot(r >= 0 || pr >= 0) == 0 && u >= nun) break;
   }
   if (wdbg && lane == 0)
     for (int k = 0; k < 6; ++k) atomicAdd((unsigned long long*)&P.dbg[12 + k], (unsigned long long)wacc[k]);
