@@ -76,6 +76,8 @@ def parse():
   ap.add_argument('--overlap', dest='overlap', action='store_true', default=False,
                   help='step k pack beside step k+1 tokenize on two streams (unmasked)')
   ap.add_argument('--no-overlap', dest='overlap', action='store_false')
+  ap.add_argument('--overlap-priority', type=int, default=1,
+                  help='with --overlap: the pack stream at the higher stream priority (1) or the same (0)')
   ap.add_argument('--frontend-c2-mb', type=float, default=2048.0,
                   help='MB of raw input for the C2-scale CLI leg (seq 512, bin 64: BASELINE configs[1] end to '
                        'end through the preprocessor CLI, rank 0 at N=1, before the GPU is touched; 0: off)')
@@ -692,7 +694,13 @@ def main():
   overlap = args.overlap and not args.masking
   if overlap:
     from lddl_amd.pipeline import TokBuffers
-    st_tok, st_pack = torch.cuda.Stream(device), torch.cuda.Stream(device)
+    # (the pack stream at the higher priority: its one-wave blocks dispatch
+    # first wherever slots free, and the tokenizer's persistent blocks --
+    # which claim their work from counters -- fill what the packer's tail
+    # leaves idle)
+    lo_pri, hi_pri = torch.cuda.Stream.priority_range()
+    st_tok = torch.cuda.Stream(device, priority=lo_pri)
+    st_pack = torch.cuda.Stream(device, priority=hi_pri if args.overlap_priority else lo_pri)
     tbufs = [TokBuffers(), TokBuffers()]
     ov = {'k': 0, 'packed': [None, None]}
 
