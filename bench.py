@@ -616,6 +616,10 @@ def run_leg(args, name, local, device, shards=None):
      'pairs': res.n_pairs, 'packed_tokens': res.n_tokens, 'masked_positions': res.n_masked,
      'tokenize_ms': float(np.mean([x.elapsed_time(y) for x, y in ev])),
      'tokenize_kernels_ms': {'scan': ks['scan_ms'], 'wordpiece': ks['wordpiece_ms'], 'expand': ks['expand_ms']}}
+  try:  # device memory left while the leg's results are live
+    out['hbm_free_gb'] = round(torch.cuda.mem_get_info(device)[0] / 1e9, 1)
+  except Exception:  # (diagnostic only)
+    pass
   if not args.no_sample_check:
     out['sample_check'] = sample_partition_check(a, pk, res, base, pdo, reps, kw['seed'])
   out['leg_seconds'] = time.perf_counter() - t0
@@ -789,7 +793,7 @@ def main():
   # entries the scan hands to wp_kernel / expand_kernel are this design's
   # intermediates, not algorithmic (they show in roofline.traffic).  Divided
   # by the scan's HIP-event time inside the call (events on the launch
-  # stream; one scan launch per segment of SPLIT_SEG_TILES KiB, 4 GiB).
+  # stream; one scan launch per segment of SPLIT_SEG_TILES KiB).
   nl = ks['launches']
   alg_call = sh.nbytes + 12 * sh.n_sent + 2 * n_tok
   alg = (sh.nbytes + 12 * sh.n_sent) / nl
@@ -832,6 +836,12 @@ def main():
       'wordpiece_records_per_gpu': ks['records'], 'tokenizer_fallback_tiles': ks['fallback_tiles'],
       'gen_s': gen_s,
   }
+  try:  # device memory left beside the corpus, the tokenizer / packer scratch and the outputs
+    free_b, total_b = torch.cuda.mem_get_info(device)
+    line['hbm_free_gb'] = round(free_b / 1e9, 1)
+    line['hbm_total_gb'] = round(total_b / 1e9, 1)
+  except Exception:  # (diagnostic only)
+    pass
   # HBM traffic of the tokenize call from the committed PMC passes of this
   # same workload (rocprofv3 cannot run inside the timed process)
   try:

@@ -82,11 +82,13 @@ int64_t fb_list_cap(int64_t seg_tiles);
 //          a tile's slots contiguous, in unit order
 //   smeta  per sentence: #entries | first slot relative to the tile's << 16,
 //          the tile's first slot
-// 4 GiB of input per segment: 48 GB of scratch (entries 2 B/byte, record
+// 8 GiB of input per segment: ~100 GB of scratch (entries 2 B/byte, record
 // slots and WordPiece outputs 64 B per 14 B each); fewer kernel boundaries
-// than 1 GiB segments (bench step 250.8 -> 246.7 ms; 2 GiB: 249.1).  The
-// masked bench at 20 GB of corpus leaves ~147 GB of the 309 GB free.
-constexpr int64_t SPLIT_SEG_TILES = int64_t(1) << 22;
+// and launch tails than 4 GiB segments (3 launches per kernel for the 21.4 GB
+// bench step instead of 5: 112.6 -> 110.9 ms, profiles/r6/seg/; earlier 4 vs
+// 1 GiB: 246.7 vs 250.8 ms).  The masked bench at 20 GB of corpus still leaves
+// ~50 GB of the 309 GB free (hbm_free_gb in the bench legs).
+constexpr int64_t SPLIT_SEG_TILES = int64_t(1) << 23;
 constexpr uint32_t SPLIT_CHUNK = 1024;                 // record slots per allocation chunk (64 KiB)
 constexpr uint32_t SPLIT_EDEF = 0xF000u;               // entry >= EDEF: a queued word
 constexpr uint16_t SPLIT_NENT_FB = 0xFFFFu;            // nent of a sentence of a fallback tile

@@ -5,7 +5,7 @@
 // tokenizer.tokenize(s, max_length=512, truncation=True),
 // lddl/dask/bert/pretrain.py:79-80 (oracle/tokenizer_oracle.c).
 //
-// Per 4 GiB segment of tiles:
+// Per segment of tiles (SPLIT_SEG_TILES):
 //   lane_kernel     waves take batches of LANE_BATCH tiles from a counter;
 //                   a lane takes the batch's next tile whenever it finishes
 //                   one (so lanes stay busy until the segment's last batch).
