@@ -432,7 +432,10 @@ def frontend_leg(mb, chunk_mb=32.0, seq=128, bin_size=None, unique_mb=256):
   command line does, started before this process touches the GPU; wall,
   host read / sentence split / GPU / parquet write seconds and the split
   time hidden behind the GPU and the writer, as preprocess.main reports
-  them (main() itself: interpreter start-up and imports excluded)."""
+  them (main() itself: interpreter start-up and imports excluded), and the
+  CPU seconds of the CLI process and of its reaped workers (split pool,
+  encoders) over the run: against host_cpus share x wall, whether the leg
+  is CPU-bound."""
   import shutil
   import tempfile
   from lddl_amd import synth
@@ -463,7 +466,11 @@ def frontend_leg(mb, chunk_mb=32.0, seq=128, bin_size=None, unique_mb=256):
     code = ('import json, sys, time; t0 = time.perf_counter(); import torch; '
             'from lddl_amd import preprocess, pipeline, writer, balance; imp = time.perf_counter() - t0; '
             'a = preprocess.attach_args().parse_args(json.loads(sys.argv[1])); '
+            'import resource; r0 = resource.getrusage(resource.RUSAGE_SELF); '
             't0 = time.perf_counter(); files, t = preprocess.main(a); el = time.perf_counter() - t0; '
+            'r1 = resource.getrusage(resource.RUSAGE_SELF); rc = resource.getrusage(resource.RUSAGE_CHILDREN); '
+            't["cpu_main_s"] = (r1.ru_utime - r0.ru_utime) + (r1.ru_stime - r0.ru_stime); '
+            't["cpu_workers_s"] = rc.ru_utime + rc.ru_stime; '
             't.pop("partitions", None); t["files"] = len(files); t["el"] = el; t["imports_s"] = imp; '
             'print("LDDL_LEG " + json.dumps({k: v for k, v in t.items() if isinstance(v, (int, float, str))}))')
     p = subprocess.run([sys.executable, '-c', code, json.dumps(argv)], stdout=subprocess.PIPE,
