@@ -120,6 +120,11 @@ struct lddl_ctx {
   int tok_algo = 5;  // 5 = split tokenizer, 6 = lane tokenizer, 0 = every tile through the exact serial path
   uint8_t* d_ovf = nullptr;
   uint32_t* d_counter = nullptr;
+  // debug counters of the tokenizer (LDDL_TOK_DEBUG=1) and of the packers
+  // (LDDL_PACK_DEBUG=1: phase ticks + per-wave start / end), on this ctx's device
+  uint64_t* d_tdbg = nullptr;
+  uint64_t* d_pdbg = nullptr;
+  int64_t pdbg_cap = 0;
   // collate: whole-token vocab table (built on first use)
   uint2* d_ctab = nullptr;
   uint32_t ctab_mask = 0;
@@ -156,6 +161,8 @@ extern "C" const char* lddl_last_error(void) { return g_err; }
 
 static void free_ctx(lddl_ctx* c) {
   if (!c) return;
+  (void)hipFree(c->d_tdbg);
+  (void)hipFree(c->d_pdbg);
   (void)hipFree(c->d_top);
   (void)hipFree(c->d_pages);
   (void)hipFree(c->d_bmp);
@@ -391,11 +398,11 @@ extern "C" int lddl_tokenize(lddl_ctx* c, const uint8_t* d_bytes, int64_t nbytes
   P.work_counter = c->d_counter;
   HIP_TRY(hipMemsetAsync(c->d_counter, 0, 64, st));
   const char* dbgenv = getenv("LDDL_TOK_DEBUG");
-  static uint64_t* d_dbg = nullptr;
+
   if (dbgenv && dbgenv[0] == '1') {
-    if (!d_dbg) HIP_TRY(hipMalloc((void**)&d_dbg, 32 * 8));
-    HIP_TRY(hipMemsetAsync(d_dbg, 0, 32 * 8, st));
-    P.dbg = d_dbg;
+    if (!c->d_tdbg) HIP_TRY(hipMalloc((void**)&c->d_tdbg, 32 * 8));
+    HIP_TRY(hipMemsetAsync(c->d_tdbg, 0, 32 * 8, st));
+    P.dbg = c->d_tdbg;
   }
   const int64_t nt = tile_count(nbytes);
   // LDDL_SPLIT_SEG (tiles per segment) / LDDL_SPLIT_CHUNKS (record chunks):
@@ -668,19 +675,19 @@ static int pack_common(lddl_ctx* c, lddl_pack* pk, int codebert, const int32_t* 
       P.mcap = k->mlm_cap;
       HIP_TRY(hipMemsetAsync(P.mcounter, 0, 8, st));
     }
-    static uint64_t* d_pdbg = nullptr;
-    static int64_t pdbg_cap = 0;
     const char* pdbg = getenv("LDDL_PACK_DEBUG");
     P.dbg = nullptr;
     const int64_t pdbg_n = 16 + 2 * (int64_t)n_part;  // counters + the BERT packer's per-wave start / end
     if (pdbg && pdbg[0] == '1') {
-      if (pdbg_cap < pdbg_n) {
-        if (d_pdbg) HIP_TRY(hipFree(d_pdbg));
-        HIP_TRY(hipMalloc((void**)&d_pdbg, pdbg_n * 8));
-        pdbg_cap = pdbg_n;
+      if (c->pdbg_cap < pdbg_n) {
+        (void)hipFree(c->d_pdbg);
+        c->d_pdbg = nullptr;
+        c->pdbg_cap = 0;
+        HIP_TRY(hipMalloc((void**)&c->d_pdbg, pdbg_n * 8));
+        c->pdbg_cap = pdbg_n;
       }
-      HIP_TRY(hipMemsetAsync(d_pdbg, 0, pdbg_n * 8, st));
-      P.dbg = d_pdbg;
+      HIP_TRY(hipMemsetAsync(c->d_pdbg, 0, pdbg_n * 8, st));
+      P.dbg = c->d_pdbg;
     }
     HIP_TRY(codebert ? launch_pack_codebert_wave(P, st) : launch_pack_bert_wave(P, st));
     if (P.dbg && !codebert) {
