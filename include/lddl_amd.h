@@ -127,7 +127,9 @@ int lddl_pack_rows(const lddl_pack *pack, int64_t *out_npairs);
  * Partition p = docs [d_part_doc_off[p], d_part_doc_off[p+1]); doc d =
  * sentences [d_doc_sent_off[d], d_doc_sent_off[d+1]); d_ids / d_ntok /
  * d_tok_off / d_sent_off are lddl_tokenize's output / input (d_ids may be
- * NULL unless masking; all of them must stay live until lddl_materialize).  Partition p is packed exactly like the reference's
+ * NULL unless masking; all of them must stay live until lddl_materialize;
+ * every d_ntok count <= 65535, as any lddl_tokenize output with max_tok <=
+ * 65535 -- the packers keep the counts as u16).  Partition p is packed exactly like the reference's
  * _to_partition_pairs (pretrain.py:386-402) after random.seed(seed + p):
  * duplicate_factor passes of create_pairs_from_document (:241-365), then
  * random.shuffle, then (bin_size > 0) the stable bin grouping of

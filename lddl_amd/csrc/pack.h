@@ -36,7 +36,7 @@ struct PackParams {
   int32_t bin_size;             // --bin-size (or max_seq when unbinned)
   int32_t nbins;                // max_seq // bin_size (1 when unbinned)
   // scratch, indexed like the corpus (sentence / doc / partition slots)
-  int32_t* fs_ntok;             // [n_sent]
+  uint16_t* fs_ntok;            // [n_sent] token count per filtered slot (<= max_tok; u16: half the L2 footprint of the random-next reads)
   int64_t* fs_base;             // [n_sent] byte offset (sent_off - base) per filtered slot (row_docs)
   int64_t* fs_dense;            // [n_sent] dense id offset (tokoff) per filtered slot
   const int64_t* tokoff;        // [n_sent+1] exclusive scan of ntok: sentence s's ids in the dense array
@@ -108,7 +108,7 @@ struct MatParams {
   const int64_t* doc_sent_off;
   const int64_t* part_doc_off;
   const int64_t* fs_base;
-  const int32_t* fs_ntok;
+  const uint16_t* fs_ntok;
   const PairRec* pairs;
   const int32_t* binned;
   const int64_t* tok_local;

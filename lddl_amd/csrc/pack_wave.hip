@@ -627,7 +627,7 @@ __global__ __launch_bounds__(64, PACK_OCC) void pack_bert_wave_kernel(PackParams
         const int slot = run + incl - keep;
         kept_before[kk] = slot;
         if (keep) {
-          P.fs_ntok[s0 + slot] = n;
+          P.fs_ntok[s0 + slot] = (uint16_t)n;
           P.fs_base[s0 + slot] = P.sent_off[s0 + kk] - base;
           P.fs_dense[s0 + slot] = P.tokoff[s0 + kk];
           if (MASK) {
@@ -1321,7 +1321,7 @@ __global__ __launch_bounds__(64) void pack_codebert_wave_kernel(PackParams P) {
         const int slot = run + incl - keep;
         kept_before[kk] = slot;
         if (keep) {
-          P.fs_ntok[s0 + slot] = n;
+          P.fs_ntok[s0 + slot] = (uint16_t)n;
           P.fs_base[s0 + slot] = P.sent_off[s0 + kk] - base;
           P.fs_dense[s0 + slot] = P.tokoff[s0 + kk];
         }
