@@ -2071,15 +2071,19 @@ hipError_t finish_segment(TokParams P, const SplitParams& S, int n_cu, int fb_gr
   if ((e = launch_scan_ntok_range(P.out_ntok, S.tile_sent + S.t0, S.tile_sent + S.t1, S.seg_sent_cap, P.out_tok_off,
                                   S.scan_bsum, s)) != hipSuccess)
     return e;
-  // blocks per CU of the grid-stride expand (4 waves each; more than fit at once: the later ones
-  // balance the tail): LDDL_EXP_BLOCKS (A/B), default 16 (finish 1.75 -> 1.65 ms per 2 GiB,
-  // profiles/r4_exp.txt)
+  // blocks per CU of the grid-stride expand (4 waves each, far more than fit at once: the
+  // hardware hands the later blocks to whichever waves finish, so each wave runs few groups and
+  // the launch's tail is short): LDDL_EXP_BLOCKS (A/B), default 192 -- 16 / 32 / 96 / 192 / 768
+  // measured 16.7 / 16.0 / 15.3 / 15.2 / 15.1 ms per 21.4 GB step with 8 GiB segments
+  // (profiles/r6/eb/; 16 was best at 2 GiB segments in round 4); no more blocks than a block-round
+  // of 256 sentences each needs
   static const int exp_blocks = [] {
     const char* v = getenv("LDDL_EXP_BLOCKS");
     const int b = v ? atoi(v) : 0;
-    return b > 0 && b <= 32 ? b : 16;
+    return b > 0 && b <= 4096 ? b : 192;
   }();
-  hipLaunchKernelGGL(tok5::expand_kernel, dim3((unsigned)std::max(1, n_cu * exp_blocks)), dim3(256), 0, s, P, S);
+  const int64_t exp_grid = std::max<int64_t>(1, std::min<int64_t>((int64_t)n_cu * exp_blocks, (S.seg_sent_cap + 255) / 256));
+  hipLaunchKernelGGL(tok5::expand_kernel, dim3((unsigned)exp_grid), dim3(256), 0, s, P, S);
   return hipGetLastError();
 }
 
