@@ -946,7 +946,7 @@ extern "C" int lddl_masked_lm(lddl_ctx* c, lddl_pack* pk, int64_t* d_out_mlm_off
     M.out_off = d_out_mlm_off;
     M.out_pos = d_out_mlm_pos;
     M.out_label = d_out_mlm_label;
-    HIP_TRY(launch_masked_lm(M, st));
+    HIP_TRY(launch_masked_lm(M, k->last_npairs, st));
   }
   k->last_nmask = -1;  // the rows are masked in place exactly once
   return 0;
@@ -990,7 +990,7 @@ extern "C" int lddl_masked_lm_spans(lddl_ctx* c, lddl_pack* pk, const uint16_t* 
     M.out_pos = d_out_mlm_pos;
     M.out_label = d_out_mlm_label;
     M.out_token = d_out_mlm_token;
-    HIP_TRY(launch_masked_lm(M, st));
+    HIP_TRY(launch_masked_lm(M, k->last_npairs, st));
   }
   return 0;
 }

@@ -163,6 +163,6 @@ hipError_t launch_bin(const int64_t* num_tokens, int64_t n, int32_t bin_size, in
                       hipStream_t s);
 hipError_t launch_sent_special(const uint16_t* ids, const int64_t* tok_off, const int32_t* ntok, int64_t n_sent,
                                uint32_t cls, uint32_t sep, uint8_t* out, hipStream_t s);
-hipError_t launch_masked_lm(const MlmParams& M, hipStream_t s);
+hipError_t launch_masked_lm(const MlmParams& M, int64_t n_rows, hipStream_t s);
 
 }  // namespace lddl

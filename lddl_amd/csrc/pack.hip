@@ -705,9 +705,20 @@ hipError_t launch_sent_special(const uint16_t* ids, const int64_t* tok_off, cons
   return hipGetLastError();
 }
 
-hipError_t launch_masked_lm(const MlmParams& M, hipStream_t s) {
-  if (M.tokens) hipLaunchKernelGGL(masked_lm_kernel, dim3(2048), dim3(256), 0, s, M);
-  else hipLaunchKernelGGL(masked_lm_spans_kernel, dim3(4096), dim3(256), 0, s, M);
+// masked_lm_spans_kernel's grid: up to one 64-row group per wave (blocks of 4
+// waves), capped at LDDL_MLM_GRID blocks -- the hardware then balances the
+// launch instead of a fixed grid-stride share per wave (4096 blocks: 424.5,
+// 65 536: 420.8 ms per masked step, profiles/r6/v/)
+#ifndef LDDL_MLM_GRID
+#define LDDL_MLM_GRID (1 << 20)
+#endif
+hipError_t launch_masked_lm(const MlmParams& M, int64_t n_rows, hipStream_t s) {
+  if (M.tokens) {
+    hipLaunchKernelGGL(masked_lm_kernel, dim3(2048), dim3(256), 0, s, M);
+  } else {
+    const int64_t grid = std::max<int64_t>(1, std::min<int64_t>((n_rows + 255) / 256, LDDL_MLM_GRID));
+    hipLaunchKernelGGL(masked_lm_spans_kernel, dim3((unsigned)grid), dim3(256), 0, s, M);
+  }
   return hipGetLastError();
 }
 

@@ -2066,7 +2066,11 @@ hipError_t finish_segment(TokParams P, const SplitParams& S, int n_cu, int fb_gr
   F.out_ids = S.ent - (S.t0 << 10);  // the serial path writes at sent_off[s] - sent_off[0]
   hipError_t e = launch_tokenize_fallback(F, S.fb_list, S.fb_count, fb_grid, s);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(tok5::count_kernel, dim3((unsigned)std::max(1, n_cu * 8)), dim3(256), 0, s, P, S);
+#ifndef LDDL_CNT_BLOCKS
+#define LDDL_CNT_BLOCKS 256
+#endif
+  const int64_t cnt_grid = std::max<int64_t>(1, std::min<int64_t>((int64_t)n_cu * LDDL_CNT_BLOCKS, (S.seg_sent_cap + 255) / 256));
+  hipLaunchKernelGGL(tok5::count_kernel, dim3((unsigned)cnt_grid), dim3(256), 0, s, P, S);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   if ((e = launch_scan_ntok_range(P.out_ntok, S.tile_sent + S.t0, S.tile_sent + S.t1, S.seg_sent_cap, P.out_tok_off,
                                   S.scan_bsum, s)) != hipSuccess)
