@@ -1,4 +1,4 @@
-// C-ABI of libldl_amd.so: the drop-in boundary (declared in include/lddl_amd.h).
+// C-ABI of liblddl_amd.so: the drop-in boundary (declared in include/lddl_amd.h).
 // Plain pointers and sizes only; device pointers come from the caller
 // (torch tensors via data_ptr(), or hipMalloc).  Every entry point returns 0
 // on success and a negative LDDL_E* code on failure; the message is kept in
@@ -615,6 +615,12 @@ static int pack_common(lddl_ctx* c, lddl_pack* pk, int codebert, const int32_t* 
       (rc = ws_get(k->ws, 14, n_part, &P.part_err)) || (rc = ws_get(k->ws, 18, n_sent + n_part + 1, &P.kept)) ||
       (rc = ws_get(k->ws, 33, n_sent, &P.fs_dense)))
     return rc;
+  {
+    uint32_t* mts;
+    if ((rc = ws_get(k->ws, 19, (size_t)n_part * MT_N, &mts))) return rc;
+    HIP_TRY(launch_mt_seed_states(seed, n_part, mts, st));
+    P.mt_states = mts;
+  }
   P.tokoff = d_tok_off;  // the tokenizer's dense offsets (lddl_tokenize d_out_tok_off)
   int64_t *pair_base, *tok_base;
   int32_t* err_any;

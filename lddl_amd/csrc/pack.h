@@ -33,6 +33,7 @@ struct PackParams {
   int32_t dup;                  // --duplicate-factor
   double short_seq_prob;        // --short-seq-prob
   uint64_t seed;                // partition p uses random.seed(seed + p)
+  const uint32_t* mt_states;    // [n_part][MT_N]: those seeded states (launch_mt_seed_states)
   int32_t bin_size;             // --bin-size (or max_seq when unbinned)
   int32_t nbins;                // max_seq // bin_size (1 when unbinned)
   // scratch, indexed like the corpus (sentence / doc / partition slots)
@@ -134,6 +135,8 @@ struct MatParams {
   int64_t* out_src1;            //                 [n_pairs] of segment B / code
 };
 
+// random.seed(seed + p) for p < n_part: states[p * MT_N ..] = the MT19937 state
+hipError_t launch_mt_seed_states(uint64_t seed, int64_t n_part, uint32_t* states, hipStream_t s);
 hipError_t launch_pack_bert_wave(const PackParams& P, hipStream_t s);
 size_t pack_dyn_bytes(int cap_lens, int cap_docs, int cap_pairs, bool mask);
 hipError_t launch_pack_codebert_wave(const PackParams& P, hipStream_t s);

@@ -147,29 +147,61 @@ constexpr MtTable mt_genrand_table(uint32_t s) {
 }
 __constant__ MtTable kMtGenrand = mt_genrand_table(19650218u);
 
-// init_by_array's chain over positions [base + l0, base + l1) (l0 even,
-// l1 - l0 even): the positions' old words one per lane (src), the chain's
-// carried word mt[i-1] in `prev`, the new words written back lane-wise (no
-// LDS round trip per step).  PASS 1: mt[i] = (mt[i] ^ f(mt[i-1]) * 1664525)
-// + key[j] + j, j = (i - 1) % klen (klen <= 2; base is even, so position
-// base + l adds kb for even l, ka for odd l); PASS 2: mt[i] = (mt[i] ^
-// f(mt[i-1]) * 1566083941) - i.
-template <int PASS>
-__device__ __forceinline__ uint32_t mt_seed_run(uint32_t src, int base, int l0, int l1, uint32_t& prev, uint32_t ka,
-                                                uint32_t kb, int lane) {
-  uint32_t out = src;
-  auto step = [&](int l, uint32_t add) {
-    const uint32_t old = (uint32_t)__builtin_amdgcn_readlane((int)src, l);
-    const uint32_t f = prev ^ (prev >> 30);
-    prev = PASS == 1 ? (old ^ (f * 1664525u)) + add : (old ^ (f * 1566083941u)) - (uint32_t)(base + l);
-    out = lane == l ? prev : out;
-  };
-#pragma unroll 2
-  for (int l = l0; l < l1; l += 2) {
-    step(l, kb);
-    step(l + 1, ka);
+// random.seed(seed + p) (CPython init_by_array, key = the seed's 32-bit words,
+// klen <= 2) for partitions [64 b, 64 b + 64): one LANE per partition runs
+// the 1247-step dependent chain on its own LDS row, so the whole corpus's
+// seeding is one short launch (vs one serial chain per packer wave on the
+// shared scalar unit); the rows then go out partition-major, 624 words per
+// partition, for the packer's coalesced load (WaveRng::load).
+constexpr int MT_ROW = MT_N + 1;  // odd row stride: the lanes' same-index words fall in distinct banks
+__global__ __launch_bounds__(64) void mt_seed_states_kernel(uint64_t seed, int64_t n_part,
+                                                            uint32_t* __restrict__ states) {
+  __shared__ uint32_t rows[64 * MT_ROW];
+  const int lane = threadIdx.x;
+  const int64_t p0 = (int64_t)blockIdx.x * 64;
+  const uint64_t n = seed + (uint64_t)(p0 + lane);
+  const uint32_t key0 = (uint32_t)n;
+  const uint32_t key1 = (uint32_t)(n >> 32) + 1u;  // key[1] + j (j = 1)
+  const bool two = (n >> 32) != 0;                 // klen 2
+  uint32_t* r = rows + lane * MT_ROW;
+  for (int i = 0; i < MT_N; ++i) r[i] = kMtGenrand.v[i];
+  // first loop, max(N, klen) = N steps from i = 1; prev is always mt[i - 1]
+  // (after the wrap, mt[0] = mt[N - 1] = prev)
+  uint32_t prev = r[0];
+  int i = 1;
+  bool odd = false;  // j == 1
+  for (int k = 0; k < MT_N; ++k) {
+    prev = (r[i] ^ ((prev ^ (prev >> 30)) * 1664525u)) + (odd ? key1 : key0);
+    r[i] = prev;
+    odd = two && !odd;
+    if (++i >= MT_N) {
+      r[0] = prev;
+      i = 1;
+    }
   }
-  return out;
+  // second loop, N - 1 steps, continuing at i (= 2)
+  for (int k = 0; k < MT_N - 1; ++k) {
+    prev = (r[i] ^ ((prev ^ (prev >> 30)) * 1566083941u)) - (uint32_t)i;
+    r[i] = prev;
+    if (++i >= MT_N) {
+      r[0] = prev;
+      i = 1;
+    }
+  }
+  r[0] = 0x80000000u;
+  __syncthreads();
+  for (int q = 0; q < 64 && p0 + q < n_part; ++q) {
+    const uint32_t* rq = rows + q * MT_ROW;
+    uint32_t* o = states + (p0 + q) * MT_N;
+    for (int c = lane; c < MT_N; c += 64) o[c] = rq[c];
+  }
+}
+
+hipError_t launch_mt_seed_states(uint64_t seed, int64_t n_part, uint32_t* states, hipStream_t s) {
+  if (n_part < 1) return hipSuccess;
+  hipLaunchKernelGGL(mt_seed_states_kernel, dim3((unsigned)((n_part + 63) / 64)), dim3(64), 0, s, seed, n_part,
+                     states);
+  return hipGetLastError();
 }
 
 struct WaveRng {
@@ -180,50 +212,10 @@ struct WaveRng {
                       // (one LDS read per 64 draws); draws below wend come from it
   uint32_t win = 0;
 
-  // random.seed(n) for 0 <= n < 2^64: init_by_array(key = n's 32-bit words,
-  // klen <= 2).  Its first loop visits positions 1..623 then 1 again (MT_N
-  // steps), its second 2..623 then 1 (MT_N - 1 steps); mt[i-1] of position 1
-  // is mt[0] = the new mt[623], i.e. the chain's carried word; mt[0] ends as
-  // 0x80000000.
-  __device__ __forceinline__ void seed(uint64_t n) {
-    const uint32_t ka = (uint32_t)n;                                // j = 0: key[0] + 0
-    const uint32_t kb = (n >> 32) ? (uint32_t)(n >> 32) + 1u : ka;  // j = 1 (klen 2): key[1] + 1
-    uint32_t* mt = L.mt;
-    constexpr int NC = (MT_N + 63) / 64;
-    // first loop: position 1 (j = 0), then 2..623, then 1 again
-    uint32_t prev;
-    {
-      const uint32_t f = 19650218u ^ (19650218u >> 30);  // init_genrand's mt[0]
-      prev = (kMtGenrand.v[1] ^ (f * 1664525u)) + ka;
-    }
-    const uint32_t m1a = prev;
-#pragma unroll 1
-    for (int c = 0; c < NC; ++c) {
-      const int i = 64 * c + lane;
-      uint32_t w = kMtGenrand.v[min(i, MT_N - 1)];
-      w = mt_seed_run<1>(w, 64 * c, c == 0 ? 2 : 0, min(64, MT_N - 64 * c), prev, ka, kb, lane);
-      if (i < MT_N) mt[i] = w;
-    }
-    uint32_t m1;
-    {  // step MT_N: position 1 again, j = (MT_N - 1) % klen -> kb
-      const uint32_t f = prev ^ (prev >> 30);
-      m1 = (m1a ^ (f * 1664525u)) + kb;
-      prev = m1;
-    }
-    // second loop: positions 2..623, then 1 (each lane re-reads only what it wrote)
-#pragma unroll 1
-    for (int c = 0; c < NC; ++c) {
-      const int i = 64 * c + lane;
-      uint32_t w = mt[min(i, MT_N - 1)];
-      w = mt_seed_run<2>(w, 64 * c, c == 0 ? 2 : 0, min(64, MT_N - 64 * c), prev, ka, kb, lane);
-      if (i < MT_N) mt[i] = w;
-    }
-    {
-      const uint32_t f = prev ^ (prev >> 30);
-      const uint32_t p1 = (m1 ^ (f * 1566083941u)) - 1u;
-      if (lane == 0) mt[0] = 0x80000000u;
-      if (lane == 1) mt[1] = p1;
-    }
+  // random.seed(seed + p): the state mt_seed_states_kernel left for this
+  // partition (624 words, coalesced), the next draw twists
+  __device__ __forceinline__ void load(const uint32_t* __restrict__ st) {
+    for (int c = lane; c < MT_N; c += 64) L.mt[c] = st[c];
     wsync();
     idx = MT_N;
   }
@@ -713,7 +705,7 @@ __global__ __launch_bounds__(64, PACK_OCC) void pack_bert_wave_kernel(PackParams
   };
 
   WaveRng rng{L, lane, MT_N};
-  rng.seed(P.seed + (uint64_t)p);
+  rng.load(P.mt_states + (int64_t)p * MT_N);
   PW_STAMP(2)
   const int max_num = P.max_seq - 3;
   PairRec* out = P.pairs + pb;
@@ -1362,7 +1354,7 @@ __global__ __launch_bounds__(64) void pack_codebert_wave_kernel(PackParams P) {
   auto len_abs = [&](int64_t slot) -> int { return P.fs_ntok[slot]; };
 
   WaveRng rng{L, lane, MT_N};
-  rng.seed(P.seed + (uint64_t)p);
+  rng.load(P.mt_states + (int64_t)p * MT_N);
   const int max_doc = P.max_seq >= 512 ? 64 : 32;
   PairRec* out = P.pairs + pb;
   int np = 0;
