@@ -1807,9 +1807,10 @@ __global__ __launch_bounds__(256) void count_kernel(TokParams P, SplitParams S) 
 // the marks at or below its lane (v_mbcnt) plus those of earlier steps; the
 // step's entries are loaded one step ahead, so each
 // step's record loads (count + first 4 pieces, one 12-B load) fly with the
-// next step's entry loads.  A segmented scan of the token counts gives each
-// token's position in its sentence, written at out_tok_off[s] + position
-// while below the sentence's final count (count_kernel) and out_cap.
+// next step's entry loads.  A scan of the step's token counts, less its value
+// at the sentence's first entry (one ds_bpermute), gives each token's position
+// in its sentence, written at out_tok_off[s] + position while below the
+// sentence's final count (count_kernel) and out_cap.
 struct ExpSent {
   int64_t eb;    // entry index of the sentence's entry g (group numbering) = eb + g
   int64_t dst;   // output index of its first token
@@ -1865,12 +1866,12 @@ __global__ __launch_bounds__(256) void expand_kernel(TokParams P, SplitParams S)
     if (ne != 0) E.sn[bits_below(nzm)] = es;
     // the sentence (non-empty rank) of each entry of step st (entries st + lane)
     uint32_t hcar = 0;  // non-empty sentences that start before the step
-    auto owner = [&](uint32_t st, bool& head) -> uint32_t {
+    auto owner = [&](uint32_t st) -> uint32_t {
       ++tag;
       if (ne != 0 && e0 - st < 64u) E.hf[e0 - st] = tag;
       wsync();
-      const uint64_t hm = __ballot(E.hf[lane] == tag);
-      head = (hm >> lane) & 1ull;
+      const bool head = E.hf[lane] == tag;
+      const uint64_t hm = __ballot(head);
       const uint32_t o = hcar + (uint32_t)bits_below(hm) + (head ? 0u : (uint32_t)-1);
       hcar += (uint32_t)__popcll(hm);
       return o;
@@ -1888,20 +1889,18 @@ __global__ __launch_bounds__(256) void expand_kernel(TokParams P, SplitParams S)
     uint32_t carry = 0;
     for (uint32_t st0 = 0; st0 < T; st0 += 64 * EXP_K) {
       uint32_t xj[EXP_K], xv[EXP_K];
-      bool xin[EXP_K], xhead[EXP_K];
+      bool xin[EXP_K];
 #pragma unroll
       for (int k = 0; k < EXP_K; ++k) {
         const uint32_t st = st0 + 64 * k;
         xj[k] = 0;
         xv[k] = 0;
-        xin[k] = xhead[k] = false;
+        xin[k] = false;
         if (st < T) {
           const uint32_t g = st + (uint32_t)lane;
-          bool hd;
-          xj[k] = min(owner(st, hd), 63u);
+          xj[k] = min(owner(st), 63u);
           xin[k] = g < T;
           const ExpSent sj = E.sn[xj[k]];
-          xhead[k] = xin[k] && hd;
           xv[k] = S.ent[xin[k] ? sj.eb + g : 0];  // (every lane loads: no branch around the load)
         }
       }
@@ -1918,30 +1917,34 @@ __global__ __launch_bounds__(256) void expand_kernel(TokParams P, SplitParams S)
         const uint32_t st = st0 + 64 * k;
         if (st >= T) break;
         const uint32_t cj = xj[k], cv = xin[k] ? xv[k] : 0u;
-        const bool cin = xin[k], chead = xhead[k], rec = cin && cv >= SPLIT_EDEF && cv != SPLIT_EHOLE;
+        const bool cin = xin[k], rec = cin && cv >= SPLIT_EDEF && cv != SPLIT_EHOLE;
         // (a hole: an empty unit, no token; a direct id: one)
         const u32x3 rq = rec ? xr[k] : u32x3{cin && cv != SPLIT_EHOLE ? 1u : 0u, 0u, 0u};
         const ExpSent sj = E.sn[cj];
         const size_t ri = (size_t)(sj.qb + (cv & 0xFFFu)) * 4;
         const uint32_t cnt = rq.x;
-        uint32_t hv = chead ? 1u : 0u, sv = cnt;
-        wave_seg_incl_add(hv, sv);
-        uint32_t ex = wave_shr1(sv);
-        if (!wave_shr1(hv)) ex += carry;
-        const uint32_t p = chead ? 0u : ex;  // tokens of the sentence before this entry
-        if (cin) {
-          uint16_t* o = P.out_ids + sj.dst;
-          const uint32_t lm = sj.lim;
+        // tokens of the sentence before this entry: the step's exclusive sum
+        // less its value at the sentence's first entry (lane e0 - st), or plus
+        // the carry when the sentence began in an earlier step
+        const uint32_t xex = wave_incl_add(cnt) - cnt;
+        const int hl = (int)(sj.e0 - st);
+        const uint32_t hb = (uint32_t)__shfl((int)xex, hl & 63);
+        const uint32_t p = xex - (hl >= 0 ? hb : 0u - carry);
+        // tokens this entry writes (a hole and a lane past the step: none; a
+        // direct id: at most one)
+        // (signed: lim and p are < 2^31)
+        const int room = (int)sj.lim - (int)p;
+        const uint32_t nw = room > 0 ? min(cnt, (uint32_t)room) : 0u;
+        if (nw) {
+          uint16_t* o = P.out_ids + sj.dst + p;
           // (the first token of a direct id and of a record in one store)
-          if (cnt && p < lm) o[p] = (uint16_t)(cv < SPLIT_EDEF ? cv : rq.y & 0xFFFFu);
-          if (rec) {
-            if (cnt > 1 && p + 1 < lm) o[p + 1] = (uint16_t)(rq.y >> 16);
-            if (cnt > 2 && p + 2 < lm) o[p + 2] = (uint16_t)(rq.z & 0xFFFFu);
-            if (cnt > 3 && p + 3 < lm) o[p + 3] = (uint16_t)(rq.z >> 16);
-            if (cnt > 4) {
-              const uint16_t* pc = reinterpret_cast<const uint16_t*>(pcs + ri);
-              for (uint32_t q = 4; q < cnt && p + q < lm; ++q) o[p + q] = pc[piece_at((int)q)];
-            }
+          o[0] = (uint16_t)(cv < SPLIT_EDEF ? cv : rq.y & 0xFFFFu);
+          if (nw > 1) o[1] = (uint16_t)(rq.y >> 16);
+          if (nw > 2) o[2] = (uint16_t)(rq.z & 0xFFFFu);
+          if (nw > 3) o[3] = (uint16_t)(rq.z >> 16);
+          if (nw > 4) {
+            const uint16_t* pc = reinterpret_cast<const uint16_t*>(pcs + ri);
+            for (uint32_t q = 4; q < nw; ++q) o[q] = pc[piece_at((int)q)];
           }
         }
         // running total of the step's last entry (its sentence may continue)
