@@ -617,7 +617,7 @@ static int pack_common(lddl_ctx* c, lddl_pack* pk, int codebert, const int32_t* 
     return rc;
   {
     uint32_t* mts;
-    if ((rc = ws_get(k->ws, 19, (size_t)n_part * MT_N, &mts))) return rc;
+    if ((rc = ws_get(k->ws, 19, (size_t)((n_part + 63) & ~(int64_t)63) * MT_N, &mts))) return rc;  // (whole 64-partition rows)
     HIP_TRY(launch_mt_seed_states(seed, n_part, mts, st));
     P.mt_states = mts;
   }

@@ -136,6 +136,7 @@ struct MatParams {
 };
 
 // random.seed(seed + p) for p < n_part: states[p * MT_N ..] = the MT19937 state
+// (states holds ceil(n_part / 64) * 64 rows)
 hipError_t launch_mt_seed_states(uint64_t seed, int64_t n_part, uint32_t* states, hipStream_t s);
 hipError_t launch_pack_bert_wave(const PackParams& P, hipStream_t s);
 size_t pack_dyn_bytes(int cap_lens, int cap_docs, int cap_pairs, bool mask);

@@ -148,59 +148,45 @@ constexpr MtTable mt_genrand_table(uint32_t s) {
 __constant__ MtTable kMtGenrand = mt_genrand_table(19650218u);
 
 // random.seed(seed + p) (CPython init_by_array, key = the seed's 32-bit words,
-// klen <= 2) for partitions [64 b, 64 b + 64): one LANE per partition runs
-// the 1247-step dependent chain on its own LDS row, so the whole corpus's
-// seeding is one short launch (vs one serial chain per packer wave on the
-// shared scalar unit); the rows then go out partition-major, 624 words per
-// partition, for the packer's coalesced load (WaveRng::load).
-constexpr int MT_ROW = MT_N + 1;  // odd row stride: the lanes' same-index words fall in distinct banks
-__global__ __launch_bounds__(64) void mt_seed_states_kernel(uint64_t seed, int64_t n_part,
-                                                            uint32_t* __restrict__ states) {
-  __shared__ uint32_t rows[64 * MT_ROW];
-  const int lane = threadIdx.x;
-  const int64_t p0 = (int64_t)blockIdx.x * 64;
-  const uint64_t n = seed + (uint64_t)(p0 + lane);
+// klen <= 2), a LANE per partition: the whole corpus's seeding is one short
+// launch (vs one serial chain per packer wave on the shared scalar unit).
+// Each lane's 1247-step chain carries mt[i-1] in a register; its words go
+// straight to the partition's 624-word row in global memory (the packer's
+// coalesced load, WaveRng::load), and the second loop reads back what the
+// first wrote there (independent of the chain, so the loads run ahead).
+// Rows exist for every lane of the grid (the buffer is rounded up to 64
+// partitions): no store guards.
+__global__ __launch_bounds__(64) void mt_seed_states_kernel(uint64_t seed, uint32_t* __restrict__ states) {
+  const int64_t p = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  const uint64_t n = seed + (uint64_t)p;
   const uint32_t key0 = (uint32_t)n;
-  const uint32_t key1 = (uint32_t)(n >> 32) + 1u;  // key[1] + j (j = 1)
-  const bool two = (n >> 32) != 0;                 // klen 2
-  uint32_t* r = rows + lane * MT_ROW;
-  for (int i = 0; i < MT_N; ++i) r[i] = kMtGenrand.v[i];
-  // first loop, max(N, klen) = N steps from i = 1; prev is always mt[i - 1]
-  // (after the wrap, mt[0] = mt[N - 1] = prev)
-  uint32_t prev = r[0];
-  int i = 1;
-  bool odd = false;  // j == 1
-  for (int k = 0; k < MT_N; ++k) {
-    prev = (r[i] ^ ((prev ^ (prev >> 30)) * 1664525u)) + (odd ? key1 : key0);
+  const uint32_t key1 = (n >> 32) ? (uint32_t)(n >> 32) + 1u : key0;  // step k odd: key[k % klen] + k % klen
+  uint32_t* const r = states + p * MT_N;
+  // first loop, N steps from i = 1 over init_genrand(19650218)'s words: i =
+  // 1..623, then mt[0] = mt[623] and i = 1 again
+  uint32_t prev = kMtGenrand.v[0];
+  prev = (kMtGenrand.v[1] ^ ((prev ^ (prev >> 30)) * 1664525u)) + key0;
+  const uint32_t m1a = prev;
+#pragma unroll 8
+  for (int i = 2; i < MT_N; ++i) {
+    prev = (kMtGenrand.v[i] ^ ((prev ^ (prev >> 30)) * 1664525u)) + ((i & 1) ? key0 : key1);
     r[i] = prev;
-    odd = two && !odd;
-    if (++i >= MT_N) {
-      r[0] = prev;
-      i = 1;
-    }
   }
-  // second loop, N - 1 steps, continuing at i (= 2)
-  for (int k = 0; k < MT_N - 1; ++k) {
+  prev = (m1a ^ ((prev ^ (prev >> 30)) * 1664525u)) + key1;  // step N - 1 (odd), position 1
+  const uint32_t m1 = prev;
+  // second loop, N - 1 steps: i = 2..623, then position 1
+#pragma unroll 8
+  for (int i = 2; i < MT_N; ++i) {
     prev = (r[i] ^ ((prev ^ (prev >> 30)) * 1566083941u)) - (uint32_t)i;
     r[i] = prev;
-    if (++i >= MT_N) {
-      r[0] = prev;
-      i = 1;
-    }
   }
+  r[1] = (m1 ^ ((prev ^ (prev >> 30)) * 1566083941u)) - 1u;
   r[0] = 0x80000000u;
-  __syncthreads();
-  for (int q = 0; q < 64 && p0 + q < n_part; ++q) {
-    const uint32_t* rq = rows + q * MT_ROW;
-    uint32_t* o = states + (p0 + q) * MT_N;
-    for (int c = lane; c < MT_N; c += 64) o[c] = rq[c];
-  }
 }
 
 hipError_t launch_mt_seed_states(uint64_t seed, int64_t n_part, uint32_t* states, hipStream_t s) {
   if (n_part < 1) return hipSuccess;
-  hipLaunchKernelGGL(mt_seed_states_kernel, dim3((unsigned)((n_part + 63) / 64)), dim3(64), 0, s, seed, n_part,
-                     states);
+  hipLaunchKernelGGL(mt_seed_states_kernel, dim3((unsigned)((n_part + 63) / 64)), dim3(64), 0, s, seed, states);
   return hipGetLastError();
 }
 
