@@ -517,10 +517,22 @@ __global__ __launch_bounds__(256) void scan_write_kernel(const int32_t* ntok, co
   }
   int64_t tot;
   int64_t run = bsum[blockIdx.x] + block_excl_scan256(sum, red, &tot);
+  // the offsets go out through LDS so that consecutive lanes store
+  // consecutive offsets (a thread's 16 offsets stored directly put 64 lines
+  // under every store instruction); one pad slot per 16 spreads the
+  // thread-major writes over the banks
+  __shared__ int64_t ob[SCAN_ITEMS + SCAN_ITEMS / 16];
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
-    if (b0 + k < hi) tokoff[b0 + k] = run;
+    ob[threadIdx.x * 17 + k] = run;
     run += v[k];
+  }
+  __syncthreads();
+  const int64_t c0 = lo + (int64_t)blockIdx.x * SCAN_ITEMS;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int j = k * 256 + threadIdx.x;
+    if (c0 + j < hi) tokoff[c0 + j] = ob[j + (j >> 4)];
   }
   if (lo + ((int64_t)blockIdx.x + 1) * SCAN_ITEMS >= hi && threadIdx.x == 0) tokoff[hi] = bsum[scan_blocks(hi - lo)];
 }
