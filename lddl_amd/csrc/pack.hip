@@ -397,35 +397,64 @@ hipError_t launch_chunk_parts(const int64_t* pair_base, const int64_t* doc_sent_
 
 // (XCD-aware blocks, as materialize2: a partition's rows run on one XCD, so
 // its pair records and binned order are fetched into one L2, not all eight)
+// RS_U consecutive 64-row chunks per wave, each metadata level loaded for all
+// of them before the next: a row's chain (partition -> bases -> binned
+// index -> pair record -> segment offsets) is ~6 dependent loads, and
+// RS_U chains in flight per wave instead of one
+#ifndef LDDL_ROWSPAN_U
+#define LDDL_ROWSPAN_U 2
+#endif
+constexpr int RS_U = LDDL_ROWSPAN_U;
 __global__ __launch_bounds__(256) void rowspan_kernel(MatParams M, int64_t total) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int64_t gbase = (LDDL_ROWSPAN_XCD ? xcd_block(blockIdx.x, gridDim.x) * 4 + wv : (int64_t)blockIdx.x * 4 + wv) * 64;
+  const int64_t gbase =
+      (LDDL_ROWSPAN_XCD ? xcd_block(blockIdx.x, gridDim.x) * 4 + wv : (int64_t)blockIdx.x * 4 + wv) * 64 * RS_U;
   if (gbase >= total) return;
-  const int64_t g = gbase + lane;
-  if (g >= total) return;
-  int64_t p = M.chunk_part[gbase >> 6];
-  while (M.pair_base[p + 1] <= g) ++p;  // partitions of < 64 pairs
-  const int64_t i = g - M.pair_base[p];
-  const int64_t pb = M.part_pb[p];
-  const PairRec r = M.pairs[pb + M.binned[pb + i]];
-  const int32_t l0 = r.hi0 - r.lo0, l1 = r.hi1 - r.lo1;
-  M.out_src0[g] = l0 > 0 ? M.fs_dense[r.fs0] + r.lo0 : 0;
-  M.out_src1[g] = l1 > 0 ? M.fs_dense[r.fs1] + r.lo1 : 0;
-  if (M.out_tok_off) {
-    const int64_t off = M.tok_base[p] + M.tok_local[pb + i];
-    M.out_tok_off[g] = off;
-    if (g == total - 1) M.out_tok_off[total] = off + r.num_tokens;
+  int64_t g[RS_U], p[RS_U];
+  bool in[RS_U];
+#pragma unroll
+  for (int u = 0; u < RS_U; ++u) {
+    g[u] = gbase + 64 * u + lane;
+    in[u] = g[u] < total;
+    p[u] = in[u] ? M.chunk_part[(gbase >> 6) + u] : 0;
   }
-  M.out_len0[g] = (uint16_t)l0;
-  M.out_len1[g] = (uint16_t)l1;
-  M.out_flags[g] = (uint8_t)r.flags;
-  const int32_t b = ((int32_t)r.num_tokens - 1) / M.bin_size;
-  M.out_bin[g] = (uint8_t)(b > M.nbins - 1 ? M.nbins - 1 : b);
-  M.out_part[g] = p;
+  int64_t i[RS_U], pb[RS_U];
+#pragma unroll
+  for (int u = 0; u < RS_U; ++u) {
+    if (in[u]) {
+      while (M.pair_base[p[u] + 1] <= g[u]) ++p[u];  // partitions of < 64 pairs
+    }
+    i[u] = in[u] ? g[u] - M.pair_base[p[u]] : 0;
+    pb[u] = in[u] ? M.part_pb[p[u]] : 0;
+  }
+  int32_t bi[RS_U];
+#pragma unroll
+  for (int u = 0; u < RS_U; ++u) bi[u] = in[u] ? M.binned[pb[u] + i[u]] : 0;
+  PairRec r[RS_U];
+#pragma unroll
+  for (int u = 0; u < RS_U; ++u) r[u] = M.pairs[in[u] ? pb[u] + bi[u] : 0];
+#pragma unroll
+  for (int u = 0; u < RS_U; ++u) {
+    if (!in[u]) continue;
+    const int32_t l0 = r[u].hi0 - r[u].lo0, l1 = r[u].hi1 - r[u].lo1;
+    M.out_src0[g[u]] = l0 > 0 ? M.fs_dense[r[u].fs0] + r[u].lo0 : 0;
+    M.out_src1[g[u]] = l1 > 0 ? M.fs_dense[r[u].fs1] + r[u].lo1 : 0;
+    if (M.out_tok_off) {
+      const int64_t off = M.tok_base[p[u]] + M.tok_local[pb[u] + i[u]];
+      M.out_tok_off[g[u]] = off;
+      if (g[u] == total - 1) M.out_tok_off[total] = off + r[u].num_tokens;
+    }
+    M.out_len0[g[u]] = (uint16_t)l0;
+    M.out_len1[g[u]] = (uint16_t)l1;
+    M.out_flags[g[u]] = (uint8_t)r[u].flags;
+    const int32_t bb = ((int32_t)r[u].num_tokens - 1) / M.bin_size;
+    M.out_bin[g[u]] = (uint8_t)(bb > M.nbins - 1 ? M.nbins - 1 : bb);
+    M.out_part[g[u]] = p[u];
+  }
 }
 
 hipError_t launch_row_spans(const MatParams& M, int64_t total_pairs, hipStream_t s) {
-  int64_t nblk = (total_pairs + 255) / 256;
+  int64_t nblk = (total_pairs + 256 * RS_U - 1) / (256 * RS_U);
   if (LDDL_ROWSPAN_XCD && nblk >= 64) nblk = (nblk + 7) & ~(int64_t)7;  // xcd_block: 8 equal ranges (extra blocks exit)
   hipLaunchKernelGGL(rowspan_kernel, dim3((unsigned)nblk), dim3(256), 0, s, M, total_pairs);
   return hipGetLastError();
