@@ -1784,17 +1784,35 @@ static hipError_t launch_wpt(const TokParams& P, const SplitParams& S, int n_cu,
 // entries that are vocab ids) + the pieces of its queued words (wp_kernel's
 // per-slot counts over the sentence's contiguous record slots), capped at
 // max_tok; a fallback tile's sentences keep the count the serial path wrote.
+// (CNT_U sentences per thread per pass, 256 apart: each level of their
+// chains -- metadata, then the slot counts -- loaded for all of them first)
+constexpr int CNT_U = 4;
 __global__ __launch_bounds__(256) void count_kernel(TokParams P, SplitParams S) {
   const int64_t sA = S.tile_sent[S.t0], sB = S.tile_sent[S.t1];
-  for (int64_t s = sA + (int64_t)blockIdx.x * 256 + threadIdx.x; s < sB; s += (int64_t)gridDim.x * 256) {
-    const uint2 m = S.smeta[s];
-    int32_t t = P.out_ntok[s];
-    if ((m.x & 0xFFFFu) != SPLIT_NENT_FB) {
-      const uint32_t n = S.snslot[s], q = m.y + (m.x >> 16);
-      for (uint32_t k = 0; k < n; ++k) t += S.cnt8[q + k];
-      t = min(t, P.max_tok);
+  const int64_t stride = (int64_t)gridDim.x * 256 * CNT_U;
+  for (int64_t s0 = sA + (int64_t)blockIdx.x * 256 * CNT_U + threadIdx.x; s0 < sB; s0 += stride) {
+    uint2 m[CNT_U];
+    int32_t t[CNT_U];
+    uint32_t n[CNT_U];
+#pragma unroll
+    for (int u = 0; u < CNT_U; ++u) {
+      const int64_t s = s0 + 256 * u;
+      const bool in = s < sB;
+      m[u] = in ? S.smeta[s] : make_uint2(SPLIT_NENT_FB, 0u);
+      t[u] = in ? P.out_ntok[s] : 0;
+      n[u] = in ? S.snslot[s] : 0u;
     }
-    P.out_ntok[s] = t;
+#pragma unroll
+    for (int u = 0; u < CNT_U; ++u) {
+      if ((m[u].x & 0xFFFFu) != SPLIT_NENT_FB) {
+        const uint32_t q = m[u].y + (m[u].x >> 16);
+        for (uint32_t k = 0; k < n[u]; ++k) t[u] += S.cnt8[q + k];
+        t[u] = min(t[u], P.max_tok);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < CNT_U; ++u)
+      if (s0 + 256 * u < sB) P.out_ntok[s0 + 256 * u] = t[u];
   }
 }
 
@@ -2072,7 +2090,8 @@ hipError_t finish_segment(TokParams P, const SplitParams& S, int n_cu, int fb_gr
 #ifndef LDDL_CNT_BLOCKS
 #define LDDL_CNT_BLOCKS 256
 #endif
-  const int64_t cnt_grid = std::max<int64_t>(1, std::min<int64_t>((int64_t)n_cu * LDDL_CNT_BLOCKS, (S.seg_sent_cap + 255) / 256));
+  const int64_t cnt_grid = std::max<int64_t>(
+      1, std::min<int64_t>((int64_t)n_cu * LDDL_CNT_BLOCKS, (S.seg_sent_cap + 256 * tok5::CNT_U - 1) / (256 * tok5::CNT_U)));
   hipLaunchKernelGGL(tok5::count_kernel, dim3((unsigned)cnt_grid), dim3(256), 0, s, P, S);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   if ((e = launch_scan_ntok_range(P.out_ntok, S.tile_sent + S.t0, S.tile_sent + S.t1, S.seg_sent_cap, P.out_tok_off,
