@@ -1901,9 +1901,9 @@ __global__ __launch_bounds__(256) void expand_kernel(TokParams P, SplitParams S)
     // across loop iterations would wait at every step; here it waits twice
     // per EXP_K steps)
 #ifndef LDDL_EXP_K
-#define LDDL_EXP_K 4
+#define LDDL_EXP_K 5
 #endif
-    constexpr int EXP_K = LDDL_EXP_K;  // 4: 46 VGPRs, 8 waves per SIMD (8 steps: 86 VGPRs, 5 waves, slower)
+    constexpr int EXP_K = LDDL_EXP_K;  // 5: 64 VGPRs, 8 waves per SIMD (6: 68 VGPRs, 7 waves; 8: 80, 6 waves)
     uint32_t carry = 0;
     for (uint32_t st0 = 0; st0 < T; st0 += 64 * EXP_K) {
       uint32_t xj[EXP_K], xv[EXP_K];
